@@ -1,0 +1,183 @@
+"""CPU restatement (oracle) of TRIAD's dense tri-modal contrastive hot path.
+
+TEST INFRASTRUCTURE ONLY. This module is the checker for the HIP product path:
+only `tests/`, `__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg may
+import it. The product package `triad_amd` never imports it and has no CPU
+fallback.
+
+It restates, op for op and in plain PyTorch on the CPU, the reference's
+algorithm (reference snapshot SajayR/TRIAD @ 2025-06-14, `src/model.py`):
+
+  similarity_matrix        model.py:355-368  (L2-normalise, bmm, * temperature)
+  similarities_av          model.py:370-392  (B x B x Na x Nv token sims, max over Nv, mean over Na)
+  temporal_smoothness      model.py:394-408  (diagonal pairs, diff along Na)
+  regularization_av        model.py:410-428  (20*l_cal + 0.15*l_nonneg[-60,0] + 0.01*l_smooth)
+  contrastive_av           model.py:430-472  (symmetric InfoNCE + stats, unbiased std)
+  similarities_tv          model.py:490-514  (masked mean over Nt)
+  regularization_tv        model.py:516-542  (0.15*l_nonneg[-20,0] + w*patch sparsity)
+  contrastive_tv           model.py:544-593
+  patch_dropout            model.py:268-308  (Bernoulli keep mask is an INPUT here, so the
+                                              compaction is reproducible across implementations)
+  projection_head          model.py:32-34,68 / 81-83,116 / 253-255,326 under bf16 autocast
+                           (model.py:483,603): bf16 Linear -> fp32 LayerNorm -> bf16 Linear
+
+Parity pinning: the functions are checked against golden vectors produced by
+running the reference's own methods (tests/golden/gen_golden.py, fixtures
+tests/golden/*.npz) in tests/test_oracle_golden.py.
+
+All functions take a `dtype` for the arithmetic (float64 by default for a tight
+checker; float32 mirrors the reference's CPU arithmetic).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Tuple
+
+import torch
+import torch.nn.functional as F
+
+AV_STAT_KEYS = ("av_pos_sim_mean", "av_pos_sim_std", "av_neg_sim_mean",
+                "av_neg_sim_std", "av_separation", "av_hardest_negative")
+TV_STAT_KEYS = tuple("tv_" + k[3:] for k in AV_STAT_KEYS)
+
+
+def similarity_matrix(f1, f2, temperature, dtype=torch.float64):
+    """model.py:355-368: per-sample (B,N1,N2) cosine-similarity map times temperature."""
+    a = F.normalize(f1.to(dtype), dim=-1)
+    b = F.normalize(f2.to(dtype), dim=-1)
+    return torch.bmm(a, b.transpose(1, 2)) * temperature.to(dtype)
+
+
+def _token_sims(q, v, temperature, dtype):
+    # (B,Nq,D) x (B,Nv,D) -> (Bq,Bk,Nq,Nv): every query sample against every key sample
+    return torch.einsum("iqd,jvd->ijqv", q.to(dtype), v.to(dtype)) * temperature.to(dtype)
+
+
+def similarities_av(audio_feats, visual_feats, temperature, dtype=torch.float64):
+    """model.py:370-392 -> (clip (B,B), token_sims (B,B,Na,Nv))."""
+    s = _token_sims(audio_feats, visual_feats, temperature, dtype)
+    return s.max(dim=3).values.mean(dim=2), s
+
+
+def temporal_smoothness(token_sims):
+    """model.py:394-408: mean squared difference of consecutive audio tokens on the diagonal pairs."""
+    diag = torch.diagonal(token_sims, dim1=0, dim2=1).permute(2, 0, 1)  # (B,Na,Nv)
+    d = diag[:, 1:] - diag[:, :-1]
+    return (d * d).mean()
+
+
+def regularization_av(token_sims, temperature):
+    """model.py:410-428 -> (reg, 0.01*l_smooth)."""
+    t = temperature.to(token_sims.dtype)
+    l_nonneg = token_sims.clamp(min=-60, max=0).pow(2).mean()
+    l_cal = (-torch.log(t)).clamp(min=0).pow(2)  # log(1) - log(temp)
+    l_smooth = temporal_smoothness(token_sims)
+    return 20 * l_cal + 0.15 * l_nonneg + 0.01 * l_smooth, 0.01 * l_smooth
+
+
+def _symmetric_ce(clip):
+    n = clip.shape[0]
+    idx = torch.arange(n)
+    row = -F.log_softmax(clip, dim=1)[idx, idx]
+    col = -F.log_softmax(clip.t(), dim=1)[idx, idx]
+    return (row + col).mean() / 2
+
+
+def _stats(clip, keys):
+    n = clip.shape[0]
+    pos = torch.diagonal(clip)
+    off = ~torch.eye(n, dtype=torch.bool)
+    neg = clip[off]
+    vals = [pos.mean(), pos.std(), neg.mean(), neg.std()]
+    vals = [float(v.detach()) for v in vals]
+    hardest = float(neg.max().detach())  # raises on B == 1, as the reference does
+    return dict(zip(keys, vals[:4] + [vals[0] - vals[2], hardest]))
+
+
+def contrastive_av(clip, token_sims, temperature):
+    """model.py:430-472 -> (total, contrastive, reg, 0.01*smooth, stats)."""
+    stats = _stats(clip, AV_STAT_KEYS)
+    ce = _symmetric_ce(clip)
+    reg, smooth = regularization_av(token_sims, temperature)
+    return ce + reg, ce, reg, smooth, stats
+
+
+def similarities_tv(text_feats, visual_feats, attention_mask, temperature, dtype=torch.float64):
+    """model.py:490-514 -> (clip (B,B), token_sims (B,B,Nt,Nv))."""
+    s = _token_sims(text_feats, visual_feats, temperature, dtype)
+    mx = s.max(dim=3).values  # (B,B,Nt)
+    m = attention_mask.to(dtype)[:, None, :]
+    return (mx * m).sum(dim=2) / m.sum(dim=2).clamp(min=1e-7), s
+
+
+def regularization_tv(token_sims, threshold, weight):
+    """model.py:516-542."""
+    l_nonneg = token_sims.clamp(min=-20, max=0).pow(2).mean()
+    diag = torch.diagonal(token_sims, dim1=0, dim2=1).permute(2, 0, 1)  # (B,Nt,Nv)
+    probs = torch.softmax(diag, dim=-1)
+    frac = probs.sum(dim=1) / probs.shape[1]
+    sparsity = F.relu(frac - threshold).pow(2).mean()
+    return 0.15 * l_nonneg + weight * sparsity
+
+
+def contrastive_tv(clip, token_sims, threshold, weight):
+    """model.py:544-593 -> (total, stats)."""
+    stats = _stats(clip, TV_STAT_KEYS)
+    return _symmetric_ce(clip) + regularization_tv(token_sims, threshold, weight), stats
+
+
+def patch_dropout(x, keep_mask):
+    """model.py:268-308 with the Bernoulli keep mask supplied by the caller.
+
+    Kept tokens of each sample stay in their original order; samples are
+    zero-padded to the longest kept length.
+    """
+    kept = [x[i][keep_mask[i].bool()] for i in range(x.shape[0])]
+    n = max(k.shape[0] for k in kept)
+    out = x.new_zeros(x.shape[0], n, x.shape[2])
+    for i, k in enumerate(kept):
+        out[i, :k.shape[0]] = k
+    return out
+
+
+def _bf16(x):
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+def projection_head(h, w1, b1, gamma, beta, w2, b2, amp=True, eps=1e-5):
+    """proj2(LN(proj1(h))) (model.py:68,116,326).
+
+    amp=True emulates CUDA bf16 autocast (model.py:483,603): Linear operands and
+    outputs rounded to bf16, LayerNorm computed in fp32 from the bf16 input.
+    """
+    if not amp:
+        y = F.linear(h, w1, b1)
+        y = F.layer_norm(y, (y.shape[-1],), gamma, beta, eps)
+        return F.linear(y, w2, b2)
+    y = _bf16(F.linear(_bf16(h), _bf16(w1), _bf16(b1)))
+    y = F.layer_norm(y, (y.shape[-1],), gamma.float(), beta.float(), eps)
+    return _bf16(F.linear(_bf16(y), _bf16(w2), _bf16(b2)))
+
+
+def av_loss(audio_feats, visual_feats, temperature, dtype=torch.float64):
+    """forward_audio_visual's loss half (model.py:486-488) on given features."""
+    clip, s = similarities_av(audio_feats, visual_feats, temperature, dtype)
+    return contrastive_av(clip, s, temperature)
+
+
+def tv_loss(text_feats, visual_feats, mask, temperature, threshold, weight, dtype=torch.float64):
+    """forward_text_visual's loss half (model.py:606-608) on given features."""
+    clip, s = similarities_tv(text_feats, visual_feats, mask, temperature, dtype)
+    return contrastive_tv(clip, s, threshold, weight)
+
+
+def loss_mix(phase, av, tv, progress=0.0, av_start=0.8, av_end=0.5):
+    """train.py:972-984 curriculum loss mixing."""
+    if phase == "av_focus":
+        return av
+    if phase == "tv_warmup":
+        return tv
+    if phase == "weighted_joint":
+        w = av_start - progress * (av_start - av_end)
+        return w * av + (1.0 - w) * tv
+    return av + tv

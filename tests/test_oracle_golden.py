@@ -1,0 +1,76 @@
+"""Pin the CPU oracle (oracle/ref_cpu.py) to the reference's own outputs.
+
+The fixtures were produced by running /root/reference/src/model.py's hot-path
+methods (tests/golden/gen_golden.py). fp32 reference vs float64 oracle.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu
+from tests import golden_io as G
+
+
+def _close(a, b, rtol=1e-4, atol=1e-5):
+    if isinstance(a, float) and math.isnan(a):
+        return math.isnan(b)
+    return abs(a - b) <= atol + rtol * abs(b)
+
+
+@pytest.mark.parametrize("name", G.names("av"))
+def test_av_matches_reference(name):
+    f = G.load(name)
+    A = G.bf16(f["A"]).double().requires_grad_(True)
+    V = G.bf16(f["V"]).double().requires_grad_(True)
+    t = torch.tensor(float(f["temp"]), dtype=torch.float64, requires_grad=True)
+    clip, s = ref_cpu.similarities_av(A, V, t)
+    total, ce, reg, smooth, stats = ref_cpu.contrastive_av(clip, s, t)
+    np.testing.assert_allclose(clip.detach().numpy(), f["clip"], rtol=1e-4, atol=1e-4)
+    assert _close(float(ce), float(f["ce"]))
+    assert _close(float(reg), float(f["reg"]))
+    assert _close(float(smooth), float(f["smooth"]))
+    assert _close(float(total), float(f["total"]))
+    for k, v in zip(ref_cpu.AV_STAT_KEYS, f["stats"]):
+        assert _close(stats[k], float(v), rtol=1e-4, atol=1e-4), k
+    # Na == 1: the smoothness mean is over an empty set, so `total` is NaN in the
+    # reference while its gradients stay finite (the empty term contributes none).
+    total.backward()
+    np.testing.assert_allclose(A.grad.numpy(), f["dA"], rtol=2e-3, atol=1e-7)
+    np.testing.assert_allclose(V.grad.numpy(), f["dV"], rtol=2e-3, atol=1e-7)
+    assert _close(float(t.grad), float(f["dtemp"]), rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", G.names("tv"))
+def test_tv_matches_reference(name):
+    f = G.load(name)
+    T = G.bf16(f["T"]).double().requires_grad_(True)
+    V = G.bf16(f["V"]).double().requires_grad_(True)
+    mask = torch.from_numpy(f["mask"])
+    t = torch.tensor(float(f["temp"]), dtype=torch.float64, requires_grad=True)
+    clip, s = ref_cpu.similarities_tv(T, V, mask, t)
+    total, stats = ref_cpu.contrastive_tv(clip, s, float(f["thr"]), float(f["w"]))
+    np.testing.assert_allclose(clip.detach().numpy(), f["clip"], rtol=1e-4, atol=1e-4)
+    assert _close(float(total), float(f["total"]))
+    for k, v in zip(ref_cpu.TV_STAT_KEYS, f["stats"]):
+        assert _close(stats[k], float(v), rtol=1e-4, atol=1e-4), k
+    total.backward()
+    np.testing.assert_allclose(T.grad.numpy(), f["dT"], rtol=2e-3, atol=1e-7)
+    np.testing.assert_allclose(V.grad.numpy(), f["dV"], rtol=2e-3, atol=1e-7)
+    assert _close(float(t.grad), float(f["dtemp"]), rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", G.names("simmat"))
+def test_similarity_matrix_matches_reference(name):
+    f = G.load(name)
+    sim = ref_cpu.similarity_matrix(G.bf16(f["f1"]), G.bf16(f["f2"]),
+                                    torch.tensor(float(f["temp"])))
+    np.testing.assert_allclose(sim.numpy(), f["sim"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", G.names("dropout"))
+def test_patch_dropout_matches_reference(name):
+    f = G.load(name)
+    out = ref_cpu.patch_dropout(G.bf16(f["x"]), torch.from_numpy(f["keep"]))
+    np.testing.assert_array_equal(out.numpy(), G.bf16(f["out"]).numpy())
