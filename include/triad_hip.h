@@ -1,0 +1,108 @@
+/* libtriad_hip.so -- C ABI of the MI355X-native dense tri-modal contrastive hot path.
+ *
+ * The reference (SajayR/TRIAD @ 2025-06-14) has no FFI: its boundary is the Python
+ * method API of src/model.py. Each entry point below replaces one step of that API;
+ * the reference file:line it replaces is cited on each declaration. The Python
+ * mirror of the reference API (triad_amd/model.py, triad_amd/ops.py) binds these
+ * with ctypes; INTEGRATION.md shows the binding a maintainer would add.
+ *
+ * Conventions
+ *   - every pointer is a device pointer to caller-owned memory (the PyTorch
+ *     caching allocator in the Python mirror); no entry point allocates, frees or
+ *     synchronises, so all of them are hipGraph-capturable;
+ *   - work is enqueued on `stream` (the caller's current HIP stream);
+ *   - return 0 on success, TRIAD_EINVAL (1001) on a bad shape/argument, or the
+ *     hipError_t of a failed launch;
+ *   - bf16 buffers are raw 16-bit bfloat16; "rows" are row-major with 512 features.
+ *   - thread-safe when each thread uses its own stream and buffers.
+ *
+ * Layouts
+ *   Q   [R_pad][512] bf16: query tokens of Bq samples flattened, row r = i*Nq + q,
+ *       R = Bq*Nq valid rows, R_pad a multiple of 256 (rows >= R zero).
+ *   K   [C_alloc][512] bf16: key tokens of Bk samples, sample j at rows
+ *       [j*Nk_pad, (j+1)*Nk_pad), Nk_pad a multiple of 32; keys k < Nk_eff are real
+ *       (zero rows from patch dropout included), keys >= Nk_eff are padding.
+ *       C_alloc >= Bk*Nk_pad, a multiple of 128, rows beyond Bk*Nk_pad zero.
+ */
+#ifndef TRIAD_HIP_H
+#define TRIAD_HIP_H
+
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TRIAD_EINVAL 1001
+
+/* Number of per-workgroup partials written by triad_pairsim_fwd / _dS. */
+int triad_pairsim_nparts(int R_pad, int Bk);
+
+/* Fused S = temp * Q K^T per (query row, key sample), never materialised:
+ * rowmax[j][r] = max_k S, argmax[j][r] = first argmax, nn_part[wg] = partial
+ * sum of clamp(S, clamp_lo, 0)^2 (double), diagS[i][q][k] = S on the diagonal
+ * pairs (j == i + diag_off) when diag != 0 and diagS != NULL.
+ * Replaces model.py:370-392 (AV) / 490-514 (TV) token_sims + max, and the
+ * l_nonneg reduction of model.py:417-418 / 524-525. */
+int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
+                      int Nk_eff, int D, const float* temp, float clamp_lo, int diag, int diag_off,
+                      float* rowmax, int* argmax, double* nn_part, float* diagS, hipStream_t stream);
+
+/* clip[i][j] = sum_q m_iq rowmax[j][i*Nq+q] / norm_i (AV: qmask NULL, norm = Nq;
+ * TV: norm = max(sum_q m_iq, 1e-7)); qw[r] = d clip / d rowmax (may be NULL).
+ * Replaces model.py:389-391 (mean over Na) / 509-512 (masked mean over Nt). */
+int triad_clip_reduce(const float* rowmax, int R_pad, int Nq, int Bq, int Bk, const float* qmask, float* clip,
+                      float* qw, hipStream_t stream);
+
+/* AV temporal smoothness on the diagonal pairs: part[i] = sum_{q>=1,k} (S[q,k]-S[q-1,k])^2,
+ * g = d(sum/cnt)/dS. cnt = B_global*(Nq-1)*Nk_eff. Replaces model.py:394-408. */
+int triad_diag_smooth(const float* diagS, int Bq, int Nq, int Nk_pad, int Nk_eff, double cnt, double* part,
+                      float* g, hipStream_t stream);
+
+/* TV patch-usage sparsity on the diagonal pairs; overwrites diagS with the gradient of
+ * sum/cnt, cnt = B_global*Nk_eff. Replaces model.py:527-540. */
+int triad_diag_sparsity(float* diagS_g, int Bq, int Nt, int Nk_pad, int Nk_eff, float thr, double cnt,
+                        double* part, hipStream_t stream);
+
+/* B x B loss head: symmetric InfoNCE, regulariser combination and similarity
+ * statistics (kind 0 = AV, 1 = TV) into out[13]; dclip = d CE / d clip.
+ * out: total, ce, reg, 0.01*smooth|sparsity, pos_mean, pos_std, neg_mean, neg_std,
+ *      separation, hardest_negative, l_nonneg, l_cal, diag_loss.
+ * Replaces model.py:430-472 (AV) / 544-593 (TV) and 410-428 / 516-542's combination. */
+int triad_losshead(const float* clip, int B, int kind, const float* temp, const double* nn_part, int n_nn,
+                   double n_el, const double* dg_part, int n_dg, double dg_cnt, float w_sparse, float* out,
+                   float* dclip, float* lse_scratch, hipStream_t stream);
+
+/* Backward of the fused head: recompute S, form
+ * dS = c_ce*dclip[i][j]*qw[r]*[k==argmax] + c_nn*clamp'(S) + c_diag*dSdiag (diag pairs),
+ * write it as bf16 [R_pad][ldS], and per-workgroup partials of sum(dS * S/temp).
+ * coef = {c_ce, c_nn, c_diag, c_cal} (device). Autograd of model.py:384-428 / 502-542. */
+int triad_pairsim_dS(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
+                     int Nk_eff, int D, const float* temp, float clamp_lo, int diag, int diag_off,
+                     const int* argmax, const float* dclip, const float* qw, const float* dSdiag,
+                     const float* coef, void* dS, long long ldS, double* dt_part, hipStream_t stream);
+
+/* dL/dtemp = sum(parts) + coef[3] * d l_cal/d temp (has_cal, AV model.py:420-424). */
+int triad_dtemp_finalize(const double* part, int n, const float* temp, const float* coef, int has_cal,
+                         float* out, hipStream_t stream);
+
+/* C = alpha * op(A) . op(B): A [M][Kd] (a_kcontig=1) or [Kd][M] (0); B [N][Kd] (b_kcontig=1)
+ * or [Kd][N] (0); C fp32 or bf16 (out_bf16). M, N multiples of 128, Kd of 64.
+ * dQ = temp * dS . K and dK = temp * dS^T . Q of S = temp * Q K^T (model.py:387/505),
+ * and the projection-head GEMMs (model.py:68/116/326). */
+int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                    int M, int N, int Kd, const float* alpha, void* C, long long ldc, int out_bf16,
+                    hipStream_t stream);
+
+/* dst[b][t] = idx[b][t] >= 0 ? src[b][idx[b][t]] : 0 (row_bytes per row). Patch-dropout
+ * compaction with zero padding (model.py:282-307) and its backward scatter. */
+int triad_gather_rows(const void* src, long long src_rows, const int* idx, int B, int M, int row_bytes, void* dst,
+                      hipStream_t stream);
+
+/* y = x / max(||x||_2, eps) per row, bf16 (F.normalize, model.py:363-364). */
+int triad_l2norm_rows(const void* x, int rows, int D, float eps, void* y, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRIAD_HIP_H */

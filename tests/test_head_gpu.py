@@ -1,0 +1,160 @@
+"""GPU parity of the fused contrastive head (HIP) against the golden fixtures
+and the CPU oracle. Tolerances: forward losses/statistics 1e-4 relative (the
+kernels compute the fp32 arithmetic exactly on bf16 inputs); feature gradients
+bf16 tolerance (dS is rounded to bf16 before the MFMA GEMMs): relative L2 error
+< 1e-2 and elementwise within 3e-2 * max|g|.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu
+from tests import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def _ops():
+    from triad_amd import ops
+    return ops
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _check_grad(got, ref):
+    got = got.detach().float().cpu().numpy()
+    assert _rel(got, ref) < 1e-2, _rel(got, ref)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=3e-2 * float(np.abs(ref).max()) + 1e-12)
+
+
+def _scalar_close(a, b, rtol=1e-4, atol=1e-5):
+    if math.isnan(b):
+        return math.isnan(a)
+    return abs(a - b) <= atol + rtol * abs(b)
+
+
+@pytest.mark.parametrize("name", G.names("av"))
+def test_av_head_matches_golden(name):
+    ops = _ops()
+    f = G.load(name)
+    A = G.bf16(f["A"]).to(dev, torch.bfloat16).requires_grad_(True)
+    V = G.bf16(f["V"]).to(dev, torch.bfloat16).requires_grad_(True)
+    t = torch.tensor(float(f["temp"]), device=dev, requires_grad=True)
+    losses, stats, clip = ops.contrastive_head(ops.AV, A, V, t)
+    losses[0].backward()
+    np.testing.assert_allclose(clip.cpu().numpy(), f["clip"], rtol=1e-4, atol=1e-4)
+    lv = losses.detach().cpu().double().numpy()
+    for got, key in zip(lv, ("total", "ce", "reg", "smooth")):
+        assert _scalar_close(float(got), float(f[key])), (key, got, f[key])
+    sv = stats.cpu().double().numpy()
+    for got, want in zip(sv[:6], f["stats"]):
+        assert _scalar_close(float(got), float(want), 1e-4, 1e-4)
+    _check_grad(A.grad, f["dA"])
+    _check_grad(V.grad, f["dV"])
+    assert _scalar_close(float(t.grad), float(f["dtemp"]), 2e-3, 1e-5)
+
+
+@pytest.mark.parametrize("name", G.names("tv"))
+def test_tv_head_matches_golden(name):
+    ops = _ops()
+    f = G.load(name)
+    T = G.bf16(f["T"]).to(dev, torch.bfloat16).requires_grad_(True)
+    V = G.bf16(f["V"]).to(dev, torch.bfloat16).requires_grad_(True)
+    mask = torch.from_numpy(f["mask"]).to(dev)
+    t = torch.tensor(float(f["temp"]), device=dev, requires_grad=True)
+    losses, stats, clip = ops.contrastive_head(ops.TV, T, V, t, q_mask=mask, threshold=float(f["thr"]),
+                                               sparsity_weight=float(f["w"]))
+    losses[0].backward()
+    np.testing.assert_allclose(clip.cpu().numpy(), f["clip"], rtol=1e-4, atol=1e-4)
+    assert _scalar_close(float(losses[0]), float(f["total"]))
+    sv = stats.cpu().double().numpy()
+    for got, want in zip(sv[:6], f["stats"]):
+        assert _scalar_close(float(got), float(want), 1e-4, 1e-4)
+    _check_grad(T.grad, f["dT"])
+    _check_grad(V.grad, f["dV"])
+    assert _scalar_close(float(t.grad), float(f["dtemp"]), 2e-3, 1e-5)
+
+
+def _rand_feats(g, shape):
+    return (torch.randn(*shape, generator=g) * 0.58).to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("B,Na,Nv,pad", [(8, 199, 256, False), (6, 199, 200, True), (16, 50, 96, True)])
+def test_av_head_vs_oracle_random(B, Na, Nv, pad):
+    ops = _ops()
+    g = torch.Generator().manual_seed(100 + B)
+    A = _rand_feats(g, (B, Na, 512))
+    V = _rand_feats(g, (B, Nv, 512))
+    if pad:
+        lens = torch.randint(Nv // 2, Nv + 1, (B,), generator=g)
+        lens[0] = Nv
+        for j in range(B):
+            V[j, lens[j]:] = 0
+    temp = 1.5
+    Ar, Vr = A.double().requires_grad_(True), V.double().requires_grad_(True)
+    tr = torch.tensor(temp, dtype=torch.float64, requires_grad=True)
+    total, ce, reg, sm, stats = ref_cpu.av_loss(Ar, Vr, tr)
+    total.backward()
+    Ag = A.to(dev, torch.bfloat16).requires_grad_(True)
+    Vg = V.to(dev, torch.bfloat16).requires_grad_(True)
+    tg = torch.tensor(temp, device=dev, requires_grad=True)
+    losses, st, clip = ops.contrastive_head(ops.AV, Ag, Vg, tg)
+    losses[0].backward()
+    lv = losses.detach().cpu().double().numpy()
+    for got, want in zip(lv, (total, ce, reg, sm)):
+        assert _scalar_close(float(got), float(want)), (got, float(want))
+    _check_grad(Ag.grad, Ar.grad.numpy())
+    _check_grad(Vg.grad, Vr.grad.numpy())
+    assert _scalar_close(float(tg.grad), float(tr.grad), 2e-3, 1e-5)
+
+
+@pytest.mark.parametrize("B,Nt,Nv", [(16, 32, 205), (12, 16, 64)])
+def test_tv_head_vs_oracle_random(B, Nt, Nv):
+    ops = _ops()
+    g = torch.Generator().manual_seed(200 + B)
+    T = _rand_feats(g, (B, Nt, 512))
+    V = _rand_feats(g, (B, Nv, 512))
+    mask = (torch.arange(Nt)[None, :] < torch.randint(1, Nt + 1, (B, 1), generator=g)).long()
+    temp, thr, w = 1.5, 0.005, 0.3
+    Tr, Vr = T.double().requires_grad_(True), V.double().requires_grad_(True)
+    tr = torch.tensor(temp, dtype=torch.float64, requires_grad=True)
+    total, stats = ref_cpu.tv_loss(Tr, Vr, mask, tr, thr, w)
+    total.backward()
+    Tg = T.to(dev, torch.bfloat16).requires_grad_(True)
+    Vg = V.to(dev, torch.bfloat16).requires_grad_(True)
+    tg = torch.tensor(temp, device=dev, requires_grad=True)
+    losses, st, clip = ops.contrastive_head(ops.TV, Tg, Vg, tg, q_mask=mask.to(dev), threshold=thr,
+                                            sparsity_weight=w)
+    losses[0].backward()
+    assert _scalar_close(float(losses[0]), float(total))
+    _check_grad(Tg.grad, Tr.grad.numpy())
+    _check_grad(Vg.grad, Vr.grad.numpy())
+    assert _scalar_close(float(tg.grad), float(tr.grad), 2e-3, 1e-5)
+
+
+@pytest.mark.parametrize("kcontig,bk", [(1, 0), (0, 0), (1, 1), (0, 1)])
+def test_gemm_layouts_vs_torch(kcontig, bk):
+    """triad_gemm_bf16 against a plain fp32 torch matmul of the same bf16 operands."""
+    from triad_amd._lib import call, ptr, stream_ptr
+    g = torch.Generator().manual_seed(7)
+    M, N, K = 256, 512, 384
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    B = torch.randn(K, N, generator=g).to(torch.bfloat16)
+    ref = 0.7 * (A.float() @ B.float())
+    Ad = (A if kcontig else A.t().contiguous()).to(dev)
+    Bd = (B.t().contiguous() if bk else B).to(dev)
+    alpha = torch.tensor([0.7], device=dev)
+    C = torch.empty(M, N, device=dev)
+    call("triad_gemm_bf16", ptr(Ad), K if kcontig else M, kcontig, ptr(Bd), K if bk else N, bk, M, N, K, ptr(alpha),
+         ptr(C), N, 0,
+         stream_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(C.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-3)

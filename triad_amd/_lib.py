@@ -1,0 +1,75 @@
+"""ctypes binding of libtriad_hip.so (the C ABI declared in include/triad_hip.h).
+
+The product path has exactly one implementation: the HIP kernels in this
+library. If the library is missing or the process has no HIP device, every op
+raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtriad_hip.so")
+
+vp, i32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_double
+
+# name -> argtypes (restype is always int status). Keep in sync with include/triad_hip.h.
+SIGNATURES = {
+    "triad_pairsim_nparts": [i32, i32],
+    "triad_pairsim_fwd": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, f32, i32, i32, vp, vp, vp, vp, vp],
+    "triad_clip_reduce": [vp, i32, i32, i32, i32, vp, vp, vp, vp],
+    "triad_diag_smooth": [vp, i32, i32, i32, i32, f64, vp, vp, vp],
+    "triad_diag_sparsity": [vp, i32, i32, i32, i32, f32, f64, vp, vp],
+    "triad_losshead": [vp, i32, i32, vp, vp, i32, f64, vp, i32, f64, f32, vp, vp, vp, vp],
+    "triad_pairsim_dS": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, f32, i32, i32, vp, vp, vp, vp, vp,
+                         vp, i64, vp, vp],
+    "triad_dtemp_finalize": [vp, i32, vp, vp, i32, vp, vp],
+    "triad_gemm_bf16": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, i32, vp],
+    "triad_gather_rows": [vp, i64, vp, i32, i32, i32, vp, vp],
+    "triad_l2norm_rows": [vp, i32, i32, f32, vp, vp],
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class TriadError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library (raises if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise TriadError(f"{LIB_PATH} not found: build it with `python -m triad_amd.build` "
+                                 "(or __graft_entry__.build()); there is no CPU fallback")
+            lib = C.CDLL(LIB_PATH)
+            for name, args in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = C.c_int
+            _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    """Invoke an entry point; non-zero status -> TriadError (RuntimeError)."""
+    rc = getattr(load(), name)(*args)
+    if name != "triad_pairsim_nparts" and rc != 0:
+        what = "invalid argument/shape" if rc == 1001 else f"hipError_t {rc}"
+        raise TriadError(f"{name} failed: {what}")
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,90 @@
+// Shared device helpers for the TRIAD MI355X (gfx950 / CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "triad_hip.h"
+
+#define TRIAD_OK 0
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+// One 16-byte global->LDS DMA per lane (global_load_lds_dwordx4). The LDS
+// destination is the wave-uniform `lds_base` + lane*16; the global source is
+// per lane (CDNA4 LDS-DMA semantics).
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(gsrc, LDS_PTR(void, lds_base), 16, 0, 0);
+}
+
+// Make this wave's LDS-DMA writes complete, then barrier: the only ordering
+// that makes global_load_lds data visible to other waves' ds_reads. (hipcc for
+// gfx950 does NOT add the vmcnt wait to __syncthreads() by itself.)
+__device__ __forceinline__ void lds_dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// 32x32x16 bf16 MFMA, fp32 accumulate.
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Transposed LDS read (ds_read_b64_tr_b16): lane 4q+p of each 16-lane group
+// supplies the address of row q, columns 4p..4p+3 of a 4x16 block; lane i of
+// the group receives column i of the 4 rows.
+__device__ __forceinline__ s16x4 lds_tr16(const void* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Block-wide double sum; every thread gets the result. `red` needs
+// blockDim.x/64 doubles of LDS.
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  v = wave_sum_d(v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+#define TRIAD_CHECK_LAUNCH()                                   \
+  do {                                                         \
+    hipError_t _e = hipGetLastError();                         \
+    if (_e != hipSuccess) return (int)_e;                      \
+  } while (0)

@@ -1,0 +1,183 @@
+// bf16 MFMA GEMMs for the backward of the fused similarity head:
+//   dQ[r][d] = temp * sum_c dS[r][c] * K[c][d]      (A = dS,   k-contiguous)
+//   dK[c][d] = temp * sum_r dS[r][c] * Q[r][d]      (A = dS^T, read transposed from dS)
+// i.e. the gradients of S = temp * Q K^T (model.py:387 / 505) w.r.t. both operands.
+// B (= K or Q, [k][n] row-major, n-contiguous) is always read with the gfx950
+// transposing LDS read ds_read_b64_tr_b16, so neither dS nor the features are
+// ever copied into a transposed layout in HBM.
+//
+// Tile 128x128x64, 4 waves (2x2), each wave 64x64 = 2x2 tiles of
+// v_mfma_f32_32x32x16_bf16. Operands are staged global->LDS with 16-byte LDS-DMA
+// (global_load_lds_dwordx4) into two buffers; swizzles are applied on the
+// global SOURCE address so the lane-linear DMA image is bank-conflict-free for
+// the reads (ds_read_b128 for k-contiguous, ds_read_b64_tr_b16 for the others).
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int A_ELEMS = BM * BK, B_ELEMS = BK * BN;
+
+// k-contiguous image [m][64 k] (128-B rows): 16-B chunk c of row m lives at chunk c ^ ((m >> 1) & 7)
+__device__ __forceinline__ int kc_off(int m, int chunk) { return m * BK + ((chunk ^ ((m >> 1) & 7)) << 3); }
+// n-contiguous image [k][128 n] (256-B rows): chunk c of row k lives at chunk c ^ ((k & 3) << 2)
+__device__ __forceinline__ int nc_off(int k, int col) {
+  return k * BN + ((((col >> 3) ^ ((k & 3) << 2))) << 3) + (col & 7);
+}
+
+template <bool A_KCONTIG>
+__device__ __forceinline__ void stage_a(const bf16* __restrict__ A, long long lda, int m0, int k0, bf16* dst,
+                                        int wave, int lane) {
+  if (A_KCONTIG) {
+    // 16 wave-instructions of 8 rows x 128 B
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int inst = wave * 4 + u;
+      const int m = inst * 8 + (lane >> 3), cp = lane & 7;
+      const int c = cp ^ ((m >> 1) & 7);
+      glds16(A + (size_t)(m0 + m) * lda + k0 + c * 8, dst + inst * 512);
+    }
+  } else {
+    // A stored [k][m]: 16 wave-instructions of 4 k-rows x 256 B
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int inst = wave * 4 + u;
+      const int k = inst * 4 + (lane >> 4), cp = lane & 15;
+      const int c = cp ^ ((k & 3) << 2);
+      glds16(A + (size_t)(k0 + k) * lda + m0 + c * 8, dst + inst * 512);
+    }
+  }
+}
+
+// B is [k][n] (B_KCONTIG=0, n-contiguous) or [n][k] (B_KCONTIG=1) -- the same two
+// images as A with the roles of m and n swapped.
+template <bool B_KCONTIG>
+__device__ __forceinline__ void stage_b(const bf16* __restrict__ B, long long ldb, int n0, int k0, bf16* dst,
+                                        int wave, int lane) {
+  stage_a<B_KCONTIG>(B, ldb, n0, k0, dst, wave, lane);
+}
+
+// Fragment of a [k][n]-image operand for MFMA 32x32x16: lane l needs
+// X[k = 16 s + 8 h + j][n = n0 + (l & 31)], j = 0..7, via two 4-row transposed reads.
+__device__ __forceinline__ bf16x8 frag_tr(const bf16* img, int n0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, hh = g >> 1;
+  const int col = n0 + 16 * (g & 1) + 4 * p;
+  const int k0 = 16 * s + 8 * hh + q;
+  const s16x4 lo = lds_tr16(img + nc_off(k0, col));
+  const s16x4 hi = lds_tr16(img + nc_off(k0 + 4, col));
+  bf16x8 r;
+  s16x4* rp = (s16x4*)&r;
+  rp[0] = lo;
+  rp[1] = hi;
+  return r;
+}
+
+template <bool A_KCONTIG, bool B_KCONTIG, typename OutT>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A, long long lda,
+                                                      const bf16* __restrict__ B, long long ldb,
+                                                      int M, int N, int Kd, const float* __restrict__ alpha_p,
+                                                      OutT* __restrict__ C, long long ldc) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * (A_ELEMS + B_ELEMS)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5;
+
+  // XCD-aware bijective remap: blocks sharing an XCD (bid % 8) get consecutive tiles,
+  // so the N/BN column tiles of one row panel of A share that XCD's L2.
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  const int ntn = N / BN;
+  const int m0 = (swz / ntn) * BM, n0 = (swz % ntn) * BN;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){};
+
+  const int nk = Kd / BK;
+  stage_a<A_KCONTIG>(A, lda, m0, 0, lds, wave, lane);
+  stage_b<B_KCONTIG>(B, ldb, n0, 0, lds + A_ELEMS, wave, lane);
+  for (int kt = 0; kt < nk; ++kt) {
+    lds_dma_barrier();
+    if (kt + 1 < nk) {
+      bf16* nb = lds + ((kt + 1) & 1) * (A_ELEMS + B_ELEMS);
+      stage_a<A_KCONTIG>(A, lda, m0, (kt + 1) * BK, nb, wave, lane);
+      stage_b<B_KCONTIG>(B, ldb, n0, (kt + 1) * BK, nb + A_ELEMS, wave, lane);
+    }
+    const bf16* ai = lds + (kt & 1) * (A_ELEMS + B_ELEMS);
+    const bf16* bi = ai + A_ELEMS;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int mrow = wm * 64 + t * 32;
+        if (A_KCONTIG) {
+          af[t] = *(const bf16x8*)(ai + kc_off(mrow + (lane & 31), 2 * s + h));
+        } else {
+          // A image is [k][m] (256-B rows, same layout as B's)
+          af[t] = frag_tr(ai, mrow, s, lane);
+        }
+        const int ncol = wn * 64 + t * 32;
+        if (B_KCONTIG) {
+          bfr[t] = *(const bf16x8*)(bi + kc_off(ncol + (lane & 31), 2 * s + h));
+        } else {
+          bfr[t] = frag_tr(bi, ncol, s, lane);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[a], bfr[b], acc[a][b]);
+    }
+  }
+
+  const float alpha = *alpha_p;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int n = n0 + wn * 64 + b * 32 + (lane & 31);
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int m = m0 + wm * 64 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v]);
+      }
+    }
+}
+
+template <bool AK, bool BK_, typename OutT>
+int launch(const void* A, long long lda, const void* B, long long ldb, int M, int N, int Kd, const float* alpha,
+           void* C, long long ldc, hipStream_t st) {
+  if (M % BM || N % BN || Kd % BK || lda % 8 || ldb % 8) return TRIAD_EINVAL;
+  const int nwg = (M / BM) * (N / BN);
+  hipLaunchKernelGGL((gemm_kernel<AK, BK_, OutT>), dim3(nwg), dim3(256), 0, st, (const bf16*)A, lda, (const bf16*)B,
+                     ldb, M, N, Kd, alpha, (OutT*)C, ldc);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// C[M][N] = alpha * op(A) . op(B). a_kcontig=1: A stored [M][Kd] (lda), 0: [Kd][M].
+// b_kcontig=1: B stored [N][Kd] (ldb), 0: [Kd][N]. out_bf16 selects a bf16 or fp32 C.
+int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                    int M, int N, int Kd, const float* alpha, void* C, long long ldc, int out_bf16,
+                    hipStream_t stream) {
+#define TRIAD_GEMM_CASE(AK, BKC)                                                                  \
+  if (!!a_kcontig == AK && !!b_kcontig == BKC)                                                   \
+    return out_bf16 ? launch<AK, BKC, bf16>(A, lda, B, ldb, M, N, Kd, alpha, C, ldc, stream)     \
+                    : launch<AK, BKC, float>(A, lda, B, ldb, M, N, Kd, alpha, C, ldc, stream);
+  TRIAD_GEMM_CASE(true, true)
+  TRIAD_GEMM_CASE(true, false)
+  TRIAD_GEMM_CASE(false, true)
+  TRIAD_GEMM_CASE(false, false)
+#undef TRIAD_GEMM_CASE
+  return TRIAD_EINVAL;
+}
+
+}  // extern "C"

@@ -1,0 +1,525 @@
+// Fused pairwise token-similarity kernels for TRIAD's dense contrastive head.
+//
+// Reference semantics (SajayR/TRIAD src/model.py):
+//   S[i,j,q,k] = temp * <Q[i,q], K[j,k]>           model.py:384-387 / 502-505
+//   clip[i,j]  = mean_q max_k S   (TV: mask-weighted) model.py:389-391 / 507-512
+//   l_nonneg   = mean clamp(S, lo, 0)^2            model.py:417-418 / 524-525
+// The (Bq,Bk,Nq,Nk) tensor is never materialised: one kernel streams key tiles
+// through LDS against query fragments held in VGPRs and reduces in registers.
+//
+// Layouts (HBM):
+//   Q      [R_pad][512] bf16  query tokens flattened (row r = i*Nq + q), rows >= R are 0
+//   K      [Bk][Nk_pad][512] bf16 key tokens, per-sample zero padded to Nk_pad (multiple of 32);
+//          columns k < Nk_eff take part in max / l_nonneg (patch-dropout zero rows included,
+//          model.py:296-307), columns k >= Nk_eff are excluded.
+//   rowmax [Bk][R_pad] f32, argmax [Bk][R_pad] i32   max_k S and its first index
+//   dS     [R_pad][C_alloc] bf16, C_alloc >= Bk*Nk_pad  dL/dS for the two backward GEMMs
+//
+// Wave tiling (CDNA4, wave64): each wave owns 32 query rows; its Q fragments
+// (32 rows x 512 d = 128 VGPRs) stay in registers for the whole launch. A key
+// tile is 32 keys x 512 d (32 KB) in LDS. One 32-step chain of
+// v_mfma_f32_32x32x16_bf16 computes S^T = K_tile . Q_rows^T with the QUERY on
+// the lane and the 32 keys in the 16 accumulator registers (x 2 lane halves), so
+// the row max/argmax is lane-local plus one half-wave exchange.
+#include "common.h"
+
+namespace {
+
+constexpr int D = 512;
+constexpr int NS = D / 16;          // MFMA k-steps per key tile
+constexpr int WAVES = 8;            // 512-thread workgroup, 2 waves per SIMD
+constexpr int ROWS_PER_WG = 32 * WAVES;
+constexpr int KT_ELEMS = 32 * D;    // one key tile in LDS (bf16 elements)
+
+struct PairArgs {
+  const bf16* Q;
+  const bf16* K;
+  int R, R_pad, Nq, Bq, Bk, Nk_pad, Nk_eff, j_per_wg;
+  int diag, diag_off;  // diag: query sample i pairs with key sample i + diag_off
+  const float* temp;
+  float clamp_lo;
+  // forward outputs
+  float* rowmax;
+  int* argmax;
+  double* part;        // per-workgroup partial (l_nonneg sum in fwd, dtemp in bwd)
+  float* diagS;        // [Bq][Nq][Nk_pad] S on the diagonal pairs (fwd, may be null)
+  // backward inputs
+  const float* dclip;  // [Bq][Bk] dCE/dclip (unit upstream gradient)
+  const float* qw;     // [R] d clip / d rowmax per row (1/Nq or mask/len)
+  const float* dSdiag; // [Bq][Nq][Nk_pad] unit grad of the diagonal regulariser (may be null)
+  const float* coef;   // [4] c_ce, c_nn (=0.15*2*c_reg/N_el), c_diag, c_cal
+  bf16* dS;
+  long long ldS;       // C_alloc
+};
+
+// Stage key tile (j, kb) into LDS buffer `dst`. Row t of the tile is one
+// wave-instruction (64 lanes x 16 B = one 1 KB key row); LDS chunk c of row t
+// holds global chunk c ^ (t & 15), which makes the later ds_read_b128 of 32
+// different rows at one chunk conflict-free.
+__device__ __forceinline__ void stage_key_tile(const PairArgs& a, bf16* dst, int j, int kb,
+                                               int wave, int lane) {
+#pragma unroll
+  for (int u = 0; u < 32 / WAVES; ++u) {
+    const int t = wave * (32 / WAVES) + u;
+    const bf16* src = a.K + ((size_t)j * a.Nk_pad + kb * 32 + t) * D + ((lane ^ (t & 15)) * 8);
+    glds16(src, dst + t * D);
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
+  // All LDS in ONE array (a second __shared__ object can make hipcc drain the
+  // in-flight LDS-DMA before every ds_read).
+  __shared__ __attribute__((aligned(16))) bf16 kbuf[2 * KT_ELEMS + 4 * WAVES];
+  double* red = (double*)(kbuf + 2 * KT_ELEMS);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, ql = lane & 31;
+  const int row = blockIdx.x * ROWS_PER_WG + wave * 32 + ql;
+  const bool row_ok = row < a.R;
+  const int qi = row_ok ? row / a.Nq : -1;
+  const int qq = row_ok ? row - qi * a.Nq : 0;
+
+  const int j0 = blockIdx.y * a.j_per_wg;
+  const int j1 = min(a.Bk, j0 + a.j_per_wg);
+  const int nkb = a.Nk_pad / 32;
+  const int nblocks = (j1 - j0) * nkb;
+  if (nblocks <= 0) {  // uniform across the workgroup
+    if (threadIdx.x == 0) a.part[blockIdx.y * gridDim.x + blockIdx.x] = 0.0;
+    return;
+  }
+
+  stage_key_tile(a, kbuf, j0, 0, wave, lane);
+
+  // Query fragments: lane holds Q[row][16 s + 8 h .. +8] for s = 0..31 (the B operand).
+  bf16x8 qf[NS];
+  {
+    const bf16* qp = a.Q + (size_t)row * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+  }
+  const float temp = *a.temp;
+  const float lo = a.clamp_lo;
+
+  float c_ce = 0.f, c_nn = 0.f, c_dg = 0.f;
+  if (EPI == 1) { c_ce = a.coef[0]; c_nn = a.coef[1]; c_dg = a.coef[2]; }
+  const float wrow = (EPI == 1 && row_ok) ? a.qw[row] : 0.f;
+
+  float m = -INFINITY;
+  int am = 0;
+  float gmax = 0.f;
+  int amax = -1;
+  double accd = 0.0;
+
+  for (int b = 0; b < nblocks; ++b) {
+    const int j = j0 + b / nkb, kb = b - (b / nkb) * nkb;
+    lds_dma_barrier();  // tile b has landed; all waves are done with buffer (b+1)&1
+    if (b + 1 < nblocks) {
+      const int b1 = b + 1;
+      stage_key_tile(a, kbuf + ((b1 & 1) ? KT_ELEMS : 0), j0 + b1 / nkb, b1 - (b1 / nkb) * nkb,
+                     wave, lane);
+    }
+    const bf16* kt = kbuf + ((b & 1) ? KT_ELEMS : 0) + ql * D;
+    const int sw = ql & 15;
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const bf16x8 af = *(const bf16x8*)(kt + (((2 * s + h) ^ sw) * 8));
+      acc = mfma32(af, qf[s], acc);
+    }
+
+    const bool diag_pair = a.diag && row_ok && (j == qi + a.diag_off);
+    const int key0 = kb * 32 + 4 * h;
+
+    if (EPI == 0) {
+      float nn = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int key = key0 + (v & 3) + 8 * (v >> 2);
+        const float s = acc[v] * temp;
+        const bool ok = row_ok && key < a.Nk_eff;
+        if (ok && s > m) { m = s; am = key; }  // keys ascend with v: strict > keeps the first index
+        const float c = fminf(fmaxf(s, lo), 0.f);
+        nn += ok ? c * c : 0.f;
+        if (diag_pair && key < a.Nk_eff && a.diagS)
+          a.diagS[((size_t)qi * a.Nq + qq) * a.Nk_pad + key] = s;
+      }
+      accd += (double)nn;
+      if (kb == nkb - 1) {
+        const float m2 = __shfl_xor(m, 32);
+        const int am2 = __shfl_xor(am, 32);
+        if (m2 > m || (m2 == m && am2 < am)) { m = m2; am = am2; }
+        if (h == 0) {
+          a.rowmax[(size_t)j * a.R_pad + row] = m;
+          a.argmax[(size_t)j * a.R_pad + row] = am;
+        }
+        m = -INFINITY;
+        am = 0;
+      }
+    } else {
+      if (kb == 0) {
+        gmax = row_ok ? c_ce * a.dclip[(size_t)qi * a.Bk + j] * wrow : 0.f;
+        amax = row_ok ? a.argmax[(size_t)j * a.R_pad + row] : -1;
+      }
+      const float* dg = (diag_pair && a.dSdiag) ? a.dSdiag + ((size_t)qi * a.Nq + qq) * a.Nk_pad : nullptr;
+      float dt = 0.f;
+      bf16 out[16];
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int key = key0 + (v & 3) + 8 * (v >> 2);
+        const float sraw = acc[v];
+        const float s = sraw * temp;
+        float g = (s >= lo && s <= 0.f) ? c_nn * s : 0.f;  // clamp grad, inclusive bounds
+        if (key == amax) g += gmax;
+        if (dg && key < a.Nk_eff) g += c_dg * dg[key];
+        g = (row_ok && key < a.Nk_eff) ? g : 0.f;
+        dt += g * sraw;
+        out[v] = (bf16)g;
+      }
+      accd += (double)dt;
+      bf16* dst = a.dS + (size_t)row * a.ldS + (size_t)j * a.Nk_pad + key0;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 w4 = {out[4 * g4], out[4 * g4 + 1], out[4 * g4 + 2], out[4 * g4 + 3]};
+        *(bf16x4*)(dst + 8 * g4) = w4;
+      }
+    }
+  }
+
+  // Workgroup partial of l_nonneg (fwd) or dL/dtemp (bwd), in double.
+  double v = wave_sum_d(accd);
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < WAVES; ++w) t += red[w];
+    a.part[blockIdx.y * gridDim.x + blockIdx.x] = t;
+  }
+}
+
+// clip[i][j] = sum_q w_q rowmax[j][i*Nq+q] / norm_i  (model.py:389-391, 507-512);
+// also writes qw[r] = d clip / d rowmax for the backward.
+__global__ __launch_bounds__(256) void clip_reduce_kernel(const float* __restrict__ rowmax, int R_pad,
+                                                          int Nq, int Bq, int Bk,
+                                                          const float* __restrict__ qmask,
+                                                          float* __restrict__ clip, float* __restrict__ qw) {
+  const int j = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int i = wave; i < Bq; i += nw) {
+    float s = 0.f, cnt = 0.f;
+    const float* rm = rowmax + (size_t)j * R_pad + (size_t)i * Nq;
+    for (int q = lane; q < Nq; q += 64) {
+      const float w = qmask ? qmask[(size_t)i * Nq + q] : 1.f;
+      s += rm[q] * w;
+      cnt += w;
+    }
+    s = wave_sum(s);
+    cnt = wave_sum(cnt);
+    const float norm = qmask ? fmaxf(cnt, 1e-7f) : (float)Nq;
+    if (lane == 0) clip[(size_t)i * Bk + j] = s / norm;
+    if (j == 0 && qw) {
+      for (int q = lane; q < Nq; q += 64) {
+        const float w = qmask ? qmask[(size_t)i * Nq + q] : 1.f;
+        qw[(size_t)i * Nq + q] = w / norm;
+      }
+    }
+  }
+}
+
+// AV temporal smoothness on the diagonal pairs (model.py:394-408):
+//   l_smooth = sum_{i,q>=1,k} (S_ii[q,k] - S_ii[q-1,k])^2 / cnt
+// Writes part[i] = the sample's sum and g[i][q][k] = d l_smooth / d S_ii[q,k].
+__global__ __launch_bounds__(256) void diag_smooth_kernel(const float* __restrict__ dS_in, int Nq, int Nk_pad,
+                                                          int Nk_eff, double inv_cnt,
+                                                          double* __restrict__ part, float* __restrict__ g) {
+  __shared__ double red[4];
+  const int i = blockIdx.x;
+  const float* S = dS_in + (size_t)i * Nq * Nk_pad;
+  float* G = g + (size_t)i * Nq * Nk_pad;
+  double acc = 0.0;
+  const float two_inv = (float)(2.0 * inv_cnt);
+  for (int e = threadIdx.x; e < Nq * Nk_eff; e += blockDim.x) {
+    const int q = e / Nk_eff, k = e - q * Nk_eff;
+    const float s = S[(size_t)q * Nk_pad + k];
+    float grad = 0.f;
+    if (q >= 1) {
+      const float d = s - S[(size_t)(q - 1) * Nk_pad + k];
+      acc += (double)(d * d);
+      grad += two_inv * d;
+    }
+    if (q + 1 < Nq) grad -= two_inv * (S[(size_t)(q + 1) * Nk_pad + k] - s);
+    G[(size_t)q * Nk_pad + k] = grad;
+  }
+  const double t = block_sum_d(acc, red);
+  if (threadIdx.x == 0) part[i] = t;
+}
+
+// TV patch-usage sparsity on the diagonal pairs (model.py:527-540):
+//   P = softmax_k S_ii[t,:];  frac[k] = sum_t P[t,k] / Nt;  loss = sum relu(frac-thr)^2 / cnt
+// Writes part[i] and g[i][t][k] = d loss / d S_ii[t,k] (in place over S_ii).
+__global__ __launch_bounds__(256) void diag_sparsity_kernel(float* __restrict__ S_g, int Nt, int Nk_pad,
+                                                            int Nk_eff, float thr, double inv_cnt,
+                                                            double* __restrict__ part) {
+  extern __shared__ float sh[];  // frac/g [Nk_eff]
+  __shared__ double red[4];
+  const int i = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  float* S = S_g + (size_t)i * Nt * Nk_pad;
+  // 1) rows -> probabilities, in place
+  for (int t = wave; t < Nt; t += nw) {
+    float* r = S + (size_t)t * Nk_pad;
+    float mx = -INFINITY;
+    for (int k = lane; k < Nk_eff; k += 64) mx = fmaxf(mx, r[k]);
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int k = lane; k < Nk_eff; k += 64) sum += __expf(r[k] - mx);
+    sum = wave_sum(sum);
+    const float inv = 1.f / sum;
+    for (int k = lane; k < Nk_eff; k += 64) r[k] = __expf(r[k] - mx) * inv;
+  }
+  __syncthreads();
+  // 2) frac, excess, loss partial, per-column gradient wrt P
+  double acc = 0.0;
+  const float scale = (float)(2.0 * inv_cnt) / (float)Nt;
+  for (int k = threadIdx.x; k < Nk_eff; k += blockDim.x) {
+    float f = 0.f;
+    for (int t = 0; t < Nt; ++t) f += S[(size_t)t * Nk_pad + k];
+    f /= (float)Nt;
+    const float ex = f - thr;
+    const float r = ex > 0.f ? ex : 0.f;
+    acc += (double)r * (double)r;
+    sh[k] = scale * r;
+  }
+  const double tot = block_sum_d(acc, red);  // includes a barrier
+  if (threadIdx.x == 0) part[i] = tot;
+  // 3) softmax backward per row
+  for (int t = wave; t < Nt; t += nw) {
+    float* r = S + (size_t)t * Nk_pad;
+    float dot = 0.f;
+    for (int k = lane; k < Nk_eff; k += 64) dot += r[k] * sh[k];
+    dot = wave_sum(dot);
+    for (int k = lane; k < Nk_eff; k += 64) r[k] = r[k] * (sh[k] - dot);
+  }
+}
+
+// Loss head over the B x B clip matrix (model.py:430-472 / 544-593), one workgroup.
+// out: [0] total [1] ce [2] reg [3] 0.01*smooth (AV) / sparsity (TV)
+//      [4..9] pos_mean pos_std neg_mean neg_std separation hardest_negative
+//      [10] l_nonneg [11] l_cal [12] diag regulariser (l_smooth / sparsity)
+// dclip: d ce / d clip (unit upstream gradient).
+__global__ __launch_bounds__(1024) void losshead_kernel(const float* __restrict__ clip, int B, int kind,
+                                                        const float* __restrict__ temp_p,
+                                                        const double* __restrict__ nn_part, int n_nn,
+                                                        double inv_nel,
+                                                        const double* __restrict__ dg_part, int n_dg,
+                                                        double inv_dg, float w_sparse,
+                                                        float* __restrict__ out, float* __restrict__ dclip,
+                                                        float* __restrict__ lse /* [2B] scratch */) {
+  __shared__ double redd[16];
+  __shared__ float redf[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // row / column log-sum-exp
+  for (int r = wave; r < 2 * B; r += nw) {
+    const bool col = r >= B;
+    const int x = col ? r - B : r;
+    float mx = -INFINITY;
+    for (int y = lane; y < B; y += 64) mx = fmaxf(mx, col ? clip[(size_t)y * B + x] : clip[(size_t)x * B + y]);
+    mx = wave_max(mx);
+    float s = 0.f;
+    for (int y = lane; y < B; y += 64) s += expf((col ? clip[(size_t)y * B + x] : clip[(size_t)x * B + y]) - mx);
+    s = wave_sum(s);
+    if (lane == 0) lse[r] = mx + logf(s);
+  }
+  __syncthreads();
+  double ce = 0.0, pos = 0.0, neg = 0.0;
+  float hard = -INFINITY;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    const float c = clip[(size_t)i * B + i];
+    ce += (double)(lse[i] - c) + (double)(lse[B + i] - c);
+    pos += c;
+  }
+  const float inv2b = 0.5f / (float)B;
+  for (size_t e = threadIdx.x; e < (size_t)B * B; e += blockDim.x) {
+    const int i = (int)(e / B), j = (int)(e - (size_t)i * B);
+    const float c = clip[e];
+    float g = expf(c - lse[i]) + expf(c - lse[B + j]);
+    if (i == j) g -= 2.f;
+    else { neg += c; hard = fmaxf(hard, c); }
+    dclip[e] = g * inv2b;
+  }
+  ce = block_sum_d(ce, redd);
+  pos = block_sum_d(pos, redd);
+  neg = block_sum_d(neg, redd);
+  hard = block_max(hard, redf);
+  const double nneg = (double)B * B - B;
+  const double pm = pos / B, nm = neg / nneg;
+  double pv = 0.0, nv = 0.0;
+  for (size_t e = threadIdx.x; e < (size_t)B * B; e += blockDim.x) {
+    const int i = (int)(e / B), j = (int)(e - (size_t)i * B);
+    const double d = (double)clip[e] - (i == j ? pm : nm);
+    if (i == j) pv += d * d; else nv += d * d;
+  }
+  pv = block_sum_d(pv, redd);
+  nv = block_sum_d(nv, redd);
+  double nn = 0.0;
+  for (int e = threadIdx.x; e < n_nn; e += blockDim.x) nn += nn_part[e];
+  nn = block_sum_d(nn, redd);
+  double dg = 0.0;
+  for (int e = threadIdx.x; e < n_dg; e += blockDim.x) dg += dg_part[e];
+  dg = block_sum_d(dg, redd);
+  if (threadIdx.x == 0) {
+    const double cev = ce / (2.0 * B);
+    const double l_nn = nn * inv_nel;
+    const double l_dg = dg * inv_dg;  // 0 * inf -> NaN when the diagonal set is empty (reference: mean of empty)
+    double l_cal = 0.0, reg, sm;
+    if (kind == 0) {
+      const double lt = -log((double)*temp_p);
+      l_cal = lt > 0.0 ? lt * lt : 0.0;
+      reg = 20.0 * l_cal + 0.15 * l_nn + 0.01 * l_dg;
+      sm = 0.01 * l_dg;
+    } else {
+      reg = 0.15 * l_nn + (double)w_sparse * l_dg;
+      sm = l_dg;
+    }
+    out[0] = (float)(cev + reg);
+    out[1] = (float)cev;
+    out[2] = (float)reg;
+    out[3] = (float)sm;
+    out[4] = (float)pm;
+    out[5] = (float)sqrt(pv / (B - 1));
+    out[6] = (float)nm;
+    out[7] = (float)sqrt(nv / (nneg - 1));
+    out[8] = (float)(pm - nm);
+    out[9] = hard;
+    out[10] = (float)l_nn;
+    out[11] = (float)l_cal;
+    out[12] = (float)l_dg;
+  }
+}
+
+// dL/dtemp = sum(dS * S_raw) + c_cal * d l_cal / d temp   (AV only has l_cal, model.py:420-424)
+__global__ void dtemp_finalize_kernel(const double* __restrict__ part, int n, const float* __restrict__ temp_p,
+                                      const float* __restrict__ coef, int has_cal, float* __restrict__ out) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) s += part[e];
+  s = block_sum_d(s, red);
+  if (threadIdx.x == 0) {
+    if (has_cal) {
+      const double t = (double)*temp_p;
+      const double x = -log(t);
+      if (x >= 0.0) s += (double)coef[3] * 2.0 * x * (-1.0 / t);
+    }
+    out[0] = (float)s;
+  }
+}
+
+int grid_for(int R_pad, int Bk, int* jpw, int* ysplit) {
+  const int xb = R_pad / ROWS_PER_WG;
+  int ys = (2048 + xb - 1) / xb;
+  if (ys > Bk) ys = Bk;
+  if (ys < 1) ys = 1;
+  *jpw = (Bk + ys - 1) / ys;
+  *ysplit = (Bk + *jpw - 1) / *jpw;
+  return xb;
+}
+
+int check_shape(int R, int R_pad, int Nq, int Bk, int Nk_pad, int Nk_eff, int D_) {
+  if (D_ != D || R_pad % ROWS_PER_WG || R > R_pad || Nq <= 0 || Bk <= 0 || Nk_pad % 32 ||
+      Nk_eff <= 0 || Nk_eff > Nk_pad)
+    return TRIAD_EINVAL;
+  return TRIAD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int triad_pairsim_nparts(int R_pad, int Bk) {
+  int jpw, ys;
+  const int xb = grid_for(R_pad, Bk, &jpw, &ys);
+  return xb * ys;
+}
+
+int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
+                      int Nk_eff, int D_, const float* temp, float clamp_lo, int diag, int diag_off,
+                      float* rowmax, int* argmax, double* nn_part, float* diagS, hipStream_t stream) {
+  if (int e = check_shape(R, R_pad, Nq, Bk, Nk_pad, Nk_eff, D_)) return e;
+  PairArgs a = {};
+  a.Q = (const bf16*)Q; a.K = (const bf16*)K;
+  a.R = R; a.R_pad = R_pad; a.Nq = Nq; a.Bq = Bq; a.Bk = Bk; a.Nk_pad = Nk_pad; a.Nk_eff = Nk_eff;
+  a.diag = diag; a.diag_off = diag_off; a.temp = temp; a.clamp_lo = clamp_lo;
+  a.rowmax = rowmax; a.argmax = argmax; a.part = nn_part; a.diagS = diagS;
+  int ys;
+  const int xb = grid_for(R_pad, Bk, &a.j_per_wg, &ys);
+  hipLaunchKernelGGL(pairsim_kernel<0>, dim3(xb, ys), dim3(512), 0, stream, a);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_clip_reduce(const float* rowmax, int R_pad, int Nq, int Bq, int Bk, const float* qmask,
+                      float* clip, float* qw, hipStream_t stream) {
+  if (Bq <= 0 || Bk <= 0 || Nq <= 0) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(clip_reduce_kernel, dim3(Bk), dim3(256), 0, stream, rowmax, R_pad, Nq, Bq, Bk, qmask,
+                     clip, qw);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_diag_smooth(const float* diagS, int Bq, int Nq, int Nk_pad, int Nk_eff, double cnt, double* part,
+                      float* g, hipStream_t stream) {
+  if (Bq <= 0) return TRIAD_EINVAL;
+  const double inv = cnt > 0.0 ? 1.0 / cnt : INFINITY;
+  hipLaunchKernelGGL(diag_smooth_kernel, dim3(Bq), dim3(256), 0, stream, diagS, Nq, Nk_pad, Nk_eff,
+                     cnt > 0.0 ? inv : 0.0, part, g);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_diag_sparsity(float* diagS_g, int Bq, int Nt, int Nk_pad, int Nk_eff, float thr, double cnt,
+                        double* part, hipStream_t stream) {
+  if (Bq <= 0 || Nk_eff > 16384) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(diag_sparsity_kernel, dim3(Bq), dim3(256), Nk_eff * sizeof(float), stream, diagS_g, Nt,
+                     Nk_pad, Nk_eff, thr, 1.0 / cnt, part);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_losshead(const float* clip, int B, int kind, const float* temp, const double* nn_part, int n_nn,
+                   double n_el, const double* dg_part, int n_dg, double dg_cnt, float w_sparse, float* out,
+                   float* dclip, float* lse_scratch, hipStream_t stream) {
+  if (B < 2 || (kind != 0 && kind != 1)) return TRIAD_EINVAL;
+  const double inv_dg = dg_cnt > 0.0 ? 1.0 / dg_cnt : NAN;
+  hipLaunchKernelGGL(losshead_kernel, dim3(1), dim3(1024), 0, stream, clip, B, kind, temp, nn_part, n_nn,
+                     1.0 / n_el, dg_part, n_dg, inv_dg, w_sparse, out, dclip, lse_scratch);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_pairsim_dS(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
+                     int Nk_eff, int D_, const float* temp, float clamp_lo, int diag, int diag_off,
+                     const int* argmax, const float* dclip, const float* qw, const float* dSdiag,
+                     const float* coef, void* dS, long long ldS, double* dt_part, hipStream_t stream) {
+  if (int e = check_shape(R, R_pad, Nq, Bk, Nk_pad, Nk_eff, D_)) return e;
+  if (ldS < (long long)Bk * Nk_pad || ldS % 8) return TRIAD_EINVAL;
+  PairArgs a = {};
+  a.Q = (const bf16*)Q; a.K = (const bf16*)K;
+  a.R = R; a.R_pad = R_pad; a.Nq = Nq; a.Bq = Bq; a.Bk = Bk; a.Nk_pad = Nk_pad; a.Nk_eff = Nk_eff;
+  a.diag = diag; a.diag_off = diag_off; a.temp = temp; a.clamp_lo = clamp_lo;
+  a.argmax = (int*)argmax; a.dclip = dclip; a.qw = qw; a.dSdiag = dSdiag; a.coef = coef;
+  a.dS = (bf16*)dS; a.ldS = ldS; a.part = dt_part;
+  int ys;
+  const int xb = grid_for(R_pad, Bk, &a.j_per_wg, &ys);
+  hipLaunchKernelGGL(pairsim_kernel<1>, dim3(xb, ys), dim3(512), 0, stream, a);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_dtemp_finalize(const double* part, int n, const float* temp, const float* coef, int has_cal,
+                         float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(dtemp_finalize_kernel, dim3(1), dim3(256), 0, stream, part, n, temp, coef, has_cal, out);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+}  // extern "C"

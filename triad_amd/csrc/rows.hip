@@ -1,0 +1,77 @@
+// Row movement kernels around the similarity head:
+//   * patch-dropout compaction (model.py:268-308): out[b][t] = x[b][idx[b][t]] or 0,
+//     where idx lists each sample's kept tokens in original order and -1 pads;
+//   * its backward (scatter == gather with the inverse index);
+//   * per-token L2 normalisation for the inference similarity maps (model.py:363-364).
+#include "common.h"
+
+namespace {
+
+// One thread moves 16 bytes; rows are row_bytes long (multiple of 16).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint4* __restrict__ src, long long src_rows,
+                                                          const int* __restrict__ idx, int M, int chunks,
+                                                          long long total, uint4* __restrict__ dst) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long rowo = e / chunks;
+    const int c = (int)(e - rowo * chunks);
+    const int b = (int)(rowo / M);
+    const int s = idx[rowo];
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (s >= 0) v = src[((long long)b * src_rows + s) * chunks + c];
+    dst[e] = v;
+  }
+}
+
+// y[r] = x[r] / max(||x[r]||_2, eps), bf16 in/out, fp32 math; one wave per row.
+__global__ __launch_bounds__(256) void l2norm_rows_kernel(const bf16* __restrict__ x, int rows, int D, float eps,
+                                                          bf16* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const bf16* xr = x + (size_t)r * D;
+  float ss = 0.f;
+  for (int d = lane * 8; d < D; d += 512) {
+    const bf16x8 v = *(const bf16x8*)(xr + d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ss += (float)v[k] * (float)v[k];
+  }
+  ss = wave_sum(ss);
+  const float inv = 1.f / fmaxf(sqrtf(ss), eps);
+  bf16* yr = y + (size_t)r * D;
+  for (int d = lane * 8; d < D; d += 512) {
+    const bf16x8 v = *(const bf16x8*)(xr + d);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (bf16)((float)v[k] * inv);
+    *(bf16x8*)(yr + d) = o;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// dst[b][t][:] = idx[b][t] >= 0 ? src[b][idx[b][t]][:] : 0, for b < B, t < M.
+int triad_gather_rows(const void* src, long long src_rows, const int* idx, int B, int M, int row_bytes,
+                      void* dst, hipStream_t stream) {
+  if (row_bytes % 16 || B <= 0 || M <= 0) return TRIAD_EINVAL;
+  const int chunks = row_bytes / 16;
+  const long long total = (long long)B * M * chunks;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const uint4*)src,
+                     src_rows, idx, M, chunks, total, (uint4*)dst);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_l2norm_rows(const void* x, int rows, int D, float eps, void* y, hipStream_t stream) {
+  if (D % 8 || rows <= 0) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(l2norm_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, (const bf16*)x, rows, D, eps,
+                     (bf16*)y);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,330 @@
+"""Drop-in mirror of SajayR/TRIAD src/model.py on MI355X.
+
+Same class names, constructor arguments, attribute names (for parameter grouping
+by name in the trainer, train.py:251-261) and method return tuples as the
+reference. The backbones run on PyTorch-ROCm; the hot path -- projection heads,
+patch-dropout compaction, the B x B x Nq x Nk token-similarity contraction,
+max/mean aggregation, InfoNCE, regularisers and their backward -- runs in the
+HIP kernels of libtriad_hip.so (triad_amd.ops).
+
+Offline differences (documented in DESIGN.md):
+  * pretrained weights / tokenizers cannot be downloaded: backbones are random-
+    init `transformers` HuBERT / DistilBERT and the local DINOv2 restatement
+    (triad_amd.vit); if a local HF cache holds the named checkpoint it is used;
+  * the text tokenizer falls back to a deterministic hashing word tokenizer when
+    the DistilBERT vocabulary is unavailable; pre-tokenised input is accepted;
+  * the patch-dropout Bernoulli mask is drawn on the host (one B x N draw) so the
+    compacted length is known without a device sync.
+"""
+from __future__ import annotations
+
+import math
+import re
+import warnings
+import zlib
+from collections.abc import Mapping
+from typing import Dict, List, Optional, Sequence, Union
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .vit import DinoVisionTransformer, apply_lora
+
+warnings.filterwarnings("ignore", message=".*torch.cuda.amp.*")
+
+_AV_KEYS = ("av_pos_sim_mean", "av_pos_sim_std", "av_neg_sim_mean", "av_neg_sim_std", "av_separation",
+            "av_hardest_negative")
+_TV_KEYS = tuple("tv_" + k[3:] for k in _AV_KEYS)
+
+
+class LazyStats(Mapping):
+    """The reference's stats dict of Python floats (model.py:463-470, 584-591).
+
+    Values stay on the device until first read, so a training step that never
+    logs them has no host synchronisation (the reference does 5 `.item()` syncs
+    per head, model.py:443-447 / 561-565).
+    """
+
+    def __init__(self, keys, values: torch.Tensor):
+        self._keys = tuple(keys)
+        self._dev = values.detach()
+        self._host = None
+
+    def _materialise(self):
+        if self._host is None:
+            v = self._dev[:6].double().cpu().tolist()
+            self._host = dict(zip(self._keys, v))
+        return self._host
+
+    def __getitem__(self, k):
+        return self._materialise()[k]
+
+    def __iter__(self):
+        return iter(self._keys)
+
+    def __len__(self):
+        return len(self._keys)
+
+    def __repr__(self):
+        return repr(dict(self._materialise()))
+
+
+def _hf_model(kind, name, config_overrides=None):
+    """Load `name` from a local HF cache if present, else random-init its architecture."""
+    import transformers
+    try:
+        return getattr(transformers, kind).from_pretrained(name, local_files_only=True)
+    except Exception:
+        pass
+    cfg_cls = {"HubertModel": transformers.HubertConfig, "DistilBertModel": transformers.DistilBertConfig}[kind]
+    cfg = cfg_cls(**(config_overrides or {}))
+    try:
+        cfg._attn_implementation = "sdpa"
+    except Exception:
+        pass
+    return getattr(transformers, kind)(cfg)
+
+
+_HUBERT_LARGE = dict(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16, intermediate_size=4096,
+                     feat_extract_norm="layer", do_stable_layer_norm=True)
+
+
+class ProjectionHead(nn.Module):
+    """Holder so `projection1`, `layer_norm`, `projection2` keep the reference names."""
+
+
+def _project(emb, h):
+    """proj2(LN(proj1(h))) (model.py:68,116,201,326) via the fused HIP projection head."""
+    return ops.projection_head(h, emb.projection1, emb.layer_norm, emb.projection2)
+
+
+class AudioEmbedder(nn.Module):
+    """HuBERT + projection head (model.py:22-70)."""
+
+    def __init__(self, embedding_dim=512, hubert_name="facebook/hubert-base-ls960"):
+        super().__init__()
+        over = _HUBERT_LARGE if "large" in hubert_name else None
+        self.hubert = _hf_model("HubertModel", hubert_name, over)
+        self.projection1 = nn.Linear(self.hubert.config.hidden_size, 512)
+        self.layer_norm = nn.LayerNorm(512)
+        self.projection2 = nn.Linear(512, embedding_dim)
+        for p in self.parameters():
+            p.requires_grad = True
+
+    def normalize(self, audio: torch.Tensor) -> torch.Tensor:
+        """The reference's processor call (model.py:56-62): Wav2Vec2FeatureExtractor with
+        do_normalize=True treats the (B,T) batch as ONE utterance: (x - mean) / sqrt(var + 1e-7)
+        over all B*T samples (measured). Done on the device: no host round trip."""
+        return ops.global_znorm(audio, 1e-7)
+
+    def forward(self, audio_input: torch.Tensor) -> torch.Tensor:
+        if audio_input.dim() == 3:
+            audio_input = audio_input.squeeze(0)
+        x = self.normalize(audio_input.to(next(self.parameters()).device))
+        h = self.hubert(x).last_hidden_state
+        return _project(self, h)
+
+
+class HashTokenizer:
+    """Deterministic offline stand-in for the DistilBERT word-piece tokenizer.
+
+    Lower-cased words/punctuation hashed into [1000, vocab); padding=True,
+    truncation to max_length, no special tokens (model.py:102-109). Token ids
+    differ from the real vocabulary (parity unpinned), shapes and masks do not.
+    """
+
+    def __init__(self, vocab_size=30522):
+        self.vocab_size = vocab_size
+
+    def __call__(self, texts, padding=True, truncation=True, add_special_tokens=False, max_length=128,
+                 return_tensors="pt"):
+        rows = []
+        for t in texts:
+            toks = re.findall(r"\w+|[^\w\s]", t.lower())
+            ids = [1000 + zlib.crc32(w.encode()) % (self.vocab_size - 1000) for w in toks]
+            rows.append(ids[:max_length] if truncation else ids)
+        n = max(1, max(len(r) for r in rows))
+        ids = torch.zeros(len(rows), n, dtype=torch.long)
+        mask = torch.zeros(len(rows), n, dtype=torch.long)
+        for i, r in enumerate(rows):
+            ids[i, :len(r)] = torch.tensor(r, dtype=torch.long)
+            mask[i, :len(r)] = 1
+        return {"input_ids": ids, "attention_mask": mask}
+
+
+class TextEmbedder(nn.Module):
+    """DistilBERT + projection head (model.py:72-118)."""
+
+    def __init__(self, embedding_dim=512, model_name="distilbert/distilbert-base-uncased"):
+        super().__init__()
+        try:
+            from transformers import AutoTokenizer
+            self.tokenizer = AutoTokenizer.from_pretrained(model_name, local_files_only=True)
+        except Exception:
+            self.tokenizer = HashTokenizer()
+        self.encoder = _hf_model("DistilBertModel", model_name)
+        self.projection1 = nn.Linear(self.encoder.config.hidden_size, 512)
+        self.layer_norm = nn.LayerNorm(512)
+        self.projection2 = nn.Linear(512, embedding_dim)
+        for p in self.parameters():
+            p.requires_grad = True
+
+    def tokenize(self, text_list):
+        return self.tokenizer(text_list, padding=True, truncation=True, add_special_tokens=False,
+                              max_length=128, return_tensors="pt")
+
+    def forward(self, text_list):
+        """text_list: list[str], or a pre-tokenised dict {input_ids, attention_mask}.
+        Returns (text_feats (B,Nt,512), attention_mask (B,Nt))."""
+        inputs = dict(text_list) if isinstance(text_list, Mapping) else self.tokenize(text_list)
+        device = next(self.parameters()).device
+        inputs = {k: v.to(device, non_blocking=True) for k, v in inputs.items()}
+        h = self.encoder(input_ids=inputs["input_ids"], attention_mask=inputs["attention_mask"]).last_hidden_state
+        return _project(self, h), inputs["attention_mask"]
+
+
+class ViTLoRAEmbedder(nn.Module):
+    """DINOv2(-reg) + LoRA + projection head + patch dropout (model.py:207-329)."""
+
+    def __init__(self, model_name="facebookresearch/dinov2", arch="dinov2_vitb14", embedding_dim=512,
+                 dropout_prob=0.1, lora_rank=8, lora_alpha=16):
+        super().__init__()
+        self.model = apply_lora(DinoVisionTransformer(arch), lora_rank, lora_alpha)
+        self.model.embed_dim = self.model.embed_dim
+        self.projection1 = nn.Linear(self.model.embed_dim, 512)
+        self.layer_norm = nn.LayerNorm(512)
+        self.projection2 = nn.Linear(512, embedding_dim)
+        self.patch_dropout_rate = dropout_prob
+        self._mask_gen = torch.Generator()
+        self._mask_gen.manual_seed(torch.initial_seed() % (2 ** 63))
+
+    def draw_keep_mask(self, B, N):
+        """Bernoulli(1 - drop) keep mask (model.py:282-284), drawn on the host."""
+        return torch.bernoulli(torch.full((B, N), 1.0 - self.patch_dropout_rate), generator=self._mask_gen).bool()
+
+    def patch_dropout(self, x, drop_rate, keep_mask=None):
+        """model.py:268-308: keep tokens of each sample in order, zero-pad to the longest."""
+        if not self.training or drop_rate == 0:
+            return x
+        B, N = x.shape[0], x.shape[1]
+        if keep_mask is None:
+            keep_mask = self.draw_keep_mask(B, N)
+        return ops.patch_dropout(x, keep_mask)
+
+    def encode_patches(self, x):
+        if x.dim() == 5:
+            x = x.squeeze(0)
+        if x.dim() == 3:
+            x = x.unsqueeze(0)
+        patches = self.model.get_intermediate_layers(x, n=1)[0]
+        return _project(self, patches)
+
+    def forward(self, x, keep_mask=None):
+        feats = self.encode_patches(x)
+        return self.patch_dropout(feats, self.patch_dropout_rate, keep_mask)
+
+
+class MultiModalModel(nn.Module):
+    """model.py:331-637 with the fused HIP loss head."""
+
+    def __init__(self, audio_model_name="facebook/hubert-base-ls960",
+                 text_model_name="distilbert/distilbert-base-uncased", temperature=1.2,
+                 patch_sparsity_threshold=0.3, patch_sparsity_weight=0.1, visual_dropout_prob=0.1, use_amp=True,
+                 vit_arch="dinov2_vitb14_reg"):
+        super().__init__()
+        self.audio_embedder = AudioEmbedder(embedding_dim=512, hubert_name=audio_model_name)
+        self.text_embedder = TextEmbedder(embedding_dim=512, model_name=text_model_name)
+        self.visual_embedder = ViTLoRAEmbedder(arch=vit_arch, embedding_dim=512, dropout_prob=visual_dropout_prob)
+        self.temperature = nn.Parameter(torch.tensor(temperature))
+        self.patch_sparsity_threshold = patch_sparsity_threshold
+        self.patch_sparsity_weight = patch_sparsity_weight
+        self.use_amp = use_amp
+        self.amp_dtype = torch.bfloat16
+
+    # ---- inference similarity maps (model.py:355-368) -------------------------------
+    def compute_similarity_matrix(self, feats1, feats2):
+        """(B,N1,D) x (B,N2,D) -> (B,N1,N2) = normalize(f1) . normalize(f2)^T * temperature."""
+        return ops.similarity_maps(feats1, feats2, self.temperature)
+
+    # ---- fused training heads -------------------------------------------------------
+    def _av_head(self, audio_feats, visual_feats):
+        losses, stats, clip = ops.contrastive_head(ops.AV, audio_feats, visual_feats, self.temperature)
+        return (losses[0], losses[1], losses[2], losses[3], LazyStats(_AV_KEYS, stats)), clip
+
+    def _tv_head(self, text_feats, visual_feats, attention_mask):
+        losses, stats, clip = ops.contrastive_head(ops.TV, text_feats, visual_feats, self.temperature,
+                                                   q_mask=attention_mask, threshold=self.patch_sparsity_threshold,
+                                                   sparsity_weight=self.patch_sparsity_weight)
+        return (losses[0], LazyStats(_TV_KEYS, stats)), clip
+
+    def compute_all_similarities_av(self, audio_feats, visual_feats):
+        """Materialising debug path (small B only): (clip (B,B), token_sims (B,B,Na,Nv))."""
+        clip = ops.clip_similarities(ops.AV, audio_feats, visual_feats, self.temperature)
+        return clip, ops.token_similarities(audio_feats, visual_feats, self.temperature)
+
+    def compute_all_similarities_tv(self, text_feats, visual_feats, attention_mask):
+        clip = ops.clip_similarities(ops.TV, text_feats, visual_feats, self.temperature, q_mask=attention_mask)
+        return clip, ops.token_similarities(text_feats, visual_feats, self.temperature)
+
+    def forward_audio_visual(self, frames, audio):
+        """-> (total, contrastive, reg, 0.01*l_smooth, stats) (model.py:474-488)."""
+        with torch.autocast("cuda", enabled=self.use_amp, dtype=self.amp_dtype):
+            visual_feats = self.visual_embedder(frames)
+            audio_feats = self.audio_embedder(audio)
+        return self._av_head(audio_feats, visual_feats)[0]
+
+    def forward_text_visual(self, frames, text_list):
+        """-> (total, stats) (model.py:595-608)."""
+        with torch.autocast("cuda", enabled=self.use_amp, dtype=self.amp_dtype):
+            visual_feats = self.visual_embedder(frames)
+            text_feats, attention_mask = self.text_embedder(text_list)
+        return self._tv_head(text_feats, visual_feats, attention_mask)[0]
+
+    def forward_triad(self, frames, audio, text_list, av_keep=None, tv_keep=None):
+        """One tri-modal triple batch: the frames are encoded once; AV and TV draw
+        independent patch-dropout masks after the head (dropout follows the head,
+        model.py:326-327, so this equals two separate encodes given the masks).
+        Returns (av_tuple, tv_tuple) as forward_audio_visual / forward_text_visual."""
+        ve = self.visual_embedder
+        with torch.autocast("cuda", enabled=self.use_amp, dtype=self.amp_dtype):
+            patches = ve.encode_patches(frames)
+            v_av = ve.patch_dropout(patches, ve.patch_dropout_rate, av_keep)
+            v_tv = ve.patch_dropout(patches, ve.patch_dropout_rate, tv_keep)
+            audio_feats = self.audio_embedder(audio)
+            text_feats, attention_mask = self.text_embedder(text_list)
+        return self._av_head(audio_feats, v_av)[0], self._tv_head(text_feats, v_tv, attention_mask)[0]
+
+    def forward(self, frames=None, audio=None, text_list=None):
+        """Embeddings + L2-normalised similarity maps (model.py:610-637). `frames` is an
+        image path (as in the reference) or a (3,H,W)/(B,3,H,W) tensor."""
+        assert frames is not None or audio is not None or text_list is not None, \
+            "At least one modality must be provided"
+        if isinstance(frames, str):
+            frames = _load_image(frames, next(self.parameters()).device)
+        emb = {}
+        if frames is not None:
+            emb["visual_feats"] = self.visual_embedder(frames)
+        if audio is not None:
+            emb["audio_feats"] = self.audio_embedder(audio)
+        if text_list is not None:
+            emb["text_feats"], _ = self.text_embedder(text_list)
+        if frames is not None and text_list is not None:
+            emb["vis_text_sim_matrix"] = self.compute_similarity_matrix(emb["text_feats"], emb["visual_feats"])
+        if audio is not None and frames is not None:
+            emb["vis_audio_sim_matrix"] = self.compute_similarity_matrix(emb["audio_feats"], emb["visual_feats"])
+        if audio is not None and text_list is not None:
+            emb["text_audio_sim_matrix"] = self.compute_similarity_matrix(emb["text_feats"], emb["audio_feats"])
+        return emb
+
+
+def _load_image(path, device):
+    """Resize 224, ToTensor, ImageNet normalise (model.py:615-622) without torchvision."""
+    from PIL import Image
+    import numpy as np
+    img = Image.open(path).convert("RGB").resize((224, 224), Image.BILINEAR)
+    x = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255.0).permute(2, 0, 1)
+    mean = torch.tensor([0.485, 0.456, 0.406])[:, None, None]
+    std = torch.tensor([0.229, 0.224, 0.225])[:, None, None]
+    return ((x - mean) / std).to(device)

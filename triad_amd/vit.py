@@ -1,0 +1,201 @@
+"""DINOv2 ViT with register tokens + LoRA adapters (PyTorch-ROCm backbone).
+
+The reference loads `torch.hub.load('facebookresearch/dinov2', 'dinov2_vitb14_reg')`
+(src/model.py:218,346) and wraps it with peft LoRA (r=8, alpha=16, dropout 0) on
+`attn.qkv` and `attn.proj` (model.py:227-248). Neither the hub code nor peft is
+available offline, so this module restates that architecture with the hub's
+parameter names (patch_embed.proj, cls_token, register_tokens, pos_embed,
+blocks.N.{norm1,attn.qkv,attn.proj,ls1,norm2,mlp.fc1,mlp.fc2,ls2}, norm), so a hub
+state_dict loads into it, and implements LoRA directly (`lora_A` / `lora_B`
+parameters, names containing "lora" as train.py:256-258 expects).
+Backbone numerics are "parity unpinned": no pretrained weights exist offline.
+Attention uses torch's fused scaled_dot_product_attention (ROCm flash kernels).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+ARCHS = {
+    # name: (embed_dim, depth, heads)
+    "dinov2_vits14_reg": (384, 12, 6),
+    "dinov2_vitb14_reg": (768, 12, 12),
+    "dinov2_vitl14_reg": (1024, 24, 16),
+    "dinov2_vits14": (384, 12, 6),
+    "dinov2_vitb14": (768, 12, 12),
+    "dinov2_vitl14": (1024, 24, 16),
+}
+
+
+class LoRALinear(nn.Module):
+    """y = base(x) + (alpha/r) * B(A(x)); base frozen by the caller, B zero-initialised."""
+
+    def __init__(self, base: nn.Linear, r: int = 8, alpha: int = 16):
+        super().__init__()
+        self.base = base
+        self.lora_A = nn.Parameter(torch.empty(r, base.in_features))
+        self.lora_B = nn.Parameter(torch.zeros(base.out_features, r))
+        nn.init.kaiming_uniform_(self.lora_A, a=math.sqrt(5))
+        self.scaling = alpha / r
+
+    @property
+    def weight(self):
+        return self.base.weight
+
+    def forward(self, x):
+        return self.base(x) + F.linear(F.linear(x, self.lora_A), self.lora_B) * self.scaling
+
+
+class Attention(nn.Module):
+    def __init__(self, dim, heads):
+        super().__init__()
+        self.heads = heads
+        self.qkv = nn.Linear(dim, 3 * dim, bias=True)
+        self.proj = nn.Linear(dim, dim, bias=True)
+
+    def forward(self, x):
+        B, N, C = x.shape
+        qkv = self.qkv(x).reshape(B, N, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
+        o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
+        return self.proj(o.transpose(1, 2).reshape(B, N, C))
+
+
+class LayerScale(nn.Module):
+    def __init__(self, dim, init=1e-5):
+        super().__init__()
+        self.gamma = nn.Parameter(torch.full((dim,), init))
+
+    def forward(self, x):
+        return x * self.gamma
+
+
+class Mlp(nn.Module):
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+    def forward(self, x):
+        return self.fc2(F.gelu(self.fc1(x)))
+
+
+class Block(nn.Module):
+    def __init__(self, dim, heads, mlp_ratio=4.0, ls_init=1e-5):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim, eps=1e-6)
+        self.attn = Attention(dim, heads)
+        self.ls1 = LayerScale(dim, ls_init)
+        self.norm2 = nn.LayerNorm(dim, eps=1e-6)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+        self.ls2 = LayerScale(dim, ls_init)
+
+    def forward(self, x):
+        x = x + self.ls1(self.attn(self.norm1(x)))
+        return x + self.ls2(self.mlp(self.norm2(x)))
+
+
+class PatchEmbed(nn.Module):
+    def __init__(self, patch, dim):
+        super().__init__()
+        self.proj = nn.Conv2d(3, dim, kernel_size=patch, stride=patch)
+
+    def forward(self, x):
+        return self.proj(x).flatten(2).transpose(1, 2)
+
+
+class DinoVisionTransformer(nn.Module):
+    """dinov2_vit*14(_reg): 518 px pretraining grid (37x37), bicubic pos-embed interpolation."""
+
+    def __init__(self, arch="dinov2_vitb14_reg", img_size=518, patch=14):
+        super().__init__()
+        dim, depth, heads = ARCHS[arch]
+        self.embed_dim = dim
+        self.patch_size = patch
+        self.num_register_tokens = 4 if arch.endswith("_reg") else 0
+        self.interpolate_antialias = self.num_register_tokens > 0
+        self.interpolate_offset = 0.0 if self.num_register_tokens > 0 else 0.1
+        grid = img_size // patch
+        self.patch_embed = PatchEmbed(patch, dim)
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, dim))
+        self.pos_embed = nn.Parameter(torch.zeros(1, 1 + grid * grid, dim))
+        self.register_tokens = (nn.Parameter(torch.zeros(1, self.num_register_tokens, dim))
+                                if self.num_register_tokens else None)
+        self.mask_token = nn.Parameter(torch.zeros(1, dim))
+        self.blocks = nn.ModuleList([Block(dim, heads) for _ in range(depth)])
+        self.norm = nn.LayerNorm(dim, eps=1e-6)
+        nn.init.trunc_normal_(self.pos_embed, std=0.02)
+        nn.init.normal_(self.cls_token, std=1e-6)
+        if self.register_tokens is not None:
+            nn.init.normal_(self.register_tokens, std=1e-6)
+        self.apply(self._init)
+        self._pos_cache = {}
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, nn.Linear):
+            nn.init.trunc_normal_(m.weight, std=0.02)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+
+    def interpolate_pos_encoding(self, n_patches_h, n_patches_w, dtype):
+        key = (n_patches_h, n_patches_w, dtype, self.pos_embed._version)
+        if not self.pos_embed.requires_grad and key in self._pos_cache:
+            return self._pos_cache[key]
+        pos = self.pos_embed.float()
+        cls_pos, patch_pos = pos[:, :1], pos[:, 1:]
+        M = int(math.sqrt(patch_pos.shape[1]))
+        if (n_patches_h, n_patches_w) != (M, M):
+            patch_pos = F.interpolate(patch_pos.reshape(1, M, M, -1).permute(0, 3, 1, 2),
+                                      size=(n_patches_h, n_patches_w), mode="bicubic",
+                                      antialias=self.interpolate_antialias)
+            patch_pos = patch_pos.permute(0, 2, 3, 1).reshape(1, -1, pos.shape[-1])
+        out = torch.cat([cls_pos, patch_pos], dim=1).to(dtype)
+        if not self.pos_embed.requires_grad:
+            self._pos_cache = {key: out.detach()}
+        return out
+
+    def prepare_tokens(self, x):
+        B, _, H, W = x.shape
+        t = self.patch_embed(x)
+        t = torch.cat([self.cls_token.expand(B, -1, -1).to(t.dtype), t], dim=1)
+        t = t + self.interpolate_pos_encoding(H // self.patch_size, W // self.patch_size, t.dtype)
+        if self.register_tokens is not None:
+            t = torch.cat([t[:, :1], self.register_tokens.expand(B, -1, -1).to(t.dtype), t[:, 1:]], dim=1)
+        return t
+
+    def get_intermediate_layers(self, x, n=1, norm=True):
+        """Hub semantics for an int n: outputs of the last n blocks, normed, patch tokens only."""
+        t = self.prepare_tokens(x)
+        outs = []
+        start = len(self.blocks) - n
+        for i, blk in enumerate(self.blocks):
+            t = blk(t)
+            if i >= start:
+                outs.append(t)
+        if norm:
+            outs = [self.norm(o) for o in outs]
+        skip = 1 + self.num_register_tokens
+        return tuple(o[:, skip:] for o in outs)
+
+    def forward(self, x):
+        t = self.prepare_tokens(x)
+        for blk in self.blocks:
+            t = blk(t)
+        return self.norm(t)[:, 0]
+
+
+def apply_lora(vit: DinoVisionTransformer, r=8, alpha=16, targets=("attn.qkv", "attn.proj")):
+    """Freeze the ViT and wrap the target Linears with LoRA (model.py:223-266)."""
+    for p in vit.parameters():
+        p.requires_grad = False
+    for blk in vit.blocks:
+        if "attn.qkv" in targets:
+            blk.attn.qkv = LoRALinear(blk.attn.qkv, r, alpha)
+        if "attn.proj" in targets:
+            blk.attn.proj = LoRALinear(blk.attn.proj, r, alpha)
+    for n, p in vit.named_parameters():
+        p.requires_grad = "lora_" in n
+    return vit
