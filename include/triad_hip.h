@@ -94,6 +94,48 @@ int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, 
                     int M, int N, int Kd, const float* alpha, void* C, long long ldc, int out_bf16,
                     hipStream_t stream);
 
+/* Split-K GEMM (weight gradients of the projection heads, train.py:987 backward):
+ * `splits` fp32 partial slabs [splits][M][N] in caller-owned `slabs`, then C = alpha * sum. */
+int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                           int M, int N, int Kd, int splits, const float* alpha, float* slabs, void* C,
+                           int out_bf16, hipStream_t stream);
+
+/* Fused projection head forward (model.py:32-34,68 / 81-83,116 / 253-255,326 under bf16
+ * autocast): y = bf16(LN(bf16(h W1^T + b1)) W2^T + b2) for M rows of H features; also
+ * saves y1 = bf16(h W1^T + b1), ln = bf16(LN(y1)), mean/rstd per row for the backward.
+ * W1 [512][H], W2 [512][512] bf16 (nn.Linear layout); b1, b2, gamma, beta fp32. */
+int triad_projhead_fwd(const void* h, int M, int H, const void* W1, const float* b1, const float* gamma,
+                       const float* beta, float eps, const void* W2, const float* b2, void* y, long long ldy,
+                       void* y1, void* ln, float* mean, float* rstd, hipStream_t stream);
+
+/* LayerNorm(512) backward: dy1 (bf16) from dln (fp32), y1, mean, rstd, gamma; per-block
+ * column partials of dgamma / dbeta in dgb_part [nblocks][2][512]. */
+int triad_ln_bwd(const float* dln, const void* y1, const float* mean, const float* rstd, const float* gamma, int M,
+                 void* dy1, float* dgb_part, int nblocks, hipStream_t stream);
+
+/* part[s][c] = sum over row slice s of X[r][c] (bias gradients); X bf16 (x_bf16) or fp32. */
+int triad_colsum_partials(const void* X, int x_bf16, long long rows, int cols, long long ld, int nsplit, float* part,
+                          hipStream_t stream);
+
+/* out[e] = alpha * sum_i slabs[i][e] (alpha may be NULL = 1), fp32 or bf16 out. */
+int triad_sum_slabs(const float* slabs, int nslab, long long n, const float* alpha, int out_bf16, void* out,
+                    hipStream_t stream);
+
+/* x <- (x - mean) / sqrt(var + eps) over ALL n elements (population variance), fp32:
+ * the Wav2Vec2/HuBERT processor normalisation of model.py:56-62 done on the device.
+ * part: >= 2*nblocks doubles of scratch. */
+int triad_global_znorm(const float* x, long long n, float eps, float* y, double* part, int nblocks,
+                       hipStream_t stream);
+
+/* Fused optimizer over flat fp32 buffers (train.py:990-1041). `chunks` is a device array of
+ * {int64 off; int32 n; int32 param} slices. triad_grad_sumsq: out[c] = sum g^2 over chunk c
+ * (grad norms train.py:992-1002, clip_grad_norm_ train.py:1004-1006).
+ * triad_adamw_step: torch.optim.AdamW (decoupled weight decay) with g scaled by scale[param]
+ * (the clip factor, NULL = 1); pp[3*param] = {lr/bc1, 1/sqrt(bc2), 1 - lr*wd}. */
+int triad_grad_sumsq(const float* g, const void* chunks, int nchunks, double* out, hipStream_t stream);
+int triad_adamw_step(float* p, const float* g, float* m, float* v, const void* chunks, int nchunks,
+                     const float* pp, const float* scale, float beta1, float beta2, float eps, hipStream_t stream);
+
 /* dst[b][t] = idx[b][t] >= 0 ? src[b][idx[b][t]] : 0 (row_bytes per row). Patch-dropout
  * compaction with zero padding (model.py:282-307) and its backward scatter. */
 int triad_gather_rows(const void* src, long long src_rows, const int* idx, int B, int M, int row_bytes, void* dst,

@@ -1,0 +1,103 @@
+"""CPU-only tests: the C-ABI library loads and exports every declared symbol, host-side
+logic (dropout plan, parameter grouping, loss mix, tokenizer), and the CPU port of the
+full step (configs[0]-style plumbing run)."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "triad_hip.h")).read()
+    return sorted(set(re.findall(r"^int\s+(triad_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from triad_amd import _lib, build
+    if not os.path.exists(_lib.LIB_PATH):
+        build.build()
+    lib = _lib.load()
+    names = _declared()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _lib.SIGNATURES, f"{n} missing from the ctypes signature table"
+    assert set(_lib.SIGNATURES) == set(names)
+
+
+def test_ops_refuse_cpu_tensors():
+    from triad_amd import ops
+    from triad_amd._lib import TriadError
+    with pytest.raises(TriadError):
+        ops.contrastive_head(ops.AV, torch.zeros(2, 3, 512), torch.zeros(2, 4, 512), torch.tensor(1.5))
+
+
+def test_dropout_plan_matches_oracle_compaction():
+    from oracle import ref_cpu
+    from triad_amd.ops import dropout_indices
+    g = torch.Generator().manual_seed(3)
+    keep = torch.rand(5, 37, generator=g) < 0.7
+    keep[2] = False
+    keep[2, 5] = True
+    idx, inv, n_out = dropout_indices(keep)
+    x = torch.randn(5, 37, 8)
+    out = ref_cpu.patch_dropout(x, keep)
+    assert n_out == out.shape[1]
+    gathered = torch.zeros_like(out)
+    for b in range(5):
+        for t in range(n_out):
+            if idx[b, t] >= 0:
+                gathered[b, t] = x[b, idx[b, t]]
+    assert torch.equal(gathered, out)
+    for b in range(5):
+        for n in range(37):
+            assert (inv[b, n] >= 0) == bool(keep[b, n])
+            if keep[b, n]:
+                assert idx[b, inv[b, n]] == n
+
+
+def test_param_groups_and_loss_mix():
+    from oracle import ref_cpu
+    from triad_amd.train import TriadTrainer, split_param_groups
+
+    class Fake(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.audio_embedder = torch.nn.Module()
+            self.audio_embedder.hubert = torch.nn.Linear(2, 2)
+            self.audio_embedder.projection1 = torch.nn.Linear(2, 2)
+            self.text_embedder = torch.nn.Module()
+            self.text_embedder.encoder = torch.nn.Linear(2, 2)
+            self.visual_embedder = torch.nn.Module()
+            self.visual_embedder.model = torch.nn.Module()
+            self.visual_embedder.model.blk = torch.nn.Linear(2, 2)
+            self.visual_embedder.model.lora_A = torch.nn.Parameter(torch.zeros(2))
+            self.temperature = torch.nn.Parameter(torch.tensor(1.5))
+
+    g = split_param_groups(Fake())
+    assert [len(g[k]) for k in ("audio", "text", "vit_lora", "vit", "others")] == [2, 2, 1, 2, 3]
+    tr = TriadTrainer.__new__(TriadTrainer)
+    tr.av_weight_start, tr.av_weight_end = 0.8, 0.5
+    for phase, prog in (("av_focus", 0), ("tv_warmup", 0), ("weighted_joint", 0.5), ("full_joint", 0)):
+        assert abs(tr._loss_mix(phase, 2.0, 3.0, prog) - ref_cpu.loss_mix(phase, 2.0, 3.0, prog)) < 1e-12
+    assert abs(tr._loss_mix("weighted_joint", 2.0, 3.0, 0.5) - (0.65 * 2 + 0.35 * 3)) < 1e-12
+
+
+def test_hash_tokenizer_shapes():
+    from triad_amd.model import HashTokenizer
+    t = HashTokenizer()(["A man, riding.", "cat"], max_length=3)
+    assert t["input_ids"].shape == (2, 3)
+    assert t["attention_mask"].tolist() == [[1, 1, 1], [1, 0, 0]]
+    assert int(t["input_ids"].min()) == 0 and int(t["input_ids"][:, 0].min()) >= 1000
+
+
+@pytest.mark.slow
+def test_cpu_port_step_runs():
+    """configs[0]-style CPU plumbing: the CPU port of the full step at B=2."""
+    from oracle import cpu_step
+    sec = cpu_step.time_steps(B=2, steps=1, warmup=0, threads=8)
+    assert sec > 0

@@ -1,0 +1,150 @@
+"""GPU parity of the non-head HIP ops: projection head (fwd + bwd), HuBERT processor
+normalisation, patch-dropout compaction, similarity maps, fused AdamW / clip."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from oracle import ref_cpu
+from tests import golden_io as G
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+@pytest.mark.parametrize("rows,H", [(130, 768), (256, 384), (64 * 5 + 3, 1024)])
+def test_projection_head_fwd_bwd(rows, H):
+    from triad_amd import ops
+    torch.manual_seed(rows + H)
+    p1, ln, p2 = nn.Linear(H, 512), nn.LayerNorm(512), nn.Linear(512, 512)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    h = torch.randn(2, rows, H)
+    # oracle (bf16 autocast emulation) forward; fp32 autograd reference for gradients
+    y_ref = ref_cpu.projection_head(h, p1.weight, p1.bias, ln.weight, ln.bias, p2.weight, p2.bias, amp=True)
+    hr = h.clone().requires_grad_(True)
+    mods = [m for m in (p1, ln, p2)]
+    y32 = p2(ln(p1(hr)))
+    gy = torch.randn_like(y32) * 0.01
+    y32.backward(gy)
+    ref_grads = [hr.grad] + [p.grad.clone() for m in mods for p in m.parameters()]
+    # device
+    d1, dln, d2 = [m.to(dev) for m in (nn.Linear(H, 512), nn.LayerNorm(512), nn.Linear(512, 512))]
+    for a, b in zip((d1, dln, d2), (p1, ln, p2)):
+        a.load_state_dict(b.state_dict())
+    hd = h.to(dev).requires_grad_(True)
+    y = ops.projection_head(hd, d1, dln, d2)
+    assert y.dtype == torch.bfloat16 and y.shape == (2, rows, 512)
+    # forward: bf16-rounded outputs of the same bf16 arithmetic (1-ulp bf16 tolerance)
+    y_ref = y_ref.detach()
+    np.testing.assert_allclose(y.detach().float().cpu().numpy(), y_ref.numpy(), rtol=1.6e-2, atol=2e-2)
+    assert _rel(y.float(), y_ref) < 4e-3
+    y.float().backward(gy.to(dev))
+    got = [hd.grad] + [p.grad for m in (d1, dln, d2) for p in m.parameters()]
+    for gg, rr in zip(got, ref_grads):
+        assert _rel(gg, rr) < 2e-2, _rel(gg, rr)
+
+
+def test_global_znorm_matches_processor_semantics():
+    from triad_amd import ops
+    x = torch.randn(4, 64000) * 0.1 + torch.arange(4)[:, None]
+    ref = (x.double() - x.double().mean()) / torch.sqrt(x.double().var(unbiased=False) + 1e-7)
+    y = ops.global_znorm(x.to(dev), 1e-7)
+    np.testing.assert_allclose(y.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", G.names("dropout"))
+def test_patch_dropout_matches_reference(name):
+    from triad_amd import ops
+    f = G.load(name)
+    x = G.bf16(f["x"]).to(dev, torch.bfloat16).requires_grad_(True)
+    keep = torch.from_numpy(f["keep"])
+    out = ops.patch_dropout(x, keep)
+    np.testing.assert_array_equal(out.float().cpu().numpy(), G.bf16(f["out"]).numpy())
+    g = torch.randn_like(out.float()).to(torch.bfloat16)
+    out.backward(g)
+    # backward scatters grads to kept positions, zero elsewhere
+    ref = torch.zeros_like(x.float()).cpu()
+    for b in range(keep.shape[0]):
+        kept = keep[b].nonzero().flatten()
+        ref[b, kept] = g[b, :len(kept)].float().cpu()
+    np.testing.assert_array_equal(x.grad.float().cpu().numpy(), ref.numpy())
+
+
+@pytest.mark.parametrize("name", G.names("simmat"))
+def test_similarity_maps_match_reference(name):
+    from triad_amd import ops
+    f = G.load(name)
+    f1, f2 = G.bf16(f["f1"]), G.bf16(f["f2"])
+    sim = ops.similarity_maps(f1.to(dev, torch.bfloat16), f2.to(dev, torch.bfloat16),
+                              torch.tensor(float(f["temp"]), device=dev))
+    # inputs re-rounded to bf16 after the L2 normalisation: bf16 tolerance
+    np.testing.assert_allclose(sim.cpu().numpy(), f["sim"], rtol=0, atol=1.5e-2)
+
+
+def test_fused_adamw_matches_torch_with_onecycle_and_clip():
+    from triad_amd import optim as fo
+    torch.manual_seed(0)
+    shapes = [(300, 17), (1025,), (64, 64)]
+    ref = [nn.Parameter(torch.randn(s)) for s in shapes]
+    mine = [nn.Parameter(p.detach().clone().to(dev)) for p in ref]
+    space = fo.FlatParamSpace(mine, dev)
+    o_ref = torch.optim.AdamW(ref, lr=1e-3)
+    o_mine = fo.FusedAdamW(space, mine, lr=1e-3)
+    s_ref = torch.optim.lr_scheduler.OneCycleLR(o_ref, max_lr=1e-3, total_steps=10, pct_start=0.1, div_factor=10,
+                                                final_div_factor=1e4, anneal_strategy="cos")
+    s_mine = torch.optim.lr_scheduler.OneCycleLR(o_mine, max_lr=1e-3, total_steps=10, pct_start=0.1,
+                                                 div_factor=10, final_div_factor=1e4, anneal_strategy="cos")
+    for it in range(5):
+        grads = [torch.randn(s) * (5.0 if it == 2 else 0.1) for s in shapes]
+        for p, g in zip(ref, grads):
+            p.grad = g.clone()
+        # autograd-style accumulation into the flat buffer
+        loss = sum((p * g.to(dev)).sum() for p, g in zip(mine, grads))
+        loss.backward()
+        nr = torch.nn.utils.clip_grad_norm_(ref[:2], 10.0)
+        nm = fo.clip_grad_norm_(space, mine[:2], 10.0)
+        assert abs(float(nr) - float(nm)) <= 1e-4 * float(nr)
+        o_ref.step()
+        o_ref.zero_grad()
+        s_ref.step()
+        o_mine.step()
+        o_mine.zero_grad()
+        s_mine.step()
+        for a, b in zip(ref, mine):
+            np.testing.assert_allclose(b.detach().cpu().numpy(), a.detach().numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_trainer_step_runs_and_moves_params():
+    from triad_amd.model import MultiModalModel
+    from triad_amd.train import TriadTrainer
+    torch.manual_seed(0)
+    m = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.8, patch_sparsity_weight=0.01,
+                        visual_dropout_prob=0.25).to(dev)
+    m.train()
+    tr = TriadTrainer(m, total_updates=100, unfreeze_audio_step=0, unfreeze_text_step=0, unfreeze_vit_step=0,
+                      device=dev)
+    B = 4
+    frames = torch.randn(B, 3, 224, 224, device=dev)
+    audio = torch.randn(B, 16000, device=dev) * 0.1
+    text = ["a man riding a bicycle", "a cat on a bed", "dogs", "the quick brown fox jumps"]
+    before = m.temperature.detach().clone()
+    w0 = m.audio_embedder.projection1.weight.detach().clone()
+    out = tr.step(frames, audio, text)
+    torch.cuda.synchronize()
+    assert math.isfinite(float(out["loss"]))
+    assert float((m.audio_embedder.projection1.weight - w0).abs().max()) > 0
+    assert float((m.temperature - before).abs()) > 0
+    s = out["av_stats"]
+    assert set(s) == {"av_pos_sim_mean", "av_pos_sim_std", "av_neg_sim_mean", "av_neg_sim_std", "av_separation",
+                      "av_hardest_negative"}
+    assert all(math.isfinite(v) for v in s.values())

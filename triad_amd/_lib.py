@@ -27,6 +27,14 @@ SIGNATURES = {
                          vp, i64, vp, vp],
     "triad_dtemp_finalize": [vp, i32, vp, vp, i32, vp, vp],
     "triad_gemm_bf16": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, i32, vp],
+    "triad_gemm_bf16_splitk": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp],
+    "triad_projhead_fwd": [vp, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, i64, vp, vp, vp, vp, vp],
+    "triad_ln_bwd": [vp, vp, vp, vp, vp, i32, vp, vp, i32, vp],
+    "triad_colsum_partials": [vp, i32, i64, i32, i64, i32, vp, vp],
+    "triad_sum_slabs": [vp, i32, i64, vp, i32, vp, vp],
+    "triad_global_znorm": [vp, i64, f32, vp, vp, i32, vp],
+    "triad_grad_sumsq": [vp, vp, i32, vp, vp],
+    "triad_adamw_step": [vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, vp],
     "triad_gather_rows": [vp, i64, vp, i32, i32, i32, vp, vp],
     "triad_l2norm_rows": [vp, i32, i32, f32, vp, vp],
 }
@@ -56,9 +64,26 @@ def load():
     return _lib
 
 
+# Optional live timing of launches: {entry point name: [(start_event, end_event, meta), ...]}.
+# Enabled by bench.py over its timed region; events are recorded on the current HIP stream,
+# which is the stream every entry point is launched on.
+TIMERS = None
+META = None  # set by callers (ops) just before a timed call: per-launch metadata (e.g. FLOPs)
+
+
 def call(name, *args):
     """Invoke an entry point; non-zero status -> TriadError (RuntimeError)."""
-    rc = getattr(load(), name)(*args)
+    global META
+    meta, META = META, None
+    if TIMERS is not None and name in TIMERS:
+        import torch
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(load(), name)(*args)
+        e1.record()
+        TIMERS[name].append((e0, e1, meta))
+    else:
+        rc = getattr(load(), name)(*args)
     if name != "triad_pairsim_nparts" and rc != 0:
         what = "invalid argument/shape" if rc == 1001 else f"hipError_t {rc}"
         raise TriadError(f"{name} failed: {what}")

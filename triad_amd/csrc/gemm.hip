@@ -76,7 +76,8 @@ template <bool A_KCONTIG, bool B_KCONTIG, typename OutT>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A, long long lda,
                                                       const bf16* __restrict__ B, long long ldb,
                                                       int M, int N, int Kd, const float* __restrict__ alpha_p,
-                                                      OutT* __restrict__ C, long long ldc) {
+                                                      OutT* __restrict__ C, long long ldc, int k_per_split,
+                                                      long long slab_stride) {
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * (A_ELEMS + B_ELEMS)];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -96,15 +97,20 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){};
 
-  const int nk = Kd / BK;
-  stage_a<A_KCONTIG>(A, lda, m0, 0, lds, wave, lane);
-  stage_b<B_KCONTIG>(B, ldb, n0, 0, lds + A_ELEMS, wave, lane);
+  // split-K: blockIdx.y owns k in [kbeg, kbeg + k_per_split) and writes its own slab of C
+  const int kbeg = blockIdx.y * k_per_split;
+  const int nk = min(k_per_split, Kd - kbeg) / BK;
+  C += (size_t)blockIdx.y * slab_stride;
+  if (nk > 0) {
+  stage_a<A_KCONTIG>(A, lda, m0, kbeg, lds, wave, lane);
+  stage_b<B_KCONTIG>(B, ldb, n0, kbeg, lds + A_ELEMS, wave, lane);
+  }
   for (int kt = 0; kt < nk; ++kt) {
     lds_dma_barrier();
     if (kt + 1 < nk) {
       bf16* nb = lds + ((kt + 1) & 1) * (A_ELEMS + B_ELEMS);
-      stage_a<A_KCONTIG>(A, lda, m0, (kt + 1) * BK, nb, wave, lane);
-      stage_b<B_KCONTIG>(B, ldb, n0, (kt + 1) * BK, nb + A_ELEMS, wave, lane);
+      stage_a<A_KCONTIG>(A, lda, m0, kbeg + (kt + 1) * BK, nb, wave, lane);
+      stage_b<B_KCONTIG>(B, ldb, n0, kbeg + (kt + 1) * BK, nb + A_ELEMS, wave, lane);
     }
     const bf16* ai = lds + (kt & 1) * (A_ELEMS + B_ELEMS);
     const bf16* bi = ai + A_ELEMS;
@@ -134,7 +140,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
     }
   }
 
-  const float alpha = *alpha_p;
+  const float alpha = alpha_p ? *alpha_p : 1.f;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -150,11 +156,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
 
 template <bool AK, bool BK_, typename OutT>
 int launch(const void* A, long long lda, const void* B, long long ldb, int M, int N, int Kd, const float* alpha,
-           void* C, long long ldc, hipStream_t st) {
-  if (M % BM || N % BN || Kd % BK || lda % 8 || ldb % 8) return TRIAD_EINVAL;
+           void* C, long long ldc, hipStream_t st, int splits = 1, long long slab_stride = 0) {
+  if (M % BM || N % BN || Kd % BK || lda % 8 || ldb % 8 || splits < 1) return TRIAD_EINVAL;
   const int nwg = (M / BM) * (N / BN);
-  hipLaunchKernelGGL((gemm_kernel<AK, BK_, OutT>), dim3(nwg), dim3(256), 0, st, (const bf16*)A, lda, (const bf16*)B,
-                     ldb, M, N, Kd, alpha, (OutT*)C, ldc);
+  const int kps = ((Kd / BK + splits - 1) / splits) * BK;
+  hipLaunchKernelGGL((gemm_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(256), 0, st, (const bf16*)A, lda,
+                     (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
@@ -178,6 +185,26 @@ int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, 
   TRIAD_GEMM_CASE(false, false)
 #undef TRIAD_GEMM_CASE
   return TRIAD_EINVAL;
+}
+
+// Split-K form for short-and-wide outputs (weight gradients: M, N = 512 / H, Kd = tokens):
+// `splits` partial fp32 slabs in `slabs` ([splits][M][N], caller-owned), then
+// C = alpha * sum(slabs) as fp32 or bf16 (ldc == N).
+int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                           int M, int N, int Kd, int splits, const float* alpha, float* slabs, void* C,
+                           int out_bf16, hipStream_t stream) {
+  const long long slab = (long long)M * N;
+  int rc = TRIAD_EINVAL;
+#define TRIAD_GEMM_SK(AK, BKC)                                                                  \
+  if (!!a_kcontig == AK && !!b_kcontig == BKC)                                                 \
+    rc = launch<AK, BKC, float>(A, lda, B, ldb, M, N, Kd, nullptr, slabs, N, stream, splits, slab);
+  TRIAD_GEMM_SK(true, true)
+  TRIAD_GEMM_SK(true, false)
+  TRIAD_GEMM_SK(false, true)
+  TRIAD_GEMM_SK(false, false)
+#undef TRIAD_GEMM_SK
+  if (rc) return rc;
+  return triad_sum_slabs(slabs, splits, slab, alpha, out_bf16, C, stream);
 }
 
 }  // extern "C"

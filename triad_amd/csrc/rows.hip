@@ -75,3 +75,54 @@ int triad_l2norm_rows(const void* x, int rows, int D, float eps, void* y, hipStr
 }
 
 }  // extern "C"
+
+namespace {
+
+// pass 1: per-block partial (sum, sum of squares) in double
+__global__ __launch_bounds__(256) void znorm_stats_kernel(const float* __restrict__ x, long long n,
+                                                          double* __restrict__ part) {
+  __shared__ double red[4];
+  double s = 0.0, q = 0.0;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const double v = x[e];
+    s += v;
+    q += v * v;
+  }
+  s = block_sum_d(s, red);
+  q = block_sum_d(q, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s;
+    part[2 * blockIdx.x + 1] = q;
+  }
+}
+
+// pass 2: every block re-reduces the partials, then normalises its slice
+__global__ __launch_bounds__(256) void znorm_apply_kernel(const float* __restrict__ x, long long n, float eps,
+                                                          const double* __restrict__ part, int nparts,
+                                                          float* __restrict__ y) {
+  __shared__ double red[4];
+  double s = 0.0, q = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+    s += part[2 * i];
+    q += part[2 * i + 1];
+  }
+  s = block_sum_d(s, red);
+  q = block_sum_d(q, red);
+  const double mean = s / (double)n;
+  const double var = q / (double)n - mean * mean;
+  const float m = (float)mean;
+  const float inv = (float)(1.0 / sqrt((var > 0.0 ? var : 0.0) + (double)eps));
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x)
+    y[e] = (x[e] - m) * inv;
+}
+
+}  // namespace
+
+extern "C" int triad_global_znorm(const float* x, long long n, float eps, float* y, double* part, int nblocks,
+                                  hipStream_t stream) {
+  if (n <= 0 || nblocks <= 0) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(znorm_stats_kernel, dim3(nblocks), dim3(256), 0, stream, x, n, part);
+  hipLaunchKernelGGL(znorm_apply_kernel, dim3(nblocks), dim3(256), 0, stream, x, n, eps, part, nblocks, y);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}

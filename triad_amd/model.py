@@ -192,7 +192,6 @@ class ViTLoRAEmbedder(nn.Module):
                  dropout_prob=0.1, lora_rank=8, lora_alpha=16):
         super().__init__()
         self.model = apply_lora(DinoVisionTransformer(arch), lora_rank, lora_alpha)
-        self.model.embed_dim = self.model.embed_dim
         self.projection1 = nn.Linear(self.model.embed_dim, 512)
         self.layer_norm = nn.LayerNorm(512)
         self.projection2 = nn.Linear(512, embedding_dim)

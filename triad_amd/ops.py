@@ -86,68 +86,93 @@ def pack_keys(k: torch.Tensor, g: Geometry) -> torch.Tensor:
 
 
 class _ContrastiveHead(torch.autograd.Function):
-    """losses = [total, ce, reg, aux] (aux = 0.01*l_smooth for AV, sparsity for TV), stats[9]."""
+    """losses = [total, ce, reg, aux] (aux = 0.01*l_smooth for AV, sparsity for TV), stats[9].
+
+    group=None: local head (the reference loss over this process's batch).
+    group=<process group>: global negatives (SURVEY §8e Mode G, triad_amd.dist): keys are
+    all-gathered, this rank computes its query rows of the B_g x B_g clip matrix, and the
+    loss head runs on the gathered clip on every rank (identical loss = reference at B_g).
+    """
 
     @staticmethod
-    def forward(ctx, q, k, temperature, kind, q_mask, thr, w_sparse):
+    def forward(ctx, q, k, temperature, kind, q_mask, thr, w_sparse, group):
         _check_device(q, k, temperature, q_mask)
         Bq, Nq, dq = q.shape
-        Bk, Nk, dk = k.shape
+        Bl, Nk, dk = k.shape
         if dq != D or dk != D:
             raise TriadError(f"feature dim must be {D}")
-        if Bq != Bk:
-            raise TriadError("local head needs matching batch sizes")
-        if Bq < 2:
+        if Bq != Bl:
+            raise TriadError("query and key batches must match")
+        W, rank = (1, 0)
+        if group is not None:
+            from . import dist as tdist
+            W, rank = tdist.world_rank(group)
+        Bg = Bq * W
+        if Bg < 2:
             # the reference takes max() of the empty off-diagonal set and raises (model.py:447/565)
             raise TriadError("batch size must be >= 2 (no negatives for B == 1)")
-        g = Geometry(Bq, Nq, Bk, Nk)
+        g = Geometry(Bq, Nq, Bg, Nk)
         dev = q.device
         st = stream_ptr(dev)
         Qb = pack_queries(q, g)
-        Kb = pack_keys(k, g)
+        if W == 1:
+            Kb = pack_keys(k, g)
+        else:
+            gl = Geometry(Bq, Nq, Bq, Nk)
+            Kb = tdist.gather_keys(pack_keys(k, gl)[:gl.C_pad], g.C_alloc, group)
         temp = temperature.detach().reshape(1).to(torch.float32).contiguous()
         nparts = call("triad_pairsim_nparts", g.R_pad, g.Bk)
         rowmax = torch.empty(g.Bk, g.R_pad, dtype=torch.float32, device=dev)
         argmax = torch.empty(g.Bk, g.R_pad, dtype=torch.int32, device=dev)
         nn_part = torch.empty(nparts, dtype=torch.float64, device=dev)
         diagS = torch.empty(g.Bq, g.Nq, g.Nk_pad, dtype=torch.float32, device=dev)
+        _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D,
+                         bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R)
         call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
-             ptr(temp), CLAMP_LO[kind], 1, 0, ptr(rowmax), ptr(argmax), ptr(nn_part), ptr(diagS), st)
+             ptr(temp), CLAMP_LO[kind], 1, rank * Bq, ptr(rowmax), ptr(argmax), ptr(nn_part), ptr(diagS), st)
         clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
         qw = torch.empty(g.R, dtype=torch.float32, device=dev)
         qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
         call("triad_clip_reduce", ptr(rowmax), g.R_pad, g.Nq, g.Bq, g.Bk, ptr(qm), ptr(clip), ptr(qw), st)
         dg_part = torch.empty(g.Bq, dtype=torch.float64, device=dev)
         if kind == AV:
-            cnt = float(g.Bq * (g.Nq - 1) * g.Nk_eff)
+            cnt = float(Bg * (g.Nq - 1) * g.Nk_eff)
             gdiag = torch.empty_like(diagS)
             call("triad_diag_smooth", ptr(diagS), g.Bq, g.Nq, g.Nk_pad, g.Nk_eff, cnt, ptr(dg_part), ptr(gdiag), st)
         else:
-            cnt = float(g.Bq * g.Nk_eff)
+            cnt = float(Bg * g.Nk_eff)
             call("triad_diag_sparsity", ptr(diagS), g.Bq, g.Nq, g.Nk_pad, g.Nk_eff, float(thr), cnt,
                  ptr(dg_part), st)
             gdiag = diagS
+        n_el = float(Bg) * Bg * g.Nq * g.Nk_eff
+        if W == 1:
+            clip_full, nn_in, n_nn, dg_in, n_dg = clip, nn_part, nparts, dg_part, g.Bq
+        else:
+            clip_full = tdist.gather_rows(clip, group)
+            sums = tdist.allreduce_sum(torch.stack([nn_part.sum(), dg_part.sum()]), group)
+            nn_in, n_nn, dg_in, n_dg = sums[0:1], 1, sums[1:2], 1
         out = torch.empty(13, dtype=torch.float32, device=dev)
-        dclip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
-        lse = torch.empty(2 * g.Bq, dtype=torch.float32, device=dev)
-        n_el = float(g.Bq) * g.Bk * g.Nq * g.Nk_eff
-        call("triad_losshead", ptr(clip), g.Bq, kind, ptr(temp), ptr(nn_part), nparts, n_el, ptr(dg_part), g.Bq,
+        dclip = torch.empty(Bg, Bg, dtype=torch.float32, device=dev)
+        lse = torch.empty(2 * Bg, dtype=torch.float32, device=dev)
+        call("triad_losshead", ptr(clip_full), Bg, kind, ptr(temp), ptr(nn_in), n_nn, n_el, ptr(dg_in), n_dg,
              cnt, float(w_sparse), ptr(out), ptr(dclip), ptr(lse), st)
+        dclip_rows = dclip[rank * Bq:(rank + 1) * Bq].contiguous() if W > 1 else dclip
 
-        ctx.save_for_backward(Qb, Kb, argmax, dclip, qw, gdiag, temp)
+        ctx.save_for_backward(Qb, Kb, argmax, dclip_rows, qw, gdiag, temp)
         ctx.geom, ctx.kind, ctx.n_el, ctx.w_sparse, ctx.nparts = g, kind, n_el, float(w_sparse), nparts
+        ctx.group, ctx.W, ctx.rank, ctx.Nk = group, W, rank, Nk
         ctx.q_dtype, ctx.k_dtype, ctx.t_dtype = q.dtype, k.dtype, temperature.dtype
         losses, stats = out[:4].clone(), out[4:].clone()
-        ctx.mark_non_differentiable(stats, clip)
+        ctx.mark_non_differentiable(stats, clip_full)
         ctx.set_materialize_grads(False)
-        return losses, stats, clip
+        return losses, stats, clip_full
 
     @staticmethod
     def backward(ctx, g_losses, g_stats, g_clip):
         if g_losses is None:
-            return None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None
         Qb, Kb, argmax, dclip, qw, gdiag, temp = ctx.saved_tensors
-        g, kind = ctx.geom, ctx.kind
+        g, kind, W, rank = ctx.geom, ctx.kind, ctx.W, ctx.rank
         dev = Qb.device
         st = stream_ptr(dev)
         gl = g_losses.to(torch.float32)
@@ -165,36 +190,46 @@ class _ContrastiveHead(torch.autograd.Function):
         if g.C_alloc > g.C_pad:
             dS[:, g.C_pad:].zero_()
         dt_part = torch.empty(ctx.nparts, dtype=torch.float64, device=dev)
+        _lib.META = dict(kind=kind, flops=0.0, recompute_flops=2.0 * g.R * g.Bk * g.Nk_eff * D)
         call("triad_pairsim_dS", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D, ptr(temp),
-             CLAMP_LO[kind], 1, 0, ptr(argmax), ptr(dclip), ptr(qw), ptr(gdiag), ptr(coef), ptr(dS), g.C_alloc,
-             ptr(dt_part), st)
+             CLAMP_LO[kind], 1, rank * g.Bq, ptr(argmax), ptr(dclip), ptr(qw), ptr(gdiag), ptr(coef), ptr(dS),
+             g.C_alloc, ptr(dt_part), st)
         gq = gk = gt = None
         if ctx.needs_input_grad[0]:
             dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
+            _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dQ")
             call("triad_gemm_bf16", ptr(dS), g.C_alloc, 1, ptr(Kb), D, 0, g.R_pad, D, g.C_alloc, ptr(temp), ptr(dQ), D,
                  1, st)
             gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(ctx.q_dtype)
         if ctx.needs_input_grad[1]:
             dK = torch.empty(g.C_alloc, D, dtype=torch.bfloat16, device=dev)
+            _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dK")
             call("triad_gemm_bf16", ptr(dS), g.C_alloc, 0, ptr(Qb), D, 0, g.C_alloc, D, g.R_pad, ptr(temp), ptr(dK), D,
                  1, st)
-            gk = dK[:g.C_pad].view(g.Bk, g.Nk_pad, D)[:, :g.Nk_eff].to(ctx.k_dtype)
+            Nk_pad = g.Nk_pad
+            if W > 1:
+                from . import dist as tdist
+                dK = tdist.reduce_scatter_rows(dK, g.Bq * Nk_pad, ctx.group)  # this rank's keys, all queries
+            gk = dK[:g.Bq * Nk_pad].view(g.Bq, Nk_pad, D)[:, :ctx.Nk].to(ctx.k_dtype)
         if ctx.needs_input_grad[2]:
             dt = torch.empty(1, dtype=torch.float32, device=dev)
-            call("triad_dtemp_finalize", ptr(dt_part), ctx.nparts, ptr(temp), ptr(coef), 1 if kind == AV else 0,
-                 ptr(dt), st)
+            has_cal = 1 if (kind == AV and rank == 0) else 0   # the l_cal term is counted once
+            call("triad_dtemp_finalize", ptr(dt_part), ctx.nparts, ptr(temp), ptr(coef), has_cal, ptr(dt), st)
             gt = dt.reshape(()).to(ctx.t_dtype)
-        return gq, gk, gt, None, None, None, None
+        return gq, gk, gt, None, None, None, None, None
 
 
-def contrastive_head(kind, q, k, temperature, q_mask=None, threshold=0.0, sparsity_weight=0.0):
+def contrastive_head(kind, q, k, temperature, q_mask=None, threshold=0.0, sparsity_weight=0.0, group=None):
     """Fused similarity + aggregation + InfoNCE + regularisers.
 
     kind AV: q = audio feats (B,Na,512), k = visual feats (B,Nv,512) (model.py:470-472)
     kind TV: q = text feats (B,Nt,512) with q_mask (B,Nt), k = visual feats (model.py:593)
-    Returns (losses[4], stats[9], clip[B,B]); losses = total, contrastive, reg, aux.
+    group: process group for global negatives (every rank must pass k with the same Nv).
+    Returns (losses[4], stats[9], clip[B_g,B_g]); losses = total, contrastive, reg, aux.
+    In global mode the gradients w.r.t. q, k, temperature are this rank's share of the
+    full-loss gradient: sum them over ranks (the trainer's Mode-G all-reduce does).
     """
-    return _ContrastiveHead.apply(q, k, temperature, kind, q_mask, threshold, sparsity_weight)
+    return _ContrastiveHead.apply(q, k, temperature, kind, q_mask, threshold, sparsity_weight, group)
 
 
 def gather_rows(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
@@ -217,3 +252,228 @@ def l2_normalize(x: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
     rows = xc.numel() // xc.shape[-1]
     call("triad_l2norm_rows", ptr(xc), rows, xc.shape[-1], eps, ptr(y), stream_ptr(x.device))
     return y
+
+
+# ----------------------------------------------------------------------------------------
+# Projection head: proj2(LN(proj1(h))) (model.py:32-34,68 / 81-83,116 / 253-255,326)
+# ----------------------------------------------------------------------------------------
+def _pad_rows(x: torch.Tensor, rows: int) -> torch.Tensor:
+    if x.shape[0] == rows:
+        return x.contiguous()
+    out = torch.empty((rows,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    out[:x.shape[0]].copy_(x)
+    out[x.shape[0]:].zero_()
+    return out
+
+
+def _splitk(Kd, mn_tiles):
+    """Split count so that tiles * splits ~ 2 x CUs, >= 1 k-block (64) per split."""
+    want = max(1, (512 + mn_tiles - 1) // mn_tiles)
+    return max(1, min(want, Kd // 256))
+
+
+def _bf16_round(t):
+    return t.detach().to(torch.bfloat16).to(torch.float32).contiguous()
+
+
+class _ProjectionHead(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, w1, b1, gamma, beta, w2, b2, eps):
+        _check_device(h, w1)
+        lead, H = h.shape[:-1], h.shape[-1]
+        M = h.numel() // H
+        if w1.shape != (D, H) or w2.shape != (D, D):
+            raise TriadError("projection head expects Linear(H->512), Linear(512->512)")
+        dev = h.device
+        st = stream_ptr(dev)
+        Mp = _rup(max(M, 1), 128)
+        hb = _pad_rows(h.reshape(M, H).to(torch.bfloat16), Mp)
+        w1b = w1.detach().to(torch.bfloat16).contiguous()
+        w2b = w2.detach().to(torch.bfloat16).contiguous()
+        # autocast runs F.linear with the bias cast to bf16 (model.py:483/603)
+        b1r, b2r = _bf16_round(b1), _bf16_round(b2)
+        g32 = gamma.detach().to(torch.float32).contiguous()
+        be32 = beta.detach().to(torch.float32).contiguous()
+        y = torch.empty(M, D, dtype=torch.bfloat16, device=dev)
+        y1 = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
+        ln = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
+        if Mp > M:
+            y1[M:].zero_()
+            ln[M:].zero_()
+        mean = torch.empty(M, dtype=torch.float32, device=dev)
+        rstd = torch.empty(M, dtype=torch.float32, device=dev)
+        call("triad_projhead_fwd", ptr(hb), M, H, ptr(w1b), ptr(b1r), ptr(g32), ptr(be32), float(eps), ptr(w2b),
+             ptr(b2r), ptr(y), D, ptr(y1), ptr(ln), ptr(mean), ptr(rstd), st)
+        ctx.save_for_backward(hb, w1b, w2b, g32, y1, ln, mean, rstd)
+        ctx.shape = (lead, H, M, Mp)
+        ctx.dtypes = (h.dtype, w1.dtype, b1.dtype, gamma.dtype, beta.dtype, w2.dtype, b2.dtype)
+        return y.view(*lead, D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        hb, w1b, w2b, g32, y1, ln, mean, rstd = ctx.saved_tensors
+        lead, H, M, Mp = ctx.shape
+        dev = dy.device
+        st = stream_ptr(dev)
+        f32 = torch.float32
+        dyp = _pad_rows(dy.reshape(M, D).to(torch.bfloat16), Mp)
+        # d ln = dy . W2          [Mp][512] fp32
+        dln = torch.empty(Mp, D, dtype=f32, device=dev)
+        call("triad_gemm_bf16", ptr(dyp), D, 1, ptr(w2b), D, 0, Mp, D, D, None, ptr(dln), D, 0, st)
+        # dW2 = dy^T . ln         [512][512], split-K over tokens
+        sp = _splitk(Mp, (D // 128) * (D // 128))
+        slabs = torch.empty(sp * max(D * D, D * H), dtype=f32, device=dev)
+        dw2 = torch.empty(D, D, dtype=f32, device=dev)
+        call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp, None, ptr(slabs), ptr(dw2), 0, st)
+        # db2 = column sums of dy
+        ns = max(1, min(64, Mp // 512))
+        cpart = torch.empty(ns, D, dtype=f32, device=dev)
+        db2 = torch.empty(D, dtype=f32, device=dev)
+        call("triad_colsum_partials", ptr(dyp), 1, Mp, D, D, ns, ptr(cpart), st)
+        call("triad_sum_slabs", ptr(cpart), ns, D, None, 0, ptr(db2), st)
+        # LayerNorm backward -> dy1 (bf16), dgamma, dbeta
+        dy1 = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
+        if Mp > M:
+            dy1[M:].zero_()
+        nb = max(1, min(1024, (M + 3) // 4))
+        gpart = torch.empty(nb, 2, D, dtype=f32, device=dev)
+        call("triad_ln_bwd", ptr(dln), ptr(y1), ptr(mean), ptr(rstd), ptr(g32), M, ptr(dy1), ptr(gpart), nb, st)
+        dgb = torch.empty(2, D, dtype=f32, device=dev)
+        call("triad_sum_slabs", ptr(gpart), nb, 2 * D, None, 0, ptr(dgb), st)
+        # dW1 = dy1^T . h         [512][H], split-K
+        sp1 = _splitk(Mp, (D // 128) * (H // 128))
+        dw1 = torch.empty(D, H, dtype=f32, device=dev)
+        call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), 0,
+             st)
+        call("triad_colsum_partials", ptr(dy1), 1, Mp, D, D, ns, ptr(cpart), st)
+        db1 = torch.empty(D, dtype=f32, device=dev)
+        call("triad_sum_slabs", ptr(cpart), ns, D, None, 0, ptr(db1), st)
+        # dh = dy1 . W1           [Mp][H] bf16
+        dh = torch.empty(Mp, H, dtype=torch.bfloat16, device=dev)
+        call("triad_gemm_bf16", ptr(dy1), D, 1, ptr(w1b), H, 0, Mp, H, D, None, ptr(dh), H, 1, st)
+        hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
+        return (dh[:M].view(*lead, H).to(hd), dw1.to(w1d), db1.to(b1d), dgb[0].to(gd), dgb[1].to(bd), dw2.to(w2d),
+                db2.to(b2d), None)
+
+
+def projection_head(h, proj1: torch.nn.Linear, layer_norm: torch.nn.LayerNorm, proj2: torch.nn.Linear):
+    """Fused HIP projection head; returns bf16 (B, N, 512) like the autocast reference."""
+    return _ProjectionHead.apply(h, proj1.weight, proj1.bias, layer_norm.weight, layer_norm.bias, proj2.weight,
+                                 proj2.bias, layer_norm.eps)
+
+
+# ----------------------------------------------------------------------------------------
+# HuBERT processor normalisation (model.py:56-62) on the device
+# ----------------------------------------------------------------------------------------
+def global_znorm(x: torch.Tensor, eps: float = 1e-7) -> torch.Tensor:
+    _check_device(x)
+    xf = x.to(torch.float32).contiguous()
+    y = torch.empty_like(xf)
+    nb = int(max(1, min(1024, xf.numel() // 4096)))
+    part = torch.empty(2 * nb, dtype=torch.float64, device=x.device)
+    call("triad_global_znorm", ptr(xf), xf.numel(), float(eps), ptr(y), ptr(part), nb, stream_ptr(x.device))
+    return y
+
+
+# ----------------------------------------------------------------------------------------
+# Patch dropout compaction (model.py:268-308)
+# ----------------------------------------------------------------------------------------
+class _GatherRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, idx, inv_idx):
+        ctx.save_for_backward(inv_idx)
+        return gather_rows(x, idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        (inv_idx,) = ctx.saved_tensors
+        return gather_rows(g.contiguous(), inv_idx), None, None
+
+
+def dropout_indices(keep_mask: torch.Tensor):
+    """Host-side compaction plan from a (B, N) keep mask: idx[b][t] = t-th kept token of
+    sample b (-1 pads to the longest kept length), inv[b][n] = its output slot or -1."""
+    keep = keep_mask.detach().to("cpu", torch.bool)
+    B, N = keep.shape
+    counts = keep.sum(1)
+    n_out = int(counts.max()) if B else 0
+    pos = torch.cumsum(keep.to(torch.int32), dim=1) - 1
+    inv = torch.where(keep, pos, torch.full_like(pos, -1)).to(torch.int32)
+    idx = torch.full((B, max(n_out, 1)), -1, dtype=torch.int32)
+    b_ix, n_ix = keep.nonzero(as_tuple=True)
+    idx[b_ix, pos[b_ix, n_ix].long()] = n_ix.to(torch.int32)
+    return idx[:, :n_out], inv, n_out
+
+
+def patch_dropout(x: torch.Tensor, keep_mask: torch.Tensor) -> torch.Tensor:
+    """(B, N, D) -> (B, max_b kept_b, D): kept tokens in order, zero padded (model.py:282-307)."""
+    _check_device(x)
+    idx, inv, n_out = dropout_indices(keep_mask)
+    idx_d = idx.to(x.device, non_blocking=True)
+    inv_d = inv.to(x.device, non_blocking=True)
+    return _GatherRows.apply(x.contiguous(), idx_d, inv_d)
+
+
+# ----------------------------------------------------------------------------------------
+# Inference similarity maps (model.py:355-368) and the materialising debug path
+# ----------------------------------------------------------------------------------------
+def _bmm_nt(a: torch.Tensor, b: torch.Tensor, alpha: torch.Tensor) -> torch.Tensor:
+    """out[i] = alpha * a[i] . b[i]^T for (B,N1,D) x (B,N2,D) bf16 via the HIP GEMM (fp32 out)."""
+    B, N1, Dd = a.shape
+    N2 = b.shape[1]
+    M, N = _rup(N1, 128), _rup(N2, 128)
+    Kd = _rup(Dd, 64)
+    out = torch.empty(B, N1, N2, dtype=torch.float32, device=a.device)
+    ap = torch.zeros(M, Kd, dtype=torch.bfloat16, device=a.device)
+    bp = torch.zeros(N, Kd, dtype=torch.bfloat16, device=a.device)
+    cp = torch.empty(M, N, dtype=torch.float32, device=a.device)
+    st = stream_ptr(a.device)
+    for i in range(B):
+        ap[:N1, :Dd].copy_(a[i])
+        bp[:N2, :Dd].copy_(b[i])
+        call("triad_gemm_bf16", ptr(ap), Kd, 1, ptr(bp), Kd, 1, M, N, Kd, ptr(alpha), ptr(cp), N, 0, st)
+        out[i].copy_(cp[:N1, :N2])
+    return out
+
+
+def similarity_maps(f1: torch.Tensor, f2: torch.Tensor, temperature: torch.Tensor) -> torch.Tensor:
+    """normalize(f1) . normalize(f2)^T * temperature per sample, (B,N1,N2) fp32 (inference)."""
+    _check_device(f1, f2)
+    if f1.dim() == 2:
+        f1 = f1.unsqueeze(0)
+    if f2.dim() == 2:
+        f2 = f2.unsqueeze(0)
+    t = temperature.detach().reshape(1).to(torch.float32).contiguous()
+    return _bmm_nt(l2_normalize(f1), l2_normalize(f2), t)
+
+
+def token_similarities(q: torch.Tensor, k: torch.Tensor, temperature: torch.Tensor) -> torch.Tensor:
+    """Materialised (Bq, Bk, Nq, Nk) token similarities (debug path for small B only)."""
+    _check_device(q, k)
+    Bq, Nq, _ = q.shape
+    Bk, Nk, _ = k.shape
+    qq = q.to(torch.bfloat16).reshape(1, Bq * Nq, D)
+    kk = k.to(torch.bfloat16).reshape(1, Bk * Nk, D)
+    t = temperature.detach().reshape(1).to(torch.float32).contiguous()
+    s = _bmm_nt(qq, kk, t)[0]
+    return s.view(Bq, Nq, Bk, Nk).permute(0, 2, 1, 3).contiguous()
+
+
+def clip_similarities(kind, q, k, temperature, q_mask=None):
+    """clip (B, B) from the fused kernel (no token tensor)."""
+    _check_device(q, k)
+    g = Geometry(q.shape[0], q.shape[1], k.shape[0], k.shape[1])
+    dev = q.device
+    st = stream_ptr(dev)
+    Qb, Kb = pack_queries(q, g), pack_keys(k, g)
+    temp = temperature.detach().reshape(1).to(torch.float32).contiguous()
+    nparts = call("triad_pairsim_nparts", g.R_pad, g.Bk)
+    rowmax = torch.empty(g.Bk, g.R_pad, dtype=torch.float32, device=dev)
+    argmax = torch.empty(g.Bk, g.R_pad, dtype=torch.int32, device=dev)
+    nn_part = torch.empty(nparts, dtype=torch.float64, device=dev)
+    call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D, ptr(temp),
+         CLAMP_LO[kind], 0, 0, ptr(rowmax), ptr(argmax), ptr(nn_part), None, st)
+    clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
+    qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
+    call("triad_clip_reduce", ptr(rowmax), g.R_pad, g.Nq, g.Bq, g.Bk, ptr(qm), ptr(clip), None, st)
+    return clip

@@ -1,0 +1,195 @@
+"""Flat-buffer fused AdamW + grad-norm / clip for the TRIAD train step.
+
+Reference semantics (SajayR/TRIAD src/train.py):
+  * four torch.optim.AdamW optimizers with defaults (betas (0.9, 0.999), eps 1e-8,
+    weight_decay 1e-2) over name-based parameter groups (train.py:251-287);
+  * OneCycleLR per optimizer (train.py:289-343) -- it also cycles beta1
+    (cycle_momentum=True), which this implementation honours per step;
+  * per-group gradient norms (train.py:992-1002) and clip_grad_norm_(..., 10.0)
+    on the audio and text embedders (train.py:1004-1006);
+  * optimizers step only once their group is unfrozen (train.py:1016-1040).
+
+MI355X design: every optimised parameter lives in ONE contiguous fp32 buffer
+(`FlatParamSpace.params`), its gradient in another (`.grads`) and the AdamW
+moments in two more; each nn.Parameter's `.data` and `.grad` are re-pointed at
+views, so autograd accumulates straight into the flat gradient buffer, the
+data-parallel all-reduce is one collective over it, and a whole optimizer step
+is one HIP launch (triad_adamw_step) after one norm launch (triad_grad_sumsq).
+Clipping is deferred into the AdamW launch as a per-parameter scale, so the
+gradients are never rewritten in HBM.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Iterable, List, Sequence
+
+import numpy as np
+import torch
+
+from ._lib import TriadError, call, ptr, stream_ptr
+
+CHUNK = 16384
+ALIGN = 64  # elements (256 B) per parameter slot
+_CHUNK_DT = np.dtype([("off", "<i8"), ("n", "<i4"), ("param", "<i4")])
+
+
+class FlatParamSpace:
+    """Owns the flat param / grad / exp_avg / exp_avg_sq buffers for a list of parameters."""
+
+    def __init__(self, params: Sequence[torch.nn.Parameter], device):
+        self.device = torch.device(device)
+        self.params: List[torch.nn.Parameter] = list(params)
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        offs, o = [], 0
+        for p in self.params:
+            offs.append(o)
+            o += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.offsets = offs
+        self.numel = max(o, ALIGN)
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.flat_p = torch.zeros(self.numel, **f32)
+        self.flat_g = torch.zeros(self.numel, **f32)
+        self.exp_avg = torch.zeros(self.numel, **f32)
+        self.exp_avg_sq = torch.zeros(self.numel, **f32)
+        self.touched = np.zeros(len(self.params), dtype=bool)
+        self.steps = np.zeros(len(self.params), dtype=np.int64)
+        self.scale = torch.ones(len(self.params), **f32)
+        self._hooks = []
+        with torch.no_grad():
+            for i, p in enumerate(self.params):
+                if p.dtype != torch.float32:
+                    raise TriadError("flat AdamW expects fp32 master parameters")
+                v = self.flat_p[offs[i]:offs[i] + p.numel()].view_as(p)
+                v.copy_(p.data)
+                p.data = v
+                p.grad = self.flat_g[offs[i]:offs[i] + p.numel()].view_as(p)
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._mark(i)))
+        self._chunk_cache: Dict[tuple, tuple] = {}
+
+    def _mark(self, i):
+        def hook(_p):
+            self.touched[i] = True
+        return hook
+
+    def param_ids(self, params: Iterable[torch.nn.Parameter]):
+        return [self.index[id(p)] for p in params if id(p) in self.index]
+
+    def chunks(self, ids: Sequence[int]):
+        """Device chunk table for the given parameter indices (cached)."""
+        key = tuple(ids)
+        hit = self._chunk_cache.get(key)
+        if hit is not None:
+            return hit
+        rows = []
+        for i in ids:
+            n = self.params[i].numel()
+            for s in range(0, n, CHUNK):
+                rows.append((self.offsets[i] + s, min(CHUNK, n - s), i))
+        arr = np.array(rows, dtype=_CHUNK_DT) if rows else np.zeros(0, dtype=_CHUNK_DT)
+        dev = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device) if rows else None
+        owner = torch.tensor([r[2] for r in rows], dtype=torch.long, device=self.device) if rows else None
+        out = (dev, len(rows), owner)
+        if len(self._chunk_cache) > 64:
+            self._chunk_cache.clear()
+        self._chunk_cache[key] = out
+        return out
+
+    def touched_ids(self, ids: Sequence[int]):
+        return [i for i in ids if self.touched[i]]
+
+    def param_sumsq(self, ids: Sequence[int]) -> torch.Tensor:
+        """Per-parameter sum of squared gradients (float64, indexed by parameter id)."""
+        out = torch.zeros(len(self.params), dtype=torch.float64, device=self.device)
+        table, n, owner = self.chunks(ids)
+        if n:
+            part = torch.empty(n, dtype=torch.float64, device=self.device)
+            call("triad_grad_sumsq", ptr(self.flat_g), ptr(table), n, ptr(part), stream_ptr(self.device))
+            out.index_add_(0, owner, part)
+        return out
+
+    def zero_grad(self, ids: Sequence[int]):
+        """Zero the gradient slots of these parameters (contiguous runs -> few memsets)."""
+        ids = sorted(ids)
+        s = 0
+        while s < len(ids):
+            e = s
+            while e + 1 < len(ids) and ids[e + 1] == ids[e] + 1:
+                e += 1
+            a = self.offsets[ids[s]]
+            b = self.offsets[ids[e]] + self.params[ids[e]].numel()
+            self.flat_g[a:b].zero_()
+            s = e + 1
+        if ids:
+            self.touched[ids] = False
+            self.scale.index_fill_(0, torch.tensor(ids, device=self.device), 1.0)
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW-compatible facade over a FlatParamSpace (one per reference optimizer),
+    so torch's LR schedulers (OneCycleLR, incl. beta1 cycling) drive it unchanged."""
+
+    def __init__(self, space: FlatParamSpace, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        params = list(params)
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.space = space
+        self.ids = space.param_ids(params)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        sp = self.space
+        ids = sp.touched_ids(self.ids)  # torch skips parameters whose .grad is None
+        if not ids:
+            return loss
+        g = self.param_groups[0]
+        lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
+        # fresh pinned block per step: the caching host allocator keeps it alive until the
+        # async H2D copy recorded on the stream has completed
+        host = torch.empty(3 * len(sp.params), dtype=torch.float32, pin_memory=sp.device.type == "cuda")
+        pp = host.numpy()
+        for i in ids:
+            sp.steps[i] += 1
+            t = int(sp.steps[i])
+            bc1 = 1.0 - b1 ** t
+            bc2 = 1.0 - b2 ** t
+            pp[3 * i] = lr / bc1
+            pp[3 * i + 1] = 1.0 / math.sqrt(bc2)
+            pp[3 * i + 2] = 1.0 - lr * wd
+        pp_dev = host.to(sp.device, non_blocking=True)
+        table, n, _ = sp.chunks(ids)
+        call("triad_adamw_step", ptr(sp.flat_p), ptr(sp.flat_g), ptr(sp.exp_avg), ptr(sp.exp_avg_sq), ptr(table), n,
+             ptr(pp_dev), ptr(sp.scale), float(b1), float(b2), float(eps), stream_ptr(sp.device))
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.space.zero_grad(self.ids)
+
+
+def grad_norms(space: FlatParamSpace, groups: Dict[str, Sequence[torch.nn.Parameter]]):
+    """{name: ||grad||_2} per group as device scalars (no host sync), train.py:992-1002."""
+    ids_all = space.touched_ids(range(len(space.params)))
+    sq = space.param_sumsq(ids_all)
+    out = {}
+    for name, params in groups.items():
+        ids = [i for i in space.param_ids(params) if space.touched[i]]
+        if ids:
+            out[name] = sq[torch.tensor(ids, device=space.device)].sum().sqrt().float()
+        else:
+            out[name] = torch.zeros((), device=space.device)
+    return out, sq
+
+
+def clip_grad_norm_(space: FlatParamSpace, params, max_norm: float, sq: torch.Tensor = None):
+    """torch.nn.utils.clip_grad_norm_ semantics (2-norm, clip_coef = max_norm/(norm+1e-6)
+    clamped to 1), applied lazily as the per-parameter scale of the next AdamW launch.
+    Returns the total norm (device scalar)."""
+    ids = [i for i in space.param_ids(params) if space.touched[i]]
+    if not ids:
+        return torch.zeros((), device=space.device)
+    if sq is None:
+        sq = space.param_sumsq(ids)
+    idx = torch.tensor(ids, device=space.device)
+    total = sq[idx].sum().sqrt().float()
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    space.scale[idx] = space.scale[idx] * coef
+    return total
