@@ -91,6 +91,9 @@ def main():
     from triad_amd.train import TriadTrainer
 
     _lib.load()
+    # MIOpen searches conv algorithms once per shape (HuBERT's conv feature encoder) instead
+    # of using its immediate-mode heuristic; the search runs in the untimed warmup.
+    torch.backends.cudnn.benchmark = True
     torch.manual_seed(1234)
     model = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.80, patch_sparsity_weight=0.01,
                             visual_dropout_prob=0.25, use_amp=True).to(dev)

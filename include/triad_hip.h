@@ -42,11 +42,15 @@ int triad_pairsim_nparts(int R_pad, int Bk);
  * rowmax[j][r] = max_k S, argmax[j][r] = first argmax, nn_part[wg] = partial
  * sum of clamp(S, clamp_lo, 0)^2 (double), diagS[i][q][k] = S on the diagonal
  * pairs (j == i + diag_off) when diag != 0 and diagS != NULL.
+ * If dS != NULL it also writes the unit l_nonneg gradient S*[clamp_lo <= S <= 0] in the
+ * tiled dS layout ([R_pad/32][CT][1024] bf16, see triad_tile_gemm) and st_part[wg] =
+ * sum S*S/temp over those entries, so the backward needs no recompute.
  * Replaces model.py:370-392 (AV) / 490-514 (TV) token_sims + max, and the
  * l_nonneg reduction of model.py:417-418 / 524-525. */
 int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
                       int Nk_eff, int D, const float* temp, float clamp_lo, int diag, int diag_off,
-                      float* rowmax, int* argmax, double* nn_part, float* diagS, hipStream_t stream);
+                      float* rowmax, int* argmax, double* nn_part, float* diagS, void* dS, long long CT,
+                      double* st_part, hipStream_t stream);
 
 /* clip[i][j] = sum_q m_iq rowmax[j][i*Nq+q] / norm_i (AV: qmask NULL, norm = Nq;
  * TV: norm = max(sum_q m_iq, 1e-7)); qw[r] = d clip / d rowmax (may be NULL).
@@ -55,14 +59,14 @@ int triad_clip_reduce(const float* rowmax, int R_pad, int Nq, int Bq, int Bk, co
                       float* qw, hipStream_t stream);
 
 /* AV temporal smoothness on the diagonal pairs: part[i] = sum_{q>=1,k} (S[q,k]-S[q-1,k])^2,
- * g = d(sum/cnt)/dS. cnt = B_global*(Nq-1)*Nk_eff. Replaces model.py:394-408. */
+ * g = d(sum/cnt)/dS, dt_part[i] = sum g*S. cnt = B_global*(Nq-1)*Nk_eff. Replaces model.py:394-408. */
 int triad_diag_smooth(const float* diagS, int Bq, int Nq, int Nk_pad, int Nk_eff, double cnt, double* part,
-                      float* g, hipStream_t stream);
+                      float* g, double* dt_part, hipStream_t stream);
 
-/* TV patch-usage sparsity on the diagonal pairs; overwrites diagS with the gradient of
- * sum/cnt, cnt = B_global*Nk_eff. Replaces model.py:527-540. */
-int triad_diag_sparsity(float* diagS_g, int Bq, int Nt, int Nk_pad, int Nk_eff, float thr, double cnt,
-                        double* part, hipStream_t stream);
+/* TV patch-usage sparsity on the diagonal pairs: part[i], g = d(sum/cnt)/dS, dt_part[i] = sum g*S;
+ * cnt = B_global*Nk_eff, Nt <= 1024. Replaces model.py:527-540. */
+int triad_diag_sparsity(const float* diagS, int Bq, int Nt, int Nk_pad, int Nk_eff, float thr, double cnt,
+                        double* part, float* g, double* dt_part, hipStream_t stream);
 
 /* B x B loss head: symmetric InfoNCE, regulariser combination and similarity
  * statistics (kind 0 = AV, 1 = TV) into out[13]; dclip = d CE / d clip.
@@ -73,18 +77,33 @@ int triad_losshead(const float* clip, int B, int kind, const float* temp, const 
                    double n_el, const double* dg_part, int n_dg, double dg_cnt, float w_sparse, float* out,
                    float* dclip, float* lse_scratch, hipStream_t stream);
 
-/* Backward of the fused head: recompute S, form
- * dS = c_ce*dclip[i][j]*qw[r]*[k==argmax] + c_nn*clamp'(S) + c_diag*dSdiag (diag pairs),
- * write it as bf16 [R_pad][ldS], and per-workgroup partials of sum(dS * S/temp).
+/* General backward of the fused head (any mix of upstream loss gradients): recompute S, form
+ * dS = c_ce*dclip[i][j]*qw[r]*[k==argmax] + c_nn*S*[lo<=S<=0] + c_diag*dSdiag (diag pairs),
+ * write it tiled (as triad_pairsim_fwd) and per-workgroup partials of sum(dS * S/temp).
  * coef = {c_ce, c_nn, c_diag, c_cal} (device). Autograd of model.py:384-428 / 502-542. */
 int triad_pairsim_dS(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
                      int Nk_eff, int D, const float* temp, float clamp_lo, int diag, int diag_off,
                      const int* argmax, const float* dclip, const float* qw, const float* dSdiag,
-                     const float* coef, void* dS, long long ldS, double* dt_part, hipStream_t stream);
+                     const float* coef, void* dS, long long CT, double* dt_part, hipStream_t stream);
 
-/* dL/dtemp = sum(parts) + coef[3] * d l_cal/d temp (has_cal, AV model.py:420-424). */
-int triad_dtemp_finalize(const double* part, int n, const float* temp, const float* coef, int has_cal,
-                         float* out, hipStream_t stream);
+/* Fast backward (only `total` differentiated): complete the forward's tiled unit l_nonneg
+ * gradient in place: += ratio_max * dclip[i][j] * qw[r] at each row's argmax key (max backward,
+ * model.py:389/507) and += ratio_diag * gdiag on the diagonal pairs. max_part[block] =
+ * sum dclip*qw*rowmax (n_max_part blocks). */
+int triad_dS_patch(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad, int Nk_eff,
+                   int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
+                   float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
+                   hipStream_t stream);
+
+/* dL/dtemp = sum_k w[k]*sum(p_k) + w[3]*d l_cal/d temp (has_cal: AV, model.py:420-424). */
+int triad_dtemp_finalize(const double* p0, int n0, const double* p1, int n1, const double* p2, int n2,
+                         const float* temp, const float* w, int has_cal, float* out, hipStream_t stream);
+
+/* dQ / dK of S = temp * Q K^T from the tiled dS (dk = 0: C = alpha * dS K, M = R_pad,
+ * nkt = C_pad/32, B = K; dk = 1: C = alpha * dS^T Q, M = CT*32, nkt = R_pad/32, B = Q);
+ * C bf16 [M][512]; splits > 1 uses fp32 slabs [splits][M][512]. */
+int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
+                    int splits, float* slabs, void* C, hipStream_t stream);
 
 /* C = alpha * op(A) . op(B): A [M][Kd] (a_kcontig=1) or [Kd][M] (0); B [N][Kd] (b_kcontig=1)
  * or [Kd][N] (0); C fp32 or bf16 (out_bf16). M, N multiples of 128, Kd of 64.

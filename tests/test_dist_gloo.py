@@ -1,0 +1,141 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the data-parallel collectives.
+
+Mode G (global negatives, triad_amd.dist + ops.contrastive_head(group=...)): each rank
+holds B_l triples; the sharded computation -- gather keys, local clip rows, gather clip
+rows, all-reduce the regulariser sums, identical loss head, reduce-scatter key grads --
+must reproduce the single-process reference loss and gradients at B_g = 2 B_l. The
+per-rank compute here is the CPU oracle (the HIP kernels need a GPU; their parity is
+tested on the box); the collectives are triad_amd.dist's.
+
+Mode R: the bucketed flat-gradient all-reduce averages gradients.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ref_cpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _global_inputs(Bg=4, Na=9, Nv=12, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    A = (torch.randn(Bg, Na, 512, generator=g) * 0.58).double()
+    V = (torch.randn(Bg, Nv, 512, generator=g) * 0.58).double()
+    V[1, 9:] = 0  # patch-dropout zero padding on one sample
+    return A, V
+
+
+def _mode_g_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from triad_amd import dist as tdist
+        A, V = _global_inputs()
+        Bg = A.shape[0]
+        Bl = Bg // world
+        Na, Nv = A.shape[1], V.shape[1]
+        A_l = A[rank * Bl:(rank + 1) * Bl].clone().requires_grad_(True)
+        V_l = V[rank * Bl:(rank + 1) * Bl].clone()
+        temp = torch.tensor(1.5, dtype=torch.float64, requires_grad=True)
+        # 1) all-gather the key tokens (rank-major rows)
+        Vg = tdist.gather_keys(V_l.reshape(Bl * Nv, 512), Bg * Nv).reshape(Bg, Nv, 512).requires_grad_(True)
+        # 2) local query rows of the similarity tensor / clip matrix
+        S = torch.einsum("iqd,jvd->ijqv", A_l, Vg) * temp            # (Bl, Bg, Na, Nv)
+        clip_l = S.max(dim=3).values.mean(dim=2)                      # (Bl, Bg)
+        nn_sum = S.clamp(-60, 0).pow(2).sum()
+        diag = torch.stack([S[i, rank * Bl + i] for i in range(Bl)])  # this rank's diagonal pairs
+        d = diag[:, 1:] - diag[:, :-1]
+        sm_sum = (d * d).sum()
+        # 3) gather clip rows, all-reduce the regulariser sums (values only; grads flow locally)
+        clip_full_val = tdist.gather_rows(clip_l.detach().contiguous())
+        sums_val = tdist.allreduce_sum(torch.stack([nn_sum.detach(), sm_sum.detach()]))
+        # splice the local rows back in so autograd sees this rank's contribution
+        clip_full = torch.cat([clip_full_val[:rank * Bl], clip_l, clip_full_val[(rank + 1) * Bl:]])
+        nn_tot = nn_sum + (sums_val[0] - nn_sum.detach())
+        sm_tot = sm_sum + (sums_val[1] - sm_sum.detach())
+        l_nn = nn_tot / (Bg * Bg * Na * Nv)
+        l_sm = sm_tot / (Bg * (Na - 1) * Nv)
+        l_cal = (-torch.log(temp)).clamp(min=0).pow(2)
+        ce = ref_cpu._symmetric_ce(clip_full)
+        total = ce + 20 * l_cal + 0.15 * l_nn + 0.01 * l_sm
+        g_cal = torch.autograd.grad(20 * l_cal, temp, retain_graph=True)[0]
+        # every rank computes the identical loss; its gradient is the full-loss gradient
+        # through this rank's tensors -> key grads are reduce-scattered, the rest summed.
+        total.backward()
+        dV_l = tdist.reduce_scatter_rows(Vg.grad.reshape(Bg * Nv, 512), Bl * Nv).reshape(Bl, Nv, 512)
+        dt = temp.grad.clone()
+        # only rank 0 keeps the (replicated) l_cal contribution when gradients are summed
+        if rank != 0:
+            dt -= g_cal
+        dt = tdist.allreduce_sum(dt.reshape(1))
+        q.put((rank, float(total), A_l.grad.numpy(), dV_l.numpy(), float(dt)))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc(), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_mode_g_global_negatives_matches_single_process():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mode_g_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r[2]
+    A, V = _global_inputs()
+    Ar, Vr = A.clone().requires_grad_(True), V.clone().requires_grad_(True)
+    t = torch.tensor(1.5, dtype=torch.float64, requires_grad=True)
+    total, *_ = ref_cpu.av_loss(Ar, Vr, t)
+    total.backward()
+    Bl = A.shape[0] // world
+    for rank, tot, dA, dV, dt in res:
+        assert abs(tot - float(total)) < 1e-9 * abs(float(total))
+        torch.testing.assert_close(torch.from_numpy(dA), Ar.grad[rank * Bl:(rank + 1) * Bl], rtol=1e-9, atol=1e-12)
+        torch.testing.assert_close(torch.from_numpy(dV), Vr.grad[rank * Bl:(rank + 1) * Bl], rtol=1e-9, atol=1e-12)
+        assert abs(dt - float(t.grad)) < 1e-9 * abs(float(t.grad)) + 1e-12
+
+
+def _mode_r_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from triad_amd import dist as tdist
+        flat = torch.arange(10, dtype=torch.float32) * (rank + 1)
+        tdist.allreduce_grads(flat, bucket_elems=3, average=True)
+        q.put((rank, flat.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_mode_r_bucketed_average():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mode_r_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for _, v in res:
+        assert v == [1.5 * i for i in range(10)]

@@ -51,7 +51,7 @@ def test_av_head_matches_golden(name):
     losses, stats, clip = ops.contrastive_head(ops.AV, A, V, t)
     losses[0].backward()
     np.testing.assert_allclose(clip.cpu().numpy(), f["clip"], rtol=1e-4, atol=1e-4)
-    lv = losses.detach().cpu().double().numpy()
+    lv = torch.stack([x.detach() for x in losses]).cpu().double().numpy()
     for got, key in zip(lv, ("total", "ce", "reg", "smooth")):
         assert _scalar_close(float(got), float(f[key])), (key, got, f[key])
     sv = stats.cpu().double().numpy()
@@ -87,8 +87,9 @@ def _rand_feats(g, shape):
     return (torch.randn(*shape, generator=g) * 0.58).to(torch.bfloat16).float()
 
 
-@pytest.mark.parametrize("B,Na,Nv,pad", [(8, 199, 256, False), (6, 199, 200, True), (16, 50, 96, True)])
-def test_av_head_vs_oracle_random(B, Na, Nv, pad):
+@pytest.mark.parametrize("B,Na,Nv,pad,mix", [(8, 199, 256, False, False), (6, 199, 200, True, False),
+                                             (16, 50, 96, True, False), (6, 40, 70, True, True)])
+def test_av_head_vs_oracle_random(B, Na, Nv, pad, mix):
     ops = _ops()
     g = torch.Generator().manual_seed(100 + B)
     A = _rand_feats(g, (B, Na, 512))
@@ -102,13 +103,15 @@ def test_av_head_vs_oracle_random(B, Na, Nv, pad):
     Ar, Vr = A.double().requires_grad_(True), V.double().requires_grad_(True)
     tr = torch.tensor(temp, dtype=torch.float64, requires_grad=True)
     total, ce, reg, sm, stats = ref_cpu.av_loss(Ar, Vr, tr)
-    total.backward()
+    # mix: a general combination of the four outputs (exercises the recompute backward)
+    obj = (0.5 * total + 1.5 * ce - 0.7 * reg + 3.0 * sm) if mix else total
+    obj.backward()
     Ag = A.to(dev, torch.bfloat16).requires_grad_(True)
     Vg = V.to(dev, torch.bfloat16).requires_grad_(True)
     tg = torch.tensor(temp, device=dev, requires_grad=True)
     losses, st, clip = ops.contrastive_head(ops.AV, Ag, Vg, tg)
-    losses[0].backward()
-    lv = losses.detach().cpu().double().numpy()
+    (0.5 * losses[0] + 1.5 * losses[1] - 0.7 * losses[2] + 3.0 * losses[3] if mix else losses[0]).backward()
+    lv = torch.stack([x.detach() for x in losses]).cpu().double().numpy()
     for got, want in zip(lv, (total, ce, reg, sm)):
         assert _scalar_close(float(got), float(want)), (got, float(want))
     _check_grad(Ag.grad, Ar.grad.numpy())
@@ -116,8 +119,8 @@ def test_av_head_vs_oracle_random(B, Na, Nv, pad):
     assert _scalar_close(float(tg.grad), float(tr.grad), 2e-3, 1e-5)
 
 
-@pytest.mark.parametrize("B,Nt,Nv", [(16, 32, 205), (12, 16, 64)])
-def test_tv_head_vs_oracle_random(B, Nt, Nv):
+@pytest.mark.parametrize("B,Nt,Nv,mix", [(16, 32, 205, False), (12, 16, 64, False), (8, 12, 40, True)])
+def test_tv_head_vs_oracle_random(B, Nt, Nv, mix):
     ops = _ops()
     g = torch.Generator().manual_seed(200 + B)
     T = _rand_feats(g, (B, Nt, 512))
@@ -127,13 +130,16 @@ def test_tv_head_vs_oracle_random(B, Nt, Nv):
     Tr, Vr = T.double().requires_grad_(True), V.double().requires_grad_(True)
     tr = torch.tensor(temp, dtype=torch.float64, requires_grad=True)
     total, stats = ref_cpu.tv_loss(Tr, Vr, mask, tr, thr, w)
-    total.backward()
+    (2.0 * total).backward() if mix else total.backward()
     Tg = T.to(dev, torch.bfloat16).requires_grad_(True)
     Vg = V.to(dev, torch.bfloat16).requires_grad_(True)
     tg = torch.tensor(temp, device=dev, requires_grad=True)
     losses, st, clip = ops.contrastive_head(ops.TV, Tg, Vg, tg, q_mask=mask.to(dev), threshold=thr,
                                             sparsity_weight=w)
-    losses[0].backward()
+    if mix:  # total = ce + reg: route the same gradient through the components (recompute backward)
+        (losses[0] + losses[1] + losses[2]).backward()
+    else:
+        losses[0].backward()
     assert _scalar_close(float(losses[0]), float(total))
     _check_grad(Tg.grad, Tr.grad.numpy())
     _check_grad(Vg.grad, Vr.grad.numpy())

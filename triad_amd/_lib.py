@@ -18,14 +18,17 @@ vp, i32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_doubl
 # name -> argtypes (restype is always int status). Keep in sync with include/triad_hip.h.
 SIGNATURES = {
     "triad_pairsim_nparts": [i32, i32],
-    "triad_pairsim_fwd": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, f32, i32, i32, vp, vp, vp, vp, vp],
+    "triad_pairsim_fwd": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, f32, i32, i32, vp, vp, vp, vp, vp,
+                          i64, vp, vp],
     "triad_clip_reduce": [vp, i32, i32, i32, i32, vp, vp, vp, vp],
-    "triad_diag_smooth": [vp, i32, i32, i32, i32, f64, vp, vp, vp],
-    "triad_diag_sparsity": [vp, i32, i32, i32, i32, f32, f64, vp, vp],
+    "triad_diag_smooth": [vp, i32, i32, i32, i32, f64, vp, vp, vp, vp],
+    "triad_diag_sparsity": [vp, i32, i32, i32, i32, f32, f64, vp, vp, vp, vp],
     "triad_losshead": [vp, i32, i32, vp, vp, i32, f64, vp, i32, f64, f32, vp, vp, vp, vp],
     "triad_pairsim_dS": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, f32, i32, i32, vp, vp, vp, vp, vp,
                          vp, i64, vp, vp],
-    "triad_dtemp_finalize": [vp, i32, vp, vp, i32, vp, vp],
+    "triad_dS_patch": [vp, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp, f32, vp, i32, vp],
+    "triad_dtemp_finalize": [vp, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp],
+    "triad_tile_gemm": [vp, i64, i32, vp, i32, i32, vp, i32, vp, vp, vp],
     "triad_gemm_bf16": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, i32, vp],
     "triad_gemm_bf16_splitk": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp],
     "triad_projhead_fwd": [vp, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, i64, vp, vp, vp, vp, vp],

@@ -1,0 +1,171 @@
+// Backward GEMMs of the fused similarity head over the TILED dS layout.
+//
+//   dQ[r][d] = alpha * sum_c dS[r][c] K[c][d]     (gradient of S = temp Q K^T w.r.t. Q)
+//   dK[c][d] = alpha * sum_r dS[r][c] Q[r][d]     (w.r.t. K)        model.py:384-387 / 502-505
+//
+// dS layout (written by pairsim_kernel straight from its MFMA accumulators): 32 x 32
+// tiles of 2 KB, tile (rt, ct) at ((rt * CT) + ct) * 1024 elements; inside a tile lane L
+// (query q = L & 31, hh = L >> 5) holds 16 bf16 at L*16 + v for keys
+// (v & 3) + 8 (v >> 2) + 4 hh -- the v_mfma_f32_32x32x16 accumulator order, stored as
+// one coalesced 2 KB write per wave.
+//
+// dQ reads a tile row-wise: lane L's 8 values v = 8s'..8s'+7 ARE the A fragment of
+// k-step s' (keys in the permuted order 16s' + 8(j>>2) + 4hh + (j&3)), so the B operand
+// K is read with the same permutation by ds_read_b64_tr_b16 (rows 16s'+4h+q and +8).
+// dK reads the same tile transposed with ds_read_b64_tr_b16 (queries on the k axis,
+// keys on the lane), no second copy of dS in HBM.
+//
+// Workgroup: 8 waves, 128 output rows x all 512 columns (A is streamed from HBM exactly
+// once); wave w owns columns [64w, 64w+64): 4 x 2 tiles of 32 x 32 accumulators. K-step
+// = one 32-deep tile; A (4 tiles, 8 KB) and B (32 rows x 512, 32 KB) double-buffered in
+// LDS via 16-byte LDS-DMA with source-side swizzles (conflict-free reads).
+// Optional split-K over grid.y with fp32 slabs.
+#include "common.h"
+
+namespace {
+
+constexpr int TBM = 128, TBN = 512, TBK = 32;
+constexpr int A_ST = 4 * 1024;           // 4 tiles
+constexpr int B_ST = TBK * TBN;          // 32 rows x 512
+constexpr int ST = A_ST + B_ST;
+
+// 16-byte chunk swizzles inside a 2 KB tile (involutions; glds writes lane-linear, the
+// source chunk is permuted instead).
+__device__ __forceinline__ int swz_q(int c) { return c ^ ((c >> 4) & 1); }          // dQ row reads
+__device__ __forceinline__ int swz_k(int c) { return c ^ (((c >> 6) & 1) << 3); }   // dK transposed reads
+// B image [32][512], 1 KB rows: chunk c of row k at c ^ ((k & 3) << 2)
+__device__ __forceinline__ int b_off(int k, int col) { return k * TBN + ((((col >> 3) ^ ((k & 3) << 2))) << 3) + (col & 7); }
+
+template <bool DK>
+__device__ __forceinline__ void stage(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ B, int mt0,
+                                      int kt, bf16* dst, int wave, int lane) {
+  {  // A: 4 tiles = 8 x 1 KB pieces, one per wave
+    const int t = wave >> 1, half = wave & 1;
+    const int pos = half * 64 + lane;
+    const int c = DK ? swz_k(pos) : swz_q(pos);
+    const long long tile = DK ? ((long long)kt * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + kt);
+    glds16(Dt + tile * 1024 + c * 8, dst + t * 1024 + half * 512);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {  // B: 32 rows of 1 KB, four per wave
+    const int k = wave * 4 + u;
+    const int c = lane ^ ((k & 3) << 2);
+    glds16(B + ((long long)kt * TBK + k) * TBN + c * 8, dst + A_ST + k * TBN);
+  }
+}
+
+// B fragment (rows = k, columns = n0 + lane&31): two 4-row transposed reads at rows r0, r0 + dr.
+__device__ __forceinline__ bf16x8 bfrag(const bf16* img, int r0, int dr, int n0, int lane) {
+  const int g = lane >> 4, i = lane & 15, p = i & 3;
+  const int col = n0 + 16 * (g & 1) + 4 * p;
+  bf16x8 r;
+  s16x4* rp = (s16x4*)&r;
+  rp[0] = lds_tr16(img + b_off(r0, col));
+  rp[1] = lds_tr16(img + b_off(r0 + dr, col));
+  return r;
+}
+
+template <bool DK, bool SLAB>
+__global__ __launch_bounds__(512, 2) void tile_gemm_kernel(const bf16* __restrict__ Dt, long long CT,
+                                                           const bf16* __restrict__ B, int M, int nkt_total,
+                                                           int kt_per_split, const float* __restrict__ alpha_p,
+                                                           void* __restrict__ Cout) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * ST];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  // XCD-aware: consecutive row panels on one XCD share the streamed B panel in that XCD's L2
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  const int m0 = swz * TBM, mt0 = m0 / 32;
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int nkt = min(kt_per_split, nkt_total - kt0);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[t][n] = (f32x16){};
+
+  if (nkt > 0) stage<DK>(Dt, CT, B, mt0, kt0, lds, wave, lane);
+  for (int it = 0; it < nkt; ++it) {
+    lds_dma_barrier();
+    if (it + 1 < nkt) stage<DK>(Dt, CT, B, mt0, kt0 + it + 1, lds + ((it + 1) & 1) * ST, wave, lane);
+    const bf16* As = lds + (it & 1) * ST;
+    const bf16* Bs = As + A_ST;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[4], bf[2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16* tile = As + t * 1024;
+        if (!DK) {
+          af[t] = *(const bf16x8*)(tile + swz_q(2 * l32 + 64 * h + s) * 8);
+        } else {
+          // queries 16s + 8h + 4tt + q4 (k axis), keys 16(g&1) + 4p4 + (0..3) on the lanes
+          const int a = 2 * (g & 1) + (p4 >> 1), hh = p4 & 1;
+          s16x4* rp = (s16x4*)&af[t];
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) {
+            const int qry = 16 * s + 8 * h + 4 * tt + q4;
+            const int c = (qry + 32 * hh) * 2 + (a >> 1);
+            rp[tt] = lds_tr16(tile + swz_k(c) * 8 + 4 * (a & 1));
+          }
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int n0 = wave * 64 + n * 32;
+        bf[n] = DK ? bfrag(Bs, 16 * s + 8 * h + q4, 4, n0, lane) : bfrag(Bs, 16 * s + 4 * h + q4, 8, n0, lane);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[t][n] = mfma32(af[t], bf[n], acc[t][n]);
+    }
+  }
+
+  const float alpha = SLAB ? 1.f : *alpha_p;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int col = wave * 64 + n * 32 + l32;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int m = m0 + t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        const float val = alpha * acc[t][n][v];
+        if (SLAB) ((float*)Cout)[((size_t)blockIdx.y * M + m) * TBN + col] = val;
+        else ((bf16*)Cout)[(size_t)m * TBN + col] = (bf16)val;
+      }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// dQ (dk = 0): M = query rows (R_pad), nkt = key tiles (C_pad / 32), B = K [C_pad][512].
+// dK (dk = 1): M = key rows (CT * 32), nkt = query tiles (R_pad / 32), B = Q [R_pad][512].
+// splits > 1: fp32 slabs [splits][M][512] in `slabs`, then C = alpha * sum (bf16).
+int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
+                    int splits, float* slabs, void* C, hipStream_t stream) {
+  if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
+  const int kps = (nkt + splits - 1) / splits;
+  dim3 grid(M / TBM, splits);
+  const bf16* d = (const bf16*)Dt;
+  const bf16* b = (const bf16*)B;
+  if (splits == 1) {
+    if (dk) hipLaunchKernelGGL((tile_gemm_kernel<true, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
+    else hipLaunchKernelGGL((tile_gemm_kernel<false, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
+    TRIAD_CHECK_LAUNCH();
+    return TRIAD_OK;
+  }
+  if (dk) hipLaunchKernelGGL((tile_gemm_kernel<true, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
+  else hipLaunchKernelGGL((tile_gemm_kernel<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
+  TRIAD_CHECK_LAUNCH();
+  return triad_sum_slabs(slabs, splits, (long long)M * TBN, alpha, 1, C, stream);
+}
+
+}  // extern "C"

@@ -48,9 +48,21 @@ struct PairArgs {
   const float* qw;     // [R] d clip / d rowmax per row (1/Nq or mask/len)
   const float* dSdiag; // [Bq][Nq][Nk_pad] unit grad of the diagonal regulariser (may be null)
   const float* coef;   // [4] c_ce, c_nn (=0.15*2*c_reg/N_el), c_diag, c_cal
-  bf16* dS;
-  long long ldS;       // C_alloc
+  bf16* dS;            // tiled dS (see bwd_gemm.hip): [R_pad/32][CT][1024]
+  long long CT;        // key tiles per row panel of dS (>= Bk*Nk_pad/32)
+  double* part2;       // fwd with dS output: per-workgroup sum of S*S_raw over lo<=S<=0
 };
+
+// Store this wave's 32x32 tile of dS (lane-contiguous accumulator order, 2 KB coalesced).
+__device__ __forceinline__ void store_tile(bf16* dS, long long CT, int rt, long long ct, int lane,
+                                           const bf16 (&v)[16]) {
+  bf16* dst = dS + ((long long)rt * CT + ct) * 1024 + lane * 16;
+  bf16x8 a, b;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { a[k] = v[k]; b[k] = v[8 + k]; }
+  *(bf16x8*)dst = a;
+  *(bf16x8*)(dst + 8) = b;
+}
 
 // Stage key tile (j, kb) into LDS buffer `dst`. Row t of the tile is one
 // wave-instruction (64 lanes x 16 B = one 1 KB key row); LDS chunk c of row t
@@ -70,7 +82,7 @@ template <int EPI>
 __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
   // All LDS in ONE array (a second __shared__ object can make hipcc drain the
   // in-flight LDS-DMA before every ds_read).
-  __shared__ __attribute__((aligned(16))) bf16 kbuf[2 * KT_ELEMS + 4 * WAVES];
+  __shared__ __attribute__((aligned(16))) bf16 kbuf[2 * KT_ELEMS + 8 * WAVES];
   double* red = (double*)(kbuf + 2 * KT_ELEMS);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -80,12 +92,19 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
   const int qi = row_ok ? row / a.Nq : -1;
   const int qq = row_ok ? row - qi * a.Nq : 0;
 
+  int koff[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) koff[k] = ((2 * k + h) ^ (ql & 15)) * 8;
+
   const int j0 = blockIdx.y * a.j_per_wg;
   const int j1 = min(a.Bk, j0 + a.j_per_wg);
   const int nkb = a.Nk_pad / 32;
   const int nblocks = (j1 - j0) * nkb;
   if (nblocks <= 0) {  // uniform across the workgroup
-    if (threadIdx.x == 0) a.part[blockIdx.y * gridDim.x + blockIdx.x] = 0.0;
+    if (threadIdx.x == 0) {
+      a.part[blockIdx.y * gridDim.x + blockIdx.x] = 0.0;
+      if (EPI == 0 && a.part2) a.part2[blockIdx.y * gridDim.x + blockIdx.x] = 0.0;
+    }
     return;
   }
 
@@ -109,7 +128,8 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
   int am = 0;
   float gmax = 0.f;
   int amax = -1;
-  double accd = 0.0;
+  double accd = 0.0, accd2 = 0.0;
+  const int rt = blockIdx.x * WAVES + wave;  // this wave's row tile of dS
 
   for (int b = 0; b < nblocks; ++b) {
     const int j = j0 + b / nkb, kb = b - (b / nkb) * nkb;
@@ -120,11 +140,12 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
                      wave, lane);
     }
     const bf16* kt = kbuf + ((b & 1) ? KT_ELEMS : 0) + ql * D;
-    const int sw = ql & 15;
     f32x16 acc = {};
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const bf16x8 af = *(const bf16x8*)(kt + (((2 * s + h) ^ sw) * 8));
+      // chunk (2s+h) ^ (key & 15): the swizzle only touches the low 4 bits, so 8 per-lane
+      // offsets + an immediate of 256 B * (s >> 3) address all 32 fragments
+      const bf16x8 af = *(const bf16x8*)(kt + koff[s & 7] + (s >> 3) * 128);
       acc = mfma32(af, qf[s], acc);
     }
 
@@ -132,7 +153,8 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
     const int key0 = kb * 32 + 4 * h;
 
     if (EPI == 0) {
-      float nn = 0.f;
+      float nn = 0.f, st = 0.f;
+      bf16 dn[16];
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int key = key0 + (v & 3) + 8 * (v >> 2);
@@ -141,10 +163,18 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
         if (ok && s > m) { m = s; am = key; }  // keys ascend with v: strict > keeps the first index
         const float c = fminf(fmaxf(s, lo), 0.f);
         nn += ok ? c * c : 0.f;
+        // unit gradient of the l_nonneg term: d/dS (clamp(S,lo,0)^2)/2 = S on [lo, 0] (inclusive)
+        const float d = (ok && s >= lo && s <= 0.f) ? s : 0.f;
+        st += d * acc[v];
+        dn[v] = (bf16)d;
         if (diag_pair && key < a.Nk_eff && a.diagS)
           a.diagS[((size_t)qi * a.Nq + qq) * a.Nk_pad + key] = s;
       }
       accd += (double)nn;
+      if (a.dS) {
+        accd2 += (double)st;
+        store_tile(a.dS, a.CT, rt, (long long)j * nkb + kb, lane, dn);
+      }
       if (kb == nkb - 1) {
         const float m2 = __shfl_xor(m, 32);
         const int am2 = __shfl_xor(am, 32);
@@ -177,23 +207,20 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
         out[v] = (bf16)g;
       }
       accd += (double)dt;
-      bf16* dst = a.dS + (size_t)row * a.ldS + (size_t)j * a.Nk_pad + key0;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        bf16x4 w4 = {out[4 * g4], out[4 * g4 + 1], out[4 * g4 + 2], out[4 * g4 + 3]};
-        *(bf16x4*)(dst + 8 * g4) = w4;
-      }
+      store_tile(a.dS, a.CT, rt, (long long)j * nkb + kb, lane, out);
     }
   }
 
-  // Workgroup partial of l_nonneg (fwd) or dL/dtemp (bwd), in double.
+  // Workgroup partials of l_nonneg (fwd) or dL/dtemp (bwd), and sum(S*S_raw) (fwd + dS), in double.
   double v = wave_sum_d(accd);
-  if (lane == 0) red[wave] = v;
+  double v2 = wave_sum_d(accd2);
+  if (lane == 0) { red[wave] = v; red[WAVES + wave] = v2; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int w = 0; w < WAVES; ++w) t += red[w];
+    double t = 0.0, t2 = 0.0;
+    for (int w = 0; w < WAVES; ++w) { t += red[w]; t2 += red[WAVES + w]; }
     a.part[blockIdx.y * gridDim.x + blockIdx.x] = t;
+    if (EPI == 0 && a.part2) a.part2[blockIdx.y * gridDim.x + blockIdx.x] = t2;
   }
 }
 
@@ -228,15 +255,17 @@ __global__ __launch_bounds__(256) void clip_reduce_kernel(const float* __restric
 
 // AV temporal smoothness on the diagonal pairs (model.py:394-408):
 //   l_smooth = sum_{i,q>=1,k} (S_ii[q,k] - S_ii[q-1,k])^2 / cnt
-// Writes part[i] = the sample's sum and g[i][q][k] = d l_smooth / d S_ii[q,k].
+// Writes part[i] = the sample's sum, g[i][q][k] = d l_smooth / d S_ii[q,k] and
+// dt_part[i] = sum g * S (for d/dtemp; S = temp * S_raw).
 __global__ __launch_bounds__(256) void diag_smooth_kernel(const float* __restrict__ dS_in, int Nq, int Nk_pad,
                                                           int Nk_eff, double inv_cnt,
-                                                          double* __restrict__ part, float* __restrict__ g) {
+                                                          double* __restrict__ part, float* __restrict__ g,
+                                                          double* __restrict__ dt_part) {
   __shared__ double red[4];
   const int i = blockIdx.x;
   const float* S = dS_in + (size_t)i * Nq * Nk_pad;
   float* G = g + (size_t)i * Nq * Nk_pad;
-  double acc = 0.0;
+  double acc = 0.0, dacc = 0.0;
   const float two_inv = (float)(2.0 * inv_cnt);
   for (int e = threadIdx.x; e < Nq * Nk_eff; e += blockDim.x) {
     const int q = e / Nk_eff, k = e - q * Nk_eff;
@@ -249,56 +278,120 @@ __global__ __launch_bounds__(256) void diag_smooth_kernel(const float* __restric
     }
     if (q + 1 < Nq) grad -= two_inv * (S[(size_t)(q + 1) * Nk_pad + k] - s);
     G[(size_t)q * Nk_pad + k] = grad;
+    dacc += (double)grad * (double)s;
   }
   const double t = block_sum_d(acc, red);
-  if (threadIdx.x == 0) part[i] = t;
+  const double dt = block_sum_d(dacc, red);
+  if (threadIdx.x == 0) { part[i] = t; dt_part[i] = dt; }
 }
 
 // TV patch-usage sparsity on the diagonal pairs (model.py:527-540):
 //   P = softmax_k S_ii[t,:];  frac[k] = sum_t P[t,k] / Nt;  loss = sum relu(frac-thr)^2 / cnt
-// Writes part[i] and g[i][t][k] = d loss / d S_ii[t,k] (in place over S_ii).
-__global__ __launch_bounds__(256) void diag_sparsity_kernel(float* __restrict__ S_g, int Nt, int Nk_pad,
+// Writes part[i], g[i][t][k] = d loss / d S_ii[t,k] and dt_part[i] = sum g * S.
+constexpr int SP_MAXT = 1024;
+__global__ __launch_bounds__(256) void diag_sparsity_kernel(const float* __restrict__ S_g, int Nt, int Nk_pad,
                                                             int Nk_eff, float thr, double inv_cnt,
-                                                            double* __restrict__ part) {
-  extern __shared__ float sh[];  // frac/g [Nk_eff]
+                                                            double* __restrict__ part, float* __restrict__ G_g,
+                                                            double* __restrict__ dt_part) {
+  extern __shared__ float sh[];  // per-column gradient wrt P [Nk_eff]
+  __shared__ float rmx[SP_MAXT], rinv[SP_MAXT];
   __shared__ double red[4];
   const int i = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  float* S = S_g + (size_t)i * Nt * Nk_pad;
-  // 1) rows -> probabilities, in place
+  const float* S = S_g + (size_t)i * Nt * Nk_pad;
+  float* G = G_g + (size_t)i * Nt * Nk_pad;
+  // 1) row softmax statistics
   for (int t = wave; t < Nt; t += nw) {
-    float* r = S + (size_t)t * Nk_pad;
+    const float* r = S + (size_t)t * Nk_pad;
     float mx = -INFINITY;
     for (int k = lane; k < Nk_eff; k += 64) mx = fmaxf(mx, r[k]);
     mx = wave_max(mx);
     float sum = 0.f;
     for (int k = lane; k < Nk_eff; k += 64) sum += __expf(r[k] - mx);
     sum = wave_sum(sum);
-    const float inv = 1.f / sum;
-    for (int k = lane; k < Nk_eff; k += 64) r[k] = __expf(r[k] - mx) * inv;
+    if (lane == 0) { rmx[t] = mx; rinv[t] = 1.f / sum; }
   }
   __syncthreads();
-  // 2) frac, excess, loss partial, per-column gradient wrt P
+  // 2) frac, excess, loss partial, per-column gradient wrt P (incl. the 1/Nt of frac)
   double acc = 0.0;
   const float scale = (float)(2.0 * inv_cnt) / (float)Nt;
   for (int k = threadIdx.x; k < Nk_eff; k += blockDim.x) {
     float f = 0.f;
-    for (int t = 0; t < Nt; ++t) f += S[(size_t)t * Nk_pad + k];
+    for (int t = 0; t < Nt; ++t) f += __expf(S[(size_t)t * Nk_pad + k] - rmx[t]) * rinv[t];
     f /= (float)Nt;
     const float ex = f - thr;
-    const float r = ex > 0.f ? ex : 0.f;
+    const float r = ex > 0.f ? ex : 0.f;   // relu'(0) = 0 as in torch
     acc += (double)r * (double)r;
     sh[k] = scale * r;
   }
   const double tot = block_sum_d(acc, red);  // includes a barrier
-  if (threadIdx.x == 0) part[i] = tot;
   // 3) softmax backward per row
+  double dacc = 0.0;
   for (int t = wave; t < Nt; t += nw) {
-    float* r = S + (size_t)t * Nk_pad;
+    const float* r = S + (size_t)t * Nk_pad;
+    float* gr = G + (size_t)t * Nk_pad;
     float dot = 0.f;
-    for (int k = lane; k < Nk_eff; k += 64) dot += r[k] * sh[k];
+    for (int k = lane; k < Nk_eff; k += 64) dot += __expf(r[k] - rmx[t]) * rinv[t] * sh[k];
     dot = wave_sum(dot);
-    for (int k = lane; k < Nk_eff; k += 64) r[k] = r[k] * (sh[k] - dot);
+    for (int k = lane; k < Nk_eff; k += 64) {
+      const float pk = __expf(r[k] - rmx[t]) * rinv[t];
+      const float gv = pk * (sh[k] - dot);
+      gr[k] = gv;
+      dacc += (double)gv * (double)r[k];
+    }
+  }
+  const double dt = block_sum_d(dacc, red);
+  if (threadIdx.x == 0) { part[i] = tot; dt_part[i] = dt; }
+}
+
+// Sparse (max) term of dS, added in place to the tiled unit l_nonneg gradient written by the
+// forward: dS[r][j*Nk_pad + argmax[j][r]] += ratio * dclip[i][j] * qw[r]  (the backward of
+// max over keys, model.py:389/507, feeding mean/masked-mean and the CE).
+// part[block] = sum dclip * qw * rowmax (-> d/dtemp of this term).
+__device__ __forceinline__ long long tile_elem(long long CT, int r, long long c) {
+  const int kl = (int)(c & 31);
+  const int lane = (r & 31) + 32 * ((kl >> 2) & 1);
+  const int v = (kl & 3) + 4 * (kl >> 3);
+  return ((long long)(r >> 5) * CT + (c >> 5)) * 1024 + lane * 16 + v;
+}
+
+__global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS, long long CT, int R, int R_pad,
+                                                           int Nq, int Bk, int Nk_pad,
+                                                           const int* __restrict__ argmax,
+                                                           const float* __restrict__ rowmax,
+                                                           const float* __restrict__ dclip,
+                                                           const float* __restrict__ qw, float ratio,
+                                                           double* __restrict__ part) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  const long long total = (long long)Bk * R;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / R), r = (int)(e - (long long)j * R);
+    const int i = r / Nq;
+    const float w = dclip[(size_t)i * Bk + j] * qw[r];
+    const int key = argmax[(size_t)j * R_pad + r];
+    bf16* p = dS + tile_elem(CT, r, (long long)j * Nk_pad + key);
+    *p = (bf16)((float)*p + ratio * w);
+    acc += (double)w * (double)rowmax[(size_t)j * R_pad + r];
+  }
+  const double t = block_sum_d(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+// Diagonal regulariser term: dS[i*Nq+q][(i+off)*Nk_pad + k] += ratio * g[i][q][k].
+__global__ __launch_bounds__(256) void dS_patch_diag_kernel(bf16* __restrict__ dS, long long CT, int Bq, int Nq,
+                                                            int Nk_pad, int Nk_eff, int diag_off,
+                                                            const float* __restrict__ g, float ratio) {
+  const long long total = (long long)Bq * Nq * Nk_eff;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(e % Nk_eff);
+    const long long iq = e / Nk_eff;
+    const int i = (int)(iq / Nq);
+    const int r = (int)iq;
+    bf16* p = dS + tile_elem(CT, r, (long long)(i + diag_off) * Nk_pad + k);
+    *p = (bf16)((float)*p + ratio * g[iq * Nk_pad + k]);
   }
 }
 
@@ -397,18 +490,27 @@ __global__ __launch_bounds__(1024) void losshead_kernel(const float* __restrict_
   }
 }
 
-// dL/dtemp = sum(dS * S_raw) + c_cal * d l_cal / d temp   (AV only has l_cal, model.py:420-424)
-__global__ void dtemp_finalize_kernel(const double* __restrict__ part, int n, const float* __restrict__ temp_p,
-                                      const float* __restrict__ coef, int has_cal, float* __restrict__ out) {
+// dL/dtemp = sum_k w[k] * sum(part_k) + w[3] * d l_cal / d temp   (AV only has l_cal, model.py:420-424)
+// fast path: parts = {sum S*S_raw (nonneg), sum dclip*qw*rowmax, sum g*S (diag)},
+//            w = {c_nn, c_ce / temp, c_diag / temp, c_cal}
+// recompute path: parts = {sum dS*S_raw}, w = {1, -, -, c_cal}
+__global__ void dtemp_finalize_kernel(const double* __restrict__ p0, int n0, const double* __restrict__ p1, int n1,
+                                      const double* __restrict__ p2, int n2, const float* __restrict__ temp_p,
+                                      const float* __restrict__ w, int has_cal, float* __restrict__ out) {
   __shared__ double red[4];
-  double s = 0.0;
-  for (int e = threadIdx.x; e < n; e += blockDim.x) s += part[e];
-  s = block_sum_d(s, red);
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int e = threadIdx.x; e < n0; e += blockDim.x) s0 += p0[e];
+  for (int e = threadIdx.x; e < n1; e += blockDim.x) s1 += p1[e];
+  for (int e = threadIdx.x; e < n2; e += blockDim.x) s2 += p2[e];
+  s0 = block_sum_d(s0, red);
+  s1 = block_sum_d(s1, red);
+  s2 = block_sum_d(s2, red);
   if (threadIdx.x == 0) {
+    double s = (double)w[0] * s0 + (n1 ? (double)w[1] * s1 : 0.0) + (n2 ? (double)w[2] * s2 : 0.0);
     if (has_cal) {
       const double t = (double)*temp_p;
       const double x = -log(t);
-      if (x >= 0.0) s += (double)coef[3] * 2.0 * x * (-1.0 / t);
+      if (x >= 0.0) s += (double)w[3] * 2.0 * x * (-1.0 / t);
     }
     out[0] = (float)s;
   }
@@ -443,13 +545,16 @@ int triad_pairsim_nparts(int R_pad, int Bk) {
 
 int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
                       int Nk_eff, int D_, const float* temp, float clamp_lo, int diag, int diag_off,
-                      float* rowmax, int* argmax, double* nn_part, float* diagS, hipStream_t stream) {
+                      float* rowmax, int* argmax, double* nn_part, float* diagS, void* dS, long long CT,
+                      double* st_part, hipStream_t stream) {
   if (int e = check_shape(R, R_pad, Nq, Bk, Nk_pad, Nk_eff, D_)) return e;
+  if (dS && (CT < (long long)Bk * (Nk_pad / 32) || !st_part)) return TRIAD_EINVAL;
   PairArgs a = {};
   a.Q = (const bf16*)Q; a.K = (const bf16*)K;
   a.R = R; a.R_pad = R_pad; a.Nq = Nq; a.Bq = Bq; a.Bk = Bk; a.Nk_pad = Nk_pad; a.Nk_eff = Nk_eff;
   a.diag = diag; a.diag_off = diag_off; a.temp = temp; a.clamp_lo = clamp_lo;
   a.rowmax = rowmax; a.argmax = argmax; a.part = nn_part; a.diagS = diagS;
+  a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part;
   int ys;
   const int xb = grid_for(R_pad, Bk, &a.j_per_wg, &ys);
   hipLaunchKernelGGL(pairsim_kernel<0>, dim3(xb, ys), dim3(512), 0, stream, a);
@@ -467,20 +572,19 @@ int triad_clip_reduce(const float* rowmax, int R_pad, int Nq, int Bq, int Bk, co
 }
 
 int triad_diag_smooth(const float* diagS, int Bq, int Nq, int Nk_pad, int Nk_eff, double cnt, double* part,
-                      float* g, hipStream_t stream) {
+                      float* g, double* dt_part, hipStream_t stream) {
   if (Bq <= 0) return TRIAD_EINVAL;
-  const double inv = cnt > 0.0 ? 1.0 / cnt : INFINITY;
   hipLaunchKernelGGL(diag_smooth_kernel, dim3(Bq), dim3(256), 0, stream, diagS, Nq, Nk_pad, Nk_eff,
-                     cnt > 0.0 ? inv : 0.0, part, g);
+                     cnt > 0.0 ? 1.0 / cnt : 0.0, part, g, dt_part);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
 
-int triad_diag_sparsity(float* diagS_g, int Bq, int Nt, int Nk_pad, int Nk_eff, float thr, double cnt,
-                        double* part, hipStream_t stream) {
-  if (Bq <= 0 || Nk_eff > 16384) return TRIAD_EINVAL;
-  hipLaunchKernelGGL(diag_sparsity_kernel, dim3(Bq), dim3(256), Nk_eff * sizeof(float), stream, diagS_g, Nt,
-                     Nk_pad, Nk_eff, thr, 1.0 / cnt, part);
+int triad_diag_sparsity(const float* diagS, int Bq, int Nt, int Nk_pad, int Nk_eff, float thr, double cnt,
+                        double* part, float* g, double* dt_part, hipStream_t stream) {
+  if (Bq <= 0 || Nk_eff > 16384 || Nt > SP_MAXT || cnt <= 0.0) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(diag_sparsity_kernel, dim3(Bq), dim3(256), Nk_eff * sizeof(float), stream, diagS, Nt,
+                     Nk_pad, Nk_eff, thr, 1.0 / cnt, part, g, dt_part);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
@@ -499,15 +603,15 @@ int triad_losshead(const float* clip, int B, int kind, const float* temp, const 
 int triad_pairsim_dS(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
                      int Nk_eff, int D_, const float* temp, float clamp_lo, int diag, int diag_off,
                      const int* argmax, const float* dclip, const float* qw, const float* dSdiag,
-                     const float* coef, void* dS, long long ldS, double* dt_part, hipStream_t stream) {
+                     const float* coef, void* dS, long long CT, double* dt_part, hipStream_t stream) {
   if (int e = check_shape(R, R_pad, Nq, Bk, Nk_pad, Nk_eff, D_)) return e;
-  if (ldS < (long long)Bk * Nk_pad || ldS % 8) return TRIAD_EINVAL;
+  if (CT < (long long)Bk * (Nk_pad / 32)) return TRIAD_EINVAL;
   PairArgs a = {};
   a.Q = (const bf16*)Q; a.K = (const bf16*)K;
   a.R = R; a.R_pad = R_pad; a.Nq = Nq; a.Bq = Bq; a.Bk = Bk; a.Nk_pad = Nk_pad; a.Nk_eff = Nk_eff;
   a.diag = diag; a.diag_off = diag_off; a.temp = temp; a.clamp_lo = clamp_lo;
   a.argmax = (int*)argmax; a.dclip = dclip; a.qw = qw; a.dSdiag = dSdiag; a.coef = coef;
-  a.dS = (bf16*)dS; a.ldS = ldS; a.part = dt_part;
+  a.dS = (bf16*)dS; a.CT = CT; a.part = dt_part;
   int ys;
   const int xb = grid_for(R_pad, Bk, &a.j_per_wg, &ys);
   hipLaunchKernelGGL(pairsim_kernel<1>, dim3(xb, ys), dim3(512), 0, stream, a);
@@ -515,9 +619,28 @@ int triad_pairsim_dS(const void* Q, const void* K, int R, int R_pad, int Nq, int
   return TRIAD_OK;
 }
 
-int triad_dtemp_finalize(const double* part, int n, const float* temp, const float* coef, int has_cal,
-                         float* out, hipStream_t stream) {
-  hipLaunchKernelGGL(dtemp_finalize_kernel, dim3(1), dim3(256), 0, stream, part, n, temp, coef, has_cal, out);
+int triad_dS_patch(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad, int Nk_eff,
+                   int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
+                   float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
+                   hipStream_t stream) {
+  if (R <= 0 || Bk <= 0 || n_max_part <= 0 || CT < (long long)Bk * (Nk_pad / 32)) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(dS_patch_max_kernel, dim3(n_max_part), dim3(256), 0, stream, (bf16*)dS, CT, R, R_pad, Nq, Bk,
+                     Nk_pad, argmax, rowmax, dclip, qw, ratio_max, max_part);
+  if (gdiag) {
+    const long long total = (long long)Bq * Nq * Nk_eff;
+    long long blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(dS_patch_diag_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (bf16*)dS, CT, Bq, Nq,
+                       Nk_pad, Nk_eff, diag_off, gdiag, ratio_diag);
+  }
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_dtemp_finalize(const double* p0, int n0, const double* p1, int n1, const double* p2, int n2,
+                         const float* temp, const float* w, int has_cal, float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(dtemp_finalize_kernel, dim3(1), dim3(256), 0, stream, p0, n0, p1, n1, p2, n2, temp, w, has_cal,
+                     out);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

@@ -30,7 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .vit import DinoVisionTransformer, apply_lora
+from .vit import DinoVisionTransformer, apply_lora, store_frozen_base_bf16
 
 warnings.filterwarnings("ignore", message=".*torch.cuda.amp.*")
 
@@ -198,19 +198,30 @@ class ViTLoRAEmbedder(nn.Module):
         self.patch_dropout_rate = dropout_prob
         self._mask_gen = torch.Generator()
         self._mask_gen.manual_seed(torch.initial_seed() % (2 ** 63))
+        self.mask_world = (1, 0)  # (W, rank): draw the global (W*B, N) mask, keep this rank's rows
+
+    def set_global_mask(self, world, rank, seed=1234):
+        """Global negatives: every rank draws the same global mask from a shared seed, so the
+        padded key length (the global max kept count) agrees without any communication."""
+        self.mask_world = (world, rank)
+        self._mask_gen.manual_seed(seed)
 
     def draw_keep_mask(self, B, N):
-        """Bernoulli(1 - drop) keep mask (model.py:282-284), drawn on the host."""
-        return torch.bernoulli(torch.full((B, N), 1.0 - self.patch_dropout_rate), generator=self._mask_gen).bool()
+        """Bernoulli(1 - drop) keep mask (model.py:282-284), drawn on the host.
+        Returns (this rank's (B, N) mask, padded output length)."""
+        W, r = self.mask_world
+        full = torch.bernoulli(torch.full((W * B, N), 1.0 - self.patch_dropout_rate), generator=self._mask_gen).bool()
+        return full[r * B:(r + 1) * B], int(full.sum(1).max())
 
     def patch_dropout(self, x, drop_rate, keep_mask=None):
         """model.py:268-308: keep tokens of each sample in order, zero-pad to the longest."""
         if not self.training or drop_rate == 0:
             return x
         B, N = x.shape[0], x.shape[1]
+        n_out = None
         if keep_mask is None:
-            keep_mask = self.draw_keep_mask(B, N)
-        return ops.patch_dropout(x, keep_mask)
+            keep_mask, n_out = self.draw_keep_mask(B, N)
+        return ops.patch_dropout(x, keep_mask, n_out)
 
     def encode_patches(self, x):
         if x.dim() == 5:
@@ -236,11 +247,20 @@ class MultiModalModel(nn.Module):
         self.audio_embedder = AudioEmbedder(embedding_dim=512, hubert_name=audio_model_name)
         self.text_embedder = TextEmbedder(embedding_dim=512, model_name=text_model_name)
         self.visual_embedder = ViTLoRAEmbedder(arch=vit_arch, embedding_dim=512, dropout_prob=visual_dropout_prob)
+        if use_amp:
+            store_frozen_base_bf16(self.visual_embedder.model)
         self.temperature = nn.Parameter(torch.tensor(temperature))
         self.patch_sparsity_threshold = patch_sparsity_threshold
         self.patch_sparsity_weight = patch_sparsity_weight
         self.use_amp = use_amp
         self.amp_dtype = torch.bfloat16
+        self.negatives_group = None  # process group for global negatives (SURVEY §8e Mode G)
+
+    def enable_global_negatives(self, group=None):
+        """Contrast every local query against the keys of all data-parallel ranks."""
+        import torch.distributed as dist
+        self.negatives_group = group if group is not None else dist.group.WORLD
+        self.visual_embedder.set_global_mask(dist.get_world_size(group), dist.get_rank(group))
 
     # ---- inference similarity maps (model.py:355-368) -------------------------------
     def compute_similarity_matrix(self, feats1, feats2):
@@ -249,13 +269,15 @@ class MultiModalModel(nn.Module):
 
     # ---- fused training heads -------------------------------------------------------
     def _av_head(self, audio_feats, visual_feats):
-        losses, stats, clip = ops.contrastive_head(ops.AV, audio_feats, visual_feats, self.temperature)
+        losses, stats, clip = ops.contrastive_head(ops.AV, audio_feats, visual_feats, self.temperature,
+                                                   group=self.negatives_group)
         return (losses[0], losses[1], losses[2], losses[3], LazyStats(_AV_KEYS, stats)), clip
 
     def _tv_head(self, text_feats, visual_feats, attention_mask):
         losses, stats, clip = ops.contrastive_head(ops.TV, text_feats, visual_feats, self.temperature,
                                                    q_mask=attention_mask, threshold=self.patch_sparsity_threshold,
-                                                   sparsity_weight=self.patch_sparsity_weight)
+                                                   sparsity_weight=self.patch_sparsity_weight,
+                                                   group=self.negatives_group)
         return (losses[0], LazyStats(_TV_KEYS, stats)), clip
 
     def compute_all_similarities_av(self, audio_feats, visual_feats):

@@ -85,13 +85,31 @@ def pack_keys(k: torch.Tensor, g: Geometry) -> torch.Tensor:
     return out
 
 
+def _gemm_splits(wgs, nkt, cus=256, max_splits=8):
+    """Split-K factor that best fills `cus` one-workgroup-per-CU slots (ties -> fewer splits)."""
+    best, best_eff = 1, 0.0
+    for sp in range(1, max_splits + 1):
+        if sp > nkt:
+            break
+        n = wgs * sp
+        eff = n / (cus * -(-n // cus))
+        if eff > best_eff + 0.02:
+            best, best_eff = sp, eff
+    return best
+
+
 class _ContrastiveHead(torch.autograd.Function):
-    """losses = [total, ce, reg, aux] (aux = 0.01*l_smooth for AV, sparsity for TV), stats[9].
+    """Outputs: total, contrastive, reg, aux (0.01*l_smooth for AV, sparsity for TV), stats[9], clip.
 
     group=None: local head (the reference loss over this process's batch).
     group=<process group>: global negatives (SURVEY §8e Mode G, triad_amd.dist): keys are
     all-gathered, this rank computes its query rows of the B_g x B_g clip matrix, and the
     loss head runs on the gathered clip on every rank (identical loss = reference at B_g).
+
+    Backward: when only `total` is differentiated (every training step) the forward has
+    already written the unit l_nonneg gradient into the tiled dS buffer, so the backward
+    only patches in the max / diagonal terms and runs the two GEMMs (no recompute of S).
+    Any other mix of upstream gradients recomputes dS (triad_pairsim_dS).
     """
 
     @staticmethod
@@ -126,24 +144,31 @@ class _ContrastiveHead(torch.autograd.Function):
         argmax = torch.empty(g.Bk, g.R_pad, dtype=torch.int32, device=dev)
         nn_part = torch.empty(nparts, dtype=torch.float64, device=dev)
         diagS = torch.empty(g.Bq, g.Nq, g.Nk_pad, dtype=torch.float32, device=dev)
+        need_grad = torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or temperature.requires_grad)
+        CT = _rup(g.C_pad // 32, 4)
+        dS = torch.empty((g.R_pad // 32) * CT * 1024, dtype=torch.bfloat16, device=dev) if need_grad else None
+        st_part = torch.empty(nparts, dtype=torch.float64, device=dev) if need_grad else None
         _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D,
-                         bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R)
+                         bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R
+                         + (2.0 * g.R_pad * g.C_pad if need_grad else 0.0))
         call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
-             ptr(temp), CLAMP_LO[kind], 1, rank * Bq, ptr(rowmax), ptr(argmax), ptr(nn_part), ptr(diagS), st)
+             ptr(temp), CLAMP_LO[kind], 1, rank * Bq, ptr(rowmax), ptr(argmax), ptr(nn_part), ptr(diagS),
+             ptr(dS), CT, ptr(st_part), st)
         clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
         qw = torch.empty(g.R, dtype=torch.float32, device=dev)
         qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
         call("triad_clip_reduce", ptr(rowmax), g.R_pad, g.Nq, g.Bq, g.Bk, ptr(qm), ptr(clip), ptr(qw), st)
         dg_part = torch.empty(g.Bq, dtype=torch.float64, device=dev)
+        dgt_part = torch.empty(g.Bq, dtype=torch.float64, device=dev)
+        gdiag = torch.empty_like(diagS)
         if kind == AV:
             cnt = float(Bg * (g.Nq - 1) * g.Nk_eff)
-            gdiag = torch.empty_like(diagS)
-            call("triad_diag_smooth", ptr(diagS), g.Bq, g.Nq, g.Nk_pad, g.Nk_eff, cnt, ptr(dg_part), ptr(gdiag), st)
+            call("triad_diag_smooth", ptr(diagS), g.Bq, g.Nq, g.Nk_pad, g.Nk_eff, cnt, ptr(dg_part), ptr(gdiag),
+                 ptr(dgt_part), st)
         else:
             cnt = float(Bg * g.Nk_eff)
             call("triad_diag_sparsity", ptr(diagS), g.Bq, g.Nq, g.Nk_pad, g.Nk_eff, float(thr), cnt,
-                 ptr(dg_part), st)
-            gdiag = diagS
+                 ptr(dg_part), ptr(gdiag), ptr(dgt_part), st)
         n_el = float(Bg) * Bg * g.Nq * g.Nk_eff
         if W == 1:
             clip_full, nn_in, n_nn, dg_in, n_dg = clip, nn_part, nparts, dg_part, g.Bq
@@ -158,63 +183,89 @@ class _ContrastiveHead(torch.autograd.Function):
              cnt, float(w_sparse), ptr(out), ptr(dclip), ptr(lse), st)
         dclip_rows = dclip[rank * Bq:(rank + 1) * Bq].contiguous() if W > 1 else dclip
 
-        ctx.save_for_backward(Qb, Kb, argmax, dclip_rows, qw, gdiag, temp)
-        ctx.geom, ctx.kind, ctx.n_el, ctx.w_sparse, ctx.nparts = g, kind, n_el, float(w_sparse), nparts
+        if need_grad:
+            ctx.save_for_backward(Qb, Kb, argmax, rowmax, dclip_rows, qw, gdiag, temp, dS, st_part, dgt_part)
+        ctx.geom, ctx.kind, ctx.n_el, ctx.w_sparse, ctx.nparts, ctx.CT = g, kind, n_el, float(w_sparse), nparts, CT
         ctx.group, ctx.W, ctx.rank, ctx.Nk = group, W, rank, Nk
         ctx.q_dtype, ctx.k_dtype, ctx.t_dtype = q.dtype, k.dtype, temperature.dtype
         losses, stats = out[:4].clone(), out[4:].clone()
         ctx.mark_non_differentiable(stats, clip_full)
         ctx.set_materialize_grads(False)
-        return losses, stats, clip_full
+        return losses[0], losses[1], losses[2], losses[3], stats, clip_full
 
     @staticmethod
-    def backward(ctx, g_losses, g_stats, g_clip):
-        if g_losses is None:
-            return None, None, None, None, None, None, None, None
-        Qb, Kb, argmax, dclip, qw, gdiag, temp = ctx.saved_tensors
-        g, kind, W, rank = ctx.geom, ctx.kind, ctx.W, ctx.rank
+    def backward(ctx, g_total, g_ce, g_reg, g_aux, g_stats, g_clip):
+        none8 = (None,) * 8
+        if g_total is None and g_ce is None and g_reg is None and g_aux is None:
+            return none8
+        Qb, Kb, argmax, rowmax, dclip, qw, gdiag, temp, dS, st_part, dgt_part = ctx.saved_tensors
+        g, kind, W, rank, CT = ctx.geom, ctx.kind, ctx.W, ctx.rank, ctx.CT
         dev = Qb.device
         st = stream_ptr(dev)
-        gl = g_losses.to(torch.float32)
-        c_ce = gl[0] + gl[1]
-        c_reg = gl[0] + gl[2]
+        f32 = torch.float32
+        zero = torch.zeros((), dtype=f32, device=dev)
+        gt_, gc_, gr_, ga_ = [zero if x is None else x.to(f32) for x in (g_total, g_ce, g_reg, g_aux)]
+        c_ce = gt_ + gc_
+        c_reg = gt_ + gr_
         c_nn = c_reg * (0.15 * 2.0 / ctx.n_el)
         if kind == AV:
-            c_diag = 0.01 * (c_reg + gl[3])   # reg = ... + 0.01*l_smooth; aux = 0.01*l_smooth
+            c_diag = 0.01 * (c_reg + ga_)   # reg = ... + 0.01*l_smooth; aux = 0.01*l_smooth
             c_cal = 20.0 * c_reg
         else:
-            c_diag = ctx.w_sparse * c_reg + gl[3]  # reg = ... + w*sparsity; aux = sparsity
+            c_diag = ctx.w_sparse * c_reg + ga_  # reg = ... + w*sparsity; aux = sparsity
             c_cal = torch.zeros_like(c_reg)
-        coef = torch.stack([c_ce, c_nn, c_diag, c_cal]).contiguous()
-        dS = torch.empty(g.R_pad, g.C_alloc, dtype=torch.bfloat16, device=dev)
-        if g.C_alloc > g.C_pad:
-            dS[:, g.C_pad:].zero_()
-        dt_part = torch.empty(ctx.nparts, dtype=torch.float64, device=dev)
-        _lib.META = dict(kind=kind, flops=0.0, recompute_flops=2.0 * g.R * g.Bk * g.Nk_eff * D)
-        call("triad_pairsim_dS", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D, ptr(temp),
-             CLAMP_LO[kind], 1, rank * g.Bq, ptr(argmax), ptr(dclip), ptr(qw), ptr(gdiag), ptr(coef), ptr(dS),
-             g.C_alloc, ptr(dt_part), st)
+        has_cal = 1 if (kind == AV and rank == 0) else 0   # the l_cal term is counted once
+        fast = g_total is not None and g_ce is None and g_reg is None and g_aux is None
+        if fast:
+            # dS = c_nn * (unit l_nonneg grad [written by the forward] + ratio_max * max term
+            #               + ratio_diag * diagonal term); the ratios are host constants here
+            ratio_max = ctx.n_el / 0.3
+            ratio_diag = (0.01 if kind == AV else ctx.w_sparse) * ctx.n_el / 0.3
+            nmp = 1024
+            max_part = torch.empty(nmp, dtype=torch.float64, device=dev)
+            call("triad_dS_patch", ptr(dS), CT, g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, rank * g.Bq,
+                 ptr(argmax), ptr(rowmax), ptr(dclip), ptr(qw), float(ratio_max), ptr(gdiag), float(ratio_diag),
+                 ptr(max_part), nmp, st)
+            alpha = (temp * c_nn).reshape(1).contiguous()
+            w = torch.stack([c_nn, c_ce / temp[0], c_diag / temp[0], c_cal]).contiguous()
+            parts = (st_part, ctx.nparts, max_part, nmp, dgt_part, g.Bq)
+        else:
+            coef = torch.stack([c_ce, c_nn, c_diag, c_cal]).contiguous()
+            dt_part = torch.empty(ctx.nparts, dtype=torch.float64, device=dev)
+            _lib.META = dict(kind=kind, flops=0.0, recompute_flops=2.0 * g.R * g.Bk * g.Nk_eff * D)
+            call("triad_pairsim_dS", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
+                 ptr(temp), CLAMP_LO[kind], 1, rank * g.Bq, ptr(argmax), ptr(dclip), ptr(qw), ptr(gdiag), ptr(coef),
+                 ptr(dS), CT, ptr(dt_part), st)
+            alpha = temp
+            w = torch.stack([torch.ones_like(c_ce), zero, zero, c_cal]).contiguous()
+            parts = (dt_part, ctx.nparts, None, 0, None, 0)
         gq = gk = gt = None
         if ctx.needs_input_grad[0]:
             dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
+            nkt = g.C_pad // 32
+            sp = _gemm_splits(g.R_pad // 128, nkt)
+            slabs = torch.empty(sp * g.R_pad * D, dtype=f32, device=dev) if sp > 1 else None
             _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dQ")
-            call("triad_gemm_bf16", ptr(dS), g.C_alloc, 1, ptr(Kb), D, 0, g.R_pad, D, g.C_alloc, ptr(temp), ptr(dQ), D,
-                 1, st)
+            call("triad_tile_gemm", ptr(dS), CT, 0, ptr(Kb), g.R_pad, nkt, ptr(alpha), sp, ptr(slabs), ptr(dQ), st)
             gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(ctx.q_dtype)
         if ctx.needs_input_grad[1]:
-            dK = torch.empty(g.C_alloc, D, dtype=torch.bfloat16, device=dev)
+            Mk = CT * 32
+            dK = torch.empty(Mk, D, dtype=torch.bfloat16, device=dev)
+            nkt = g.R_pad // 32
+            sp = _gemm_splits(Mk // 128, nkt)
+            slabs = torch.empty(sp * Mk * D, dtype=f32, device=dev) if sp > 1 else None
             _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dK")
-            call("triad_gemm_bf16", ptr(dS), g.C_alloc, 0, ptr(Qb), D, 0, g.C_alloc, D, g.R_pad, ptr(temp), ptr(dK), D,
-                 1, st)
+            call("triad_tile_gemm", ptr(dS), CT, 1, ptr(Qb), Mk, nkt, ptr(alpha), sp, ptr(slabs), ptr(dK), st)
             Nk_pad = g.Nk_pad
             if W > 1:
                 from . import dist as tdist
                 dK = tdist.reduce_scatter_rows(dK, g.Bq * Nk_pad, ctx.group)  # this rank's keys, all queries
             gk = dK[:g.Bq * Nk_pad].view(g.Bq, Nk_pad, D)[:, :ctx.Nk].to(ctx.k_dtype)
         if ctx.needs_input_grad[2]:
-            dt = torch.empty(1, dtype=torch.float32, device=dev)
-            has_cal = 1 if (kind == AV and rank == 0) else 0   # the l_cal term is counted once
-            call("triad_dtemp_finalize", ptr(dt_part), ctx.nparts, ptr(temp), ptr(coef), has_cal, ptr(dt), st)
+            dt = torch.empty(1, dtype=f32, device=dev)
+            p0, n0, p1, n1, p2, n2 = parts
+            call("triad_dtemp_finalize", ptr(p0), n0, ptr(p1), n1, ptr(p2), n2, ptr(temp), ptr(w), has_cal,
+                 ptr(dt), st)
             gt = dt.reshape(()).to(ctx.t_dtype)
         return gq, gk, gt, None, None, None, None, None
 
@@ -225,11 +276,13 @@ def contrastive_head(kind, q, k, temperature, q_mask=None, threshold=0.0, sparsi
     kind AV: q = audio feats (B,Na,512), k = visual feats (B,Nv,512) (model.py:470-472)
     kind TV: q = text feats (B,Nt,512) with q_mask (B,Nt), k = visual feats (model.py:593)
     group: process group for global negatives (every rank must pass k with the same Nv).
-    Returns (losses[4], stats[9], clip[B_g,B_g]); losses = total, contrastive, reg, aux.
+    Returns (losses, stats[9], clip[B_g,B_g]); losses = (total, contrastive, reg, aux) 0-dim tensors.
     In global mode the gradients w.r.t. q, k, temperature are this rank's share of the
     full-loss gradient: sum them over ranks (the trainer's Mode-G all-reduce does).
     """
-    return _ContrastiveHead.apply(q, k, temperature, kind, q_mask, threshold, sparsity_weight, group)
+    total, ce, reg, aux, stats, clip = _ContrastiveHead.apply(q, k, temperature, kind, q_mask, threshold,
+                                                              sparsity_weight, group)
+    return (total, ce, reg, aux), stats, clip
 
 
 def gather_rows(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
@@ -390,13 +443,16 @@ class _GatherRows(torch.autograd.Function):
         return gather_rows(g.contiguous(), inv_idx), None, None
 
 
-def dropout_indices(keep_mask: torch.Tensor):
+def dropout_indices(keep_mask: torch.Tensor, n_out: Optional[int] = None):
     """Host-side compaction plan from a (B, N) keep mask: idx[b][t] = t-th kept token of
-    sample b (-1 pads to the longest kept length), inv[b][n] = its output slot or -1."""
+    sample b (-1 pads to the longest kept length, or to n_out), inv[b][n] = its slot or -1."""
     keep = keep_mask.detach().to("cpu", torch.bool)
     B, N = keep.shape
     counts = keep.sum(1)
-    n_out = int(counts.max()) if B else 0
+    if n_out is None:
+        n_out = int(counts.max()) if B else 0
+    elif B and int(counts.max()) > n_out:
+        raise TriadError("n_out is shorter than the longest kept sample")
     pos = torch.cumsum(keep.to(torch.int32), dim=1) - 1
     inv = torch.where(keep, pos, torch.full_like(pos, -1)).to(torch.int32)
     idx = torch.full((B, max(n_out, 1)), -1, dtype=torch.int32)
@@ -405,10 +461,11 @@ def dropout_indices(keep_mask: torch.Tensor):
     return idx[:, :n_out], inv, n_out
 
 
-def patch_dropout(x: torch.Tensor, keep_mask: torch.Tensor) -> torch.Tensor:
-    """(B, N, D) -> (B, max_b kept_b, D): kept tokens in order, zero padded (model.py:282-307)."""
+def patch_dropout(x: torch.Tensor, keep_mask: torch.Tensor, n_out: Optional[int] = None) -> torch.Tensor:
+    """(B, N, D) -> (B, max_b kept_b, D): kept tokens in order, zero padded (model.py:282-307).
+    n_out overrides the padded length (global negatives pad to the global maximum)."""
     _check_device(x)
-    idx, inv, n_out = dropout_indices(keep_mask)
+    idx, inv, n_out = dropout_indices(keep_mask, n_out)
     idx_d = idx.to(x.device, non_blocking=True)
     inv_d = inv.to(x.device, non_blocking=True)
     return _GatherRows.apply(x.contiguous(), idx_d, inv_d)
@@ -472,7 +529,7 @@ def clip_similarities(kind, q, k, temperature, q_mask=None):
     argmax = torch.empty(g.Bk, g.R_pad, dtype=torch.int32, device=dev)
     nn_part = torch.empty(nparts, dtype=torch.float64, device=dev)
     call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D, ptr(temp),
-         CLAMP_LO[kind], 0, 0, ptr(rowmax), ptr(argmax), ptr(nn_part), None, st)
+         CLAMP_LO[kind], 0, 0, ptr(rowmax), ptr(argmax), ptr(nn_part), None, None, 0, None, st)
     clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
     qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
     call("triad_clip_reduce", ptr(rowmax), g.R_pad, g.Nq, g.Bq, g.Bk, ptr(qm), ptr(clip), None, st)

@@ -27,6 +27,7 @@ from typing import Dict, Optional
 import torch
 import torch.distributed as dist
 
+from . import dist as tdist
 from . import optim as fo
 
 
@@ -56,7 +57,7 @@ class TriadTrainer:
     def __init__(self, model, learning_rate=1e-4, total_updates=10000, gradient_accumulation_steps=1,
                  unfreeze_audio_step=5000, unfreeze_text_step=5000, unfreeze_vit_step=5000,
                  optimizer="fused", device="cuda", process_group=None, bucket_mb=256.0,
-                 av_weight_start=0.8, av_weight_end=0.5):
+                 av_weight_start=0.8, av_weight_end=0.5, global_negatives=False):
         self.model = model
         self.device = torch.device(device)
         self.grad_accum = gradient_accumulation_steps
@@ -66,6 +67,9 @@ class TriadTrainer:
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self.bucket_elems = int(bucket_mb * (1 << 20) / 4)
+        self.global_negatives = global_negatives and self.world > 1
+        if self.global_negatives:
+            model.enable_global_negatives(process_group)
         opt_params = self.groups["others"] + self.groups["audio"] + self.groups["text"] + self.groups["vit_lora"]
         self.kind = optimizer
         if optimizer == "fused":
@@ -114,21 +118,19 @@ class TriadTrainer:
         return av + tv
 
     def _allreduce_grads(self):
-        """Average the flat gradient buffer over data-parallel ranks (bucketed RCCL all-reduce)."""
+        """Data-parallel gradient reduction over the flat gradient buffer (bucketed RCCL
+        all-reduce). Mode R averages (replicas of the reference loss); Mode G sums (every rank
+        holds its share of the one global loss's gradient). Every rank runs the same phases, so
+        the set of parameters with gradients is identical across ranks by construction."""
         if self.world <= 1:
             return
+        avg = not self.global_negatives
         if self.space is None:
             for p in self.model.parameters():
                 if p.grad is not None:
-                    dist.all_reduce(p.grad, op=dist.ReduceOp.AVG, group=self.pg)
+                    tdist.allreduce_grads(p.grad.view(-1), p.grad.numel(), avg, self.pg)
             return
-        g = self.space.flat_g
-        for s in range(0, g.numel(), self.bucket_elems):
-            dist.all_reduce(g[s:s + self.bucket_elems], op=dist.ReduceOp.AVG, group=self.pg)
-        # a parameter that received a gradient on any rank is stepped on every rank
-        t = torch.from_numpy(self.space.touched.astype("uint8")).to(self.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.pg)
-        self.space.touched[:] = t.cpu().numpy().astype(bool)
+        tdist.allreduce_grads(self.space.flat_g, self.bucket_elems, avg, self.pg)
 
     def step(self, frames, audio, text, phase="full_joint", progress=0.0, av_keep=None, tv_keep=None,
              shared_frames=True, frames_tv=None):
