@@ -107,8 +107,13 @@ def main():
         return trainer.step(frames, audio, text, phase="full_joint", shared_frames=not a.separate_frames,
                             frames_tv=frames_tv)
 
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
+        t_w = time.perf_counter()
         out = step()
+        torch.cuda.synchronize()
+        if rank == 0:  # progress (the first step includes MIOpen's conv-algorithm search)
+            print(f"[bench] warmup step {i + 1}/{a.warmup}: {time.perf_counter() - t_w:.1f} s", file=sys.stderr,
+                  flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

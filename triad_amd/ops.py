@@ -144,7 +144,7 @@ class _ContrastiveHead(torch.autograd.Function):
         argmax = torch.empty(g.Bk, g.R_pad, dtype=torch.int32, device=dev)
         nn_part = torch.empty(nparts, dtype=torch.float64, device=dev)
         diagS = torch.empty(g.Bq, g.Nq, g.Nk_pad, dtype=torch.float32, device=dev)
-        need_grad = torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or temperature.requires_grad)
+        need_grad = any(ctx.needs_input_grad[:3])  # (forward itself runs under no_grad)
         CT = _rup(g.C_pad // 32, 4)
         dS = torch.empty((g.R_pad // 32) * CT * 1024, dtype=torch.bfloat16, device=dev) if need_grad else None
         st_part = torch.empty(nparts, dtype=torch.float64, device=dev) if need_grad else None
