@@ -67,6 +67,18 @@ def synthetic(B, rank, device):
     return frames, audio, {"input_ids": ids, "attention_mask": mask}
 
 
+def pmc_traffic(kernel_prefix, grid):
+    """HBM bytes per launch of this kernel/grid from the committed rocprofv3 PMC summary
+    (tools/pmc_summary.py: FETCH_SIZE x2 x1024 + WRITE_SIZE x1024, separate passes), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if grid is None or not os.path.exists(path):
+        return None
+    for k, v in json.load(open(path)).items():
+        if k.startswith(kernel_prefix) and k.endswith(f"@grid{grid}"):
+            return v["hbm_bytes_per_launch"]
+    return None
+
+
 def kernel_report(timers):
     rep = {}
     for name, evs in timers.items():
@@ -75,10 +87,12 @@ def kernel_report(timers):
             if meta is not None:
                 key += "[" + ("AV" if meta.get("kind") == 0 else "TV") + ("/" + meta["what"] if "what" in meta else "") + "]"
             ms = e0.elapsed_time(e1)
-            r = rep.setdefault(key, {"launches": 0, "ms": 0.0, "flops": 0.0})
+            r = rep.setdefault(key, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "grid": None})
             r["launches"] += 1
             r["ms"] += ms
             r["flops"] += (meta or {}).get("flops", 0.0)
+            r["bytes"] += (meta or {}).get("bytes", 0.0)
+            r["grid"] = (meta or {}).get("grid")
     return rep
 
 
@@ -138,7 +152,7 @@ def main():
         value = world * a.batch * a.steps / dt
         # dominant hot-path kernel: the fused AV pair-similarity forward (S = temp*A V^T, max/argmax,
         # l_nonneg; never materialised). Algorithmic FLOPs = 2*B^2*Na*Nv_eff*512 per launch.
-        fwd = rep.get("triad_pairsim_fwd[AV]", {"launches": 0, "ms": 1.0, "flops": 0.0})
+        fwd = rep.get("triad_pairsim_fwd[AV]", {"launches": 0, "ms": 1.0, "flops": 0.0, "bytes": 0.0, "grid": None})
         avg_ms = fwd["ms"] / max(1, fwd["launches"])
         achieved = (fwd["flops"] / max(1, fwd["launches"])) / (avg_ms * 1e-3) / 1e12
         head_keys = [k for k in rep if k.startswith(("triad_pairsim", "triad_gemm_bf16["))]
@@ -157,7 +171,10 @@ def main():
             "loss": loss,
             "roofline": {"kernel": "triad_pairsim_fwd[AV]", "bound": "mfma", "achieved": achieved,
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
-                         "traffic": None, "avg_ms": avg_ms},
+                         "traffic": pmc_traffic("pairsim_kernel<0>", fwd["grid"]), "avg_ms": avg_ms,
+                         "algorithmic_bytes": fwd["bytes"] / max(1, fwd["launches"]),
+                         "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+                                           "same kernel and grid; FETCH x2 gfx950 correction)"},
             "head": {"ms_per_step": head_ms, "algo_TFLOPs_per_step": head_flops / 1e12,
                      "achieved_TFLOPs": head_flops / max(head_ms, 1e-9) / 1e9,
                      "kernels": {k: {"avg_ms": v["ms"] / max(1, v["launches"]), "launches": v["launches"]}

@@ -45,12 +45,14 @@ int triad_pairsim_nparts(int R_pad, int Bk);
  * If dS != NULL it also writes the unit l_nonneg gradient S*[clamp_lo <= S <= 0] in the
  * tiled dS layout ([R_pad/32][CT][1024] bf16, see triad_tile_gemm) and st_part[wg] =
  * sum S*S/temp over those entries, so the backward needs no recompute.
- * Replaces model.py:370-392 (AV) / 490-514 (TV) token_sims + max, and the
- * l_nonneg reduction of model.py:417-418 / 524-525. */
+ * k_len (optional, forward-only: dS and diagS must be NULL): per-key-sample valid length,
+ * keys >= k_len[j] are excluded (retrieval over trimmed token lists, retrieval.py:243-244).
+ * Replaces model.py:370-392 (AV) / 490-514 (TV) token_sims + max, the
+ * l_nonneg reduction of model.py:417-418 / 524-525, and retrieval.py:106-115 / 190-198. */
 int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
                       int Nk_eff, int D, const float* temp, float clamp_lo, int diag, int diag_off,
                       float* rowmax, int* argmax, double* nn_part, float* diagS, void* dS, long long CT,
-                      double* st_part, hipStream_t stream);
+                      double* st_part, const int* k_len, hipStream_t stream);
 
 /* clip[i][j] = sum_q m_iq rowmax[j][i*Nq+q] / norm_i (AV: qmask NULL, norm = Nq;
  * TV: norm = max(sum_q m_iq, 1e-7)); qw[r] = d clip / d rowmax (may be NULL).

@@ -181,3 +181,41 @@ def loss_mix(phase, av, tv, progress=0.0, av_start=0.8, av_end=0.5):
         w = av_start - progress * (av_start - av_end)
         return w * av + (1.0 - w) * tv
     return av + tv
+
+
+# ---- 1000-way retrieval (src/retrieval.py) ---------------------------------------------
+def aggregator_a2v(a_feats, v_feats, temperature):
+    """retrieval.py:106-109 (and 190-193 for text): mean over query tokens of the max over keys,
+    similarities divided by the temperature."""
+    s = a_feats.double() @ v_feats.double().t() / temperature
+    return float(s.max(dim=1).values.mean())
+
+
+def aggregator_v2a(a_feats, v_feats, temperature):
+    """retrieval.py:111-114 (and 195-198): mean over the visual tokens of the max over audio tokens."""
+    s = a_feats.double() @ v_feats.double().t() / temperature
+    return float(s.max(dim=0).values.mean())
+
+
+def retrieval_matrices(q_list, k_list, temperature):
+    """(N x N) q->k and k->q aggregation matrices of retrieval.py:161-174 / 255-264."""
+    import numpy as np
+    n = len(q_list)
+    q2k = np.zeros((n, n))
+    k2q = np.zeros((n, n))
+    for i in range(n):
+        for j in range(n):
+            q2k[i, j] = aggregator_a2v(q_list[i], k_list[j], temperature)
+            k2q[i, j] = aggregator_v2a(q_list[j], k_list[i], temperature)
+    return q2k, k2q
+
+
+def recall_at_k(sim):
+    """retrieval.py:117-144 with a stable sort (ties resolved by index)."""
+    import numpy as np
+    ranks = []
+    for i in range(sim.shape[0]):
+        order = np.argsort(-sim[i], kind="stable")
+        ranks.append(int(np.where(order == i)[0][0]))
+    ranks = np.array(ranks)
+    return {f"r{k}": float(np.mean(ranks < k)) for k in (1, 5, 10, 20)}

@@ -148,3 +148,34 @@ def test_trainer_step_runs_and_moves_params():
     assert set(s) == {"av_pos_sim_mean", "av_pos_sim_std", "av_neg_sim_mean", "av_neg_sim_std", "av_separation",
                       "av_hardest_negative"}
     assert all(math.isfinite(v) for v in s.values())
+
+
+def test_trainer_fused_optimizer_matches_torch_adamw():
+    """Same model / batch / masks: TriadTrainer(optimizer='fused') vs 'torch' (torch.optim.AdamW +
+    clip_grad_norm_, the reference's step, train.py:990-1041) give the same parameters."""
+    from triad_amd.model import MultiModalModel
+    from triad_amd.train import TriadTrainer
+    B = 4
+    frames = torch.randn(B, 3, 224, 224, device=dev)
+    audio = torch.randn(B, 16000, device=dev) * 0.1
+    text = ["a man riding a bicycle", "a cat on a bed", "dogs", "the quick brown fox jumps"]
+    keep = [torch.rand(B, 256) < 0.75 for _ in range(4)]
+    res = []
+    for kind in ("torch", "fused"):
+        torch.manual_seed(0)
+        np.random.seed(0)
+        m = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.8, patch_sparsity_weight=0.01,
+                            visual_dropout_prob=0.25).to(dev).train()
+        tr = TriadTrainer(m, total_updates=100, unfreeze_audio_step=0, unfreeze_text_step=0, unfreeze_vit_step=0,
+                          optimizer=kind, device=dev)
+        for s in range(2):
+            tr.step(frames, audio, text, av_keep=keep[2 * s], tv_keep=keep[2 * s + 1])
+        torch.cuda.synchronize()
+        res.append({n: p.detach().float().cpu().clone() for n, p in m.named_parameters()})
+    worst = 0.0
+    for n in res[0]:
+        a, b = res[0][n], res[1][n]
+        d = float((a - b).abs().max() / (a.abs().max() + 1e-12))
+        worst = max(worst, d)
+        assert d < 1e-3, (n, d)
+    print("worst relative param difference", worst)

@@ -19,7 +19,7 @@ vp, i32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_doubl
 SIGNATURES = {
     "triad_pairsim_nparts": [i32, i32],
     "triad_pairsim_fwd": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, f32, i32, i32, vp, vp, vp, vp, vp,
-                          i64, vp, vp],
+                          i64, vp, vp, vp],
     "triad_clip_reduce": [vp, i32, i32, i32, i32, vp, vp, vp, vp],
     "triad_diag_smooth": [vp, i32, i32, i32, i32, f64, vp, vp, vp, vp],
     "triad_diag_sparsity": [vp, i32, i32, i32, i32, f32, f64, vp, vp, vp, vp],

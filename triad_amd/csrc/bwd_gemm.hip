@@ -16,17 +16,19 @@
 // keys on the lane), no second copy of dS in HBM.
 //
 // Workgroup: 8 waves, 128 output rows x all 512 columns (A is streamed from HBM exactly
-// once); wave w owns columns [64w, 64w+64): 4 x 2 tiles of 32 x 32 accumulators. K-step
-// = one 32-deep tile; A (4 tiles, 8 KB) and B (32 rows x 512, 32 KB) double-buffered in
-// LDS via 16-byte LDS-DMA with source-side swizzles (conflict-free reads).
+// once); wave w owns columns [64w, 64w+64): 4 x 2 tiles of 32 x 32 accumulators. Stage =
+// two 32-deep k tiles (32 MFMAs per wave per barrier); A (8 tiles, 16 KB) and B (64 rows x
+// 512, 64 KB) double-buffered in LDS (the full 160 KB) via 16-byte LDS-DMA with source-side
+// swizzles (conflict-free reads).
 // Optional split-K over grid.y with fp32 slabs.
 #include "common.h"
 
 namespace {
 
 constexpr int TBM = 128, TBN = 512, TBK = 32;
-constexpr int A_ST = 4 * 1024;           // 4 tiles
-constexpr int B_ST = TBK * TBN;          // 32 rows x 512
+constexpr int KPS = 2;                   // k tiles per stage
+constexpr int A_ST = KPS * 4 * 1024;     // 8 tiles
+constexpr int B_ST = KPS * TBK * TBN;    // 64 rows x 512
 constexpr int ST = A_ST + B_ST;
 
 // 16-byte chunk swizzles inside a 2 KB tile (involutions; glds writes lane-linear, the
@@ -36,21 +38,28 @@ __device__ __forceinline__ int swz_k(int c) { return c ^ (((c >> 6) & 1) << 3); 
 // B image [32][512], 1 KB rows: chunk c of row k at c ^ ((k & 3) << 2)
 __device__ __forceinline__ int b_off(int k, int col) { return k * TBN + ((((col >> 3) ^ ((k & 3) << 2))) << 3) + (col & 7); }
 
+// Stage k tiles [kt, kt + nk) (nk = 1 or 2) into `dst`: A tile (kk, t) at kk*4096 + t*1024,
+// B rows kk*32 .. at A_ST + (kk*32 + k)*512.
 template <bool DK>
 __device__ __forceinline__ void stage(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ B, int mt0,
-                                      int kt, bf16* dst, int wave, int lane) {
-  {  // A: 4 tiles = 8 x 1 KB pieces, one per wave
-    const int t = wave >> 1, half = wave & 1;
-    const int pos = half * 64 + lane;
-    const int c = DK ? swz_k(pos) : swz_q(pos);
-    const long long tile = DK ? ((long long)kt * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + kt);
-    glds16(Dt + tile * 1024 + c * 8, dst + t * 1024 + half * 512);
-  }
+                                      int kt, int nk, bf16* dst, int wave, int lane) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {  // B: 32 rows of 1 KB, four per wave
-    const int k = wave * 4 + u;
-    const int c = lane ^ ((k & 3) << 2);
-    glds16(B + ((long long)kt * TBK + k) * TBN + c * 8, dst + A_ST + k * TBN);
+  for (int kk = 0; kk < KPS; ++kk) {
+    if (kk < nk) {  // uniform
+      {  // A: 4 tiles = 8 x 1 KB pieces, one per wave
+        const int t = wave >> 1, half = wave & 1;
+        const int pos = half * 64 + lane;
+        const int c = DK ? swz_k(pos) : swz_q(pos);
+        const long long tile = DK ? ((long long)(kt + kk) * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + kt + kk);
+        glds16(Dt + tile * 1024 + c * 8, dst + kk * 4096 + t * 1024 + half * 512);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // B: 32 rows of 1 KB, four per wave
+        const int k = wave * 4 + u;
+        const int c = lane ^ ((k & 3) << 2);
+        glds16(B + ((long long)(kt + kk) * TBK + k) * TBN + c * 8, dst + A_ST + (kk * TBK + k) * TBN);
+      }
+    }
   }
 }
 
@@ -88,12 +97,19 @@ __global__ __launch_bounds__(512, 2) void tile_gemm_kernel(const bf16* __restric
 #pragma unroll
     for (int n = 0; n < 2; ++n) acc[t][n] = (f32x16){};
 
-  if (nkt > 0) stage<DK>(Dt, CT, B, mt0, kt0, lds, wave, lane);
-  for (int it = 0; it < nkt; ++it) {
+  const int nst = (nkt + KPS - 1) / KPS;
+  if (nst > 0) stage<DK>(Dt, CT, B, mt0, kt0, min(KPS, nkt), lds, wave, lane);
+  for (int it = 0; it < nst; ++it) {
     lds_dma_barrier();
-    if (it + 1 < nkt) stage<DK>(Dt, CT, B, mt0, kt0 + it + 1, lds + ((it + 1) & 1) * ST, wave, lane);
-    const bf16* As = lds + (it & 1) * ST;
-    const bf16* Bs = As + A_ST;
+    if (it + 1 < nst)
+      stage<DK>(Dt, CT, B, mt0, kt0 + (it + 1) * KPS, min(KPS, nkt - (it + 1) * KPS), lds + ((it + 1) & 1) * ST,
+                wave, lane);
+    const int nk_here = min(KPS, nkt - it * KPS);
+#pragma unroll
+    for (int kk = 0; kk < KPS; ++kk) {
+    if (kk >= nk_here) break;  // uniform: odd tail
+    const bf16* As = lds + (it & 1) * ST + kk * 4096;
+    const bf16* Bs = lds + (it & 1) * ST + A_ST + kk * TBK * TBN;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 af[4], bf[2];
@@ -124,6 +140,7 @@ __global__ __launch_bounds__(512, 2) void tile_gemm_kernel(const bf16* __restric
 #pragma unroll
         for (int n = 0; n < 2; ++n) acc[t][n] = mfma32(af[t], bf[n], acc[t][n]);
     }
+    }
   }
 
   const float alpha = SLAB ? 1.f : *alpha_p;
@@ -152,7 +169,8 @@ extern "C" {
 int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
                     int splits, float* slabs, void* C, hipStream_t stream) {
   if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
-  const int kps = (nkt + splits - 1) / splits;
+  int kps = (nkt + splits - 1) / splits;
+  kps = (kps + KPS - 1) / KPS * KPS;  // whole stages per split
   dim3 grid(M / TBM, splits);
   const bf16* d = (const bf16*)Dt;
   const bf16* b = (const bf16*)B;

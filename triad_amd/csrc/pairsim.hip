@@ -23,6 +23,13 @@
 // the row max/argmax is lane-local plus one half-wave exchange.
 #include "common.h"
 
+#include <stdlib.h>
+
+int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
+                              int Nk_eff, const float* temp, float clamp_lo, int diag, int diag_off, float* rowmax,
+                              int* argmax, double* nn_part, float* diagS, void* dS, long long CT, double* st_part,
+                              const int* k_len, int xb, int ys, int jpw, hipStream_t stream);
+
 namespace {
 
 constexpr int D = 512;
@@ -51,6 +58,7 @@ struct PairArgs {
   bf16* dS;            // tiled dS (see bwd_gemm.hip): [R_pad/32][CT][1024]
   long long CT;        // key tiles per row panel of dS (>= Bk*Nk_pad/32)
   double* part2;       // fwd with dS output: per-workgroup sum of S*S_raw over lo<=S<=0
+  const int* klen;     // optional per-key-sample valid length (forward only; retrieval)
 };
 
 // Store this wave's 32x32 tile of dS (lane-contiguous accumulator order, 2 KB coalesced).
@@ -128,6 +136,7 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
   int am = 0;
   float gmax = 0.f;
   int amax = -1;
+  int nk = a.Nk_eff;  // valid keys of the current key sample
   double accd = 0.0, accd2 = 0.0;
   const int rt = blockIdx.x * WAVES + wave;  // this wave's row tile of dS
 
@@ -151,29 +160,39 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
 
     const bool diag_pair = a.diag && row_ok && (j == qi + a.diag_off);
     const int key0 = kb * 32 + 4 * h;
+    if (kb == 0 && a.klen) nk = min(a.klen[j], a.Nk_eff);
 
     if (EPI == 0) {
       float nn = 0.f, st = 0.f;
       bf16 dn[16];
+      // nvalid: keys of this tile that take part (0 for padded query rows); most tiles are full
+      const int nvalid = row_ok ? min(32, nk - kb * 32) : 0;
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const int key = key0 + (v & 3) + 8 * (v >> 2);
+        const bool ok = 4 * h + (v & 3) + 8 * (v >> 2) < nvalid;
         const float s = acc[v] * temp;
-        const bool ok = row_ok && key < a.Nk_eff;
-        if (ok && s > m) { m = s; am = key; }  // keys ascend with v: strict > keeps the first index
-        const float c = fminf(fmaxf(s, lo), 0.f);
-        nn += ok ? c * c : 0.f;
-        // unit gradient of the l_nonneg term: d/dS (clamp(S,lo,0)^2)/2 = S on [lo, 0] (inclusive)
-        const float d = (ok && s >= lo && s <= 0.f) ? s : 0.f;
+        if (ok && s > m) { m = s; am = key0 + (v & 3) + 8 * (v >> 2); }  // keys ascend with v: first index kept
+        const float c = ok ? fminf(fmaxf(s, lo), 0.f) : 0.f;
+        nn += c * c;
+        // unit gradient of the l_nonneg term, (d/dS clamp(S,lo,0)^2)/2 = S on [lo, 0] (inclusive)
+        const float d = (ok && c == s) ? s : 0.f;
         st += d * acc[v];
         dn[v] = (bf16)d;
-        if (diag_pair && key < a.Nk_eff && a.diagS)
-          a.diagS[((size_t)qi * a.Nq + qq) * a.Nk_pad + key] = s;
       }
       accd += (double)nn;
       if (a.dS) {
         accd2 += (double)st;
         store_tile(a.dS, a.CT, rt, (long long)j * nkb + kb, lane, dn);
+      }
+      if (a.diagS && __any(diag_pair)) {  // only the key sample paired with this wave's rows
+        if (diag_pair) {
+          float* drow = a.diagS + ((size_t)qi * a.Nq + qq) * a.Nk_pad;
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const int key = key0 + (v & 3) + 8 * (v >> 2);
+            if (key < nk) drow[key] = acc[v] * temp;
+          }
+        }
       }
       if (kb == nkb - 1) {
         const float m2 = __shfl_xor(m, 32);
@@ -546,17 +565,23 @@ int triad_pairsim_nparts(int R_pad, int Bk) {
 int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
                       int Nk_eff, int D_, const float* temp, float clamp_lo, int diag, int diag_off,
                       float* rowmax, int* argmax, double* nn_part, float* diagS, void* dS, long long CT,
-                      double* st_part, hipStream_t stream) {
+                      double* st_part, const int* k_len, hipStream_t stream) {
   if (int e = check_shape(R, R_pad, Nq, Bk, Nk_pad, Nk_eff, D_)) return e;
   if (dS && (CT < (long long)Bk * (Nk_pad / 32) || !st_part)) return TRIAD_EINVAL;
+  if (k_len && (dS || diagS)) return TRIAD_EINVAL;  // per-sample key lengths: forward-only use
   PairArgs a = {};
   a.Q = (const bf16*)Q; a.K = (const bf16*)K;
   a.R = R; a.R_pad = R_pad; a.Nq = Nq; a.Bq = Bq; a.Bk = Bk; a.Nk_pad = Nk_pad; a.Nk_eff = Nk_eff;
   a.diag = diag; a.diag_off = diag_off; a.temp = temp; a.clamp_lo = clamp_lo;
   a.rowmax = rowmax; a.argmax = argmax; a.part = nn_part; a.diagS = diagS;
-  a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part;
+  a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part; a.klen = k_len;
   int ys;
   const int xb = grid_for(R_pad, Bk, &a.j_per_wg, &ys);
+  static const bool fwd2 = getenv("TRIAD_FWD_V2") != nullptr;  // experimental (pairsim_fwd.hip)
+  if (fwd2)
+    return triad_pairsim_fwd2_launch(Q, K, R, R_pad, Nq, Bq, Bk, Nk_pad, Nk_eff, temp, clamp_lo, diag, diag_off,
+                                     rowmax, argmax, nn_part, diagS, dS, CT, st_part, k_len, xb, ys, a.j_per_wg,
+                                     stream);
   hipLaunchKernelGGL(pairsim_kernel<0>, dim3(xb, ys), dim3(512), 0, stream, a);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;

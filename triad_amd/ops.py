@@ -148,12 +148,12 @@ class _ContrastiveHead(torch.autograd.Function):
         CT = _rup(g.C_pad // 32, 4)
         dS = torch.empty((g.R_pad // 32) * CT * 1024, dtype=torch.bfloat16, device=dev) if need_grad else None
         st_part = torch.empty(nparts, dtype=torch.float64, device=dev) if need_grad else None
-        _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D,
+        _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, grid=nparts * 512,
                          bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R
                          + (2.0 * g.R_pad * g.C_pad if need_grad else 0.0))
         call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
              ptr(temp), CLAMP_LO[kind], 1, rank * Bq, ptr(rowmax), ptr(argmax), ptr(nn_part), ptr(diagS),
-             ptr(dS), CT, ptr(st_part), st)
+             ptr(dS), CT, ptr(st_part), None, st)
         clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
         qw = torch.empty(g.R, dtype=torch.float32, device=dev)
         qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
@@ -529,7 +529,7 @@ def clip_similarities(kind, q, k, temperature, q_mask=None):
     argmax = torch.empty(g.Bk, g.R_pad, dtype=torch.int32, device=dev)
     nn_part = torch.empty(nparts, dtype=torch.float64, device=dev)
     call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D, ptr(temp),
-         CLAMP_LO[kind], 0, 0, ptr(rowmax), ptr(argmax), ptr(nn_part), None, None, 0, None, st)
+         CLAMP_LO[kind], 0, 0, ptr(rowmax), ptr(argmax), ptr(nn_part), None, None, 0, None, None, st)
     clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
     qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
     call("triad_clip_reduce", ptr(rowmax), g.R_pad, g.Nq, g.Bq, g.Bk, ptr(qm), ptr(clip), None, st)
