@@ -29,7 +29,10 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "tri-modal triples/sec (whole node) + loss parity, B=256 at 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 TRACKED = ("triad_pairsim_fwd", "triad_pairsim_dS", "triad_gemm_bf16", "triad_projhead_fwd",
-           "triad_gemm_bf16_splitk")
+           "triad_gemm_bf16_splitk", "triad_tile_gemm", "triad_dS_patch", "triad_clip_reduce", "triad_losshead",
+           "triad_diag_smooth", "triad_diag_sparsity", "triad_dtemp_finalize", "triad_ln_bwd",
+           "triad_colsum_partials", "triad_sum_slabs", "triad_gather_rows", "triad_global_znorm",
+           "triad_grad_sumsq", "triad_adamw_step")
 
 
 def parse():
@@ -131,6 +134,10 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    if os.environ.get("TRIAD_PROFILE_MARK"):  # marker launch for tools/trace_summary.py (never in a step)
+        from triad_amd import ops
+        ops.l2_normalize(torch.ones(64, 512, device=dev, dtype=torch.bfloat16))
+        torch.cuda.synchronize()
     _lib.TIMERS = {k: [] for k in TRACKED}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -155,7 +162,7 @@ def main():
         fwd = rep.get("triad_pairsim_fwd[AV]", {"launches": 0, "ms": 1.0, "flops": 0.0, "bytes": 0.0, "grid": None})
         avg_ms = fwd["ms"] / max(1, fwd["launches"])
         achieved = (fwd["flops"] / max(1, fwd["launches"])) / (avg_ms * 1e-3) / 1e12
-        head_keys = [k for k in rep if k.startswith(("triad_pairsim", "triad_gemm_bf16["))]
+        head_keys = list(rep)  # every hand-written kernel of the hot path (heads fwd+bwd, optimizer)
         head_ms = sum(rep[k]["ms"] for k in head_keys) / a.steps
         head_flops = sum(rep[k]["flops"] for k in head_keys) / a.steps
         res = {
@@ -171,7 +178,8 @@ def main():
             "loss": loss,
             "roofline": {"kernel": "triad_pairsim_fwd[AV]", "bound": "mfma", "achieved": achieved,
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
-                         "traffic": pmc_traffic("pairsim_kernel<0>", fwd["grid"]), "avg_ms": avg_ms,
+                         "traffic": pmc_traffic("pairsim_kernel<0>" if os.environ.get("TRIAD_FWD_V1")
+                                                else "pairsim_fwd2_kernel<true>", fwd["grid"]), "avg_ms": avg_ms,
                          "algorithmic_bytes": fwd["bytes"] / max(1, fwd["launches"]),
                          "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                                            "same kernel and grid; FETCH x2 gfx950 correction)"},

@@ -20,6 +20,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("TRIAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", os.path.join(ROOT, "include"),
          "-Wno-unused-result"]
+# per-file extras: the pipelined forward wants scalar f32 VALU beside its MFMAs (SLP-packed
+# v_pk_mul_f32 + operand moves cost more issue slots than two v_mul_f32 there)
+EXTRA = {"pairsim_fwd.hip": ["-fno-slp-vectorize"]}
 
 
 def sources():
@@ -33,7 +36,7 @@ def _compile(src, save_temps=False):
     if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps if os.path.exists(d)) \
             and not save_temps:
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *EXTRA.get(os.path.basename(src), []), "-c", src, "-o", obj]
     if save_temps:
         cmd += ["-save-temps=obj"]
     r = subprocess.run(cmd, capture_output=True, text=True, cwd=OBJ)

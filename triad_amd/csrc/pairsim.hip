@@ -577,8 +577,10 @@ int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, in
   a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part; a.klen = k_len;
   int ys;
   const int xb = grid_for(R_pad, Bk, &a.j_per_wg, &ys);
-  static const bool fwd2 = getenv("TRIAD_FWD_V2") != nullptr;  // experimental (pairsim_fwd.hip)
-  if (fwd2)
+  // pipelined forward (pairsim_fwd.hip) unless TRIAD_FWD_V1 is set or K exceeds its 32-bit
+  // buffer offsets; pairsim_kernel<0> below is the serialised-epilogue original
+  static const bool v1 = getenv("TRIAD_FWD_V1") != nullptr;
+  if (!v1 && (unsigned long long)Bk * Nk_pad * 512 * 2 < (1ull << 31))
     return triad_pairsim_fwd2_launch(Q, K, R, R_pad, Nq, Bq, Bk, Nk_pad, Nk_eff, temp, clamp_lo, diag, diag_off,
                                      rowmax, argmax, nn_part, diagS, dS, CT, st_part, k_len, xb, ys, a.j_per_wg,
                                      stream);

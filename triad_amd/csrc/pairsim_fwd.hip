@@ -1,107 +1,111 @@
-// Forward of the fused similarity head, one wave per SIMD ("64 query rows per wave").
+// Forward of the fused similarity head with the epilogue software-pipelined into the MFMA chain.
 //
 // Same contract as pairsim_kernel<0> (pairsim.hip; SajayR/TRIAD model.py:370-392 / 490-514 /
 // 417-418 / 524-525): rowmax / argmax per (key sample, query row), l_nonneg partial sums,
-// diagonal S, and (training) the unit l_nonneg gradient written in the tiled dS layout.
+// diagonal S (diag_sim_kernel below), and (training) the unit l_nonneg gradient written in the
+// tiled dS layout.
 //
-// Structure (gfx950, 256-thread workgroup = 4 waves = one per SIMD, 512 VGPRs each):
-//  * each wave keeps the bf16 fragments of 64 query rows x 512 features in VGPRs
-//    (2 x 128 registers) for the whole launch: every key fragment read from LDS feeds two
-//    v_mfma_f32_32x32x16_bf16 (halving LDS traffic per MFMA vs 32 rows per wave);
+// Structure (gfx950): 512-thread workgroup = 8 waves x 32 query rows (two waves per SIMD);
+// each wave keeps its rows' bf16 fragments (32 x 512 = 128 VGPRs) for the whole launch.
 //  * key tiles (32 keys x 512 x bf16 = 32 KB) stream through a 3-slot LDS ring by 16-byte
-//    LDS-DMA issued two tiles ahead; one counted `s_waitcnt vmcnt(8)` + raw s_barrier per tile
-//    (the DMA of the next tile stays in flight across it);
-//  * the epilogue of tile b-1 (scale, max/argmax, clamp^2, unit dS, stores) is software-
-//    pipelined against the MFMA chain of tile b in one basic block, so its VALU work issues
-//    in the MFMA shadows instead of after them.
+//    buffer LDS-DMA issued two tiles ahead; one counted `s_waitcnt vmcnt(N)` + s_barrier per
+//    tile (the next tile's DMA stays in flight across it);
+//  * the epilogue of tile b-1 (scale, max/argmax, clamp^2, unit dS, bf16 pack) is carried by
+//    tile b's 32-step MFMA chain, one element per two k-steps, so its VALU issues in the MFMA
+//    shadows (pairsim_kernel<0> runs it after the chain, serialised with it).
 #include "common.h"
+
+#include <type_traits>
 
 namespace {
 
 constexpr int D = 512;
-constexpr int NS = D / 16;
-constexpr int WAVES = 4;
-constexpr int ROWS_PER_WG = 64 * WAVES;  // 256, as pairsim_kernel
+constexpr int NS = D / 16;  // 32 k-steps
+constexpr int WAVES = 8;
+constexpr int ROWS_PER_WG = 32 * WAVES;  // 256, as pairsim_kernel (same grid / partial arrays)
 constexpr int KT_ELEMS = 32 * D;
 constexpr int NBUF = 3;
-constexpr int GLDS_PER_TILE = 32 / WAVES;  // wave-instructions per wave per key tile (8)
+constexpr int GLDS_PER_TILE = 32 / WAVES;  // 1-KB LDS-DMA pieces per wave per key tile (4)
 
 struct FwdArgs {
   const bf16* Q;
   const bf16* K;
   int R, R_pad, Nq, Bq, Bk, Nk_pad, Nk_eff, j_per_wg;
-  int diag, diag_off;
   const float* temp;
   float clamp_lo;
   float* rowmax;
   int* argmax;
   double* part;
-  float* diagS;
   bf16* dS;
   long long CT;
   double* part2;
   const int* klen;
 };
 
-__device__ __forceinline__ void stage_tile(const FwdArgs& a, bf16* dst, int j, int kb, int wave, int lane) {
+// One key tile (32 rows x 1 KB) into an LDS slot: 1-KB buffer LDS-DMA pieces, the row offset
+// in soffset (uniform), the source-side swizzle chunk ^ (row & 15) in voffset.
+__device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t kr, const FwdArgs& a, bf16* dst, int j, int kb,
+                                           int wave, int lane) {
+  const unsigned row0 = (unsigned)(j * a.Nk_pad + kb * 32 + wave * GLDS_PER_TILE);
+  asm volatile("" : "+v"(lane));  // recompute the lane offsets here, do not keep them live
 #pragma unroll
   for (int u = 0; u < GLDS_PER_TILE; ++u) {
     const int t = wave * GLDS_PER_TILE + u;
-    const bf16* src = a.K + ((size_t)j * a.Nk_pad + kb * 32 + t) * D + ((lane ^ (t & 15)) * 8);
-    glds16(src, dst + t * D);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (__attribute__((address_space(3))) void*)(dst + t * D), 16,
+                                             (unsigned)((lane ^ (t & 15)) * 16), (row0 + u) * (D * 2), 0, 0);
   }
 }
 
-struct RowState {
-  int row, qi, qq;
-  bool ok;
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {  // one v_cvt_pk_bf16_f32
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
+}
+
+struct Epi {  // per-lane epilogue state (one 32-row block)
   float m;
   int am;
+  int lim;  // valid keys of the tile being finished, minus 4h
+  float nn, st;
+  float prev;  // previous element's unit dS (pairs into one bf16x2)
+  unsigned pk[8];
 };
 
-// one 32x32 tile epilogue (branch-free math): running max/argmax, l_nonneg sum, sum of S*S_raw,
-// and (training) the unit dS tile, packed to bf16 pairs and stored at once (short live range)
-__device__ __forceinline__ void tile_epi(const f32x16& acc, RowState& rs, int nvalid, int key0, int h, float temp,
-                                         float lo, float& nn, float& st, bf16* dst) {
-  unsigned pk[8];
-#pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    const bool ok = 4 * h + (v & 3) + 8 * (v >> 2) < nvalid;
-    const float s = acc[v] * temp;
-    const bool better = ok && s > rs.m;  // keys ascend with v: strict > keeps the first index
-    rs.m = better ? s : rs.m;
-    rs.am = better ? key0 + (v & 3) + 8 * (v >> 2) : rs.am;
-    const float c = ok ? fminf(fmaxf(s, lo), 0.f) : 0.f;
-    nn += c * c;
-    const float d = (ok && c == s) ? s : 0.f;  // S on [lo, 0]: unit grad of the l_nonneg term
-    st += d * acc[v];
-    const bf16 db = (bf16)d;
-    const unsigned u = (unsigned)__builtin_bit_cast(unsigned short, db);
-    pk[v >> 1] = (v & 1) ? (pk[v >> 1] | (u << 16)) : u;
-  }
-  if (dst) {
-    *(uint4*)dst = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-    *(uint4*)(dst + 8) = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+// key offset of accumulator element v inside a 32-key tile, without the 4h lane part
+__device__ __forceinline__ constexpr int vkey(int v) { return (v & 3) + 8 * (v >> 2); }
+
+template <bool TRAIN>
+__device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, float temp, float lo, int& kbase) {
+  // opaque per element: keeps hipcc from precomputing all 16 compare masks / key indices at
+  // the top of the tile (32 SGPRs + 16 VGPRs live across the chain)
+  asm volatile("" : "+v"(e.lim), "+v"(kbase));
+  const float raw = p[v];
+  const float s = raw * temp;
+  const bool better = vkey(v) < e.lim && s > e.m;  // keys ascend with v: strict > keeps the first
+  e.m = better ? s : e.m;
+  e.am = better ? (kbase | vkey(v)) : e.am;  // kbase = 32 kb + 4h: bit 2 only, vkey never sets it
+  // padded keys / rows are zero vectors (s = 0): they add nothing below without a mask
+  const float c = __builtin_amdgcn_fmed3f(s, lo, 0.f);
+  e.nn = fmaf(c, c, e.nn);
+  if constexpr (TRAIN) {
+    const float d = (c == s) ? s : 0.f;  // S on [lo, 0]: unit grad of the l_nonneg term
+    e.st = fmaf(d, raw, e.st);
+    if (v & 1) e.pk[v >> 1] = pack_bf16x2(e.prev, d);
+    else e.prev = d;
   }
 }
 
-__global__ __launch_bounds__(256, 1) void pairsim_fwd2_kernel(FwdArgs a) {
+template <bool TRAIN>
+__global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 kbuf[NBUF * KT_ELEMS + 16 * WAVES];
   double* red = (double*)(kbuf + NBUF * KT_ELEMS);
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
-  RowState rs[2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x) {
-    rs[x].row = blockIdx.x * ROWS_PER_WG + wave * 64 + x * 32 + ql;
-    rs[x].ok = rs[x].row < a.R;
-    rs[x].qi = rs[x].ok ? rs[x].row / a.Nq : -1;
-    rs[x].qq = rs[x].ok ? rs[x].row - rs[x].qi * a.Nq : 0;
-    rs[x].m = -INFINITY;
-    rs[x].am = 0;
-  }
-  const int rt0 = (blockIdx.x * ROWS_PER_WG + wave * 64) / 32;
+  const int row = blockIdx.x * ROWS_PER_WG + wave * 32 + ql;
+  const bool rok = row < a.R;
+  const int rt = (blockIdx.x * ROWS_PER_WG + wave * 32) / 32;
 
   const int j0 = blockIdx.y * a.j_per_wg;
   const int j1 = min(a.Bk, j0 + a.j_per_wg);
@@ -115,135 +119,126 @@ __global__ __launch_bounds__(256, 1) void pairsim_fwd2_kernel(FwdArgs a) {
     return;
   }
 
+  // K through a buffer descriptor (32-bit offsets; the host guarantees < 2 GB)
+  const __amdgpu_buffer_rsrc_t kr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.K, 0, (int)((unsigned)a.Bk * a.Nk_pad * (D * 2)), 0x00020000);
   // prologue: two tiles in flight
-  stage_tile(a, kbuf, j0, 0, wave, lane);
-  if (nblocks > 1) stage_tile(a, kbuf + KT_ELEMS, j0 + 1 / nkb, 1 % nkb, wave, lane);
+  stage_tile(kr, a, kbuf, j0, 0, wave, lane);
+  if (nblocks > 1) stage_tile(kr, a, kbuf + KT_ELEMS, j0 + 1 / nkb, 1 % nkb, wave, lane);
 
-  // query fragments live in AGPRs (the MFMA reads srcB from the AccVGPR file), leaving the
-  // 256 architectural VGPRs to accumulators, key fragments and the epilogue
-  bf16x8 qf0[NS], qf1[NS];
+  bf16x8 qf[NS];
   {
-    const bf16* q0 = a.Q + (size_t)rs[0].row * D + 8 * h;
-    const bf16* q1 = a.Q + (size_t)rs[1].row * D + 8 * h;
+    const bf16* q0 = a.Q + (size_t)row * D + 8 * h;  // rows < R_pad: zero tail, in the allocation
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const bf16x8 t0 = *(const bf16x8*)(q0 + 16 * s);
-      const bf16x8 t1 = *(const bf16x8*)(q1 + 16 * s);
-      asm volatile("; q0 -> agpr" : "=a"(qf0[s]) : "0"(t0));
-      asm volatile("; q1 -> agpr" : "=a"(qf1[s]) : "0"(t1));
-    }
+    for (int s = 0; s < NS; ++s) qf[s] = *(const bf16x8*)(q0 + 16 * s);
   }
-  int koff[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) koff[k] = ((2 * k + h) ^ (ql & 15)) * 8;
   const float temp = *a.temp;
   const float lo = a.clamp_lo;
   double accd = 0.0, accd2 = 0.0;
-  int nk = a.Nk_eff;  // valid keys of the sample whose tile is being finished
 
-  f32x16 cA0, cA1, cB0, cB1;
+  Epi e;
+  e.m = -INFINITY;
+  e.am = 0;
 
-  // MFMA chain of tile b into (c0, c1) from ring slot b % NBUF
-  auto chain = [&](int b, f32x16& c0, f32x16& c1) {
-    const bf16* kt = kbuf + (b % NBUF) * KT_ELEMS + ql * D;
-    c0 = (f32x16){};
-    c1 = (f32x16){};
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const bf16x8 af = *(const bf16x8*)(kt + koff[s & 7] + (s >> 3) * 128);
-      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c0) : "v"(af), "a"(qf0[s]));
-      asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c1) : "v"(af), "a"(qf1[s]));
-    }
-    // the compiler's hazard recognizer does not see through inline asm: cover the
-    // MFMA-result -> VALU-read wait states before anyone reads (c0, c1)
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(c0), "+v"(c1));
-  };
-
-  // epilogue of tile b from (p0, p1)
-  auto finish = [&](int b, const f32x16& p0, const f32x16& p1) {
-    const int j = j0 + b / nkb, kb = b - (b / nkb) * nkb;
-    if (kb == 0 && a.klen) nk = min(a.klen[j], a.Nk_eff);
-    const int key0 = kb * 32 + 4 * h;
-    float nn = 0.f, st = 0.f;
-    const int nv0 = rs[0].ok ? min(32, nk - kb * 32) : 0;
-    const int nv1 = rs[1].ok ? min(32, nk - kb * 32) : 0;
-    const long long ct = (long long)j * nkb + kb;
-    bf16* d0 = a.dS ? a.dS + ((long long)rt0 * a.CT + ct) * 1024 + lane * 16 : nullptr;
-    bf16* d1 = a.dS ? d0 + a.CT * 1024 : nullptr;
-    tile_epi(p0, rs[0], nv0, key0, h, temp, lo, nn, st, d0);
-    tile_epi(p1, rs[1], nv1, key0, h, temp, lo, nn, st, d1);
-    accd += (double)nn;
-    accd2 += (double)st;
-    if (a.diagS) {
-#pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        const bool dp = a.diag && rs[x].ok && (j == rs[x].qi + a.diag_off);
-        if (__any(dp)) {
-          if (dp) {
-            const f32x16& p = x ? p1 : p0;
-            float* drow = a.diagS + ((size_t)rs[x].qi * a.Nq + rs[x].qq) * a.Nk_pad;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-              const int key = key0 + (v & 3) + 8 * (v >> 2);
-              if (key < nk) drow[key] = p[v] * temp;
-            }
-          }
-        }
-      }
-    }
-    if (kb == nkb - 1) {
-#pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        float m = rs[x].m;
-        int am = rs[x].am;
-        const float m2 = __shfl_xor(m, 32);
-        const int am2 = __shfl_xor(am, 32);
-        if (m2 > m || (m2 == m && am2 < am)) { m = m2; am = am2; }
-        if (h == 0) {
-          a.rowmax[(size_t)j * a.R_pad + rs[x].row] = m;
-          a.argmax[(size_t)j * a.R_pad + rs[x].row] = am;
-        }
-        rs[x].m = -INFINITY;
-        rs[x].am = 0;
-      }
-    }
-  };
+  f32x16 cA, cB;
 
   auto sync_tile = [&](int b) {
-    // tile b was issued two iterations ago; only tile b+1's 8 DMAs may still be outstanding
-    if (b + 1 < nblocks) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // VMEM ops younger than tile b's DMA, at least: tile b+1's 4 pieces (if any) and, in
+    // training, one epilogue's 2 dS stores (b >= 2); vmcnt counts both, in issue order
+    const bool more = b + 1 < nblocks;
+    if (TRAIN && b >= 2) {
+      if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
   };
-  auto prefetch = [&](int b) {  // tile b + 2 into the slot read by tile b - 1 (all waves are past it)
+  auto prefetch = [&](int b) {  // tile b+2 into the slot tile b-1 used (every wave is past it)
     const int b2 = b + 2;
-    if (b2 < nblocks) stage_tile(a, kbuf + (b2 % NBUF) * KT_ELEMS, j0 + b2 / nkb, b2 % nkb, wave, lane);
+    if (b2 < nblocks) stage_tile(kr, a, kbuf + (b2 % NBUF) * KT_ELEMS, j0 + b2 / nkb, b2 % nkb, wave, lane);
   };
 
-  // b = 0: chain only
-  sync_tile(0);
-  chain(0, cA0, cA1);
-  prefetch(0);
-  int b = 1;
-  for (; b + 1 < nblocks; b += 2) {
-    sync_tile(b);
-    chain(b, cB0, cB1);
-    finish(b - 1, cA0, cA1);
-    prefetch(b);
-    sync_tile(b + 1);
-    chain(b + 1, cA0, cA1);
-    finish(b, cB0, cB1);
-    prefetch(b + 1);
+  // per-tile epilogue setup for tile pb (uniform scalars) -> e.lim, returns kbase
+  auto epi_begin = [&](int pb) {
+    const int j = j0 + pb / nkb, kb = pb - (pb / nkb) * nkb;
+    const int nk = a.klen ? min(a.klen[j], a.Nk_eff) : a.Nk_eff;
+    e.lim = rok ? min(32, nk - kb * 32) - 4 * h : -64;
+    e.nn = 0.f;
+    e.st = 0.f;
+    return kb * 32 + 4 * h;
+  };
+  auto epi_end = [&](int pb) {
+    const int j = j0 + pb / nkb, kb = pb - (pb / nkb) * nkb;
+    accd += (double)e.nn;
+    if (TRAIN) {
+      accd2 += (double)e.st;
+      bf16* d = a.dS + ((long long)rt * a.CT + (long long)j * nkb + kb) * 1024 + lane * 16;
+      *(uint4*)d = make_uint4(e.pk[0], e.pk[1], e.pk[2], e.pk[3]);
+      *(uint4*)(d + 8) = make_uint4(e.pk[4], e.pk[5], e.pk[6], e.pk[7]);
+    }
+    if (kb == nkb - 1) {  // end of a key sample: combine the half-waves' max / argmax
+      float m = e.m;
+      int am = e.am;
+      const float m2 = __shfl_xor(m, 32);
+      const int am2 = __shfl_xor(am, 32);
+      if (m2 > m || (m2 == m && am2 < am)) { m = m2; am = am2; }
+      if (h == 0 && rok) {
+        a.rowmax[(size_t)j * a.R_pad + row] = m;
+        a.argmax[(size_t)j * a.R_pad + row] = am;
+      }
+      e.m = -INFINITY;
+      e.am = 0;
+    }
+  };
+
+  // one tile iteration: chain of tile b into c (CH) with the epilogue of tile b-1 from p (EP),
+  // one element per two k-steps
+  auto iter = [&](auto CH, auto EP, int b, f32x16& c, const f32x16& p) {
+    constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value;
+    int kbase = 0;
+    if constexpr (ep) kbase = epi_begin(b - 1);
+    if constexpr (ch) {
+      sync_tile(b);
+      prefetch(b);
+      int lq = ql;
+      asm volatile("" : "+v"(lq));  // per-tile address math (short live ranges)
+      const bf16* kt = kbuf + (b % NBUF) * KT_ELEMS + lq * D;
+      bf16x8 af[3];
+      af[0] = *(const bf16x8*)(kt + ((h ^ (lq & 15)) * 8));
+      af[1] = *(const bf16x8*)(kt + (((2 + h) ^ (lq & 15)) * 8));
+      c = (f32x16){};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (s + 2 < NS) {
+          const int k = (s + 2) & 7;
+          af[(s + 2) % 3] = *(const bf16x8*)(kt + (((2 * k + h) ^ (lq & 15)) * 8) + ((s + 2) >> 3) * 128);
+        }
+        c = mfma32(af[s % 3], qf[s], c);
+        if constexpr (ep) {
+          if (s & 1) epi_elem<TRAIN>(e, p, s >> 1, temp, lo, kbase);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (ep) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) epi_elem<TRAIN>(e, p, v, temp, lo, kbase);
+    }
+    if constexpr (ep) epi_end(b - 1);
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+
+  // chain(b) accumulates into c while the epilogue of b-1 reads p; p = c after each chain
+  iter(T{}, F{}, 0, cA, cB);
+  cB = cA;
+  for (int b = 1; b < nblocks; ++b) {
+    iter(T{}, T{}, b, cA, cB);
+    cB = cA;
   }
-  if (b < nblocks) {  // odd count: one more chain, then its predecessor's epilogue
-    sync_tile(b);
-    chain(b, cB0, cB1);
-    finish(b - 1, cA0, cA1);
-    prefetch(b);
-    finish(b, cB0, cB1);
-  } else {
-    finish(b - 1, cA0, cA1);
-  }
+  iter(F{}, T{}, nblocks, cA, cB);
 
   double v = wave_sum_d(accd);
   double v2 = wave_sum_d(accd2);
@@ -258,20 +253,62 @@ __global__ __launch_bounds__(256, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   }
 }
 
+// Diagonal blocks of S for the regularisers (model.py:417-418 / 524-525):
+// diagS[i][q][k] = temp * <Q[i*Nq + q], K[(i + diag_off)*Nk_pad + k]>, k < Nk_eff.
+// 1/B of the forward's FLOPs, kept out of the streaming kernel: grid (query blocks of 32,
+// samples), 4 waves striding over 32-key tiles; query fragments in registers, key fragments
+// straight from global (L2-resident), query-on-row orientation so each accumulator
+// register stores 32 consecutive keys (128 B) per row.
+__global__ __launch_bounds__(256) void diag_sim_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K, int Nq,
+                                                       int Nk_pad, int Nk_eff, int diag_off,
+                                                       const float* __restrict__ temp_p, float* __restrict__ diagS) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int i = blockIdx.y, q0 = blockIdx.x * 32;
+  const int qa = min(q0 + l32, Nq - 1);  // clamp: rows past Nq are computed, never stored
+  const bf16* qrow = Q + ((size_t)i * Nq + qa) * D + 8 * h;
+  bf16x8 qf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) qf[s] = *(const bf16x8*)(qrow + 16 * s);
+  const float temp = *temp_p;
+  const int ntiles = (Nk_eff + 31) / 32;
+  const size_t kbase = (size_t)(i + diag_off) * Nk_pad;
+  for (int kt = wave; kt < ntiles; kt += 4) {  // 4 waves (256 threads)
+    const bf16* krow = K + (kbase + kt * 32 + l32) * D + 8 * h;  // rows < Nk_pad: in the allocation
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc = mfma32(qf[s], *(const bf16x8*)(krow + 16 * s), acc);
+    const int key = kt * 32 + l32;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int q = q0 + (v & 3) + 8 * (v >> 2) + 4 * h;
+      if (q < Nq && key < Nk_eff) diagS[((size_t)i * Nq + q) * Nk_pad + key] = acc[v] * temp;
+    }
+  }
+}
+
 }  // namespace
 
 // Same grid decomposition as pairsim_kernel (triad_pairsim_nparts), so partial arrays match.
+// The diagonal S (diagS != null) comes from diag_sim_kernel, launched after on the same stream.
 int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
                               int Nk_eff, const float* temp, float clamp_lo, int diag, int diag_off, float* rowmax,
                               int* argmax, double* nn_part, float* diagS, void* dS, long long CT, double* st_part,
                               const int* k_len, int xb, int ys, int jpw, hipStream_t stream) {
+  if ((unsigned long long)Bk * Nk_pad * D * 2 >= (1ull << 31)) return TRIAD_EINVAL;  // 32-bit buffer offsets
   FwdArgs a = {};
   a.Q = (const bf16*)Q; a.K = (const bf16*)K;
   a.R = R; a.R_pad = R_pad; a.Nq = Nq; a.Bq = Bq; a.Bk = Bk; a.Nk_pad = Nk_pad; a.Nk_eff = Nk_eff;
-  a.j_per_wg = jpw; a.diag = diag; a.diag_off = diag_off; a.temp = temp; a.clamp_lo = clamp_lo;
-  a.rowmax = rowmax; a.argmax = argmax; a.part = nn_part; a.diagS = diagS;
+  a.j_per_wg = jpw; a.temp = temp; a.clamp_lo = clamp_lo;
+  a.rowmax = rowmax; a.argmax = argmax; a.part = nn_part;
   a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part; a.klen = k_len;
-  hipLaunchKernelGGL(pairsim_fwd2_kernel, dim3(xb, ys), dim3(256), 0, stream, a);
+  if (dS) hipLaunchKernelGGL(pairsim_fwd2_kernel<true>, dim3(xb, ys), dim3(512), 0, stream, a);
+  else hipLaunchKernelGGL(pairsim_fwd2_kernel<false>, dim3(xb, ys), dim3(512), 0, stream, a);
   TRIAD_CHECK_LAUNCH();
+  if (diagS && diag) {
+    hipLaunchKernelGGL(diag_sim_kernel, dim3((Nq + 31) / 32, Bq), dim3(256), 0, stream, (const bf16*)Q,
+                       (const bf16*)K, Nq, Nk_pad, Nk_eff, diag_off, temp, diagS);
+    TRIAD_CHECK_LAUNCH();
+  }
   return TRIAD_OK;
 }

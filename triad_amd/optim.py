@@ -164,6 +164,58 @@ class FusedAdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = False):
         self.space.zero_grad(self.ids)
 
+    # torch.optim.AdamW's state_dict format, so reference checkpoints (train.py:412-415,
+    # 460-463) load here and ours load into torch: per-parameter {"step" (CPU f32 tensor),
+    # "exp_avg", "exp_avg_sq"} keyed by position, one param group with AdamW's keys.
+    def state_dict(self):
+        sp = self.space
+        state = {}
+        for k, i in enumerate(self.ids):
+            if sp.steps[i] > 0:
+                p, o = sp.params[i], sp.offsets[i]
+                n = p.numel()
+                state[k] = {"step": torch.tensor(float(sp.steps[i])),
+                            "exp_avg": sp.exp_avg[o:o + n].view_as(p).clone(),
+                            "exp_avg_sq": sp.exp_avg_sq[o:o + n].view_as(p).clone()}
+        groups = []
+        for g in self.param_groups:
+            d = dict(_ADAMW_GROUP_DEFAULTS)
+            d.update({k: v for k, v in g.items() if k != "params"})
+            d["params"] = list(range(len(self.ids)))
+            groups.append(d)
+        return {"state": state, "param_groups": groups}
+
+    @torch.no_grad()
+    def load_state_dict(self, sd):
+        groups = sd["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(self.ids):
+            raise ValueError("optimizer state does not match this parameter group")
+        for k, v in groups[0].items():
+            if k != "params" and k in self.param_groups[0] or k in ("initial_lr", "max_lr", "min_lr",
+                                                                     "max_momentum", "base_momentum"):
+                self.param_groups[0][k] = tuple(v) if k == "betas" else v
+        sp = self.space
+        for k, i in enumerate(self.ids):
+            st = sd["state"].get(k, sd["state"].get(str(k)))
+            o, p = sp.offsets[i], sp.params[i]
+            n = p.numel()
+            if st is None:
+                sp.steps[i] = 0
+                sp.exp_avg[o:o + n].zero_()
+                sp.exp_avg_sq[o:o + n].zero_()
+                continue
+            sp.steps[i] = int(float(st["step"]))
+            sp.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1).to(sp.exp_avg))
+            sp.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1).to(sp.exp_avg_sq))
+
+
+def _adamw_group_defaults():
+    d = torch.optim.AdamW([torch.zeros(1, requires_grad=True)]).param_groups[0]
+    return {k: v for k, v in d.items() if k != "params"}
+
+
+_ADAMW_GROUP_DEFAULTS = _adamw_group_defaults()
+
 
 def grad_norms(space: FlatParamSpace, groups: Dict[str, Sequence[torch.nn.Parameter]]):
     """{name: ||grad||_2} per group as device scalars (no host sync), train.py:992-1002."""
