@@ -64,8 +64,8 @@ __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {  // one v_
 
 struct Epi {  // per-lane epilogue state (one 32-row block)
   float m;
-  int am;
-  int lim;  // valid keys of the tile being finished, minus 4h
+  int am;   // argmax within the sample, without the 4h lane part (added at the sample's end)
+  int lim;  // masked tiles: valid keys of the tile minus 4h
   float nn, st;
   float prev;  // previous element's unit dS (pairs into one bf16x2)
   unsigned pk[8];
@@ -74,17 +74,17 @@ struct Epi {  // per-lane epilogue state (one 32-row block)
 // key offset of accumulator element v inside a 32-key tile, without the 4h lane part
 __device__ __forceinline__ constexpr int vkey(int v) { return (v & 3) + 8 * (v >> 2); }
 
-template <bool TRAIN>
-__device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, float temp, float lo, int& kbase) {
-  // opaque per element: keeps hipcc from precomputing all 16 compare masks / key indices at
-  // the top of the tile (32 SGPRs + 16 VGPRs live across the chain)
-  asm volatile("" : "+v"(e.lim), "+v"(kbase));
+// One element of a tile's epilogue (~9 VALU). FULL: every key of the tile is valid (no mask;
+// padded query rows are zero vectors, S = 0, and add nothing). key = 32 kb + vkey(v), uniform.
+template <bool TRAIN, bool FULL>
+__device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, float temp, float lo, int key) {
+  if constexpr (!FULL) asm volatile("" : "+v"(e.lim));  // keep the 16 masks from being hoisted
   const float raw = p[v];
   const float s = raw * temp;
-  const bool better = vkey(v) < e.lim && s > e.m;  // keys ascend with v: strict > keeps the first
-  e.m = better ? s : e.m;
-  e.am = better ? (kbase | vkey(v)) : e.am;  // kbase = 32 kb + 4h: bit 2 only, vkey never sets it
-  // padded keys / rows are zero vectors (s = 0): they add nothing below without a mask
+  const bool better = (FULL || vkey(v) < e.lim) && s > e.m;  // keys ascend with v: strict >
+  e.m = better ? s : e.m;                                     // keeps the first index
+  e.am = better ? key : e.am;
+  // padded keys are zero vectors (s = 0): they add nothing below without a mask
   const float c = __builtin_amdgcn_fmed3f(s, lo, 0.f);
   e.nn = fmaf(c, c, e.nn);
   if constexpr (TRAIN) {
@@ -94,6 +94,15 @@ __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, float t
     else e.prev = d;
   }
 }
+
+struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in the walk
+  int j, kb;
+  __device__ __forceinline__ void next(int nkb) {  // readfirstlane: provably uniform (SGPRs)
+    const int k1 = kb + 1 == nkb ? 0 : kb + 1;
+    j = __builtin_amdgcn_readfirstlane(k1 == 0 ? j + 1 : j);
+    kb = __builtin_amdgcn_readfirstlane(k1);
+  }
+};
 
 template <bool TRAIN>
 __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
@@ -122,9 +131,17 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   // K through a buffer descriptor (32-bit offsets; the host guarantees < 2 GB)
   const __amdgpu_buffer_rsrc_t kr =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.K, 0, (int)((unsigned)a.Bk * a.Nk_pad * (D * 2)), 0x00020000);
+  // walk cursors: prefetch (tile b+2), chain (tile b), epilogue (tile b-1); ring slots
+  Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
+  int fslot = 0, cslot = 0;
+  auto prefetch = [&](int b2) {
+    if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j, fc.kb, wave, lane);
+    fc.next(nkb);
+    fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
+  };
   // prologue: two tiles in flight
-  stage_tile(kr, a, kbuf, j0, 0, wave, lane);
-  if (nblocks > 1) stage_tile(kr, a, kbuf + KT_ELEMS, j0 + 1 / nkb, 1 % nkb, wave, lane);
+  prefetch(0);
+  prefetch(1);
 
   bf16x8 qf[NS];
   {
@@ -135,6 +152,12 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   const float temp = *a.temp;
   const float lo = a.clamp_lo;
   double accd = 0.0, accd2 = 0.0;
+  // lane part of the swizzled LDS fragment offsets (bytes), k-step s reads chunk 2(s&7)+h
+  int xo[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) xo[k] = ql * (D * 2) + (((2 * k + h) ^ (ql & 15)) * 16);
+  // this wave's dS row block (TRAIN): tile (rt, ct) at (rt*CT + ct)*1024 elements
+  bf16* const dS_w = TRAIN ? a.dS + (long long)rt * a.CT * 1024 : nullptr;
 
   Epi e;
   e.m = -INFINITY;
@@ -156,89 +179,84 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  auto prefetch = [&](int b) {  // tile b+2 into the slot tile b-1 used (every wave is past it)
-    const int b2 = b + 2;
-    if (b2 < nblocks) stage_tile(kr, a, kbuf + (b2 % NBUF) * KT_ELEMS, j0 + b2 / nkb, b2 % nkb, wave, lane);
-  };
 
-  // per-tile epilogue setup for tile pb (uniform scalars) -> e.lim, returns kbase
-  auto epi_begin = [&](int pb) {
-    const int j = j0 + pb / nkb, kb = pb - (pb / nkb) * nkb;
-    const int nk = a.klen ? min(a.klen[j], a.Nk_eff) : a.Nk_eff;
-    e.lim = rok ? min(32, nk - kb * 32) - 4 * h : -64;
-    e.nn = 0.f;
-    e.st = 0.f;
-    return kb * 32 + 4 * h;
-  };
-  auto epi_end = [&](int pb) {
-    const int j = j0 + pb / nkb, kb = pb - (pb / nkb) * nkb;
+  auto epi_end = [&]() {
     accd += (double)e.nn;
     if (TRAIN) {
       accd2 += (double)e.st;
-      bf16* d = a.dS + ((long long)rt * a.CT + (long long)j * nkb + kb) * 1024 + lane * 16;
+      bf16* d = dS_w + ((long long)ec.j * nkb + ec.kb) * 1024 + lane * 16;
       *(uint4*)d = make_uint4(e.pk[0], e.pk[1], e.pk[2], e.pk[3]);
       *(uint4*)(d + 8) = make_uint4(e.pk[4], e.pk[5], e.pk[6], e.pk[7]);
     }
-    if (kb == nkb - 1) {  // end of a key sample: combine the half-waves' max / argmax
+    if (ec.kb == nkb - 1) {  // end of a key sample: combine the half-waves' max / argmax
       float m = e.m;
-      int am = e.am;
+      int am = e.am + 4 * h;
       const float m2 = __shfl_xor(m, 32);
       const int am2 = __shfl_xor(am, 32);
       if (m2 > m || (m2 == m && am2 < am)) { m = m2; am = am2; }
       if (h == 0 && rok) {
-        a.rowmax[(size_t)j * a.R_pad + row] = m;
-        a.argmax[(size_t)j * a.R_pad + row] = am;
+        a.rowmax[(size_t)ec.j * a.R_pad + row] = m;
+        a.argmax[(size_t)ec.j * a.R_pad + row] = am;
       }
       e.m = -INFINITY;
       e.am = 0;
     }
+    ec.next(nkb);
   };
 
-  // one tile iteration: chain of tile b into c (CH) with the epilogue of tile b-1 from p (EP),
-  // one element per two k-steps
-  auto iter = [&](auto CH, auto EP, int b, f32x16& c, const f32x16& p) {
-    constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value;
-    int kbase = 0;
-    if constexpr (ep) kbase = epi_begin(b - 1);
+  // one tile iteration: chain of tile b into c (CH) with the epilogue of tile b-1 from p (EP,
+  // FULL or masked), one element per two k-steps
+  auto iter = [&](auto CH, auto EP, auto FULLT, int b, f32x16& c, const f32x16& p) {
+    constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value, full = decltype(FULLT)::value;
+    const int kbase = ec.kb * 32;
     if constexpr (ch) {
       sync_tile(b);
-      prefetch(b);
-      int lq = ql;
-      asm volatile("" : "+v"(lq));  // per-tile address math (short live ranges)
-      const bf16* kt = kbuf + (b % NBUF) * KT_ELEMS + lq * D;
+      prefetch(b + 2);
+      const char* kt = (const char*)kbuf + cslot * (KT_ELEMS * 2);
+      cslot = __builtin_amdgcn_readfirstlane(cslot == NBUF - 1 ? 0 : cslot + 1);
       bf16x8 af[3];
-      af[0] = *(const bf16x8*)(kt + ((h ^ (lq & 15)) * 8));
-      af[1] = *(const bf16x8*)(kt + (((2 + h) ^ (lq & 15)) * 8));
+      af[0] = *(const bf16x8*)(kt + xo[0]);
+      af[1] = *(const bf16x8*)(kt + xo[1]);
       c = (f32x16){};
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        if (s + 2 < NS) {
-          const int k = (s + 2) & 7;
-          af[(s + 2) % 3] = *(const bf16x8*)(kt + (((2 * k + h) ^ (lq & 15)) * 8) + ((s + 2) >> 3) * 128);
-        }
+        if (s + 2 < NS) af[(s + 2) % 3] = *(const bf16x8*)(kt + xo[(s + 2) & 7] + ((s + 2) >> 3) * 256);
         c = mfma32(af[s % 3], qf[s], c);
         if constexpr (ep) {
-          if (s & 1) epi_elem<TRAIN>(e, p, s >> 1, temp, lo, kbase);
+          if (s & 1) epi_elem<TRAIN, full>(e, p, s >> 1, temp, lo, kbase + vkey(s >> 1));
         }
-        __builtin_amdgcn_sched_barrier(0);
+        // scheduling regions of 4 k-steps: two epilogue elements interleave and fill each
+        // other's VALU->SGPR-mask wait states
+        if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     } else if constexpr (ep) {
 #pragma unroll
-      for (int v = 0; v < 16; ++v) epi_elem<TRAIN>(e, p, v, temp, lo, kbase);
+      for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full>(e, p, v, temp, lo, kbase + vkey(v));
     }
-    if constexpr (ep) epi_end(b - 1);
+    if constexpr (ep) epi_end();
   };
   using T = std::true_type;
   using F = std::false_type;
+  // epilogue variant of tile ec: FULL unless its sample's valid keys end inside it
+  auto tile_full = [&]() {
+    const int nk = a.klen ? min(a.klen[ec.j], a.Nk_eff) : a.Nk_eff;
+    const int nv = __builtin_amdgcn_readfirstlane(nk - ec.kb * 32);
+    e.nn = 0.f;
+    e.st = 0.f;
+    e.lim = (rok ? min(32, nv) : 0) - 4 * h;
+    return nv >= 32;
+  };
 
-  // chain(b) accumulates into c while the epilogue of b-1 reads p; p = c after each chain
-  iter(T{}, F{}, 0, cA, cB);
+  // chain(b) accumulates into cA while the epilogue of b-1 reads cB; cB = cA after each chain
+  iter(T{}, F{}, T{}, 0, cA, cB);
   cB = cA;
   for (int b = 1; b < nblocks; ++b) {
-    iter(T{}, T{}, b, cA, cB);
+    if (tile_full()) iter(T{}, T{}, T{}, b, cA, cB);
+    else iter(T{}, T{}, F{}, b, cA, cB);
     cB = cA;
   }
-  iter(F{}, T{}, nblocks, cA, cB);
+  if (tile_full()) iter(F{}, T{}, T{}, nblocks, cA, cB);
+  else iter(F{}, T{}, F{}, nblocks, cA, cB);
 
   double v = wave_sum_d(accd);
   double v2 = wave_sum_d(accd2);
