@@ -153,6 +153,7 @@ def test_trainer_step_runs_and_moves_params():
 def test_trainer_fused_optimizer_matches_torch_adamw():
     """Same model / batch / masks: TriadTrainer(optimizer='fused') vs 'torch' (torch.optim.AdamW +
     clip_grad_norm_, the reference's step, train.py:990-1041) give the same parameters."""
+    from triad_amd import checkpoint as ck
     from triad_amd.model import MultiModalModel
     from triad_amd.train import TriadTrainer
     B = 4
@@ -177,7 +178,10 @@ def test_trainer_fused_optimizer_matches_torch_adamw():
             tr.step(frames, audio, text, av_keep=keep[2 * s], tv_keep=keep[2 * s + 1])
         torch.cuda.synchronize()
         lr_sum.append(tot)
-        res.append({n: p.detach().float().cpu().clone() for n, p in m.named_parameters()})
+        # fp32 masters (the fused path keeps the backbone Linear/Conv weights as bf16 model
+        # weights over fp32 masters in its flat space; the masters are the parameters)
+        sd = ck.reference_state_dict(m, tr.space)
+        res.append({n: sd[ck.to_reference_key(n)].cpu() for n, _ in m.named_parameters()})
     # AdamW moves every element by ~lr per step whatever its gradient's size (step 1: lr*sign(g)),
     # so an element whose gradient is ~0 (zero-init biases, key biases under softmax) can step
     # with either sign under run-to-run atomics in the backbone backward. Bars: every element
@@ -199,3 +203,40 @@ def test_trainer_fused_optimizer_matches_torch_adamw():
     print("elements whose updates disagree:", frac)
     assert frac < 0.02, frac
     print("worst relative param difference", worst)
+
+
+def test_trainer_bf16_model_weights_track_fp32_masters():
+    """Mixed-precision backbone weights (optim.FlatParamSpace shadow): the Linear / Conv1d
+    weights of HuBERT / DistilBERT are bf16 model parameters equal to bf16(fp32 master) after
+    every AdamW launch, their bf16 grads reach the flat fp32 buffer, and the checkpoint carries
+    the fp32 masters."""
+    from triad_amd import checkpoint as ck
+    from triad_amd.model import MultiModalModel
+    from triad_amd.train import TriadTrainer
+    torch.manual_seed(0)
+    m = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.8, patch_sparsity_weight=0.01,
+                        visual_dropout_prob=0.25).to(dev).train()
+    tr = TriadTrainer(m, total_updates=100, unfreeze_audio_step=0, unfreeze_text_step=0, unfreeze_vit_step=0,
+                      device=dev)
+    sp = tr.space
+    idx = np.nonzero(sp.shadowed)[0]
+    assert len(idx) > 100
+    assert all(sp.params[i].dtype == torch.bfloat16 for i in idx)
+    before = {int(i): sp.master(i).clone() for i in idx[:40]}
+    B = 4
+    frames = torch.randn(B, 3, 224, 224, device=dev)
+    audio = torch.randn(B, 16000, device=dev) * 0.1
+    text = ["a man riding a bicycle", "a cat on a bed", "dogs", "the quick brown fox jumps"]
+    tr.step(frames, audio, text)
+    torch.cuda.synchronize()
+    moved = 0
+    for i in idx:
+        assert torch.equal(sp.params[i].data, sp.master(i).to(torch.bfloat16)), i
+        assert sp.params[i].grad is None
+    for i, b in before.items():
+        moved += int(not torch.equal(b, sp.master(i)))
+    assert moved > 30
+    sd = ck.reference_state_dict(m, sp)
+    name = "audio_embedder.hubert.encoder.layers.0.attention.q_proj.weight"
+    i = sp.index[id(dict(m.named_parameters())[name])]
+    assert sd[name].dtype == torch.float32 and torch.equal(sd[name], sp.master(i).cpu())

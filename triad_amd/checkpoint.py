@@ -55,20 +55,37 @@ def from_reference_key(k: str) -> str:
     return VIT + rest
 
 
-def reference_state_dict(model: torch.nn.Module) -> "OrderedDict[str, torch.Tensor]":
+def _masters(model, space):
+    """{state_dict key: fp32 master} for parameters held as bf16 model weights by `space`."""
+    if space is None or not getattr(space, "shadowed", np.zeros(0, bool)).any():
+        return {}
+    by_id = {id(p): k for k, p in model.named_parameters()}
+    return {by_id[id(space.params[i])]: space.master(i) for i in np.nonzero(space.shadowed)[0]
+            if id(space.params[i]) in by_id}
+
+
+def reference_state_dict(model: torch.nn.Module, space=None) -> "OrderedDict[str, torch.Tensor]":
     """The mirror's parameters and buffers under the reference model's state_dict names
-    (fp32, as the reference keeps them; frozen bf16 copies are an execution detail)."""
+    (fp32, as the reference keeps them: bf16 model weights are replaced by their fp32 masters
+    from the optimizer's flat space; frozen bf16 copies are an execution detail)."""
+    masters = _masters(model, space)
     out = OrderedDict()
     for k, v in model.state_dict().items():
+        v = masters.get(k, v)
         out[to_reference_key(k)] = v.detach().float().clone() if v.is_floating_point() else v.detach().clone()
     return out
 
 
 @torch.no_grad()
-def load_reference_state_dict(model: torch.nn.Module, sd: Dict[str, torch.Tensor], strict: bool = True):
+def load_reference_state_dict(model: torch.nn.Module, sd: Dict[str, torch.Tensor], strict: bool = True,
+                              space=None):
     """Load a reference `model_state_dict` (with or without `_orig_mod.`) into the mirror.
-    Copies in place, so flat optimizer buffers that alias the parameters stay valid."""
+    Copies in place, so flat optimizer buffers that alias the parameters stay valid; bf16
+    model weights get the fp32 value in their master and its bf16 rounding."""
     mapped = {from_reference_key(k): v for k, v in sd.items()}
+    for k, m in _masters(model, space).items():
+        if k in mapped:
+            m.copy_(mapped[k].to(device=m.device, dtype=m.dtype))
     own = model.state_dict(keep_vars=True)
     missing = [k for k in own if k not in mapped]
     unexpected = [k for k in mapped if k not in own]
@@ -96,7 +113,7 @@ def trainer_checkpoint(trainer, epoch: int, step: int, best_loss: float = float(
                  "cuda": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else [],
                  "numpy": np.random.get_state(), "python": random.getstate()}
     ck = {"epoch": epoch, "step": step, "current_batch_idx": current_batch_idx, "current_segment": current_segment,
-          "rng_state": rng_state, "model_state_dict": reference_state_dict(trainer.model)}
+          "rng_state": rng_state, "model_state_dict": reference_state_dict(trainer.model, trainer.space)}
     for n in _OPTS:
         ck[f"opt_{n}_state"] = getattr(trainer, f"opt_{n}").state_dict()
     for n in _OPTS:
@@ -137,7 +154,7 @@ def load_checkpoint(trainer, path_or_dict, restore_rng: bool = True) -> dict:
         ck = path_or_dict
     else:
         ck = load_file(path_or_dict, trainer.device)
-    load_reference_state_dict(trainer.model, ck["model_state_dict"])
+    load_reference_state_dict(trainer.model, ck["model_state_dict"], space=trainer.space)
     for n in _OPTS:
         getattr(trainer, f"opt_{n}").load_state_dict(ck[f"opt_{n}_state"])
     for n in _OPTS:

@@ -80,7 +80,7 @@ __global__ __launch_bounds__(512, 2) void tile_gemm_kernel(const bf16* __restric
                                                            int kt_per_split, const float* __restrict__ alpha_p,
                                                            void* __restrict__ Cout) {
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * ST];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, l32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
   // XCD-aware: consecutive row panels on one XCD share the streamed B panel in that XCD's L2

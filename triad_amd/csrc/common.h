@@ -19,8 +19,23 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // One 16-byte global->LDS DMA per lane (global_load_lds_dwordx4). The LDS
 // destination is the wave-uniform `lds_base` + lane*16; the global source is
 // per lane (CDNA4 LDS-DMA semantics).
+// Inline asm on purpose: hipcc models the builtin as an LDS write it cannot tell apart from
+// the ring slot being read, and drains vmcnt(0) -- the prefetch just issued included --
+// before the next ds_read, serialising every double-buffered loop. Completion is the
+// caller's: lds_dma_barrier() (vmcnt + barrier) before the data is read. M0 is written and
+// restored inside the statement (cdna_hip_programming.md §5.7).
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
-  __builtin_amdgcn_global_load_lds(gsrc, LDS_PTR(void, lds_base), 16, 0, 0);
+  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)LDS_PTR(void, lds_base));
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds)
+      : "memory");
 }
 
 // Make this wave's LDS-DMA writes complete, then barrier: the only ordering

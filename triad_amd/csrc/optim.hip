@@ -6,6 +6,12 @@
 // Parameters, gradients and both moments live in single contiguous fp32 buffers
 // (the Python side re-points each nn.Parameter's .data/.grad at views), so the
 // whole step is two launches and the data-parallel all-reduce is one buffer.
+// Mixed precision (bf16 autocast backbones, model.py:483,603): the Linear / Conv weights that
+// autocast would cast to bf16 on every forward can instead BE bf16 model parameters backed by
+// the fp32 master in the flat buffer: the AdamW pass writes their bf16 copy (what autocast's
+// cast would produce), and their bf16 gradients (what autocast's backward produces before
+// the cast to fp32) are gathered into the flat fp32 gradient buffer by one multi-tensor launch
+// instead of one cast + one accumulate launch per parameter.
 #include "common.h"
 
 namespace {
@@ -39,8 +45,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     const Chunk* __restrict__ chunks, const float* __restrict__ pp,
                                                     const float* __restrict__ scale, float beta1, float beta2,
-                                                    float eps) {
+                                                    float eps, const unsigned long long* __restrict__ shadow) {
   const Chunk c = chunks[blockIdx.x];
+  // shadow[param]: address of the bf16 model weight minus 2 * (its flat offset), 0 = none
+  bf16* const sh = shadow && shadow[c.param] ? (bf16*)(shadow[c.param]) : nullptr;
   const float step_size = pp[3 * c.param], inv_bc2 = pp[3 * c.param + 1], wdf = pp[3 * c.param + 2];
   const float sc = scale ? scale[c.param] : 1.f;
   const float omb1 = 1.f - beta1, omb2 = 1.f - beta2;
@@ -56,6 +64,24 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
     p[e] = pv;
     m[e] = mv;
     v[e] = vv;
+    if (sh) sh[e] = (bf16)pv;
+  }
+}
+
+struct GradPiece {  // bf16 gradient slice -> flat fp32 gradient elements [dst, dst + n)
+  const bf16* src;
+  long long dst;
+  int n;
+  int pad;
+};
+
+__global__ __launch_bounds__(256) void gather_grads_kernel(const GradPiece* __restrict__ pieces,
+                                                           float* __restrict__ g, int accumulate) {
+  const GradPiece c = pieces[blockIdx.x];
+  float* out = g + c.dst;
+  for (int i = threadIdx.x; i < c.n; i += blockDim.x) {
+    const float x = (float)c.src[i];
+    out[i] = accumulate ? out[i] + x : x;
   }
 }
 
@@ -72,10 +98,19 @@ int triad_grad_sumsq(const float* g, const void* chunks, int nchunks, double* ou
 }
 
 int triad_adamw_step(float* p, const float* g, float* m, float* v, const void* chunks, int nchunks,
-                     const float* pp, const float* scale, float beta1, float beta2, float eps, hipStream_t stream) {
+                     const float* pp, const float* scale, float beta1, float beta2, float eps,
+                     const unsigned long long* shadow, hipStream_t stream) {
   if (nchunks <= 0) return TRIAD_OK;
   hipLaunchKernelGGL(adamw_kernel, dim3(nchunks), dim3(256), 0, stream, p, g, m, v, (const Chunk*)chunks, pp, scale,
-                     beta1, beta2, eps);
+                     beta1, beta2, eps, shadow);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_gather_grads(const void* pieces, int npieces, float* g, int accumulate, hipStream_t stream) {
+  if (npieces <= 0) return TRIAD_OK;
+  hipLaunchKernelGGL(gather_grads_kernel, dim3(npieces), dim3(256), 0, stream, (const GradPiece*)pieces, g,
+                     accumulate);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

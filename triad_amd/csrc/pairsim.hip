@@ -93,7 +93,7 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 kbuf[2 * KT_ELEMS + 8 * WAVES];
   double* red = (double*)(kbuf + 2 * KT_ELEMS);
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const int row = blockIdx.x * ROWS_PER_WG + wave * 32 + ql;
   const bool row_ok = row < a.R;

@@ -42,18 +42,47 @@ struct FwdArgs {
   const int* klen;
 };
 
-// One key tile (32 rows x 1 KB) into an LDS slot: 1-KB buffer LDS-DMA pieces, the row offset
-// in soffset (uniform), the source-side swizzle chunk ^ (row & 15) in voffset.
-__device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t kr, const FwdArgs& a, bf16* dst, int j, int kb,
-                                           int wave, int lane) {
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte-per-lane buffer LDS-DMA (buffer_load_dwordx4 ... lds), written as inline asm so the
+// compiler does not see an LDS write: it would otherwise drain vmcnt(0) -- including the DMA
+// of the tile two ahead -- before every ds_read of the ring (it cannot tell the slots apart).
+// Completion is counted by sync_tile's s_waitcnt vmcnt(N) + barrier. M0 = LDS destination
+// (uniform), written and restored inside the statement.
+__device__ __forceinline__ void dma16(i32x4 rsrc, unsigned lds_addr, unsigned voff, unsigned soff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds_addr), "v"(voff), "s"(rsrc), "s"(soff)
+      : "memory");
+}
+
+// One key tile (32 rows x 1 KB) into an LDS slot: 1-KB pieces, the row offset in soffset
+// (uniform), the source-side swizzle chunk ^ (row & 15) in voffset.
+__device__ __forceinline__ void stage_tile(i32x4 kr, const FwdArgs& a, bf16* dst, int j, int kb, int wave,
+                                           int lane) {
   const unsigned row0 = (unsigned)(j * a.Nk_pad + kb * 32 + wave * GLDS_PER_TILE);
+  const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) bf16*)dst;
   asm volatile("" : "+v"(lane));  // recompute the lane offsets here, do not keep them live
 #pragma unroll
   for (int u = 0; u < GLDS_PER_TILE; ++u) {
     const int t = wave * GLDS_PER_TILE + u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (__attribute__((address_space(3))) void*)(dst + t * D), 16,
-                                             (unsigned)((lane ^ (t & 15)) * 16), (row0 + u) * (D * 2), 0, 0);
+    dma16(kr, __builtin_amdgcn_readfirstlane(lds0 + t * D * 2), (unsigned)((lane ^ (t & 15)) * 16),
+          __builtin_amdgcn_readfirstlane((row0 + u) * (D * 2)));
   }
+}
+
+// 16-byte store hidden from hipcc's waitcnt bookkeeping (it would otherwise drain vmcnt(0) --
+// the in-flight key DMA included -- before reusing the data registers); the trailing
+// s_nop 1 covers the store-data read (cdna_hip_programming.md §5.7). Counted in sync_tile.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store16(void* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {  // one v_cvt_pk_bf16_f32
@@ -129,8 +158,11 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   }
 
   // K through a buffer descriptor (32-bit offsets; the host guarantees < 2 GB)
-  const __amdgpu_buffer_rsrc_t kr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.K, 0, (int)((unsigned)a.Bk * a.Nk_pad * (D * 2)), 0x00020000);
+  // buffer descriptor words: base, stride 0, num_records, gfx950 raw-buffer flags
+  const unsigned long long kaddr = (unsigned long long)a.K;
+  const i32x4 kr = {__builtin_amdgcn_readfirstlane((int)(unsigned)kaddr),
+                    __builtin_amdgcn_readfirstlane((int)((unsigned)(kaddr >> 32) & 0xffffu)),
+                    __builtin_amdgcn_readfirstlane((int)((unsigned)a.Bk * a.Nk_pad * (D * 2))), 0x00020000};
   // walk cursors: prefetch (tile b+2), chain (tile b), epilogue (tile b-1); ring slots
   Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
   int fslot = 0, cslot = 0;
@@ -149,7 +181,8 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) qf[s] = *(const bf16x8*)(q0 + 16 * s);
   }
-  const float temp = *a.temp;
+  // uniform (SGPR) temperature: the load completes here, not at a wait inside the loop
+  const float temp = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, *a.temp)));
   const float lo = a.clamp_lo;
   double accd = 0.0, accd2 = 0.0;
   // lane part of the swizzled LDS fragment offsets (bytes), k-step s reads chunk 2(s&7)+h
@@ -185,8 +218,8 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
     if (TRAIN) {
       accd2 += (double)e.st;
       bf16* d = dS_w + ((long long)ec.j * nkb + ec.kb) * 1024 + lane * 16;
-      *(uint4*)d = make_uint4(e.pk[0], e.pk[1], e.pk[2], e.pk[3]);
-      *(uint4*)(d + 8) = make_uint4(e.pk[4], e.pk[5], e.pk[6], e.pk[7]);
+      store16(d, (u32x4){e.pk[0], e.pk[1], e.pk[2], e.pk[3]});
+      store16(d + 8, (u32x4){e.pk[4], e.pk[5], e.pk[6], e.pk[7]});
     }
     if (ec.kb == nkb - 1) {  // end of a key sample: combine the half-waves' max / argmax
       float m = e.m;

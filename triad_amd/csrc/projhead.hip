@@ -47,7 +47,8 @@ __global__ __launch_bounds__(512, 1) void projhead_fwd_kernel(
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * STAGE + LN_ELEMS + 2 * PWAVES * PM * 2];
   bf16* lnimg = lds + 2 * STAGE;
   float* red = (float*)(lnimg + LN_ELEMS);  // [PWAVES][PM]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h2 = lane >> 5, l32 = lane & 31;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h2 = lane >> 5,
+            l32 = lane & 31;
   const int r0 = blockIdx.x * PM;
 
   f32x16 acc[2][2];
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
                                                      const float* __restrict__ gamma, int M, bf16* __restrict__ dy1,
                                                      float* __restrict__ dgb_part /* [grid][2][512] */) {
   __shared__ float sg[4][PN], sb[4][PN];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float pg[8], pb[8], gm[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { pg[k] = 0.f; pb[k] = 0.f; gm[k] = gamma[lane * 8 + k]; }

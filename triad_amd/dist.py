@@ -79,10 +79,10 @@ def allreduce_grads(flat: torch.Tensor, bucket_elems: int, average: bool, group=
     W, _ = world_rank(group)
     if W <= 1:
         return
-    nccl = _is_nccl(group)
-    op = dist.ReduceOp.AVG if (average and nccl) else dist.ReduceOp.SUM
+    # SUM then scale: ReduceOp.AVG needs the collective library's avg op, not guaranteed on
+    # every RCCL build; the scale is one streaming pass per bucket
     for s in range(0, flat.numel(), bucket_elems):
         b = flat[s:s + bucket_elems]
-        dist.all_reduce(b, op=op, group=group)
-        if average and not nccl:
-            b.div_(W)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM, group=group)
+        if average:
+            b.mul_(1.0 / W)

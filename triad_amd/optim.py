@@ -31,15 +31,26 @@ from ._lib import TriadError, call, ptr, stream_ptr
 CHUNK = 16384
 ALIGN = 64  # elements (256 B) per parameter slot
 _CHUNK_DT = np.dtype([("off", "<i8"), ("n", "<i4"), ("param", "<i4")])
+_PIECE_DT = np.dtype([("src", "<u8"), ("dst", "<i8"), ("n", "<i4"), ("pad", "<i4")])
 
 
 class FlatParamSpace:
-    """Owns the flat param / grad / exp_avg / exp_avg_sq buffers for a list of parameters."""
+    """Owns the flat param / grad / exp_avg / exp_avg_sq buffers for a list of parameters.
 
-    def __init__(self, params: Sequence[torch.nn.Parameter], device):
+    `shadow`: parameters to hold as bf16 MODEL weights backed by the fp32 master in the flat
+    buffer (mixed precision for the bf16-autocast backbones): the nn.Parameter's .data becomes
+    bf16 (what autocast would cast it to on every forward), autograd leaves its bf16 gradient
+    in .grad (what autocast's backward produces before casting to fp32), `gather_shadow_grads`
+    moves those into the flat fp32 gradient buffer in one launch, and the AdamW launch writes
+    the new bf16 weight. Only for weights consumed exactly as autocast consumes them (Linear /
+    Conv inputs), used once per backward (a second use would accumulate in bf16)."""
+
+    def __init__(self, params: Sequence[torch.nn.Parameter], device, shadow: Sequence[torch.nn.Parameter] = ()):
         self.device = torch.device(device)
         self.params: List[torch.nn.Parameter] = list(params)
         self.index = {id(p): i for i, p in enumerate(self.params)}
+        shadow_ids = {id(p) for p in shadow}
+        self.shadowed = np.array([id(p) in shadow_ids for p in self.params], dtype=bool)
         offs, o = [], 0
         for p in self.params:
             offs.append(o)
@@ -55,15 +66,23 @@ class FlatParamSpace:
         self.steps = np.zeros(len(self.params), dtype=np.int64)
         self.scale = torch.ones(len(self.params), **f32)
         self._hooks = []
+        shadow_base = np.zeros(len(self.params), dtype=np.uint64)
         with torch.no_grad():
             for i, p in enumerate(self.params):
                 if p.dtype != torch.float32:
                     raise TriadError("flat AdamW expects fp32 master parameters")
                 v = self.flat_p[offs[i]:offs[i] + p.numel()].view_as(p)
                 v.copy_(p.data)
-                p.data = v
-                p.grad = self.flat_g[offs[i]:offs[i] + p.numel()].view_as(p)
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._mark(i)))
+                if self.shadowed[i]:
+                    p.data = v.to(torch.bfloat16)
+                    p.grad = None
+                    shadow_base[i] = (p.data_ptr() - 2 * offs[i]) % (1 << 64)
+                else:
+                    p.data = v
+                    p.grad = self.flat_g[offs[i]:offs[i] + p.numel()].view_as(p)
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._mark(i)))
+        self.shadow_base = (torch.from_numpy(shadow_base.view(np.int64)).to(self.device)
+                            if self.shadowed.any() else None)
         self._chunk_cache: Dict[tuple, tuple] = {}
 
     def _mark(self, i):
@@ -107,6 +126,42 @@ class FlatParamSpace:
             out.index_add_(0, owner, part)
         return out
 
+    def master(self, i: int) -> torch.Tensor:
+        """fp32 master of parameter i (a view of the flat buffer)."""
+        p = self.params[i]
+        return self.flat_p[self.offsets[i]:self.offsets[i] + p.numel()].view(p.shape)
+
+    @torch.no_grad()
+    def gather_shadow_grads(self, accumulate: bool):
+        """bf16 .grad of the shadowed parameters -> flat fp32 gradient buffer (one launch);
+        the .grad tensors are released (stream-ordered reuse by the caching allocator)."""
+        if not self.shadowed.any():
+            return
+        rows, ids = [], []
+        for i in np.nonzero(self.shadowed)[0]:
+            p = self.params[i]
+            gr = p.grad
+            if gr is None:
+                continue
+            if gr.dtype != torch.bfloat16 or not gr.is_contiguous():
+                gr = gr.to(torch.bfloat16).contiguous()
+                p.grad = gr
+            base, n = gr.data_ptr(), gr.numel()
+            for s0 in range(0, n, CHUNK):
+                rows.append((base + 2 * s0, self.offsets[i] + s0, min(CHUNK, n - s0), 0))
+            ids.append(int(i))
+        if not rows:
+            return
+        arr = np.array(rows, dtype=_PIECE_DT)
+        host = torch.from_numpy(arr.view(np.uint8)).pin_memory() if self.device.type == "cuda" else \
+            torch.from_numpy(arr.view(np.uint8).copy())
+        table = host.to(self.device, non_blocking=True)
+        call("triad_gather_grads", ptr(table), len(rows), ptr(self.flat_g), int(accumulate and True),
+             stream_ptr(self.device))
+        for i in ids:
+            self.params[i].grad = None
+        self.touched[ids] = True
+
     def zero_grad(self, ids: Sequence[int]):
         """Zero the gradient slots of these parameters (contiguous runs -> few memsets)."""
         ids = sorted(ids)
@@ -122,6 +177,9 @@ class FlatParamSpace:
         if ids:
             self.touched[ids] = False
             self.scale.index_fill_(0, torch.tensor(ids, device=self.device), 1.0)
+            for i in ids:
+                if self.shadowed[i]:
+                    self.params[i].grad = None
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -158,7 +216,8 @@ class FusedAdamW(torch.optim.Optimizer):
         pp_dev = host.to(sp.device, non_blocking=True)
         table, n, _ = sp.chunks(ids)
         call("triad_adamw_step", ptr(sp.flat_p), ptr(sp.flat_g), ptr(sp.exp_avg), ptr(sp.exp_avg_sq), ptr(table), n,
-             ptr(pp_dev), ptr(sp.scale), float(b1), float(b2), float(eps), stream_ptr(sp.device))
+             ptr(pp_dev), ptr(sp.scale), float(b1), float(b2), float(eps), ptr(sp.shadow_base),
+             stream_ptr(sp.device))
         return loss
 
     def zero_grad(self, set_to_none: bool = False):

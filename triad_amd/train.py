@@ -48,6 +48,20 @@ def split_param_groups(model):
     return groups
 
 
+def bf16_weight_params(model):
+    """Backbone weights autocast feeds to bf16 matmuls/convs exactly once per forward: every
+    nn.Linear / nn.Conv1d parameter of HuBERT and DistilBERT (model.py:29-30,79-80), except
+    weight-normalised convolutions (HuBERT's positional conv computes its weight from g, v in
+    fp32 before the cast). These can live as bf16 model weights over fp32 masters."""
+    out = []
+    for root in (model.audio_embedder.hubert, model.text_embedder.encoder):
+        for mod in root.modules():
+            if isinstance(mod, (torch.nn.Linear, torch.nn.Conv1d)) and not hasattr(mod, "parametrizations") \
+                    and not hasattr(mod, "weight_g"):
+                out.extend(p for p in mod.parameters(recurse=False) if p.dtype == torch.float32)
+    return out
+
+
 def _one_cycle(opt, max_lr, total):
     return torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=max_lr, total_steps=max(1, total), pct_start=0.1,
                                                div_factor=10, final_div_factor=1e4, anneal_strategy="cos")
@@ -57,7 +71,7 @@ class TriadTrainer:
     def __init__(self, model, learning_rate=1e-4, total_updates=10000, gradient_accumulation_steps=1,
                  unfreeze_audio_step=5000, unfreeze_text_step=5000, unfreeze_vit_step=5000,
                  optimizer="fused", device="cuda", process_group=None, bucket_mb=256.0,
-                 av_weight_start=0.8, av_weight_end=0.5, global_negatives=False):
+                 av_weight_start=0.8, av_weight_end=0.5, global_negatives=False, bf16_weights=None):
         self.model = model
         self.device = torch.device(device)
         self.grad_accum = gradient_accumulation_steps
@@ -73,7 +87,12 @@ class TriadTrainer:
         opt_params = self.groups["others"] + self.groups["audio"] + self.groups["text"] + self.groups["vit_lora"]
         self.kind = optimizer
         if optimizer == "fused":
-            self.space = fo.FlatParamSpace(opt_params, self.device)
+            # mixed-precision model weights for the autocast backbones (default: when the
+            # model runs under bf16 autocast on the GPU); see optim.FlatParamSpace
+            if bf16_weights is None:
+                bf16_weights = bool(getattr(model, "use_amp", False)) and self.device.type == "cuda"
+            shadow = bf16_weight_params(model) if bf16_weights else []
+            self.space = fo.FlatParamSpace(opt_params, self.device, shadow=shadow)
             mk = lambda ps: fo.FusedAdamW(self.space, ps, lr=learning_rate)  # noqa: E731
         elif optimizer == "torch":
             self.space = None
@@ -151,6 +170,8 @@ class TriadTrainer:
         tv_loss = tv[0] if tv is not None else None
         loss_total = self._loss_mix(phase, av_loss, tv_loss, progress)
         (loss_total / self.grad_accum).backward()
+        if self.space is not None:  # bf16 weight grads -> flat fp32 grads (accumulating micro-steps)
+            self.space.gather_shadow_grads(accumulate=self.accumulation_counter % self.grad_accum != 0)
         self.accumulation_counter += 1
         out["loss"] = loss_total.detach()
         if av is not None:
