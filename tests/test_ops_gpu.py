@@ -239,4 +239,4 @@ def test_trainer_bf16_model_weights_track_fp32_masters():
     sd = ck.reference_state_dict(m, sp)
     name = "audio_embedder.hubert.encoder.layers.0.attention.q_proj.weight"
     i = sp.index[id(dict(m.named_parameters())[name])]
-    assert sd[name].dtype == torch.float32 and torch.equal(sd[name], sp.master(i).cpu())
+    assert sd[name].dtype == torch.float32 and torch.equal(sd[name].cpu(), sp.master(i).cpu())
