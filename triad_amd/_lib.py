@@ -12,6 +12,9 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtriad_hip.so")
+# A/B experiments only: load a variant build of the same library (tools/build_variants.py);
+# the default is the in-tree build above
+LIB_PATH = os.environ.get("TRIAD_LIB_VARIANT", LIB_PATH)
 
 vp, i32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_double
 

@@ -14,12 +14,12 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 ROOT = os.path.dirname(PKG)
-LIB = os.path.join(PKG, "libtriad_hip.so")
-OBJ = os.path.join(PKG, "_build")
+LIB = os.environ.get("TRIAD_LIB_OUT", os.path.join(PKG, "libtriad_hip.so"))
+OBJ = os.environ.get("TRIAD_OBJ_DIR", os.path.join(PKG, "_build"))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("TRIAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", os.path.join(ROOT, "include"),
-         "-Wno-unused-result"]
+         "-Wno-unused-result"] + os.environ.get("TRIAD_EXTRA_FLAGS", "").split()
 # per-file extras: the pipelined forward wants scalar f32 VALU beside its MFMAs (SLP-packed
 # v_pk_mul_f32 + operand moves cost more issue slots than two v_mul_f32 there)
 EXTRA = {"pairsim_fwd.hip": ["-fno-slp-vectorize"]}

@@ -27,6 +27,14 @@ constexpr int KT_ELEMS = 32 * D;
 constexpr int NBUF = 3;
 constexpr int GLDS_PER_TILE = 32 / WAVES;  // 1-KB LDS-DMA pieces per wave per key tile (4)
 
+// tuning knobs (A/B builds, tools/build_variants.py)
+#ifndef FWD_SETPRIO
+#define FWD_SETPRIO 0  // 1: waves 4-7 at s_setprio 1 (MI355X_MICROARCH.md "two waves per SIMD" item 4)
+#endif
+#ifndef FWD_REGION
+#define FWD_REGION 2  // k-steps per scheduling region (sched_barrier spacing; 2 measured best)
+#endif
+
 struct FwdArgs {
   const bf16* Q;
   const bf16* K;
@@ -144,6 +152,7 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   const int row = blockIdx.x * ROWS_PER_WG + wave * 32 + ql;
   const bool rok = row < a.R;
   const int rt = (blockIdx.x * ROWS_PER_WG + wave * 32) / 32;
+  if (FWD_SETPRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   const int j0 = blockIdx.y * a.j_per_wg;
   const int j1 = min(a.Bk, j0 + a.j_per_wg);
@@ -260,7 +269,7 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
         }
         // scheduling regions of 4 k-steps: two epilogue elements interleave and fill each
         // other's VALU->SGPR-mask wait states
-        if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        if (s % FWD_REGION == FWD_REGION - 1) __builtin_amdgcn_sched_barrier(0);
       }
     } else if constexpr (ep) {
 #pragma unroll
