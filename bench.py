@@ -108,9 +108,10 @@ def main():
     from triad_amd.train import TriadTrainer
 
     _lib.load()
-    # MIOpen searches conv algorithms once per shape (HuBERT's conv feature encoder) instead
-    # of using its immediate-mode heuristic; the search runs in the untimed warmup.
-    torch.backends.cudnn.benchmark = True
+    # The only MIOpen convolution left is HuBERT's positional conv (the feature encoder and the
+    # patch embedding run as GEMMs, triad_amd.frontend): immediate mode, no per-shape search /
+    # runtime kernel compilation on a fresh box.
+    torch.backends.cudnn.benchmark = False
     torch.manual_seed(1234)
     model = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.80, patch_sparsity_weight=0.01,
                             visual_dropout_prob=0.25, use_amp=True).to(dev)

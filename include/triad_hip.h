@@ -173,6 +173,29 @@ int triad_gather_rows(const void* src, long long src_rows, const int* idx, int B
 /* y = x / max(||x||_2, eps) per row, bf16 (F.normalize, model.py:363-364). */
 int triad_l2norm_rows(const void* x, int rows, int D, float eps, void* y, hipStream_t stream);
 
+/* Audio front-end (model.py:29-30,66: the HuBERT conv feature encoder's layer 0,
+ * transformers HubertGroupNormConvLayer = conv -> GroupNorm(C groups) -> GELU), fused
+ * GroupNorm + exact GELU over channels-last x[B][T][C] bf16 (C % 8 == 0, 256 % (C/8) == 0).
+ * fwd: y = bf16(gelu((x - mean[b][c]) * rstd[b][c] * gamma[c] + beta[c])), statistics over t
+ *      in fp32/fp64, mean / rstd (B*C floats) saved for the backward.
+ * bwd: dx (bf16) and dgamma / dbeta (C floats, overwritten) from dy (bf16).
+ * ws: triad_chgn_workspace_bytes(B, T, C) bytes of scratch. */
+long long triad_chgn_workspace_bytes(int B, int T, int C);
+int triad_chgn_gelu_fwd(const void* x, int B, int T, int C, const float* gamma, const float* beta, float eps,
+                        float* mean, float* rstd, void* ws, void* y, hipStream_t stream);
+int triad_chgn_gelu_bwd(const void* x, const void* dy, int B, int T, int C, const float* gamma, const float* beta,
+                        const float* mean, const float* rstd, void* ws, void* dx, float* dgamma, float* dbeta,
+                        hipStream_t stream);
+
+/* HuBERT positional convolution (model.py:29-30,66: transformers HubertPositionalConvEmbedding,
+ * Conv1d(C, C, 128, padding 64, groups) + SamePad) as an implicit GEMM over channels-last bf16:
+ * y[b][t][g*CG+n] = bias + sum_{j<128, c<CG} x[b][t+j-pad][g*CG+c] * wt[g][n][j*CG+c], t < T,
+ * x zero outside [0, T); CG = C/groups in {48, 64}; bias f32 (may be NULL).
+ * Forward: wt[g][n][j*CG+c] = W[g*CG+n][c][j], pad = 64. Input gradient: x = dy,
+ * wt[g][c][j*CG+n] = W[g*CG+n][c][127-j], pad = 63. */
+int triad_posconv(const void* x, const void* wt, const float* bias, void* y, int B, int T, int C, int groups,
+                  int pad, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared():
     src = open(os.path.join(ROOT, "include", "triad_hip.h")).read()
-    return sorted(set(re.findall(r"^int\s+(triad_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^(?:int|long long)\s+(triad_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_declared_symbol():

@@ -1,0 +1,95 @@
+"""GPU parity of the backbone front-ends (triad_amd.frontend): the fused channels-last
+GroupNorm(C groups) + GELU HIP kernels against torch fp32 (values, dx, dgamma, dbeta), and the
+whole HuBERT conv feature encoder in GEMM form against the transformers modules it replaces,
+both under bf16 autocast on the device."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+@pytest.mark.parametrize("B,T,C", [(3, 1000, 512), (2, 12799, 512), (4, 77, 64), (1, 5, 512)])
+def test_channel_group_norm_gelu(B, T, C):
+    from triad_amd import frontend
+    g = torch.Generator(device=dev).manual_seed(T)
+    x = (torch.randn(B, T, C, device=dev, generator=g) * 2.0 + 0.5).to(torch.bfloat16)
+    gamma = (torch.rand(C, device=dev, generator=g) + 0.5).requires_grad_(True)
+    beta = (torch.randn(C, device=dev, generator=g) * 0.2).requires_grad_(True)
+    xr = x.float().requires_grad_(True)
+    gr = gamma.detach().clone().requires_grad_(True)
+    br = beta.detach().clone().requires_grad_(True)
+    ref = F.gelu(F.group_norm(xr.transpose(1, 2), C, gr, br, 1e-5)).transpose(1, 2)
+    xd = x.clone().requires_grad_(True)
+    y = frontend.channel_group_norm_gelu(xd, gamma, beta, 1e-5)
+    assert y.dtype == torch.bfloat16 and y.shape == x.shape
+    # bf16 output of fp32 arithmetic: within one bf16 rounding of the fp32 reference
+    torch.testing.assert_close(y.float(), ref.detach(), rtol=8e-3, atol=8e-3)
+    dy = (torch.randn(B, T, C, device=dev, generator=g)).to(torch.bfloat16)
+    ref.backward(dy.float())
+    y.backward(dy)
+    assert xd.grad.dtype == torch.bfloat16
+    assert _rel(xd.grad.float(), xr.grad) < 8e-3
+    assert _rel(gamma.grad, gr.grad) < 1e-4
+    assert _rel(beta.grad, br.grad) < 1e-4
+
+
+def test_hubert_feature_encoder_gemm_matches_transformers():
+    import transformers
+    from triad_amd import frontend
+    torch.manual_seed(0)
+    ref_m = transformers.HubertModel(transformers.HubertConfig()).to(dev).train()
+    m = transformers.HubertModel(transformers.HubertConfig()).to(dev).train()
+    m.load_state_dict(ref_m.state_dict())
+    frontend.install_hubert_frontend(m)
+    x = torch.randn(3, 16000, device=dev) * 0.5
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ref = ref_m.feature_extractor(x)
+        got = m.feature_extractor(x)
+    assert got.shape == ref.shape
+    assert _rel(got.float(), ref.float()) < 2e-2
+    gy = torch.randn_like(ref.float())
+    (ref.float() * gy).sum().backward()
+    (got.float() * gy).sum().backward()
+    for (n, p), (_, q) in zip(m.feature_extractor.named_parameters(), ref_m.feature_extractor.named_parameters()):
+        assert _rel(p.grad, q.grad) < 5e-2, n
+
+
+@pytest.mark.parametrize("C,G,T", [(768, 16, 199), (768, 16, 37), (1024, 16, 499), (768, 16, 1)])
+def test_hubert_pos_conv_matches_transformers(C, G, T):
+    """Implicit-GEMM positional conv (forward + input grad) + MIOpen weight grad vs the
+    transformers module (conv -> SamePad -> GELU) under bf16 autocast."""
+    import transformers
+    from transformers.models.hubert.modeling_hubert import HubertPositionalConvEmbedding
+    from triad_amd import frontend
+    cfg = transformers.HubertConfig(hidden_size=C, num_conv_pos_embedding_groups=G)
+    torch.manual_seed(T)
+    ref_m = HubertPositionalConvEmbedding(cfg).to(dev)
+    m = HubertPositionalConvEmbedding(cfg).to(dev)
+    m.load_state_dict(ref_m.state_dict())
+    m._triad_hf_forward = m.forward
+    import types
+    m.forward = types.MethodType(frontend._hubert_pos_conv_forward, m)
+    x = torch.randn(3, T, C, device=dev)
+    xr = x.clone().requires_grad_(True)
+    xd = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        xr_b = xr.to(torch.bfloat16)
+        xd_b = xd.to(torch.bfloat16)
+        ref = ref_m(xr_b)
+        got = m(xd_b)
+    assert got.shape == ref.shape == (3, T, C)
+    assert _rel(got.float(), ref.float()) < 1e-2
+    gy = torch.randn_like(ref.float())
+    (ref.float() * gy).sum().backward()
+    (got.float() * gy).sum().backward()
+    assert _rel(xd.grad, xr.grad) < 2e-2
+    for (n, p), (_, q) in zip(m.named_parameters(), ref_m.named_parameters()):
+        assert _rel(p.grad, q.grad) < 3e-2, n

@@ -44,7 +44,13 @@ SIGNATURES = {
     "triad_gather_grads": [vp, i32, vp, i32, vp],
     "triad_gather_rows": [vp, i64, vp, i32, i32, i32, vp, vp],
     "triad_l2norm_rows": [vp, i32, i32, f32, vp, vp],
+    "triad_chgn_workspace_bytes": [i32, i32, i32],
+    "triad_chgn_gelu_fwd": [vp, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp],
+    "triad_chgn_gelu_bwd": [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "triad_posconv": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
 }
+# entry points returning a value rather than a status
+RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_longlong}
 
 _lock = threading.Lock()
 _lib = None
@@ -66,7 +72,7 @@ def load():
             for name, args in SIGNATURES.items():
                 fn = getattr(lib, name)
                 fn.argtypes = args
-                fn.restype = C.c_int
+                fn.restype = RESTYPES.get(name, C.c_int)
             _lib = lib
     return _lib
 
@@ -91,7 +97,7 @@ def call(name, *args):
         TIMERS[name].append((e0, e1, meta))
     else:
         rc = getattr(load(), name)(*args)
-    if name != "triad_pairsim_nparts" and rc != 0:
+    if name not in RESTYPES and rc != 0:
         what = "invalid argument/shape" if rc == 1001 else f"hipError_t {rc}"
         raise TriadError(f"{name} failed: {what}")
     return rc

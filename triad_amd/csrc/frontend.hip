@@ -1,0 +1,256 @@
+// HuBERT conv feature encoder, layer 0 (SajayR/TRIAD model.py:29-30,66 -> transformers
+// HubertGroupNormConvLayer): GroupNorm(num_groups = C) + exact GELU over the conv output,
+// fused, in channels-last (B, T, C) bf16 layout.
+//
+// GroupNorm with one channel per group normalises every (sample, channel) over time. Under the
+// reference's bf16 autocast the norm runs in fp32 and GELU on its fp32 output; the next conv
+// casts to bf16. Here the statistics and the whole elementwise chain are fp32 in registers
+// and only the bf16 result is stored: bf16(gelu(gn(x))) -- the value the next conv reads.
+//
+// Layout: x[b][t][c], C % 8 == 0 and C / 8 a divisor of 256 (HuBERT: C = 512). One thread owns
+// 8 channels (one 16-byte vector) of a time row; a 256-thread block covers 256 / (C/8) rows per
+// sweep over a chunk of CHUNK time steps. HBM-bound: fwd reads x twice and writes y once; bwd
+// reads x, dy twice and writes dx once.
+#include "common.h"
+
+namespace {
+
+constexpr int CHUNK = 128;
+constexpr int NT = 256;
+
+struct V8 {
+  float v[8];
+};
+
+__device__ __forceinline__ V8 load8(const bf16* p) {
+  const bf16x8 r = *(const bf16x8*)p;
+  V8 o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o.v[i] = (float)r[i];
+  return o;
+}
+
+__device__ __forceinline__ void store8(bf16* p, const V8& x) {
+  bf16x8 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = (bf16)x.v[i];
+  *(bf16x8*)p = r;
+}
+
+__device__ __forceinline__ float gelu(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float z) {
+  return 0.5f * (1.f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * __expf(-0.5f * z * z);
+}
+
+// partial[b][chunk][c] = (sum, sumsq) over the chunk's rows (fp32; < CHUNK terms each)
+// MODE 0: x itself (forward statistics)
+// MODE 1: (dz, dz * xhat) with dz = dy * gelu'(xhat * gamma + beta) (backward sums)
+template <int MODE>
+__global__ __launch_bounds__(NT) void chgn_sums_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                       int T, int C, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float2* __restrict__ part) {
+  __shared__ float2 red[NT * 8];
+  const int b = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int tpr = C / 8;                // threads per row
+  const int rows = NT / tpr;            // rows per sweep
+  const int cg = threadIdx.x % tpr, r0 = threadIdx.x / tpr;
+  const int c0 = cg * 8;
+  float s[8], q[8], mu[8], rs[8], g[8], be[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s[i] = 0.f;
+    q[i] = 0.f;
+    if (MODE == 1) {
+      mu[i] = mean[(size_t)b * C + c0 + i];
+      rs[i] = rstd[(size_t)b * C + c0 + i];
+      g[i] = gamma[c0 + i];
+      be[i] = beta[c0 + i];
+    }
+  }
+  const int t1 = min(T, (chunk + 1) * CHUNK);
+  for (int t = chunk * CHUNK + r0; t < t1; t += rows) {
+    const size_t off = ((size_t)b * T + t) * C + c0;
+    const V8 xv = load8(x + off);
+    if (MODE == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        s[i] += xv.v[i];
+        q[i] = fmaf(xv.v[i], xv.v[i], q[i]);
+      }
+    } else {
+      const V8 dv = load8(dy + off);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xh = (xv.v[i] - mu[i]) * rs[i];
+        const float dz = dv.v[i] * gelu_grad(fmaf(xh, g[i], be[i]));
+        s[i] += dz;
+        q[i] = fmaf(dz, xh, q[i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[threadIdx.x * 8 + i] = make_float2(s[i], q[i]);
+  __syncthreads();
+  // one thread per channel: sum the `rows` row-groups
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const int g8 = c / 8, i = c % 8;
+    float2 acc = make_float2(0.f, 0.f);
+    for (int r = 0; r < rows; ++r) {
+      const float2 v = red[(r * tpr + g8) * 8 + i];
+      acc.x += v.x;
+      acc.y += v.y;
+    }
+    part[((size_t)b * nchunk + chunk) * C + c] = acc;
+  }
+}
+
+// Forward finalize: mean / rstd per (b, c) from the chunk partials (double accumulation).
+__global__ void chgn_stats_kernel(const float2* __restrict__ part, int nchunk, int T, int C, float eps,
+                                  float* __restrict__ mean, float* __restrict__ rstd) {
+  const int b = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    const float2 v = part[((size_t)b * nchunk + k) * C + c];
+    s += v.x;
+    q += v.y;
+  }
+  const double m = s / T;
+  double var = q / T - m * m;
+  if (var < 0.0) var = 0.0;
+  mean[(size_t)b * C + c] = (float)m;
+  rstd[(size_t)b * C + c] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// Backward finalize, per (b, c): cA = gamma * sum(dz) / T, cB = gamma * sum(dz * xhat) / T into
+// coef[b][c] (float2); per-(b, c) totals into tot[b][c] for dgamma / dbeta.
+__global__ void chgn_bwd_coef_kernel(const float2* __restrict__ part, int nchunk, int T, int C,
+                                     const float* __restrict__ gamma, float2* __restrict__ coef,
+                                     double2* __restrict__ tot) {
+  const int b = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    const float2 v = part[((size_t)b * nchunk + k) * C + c];
+    s += v.x;
+    q += v.y;
+  }
+  const double gm = gamma[c];
+  coef[(size_t)b * C + c] = make_float2((float)(gm * s / T), (float)(gm * q / T));
+  tot[(size_t)b * C + c] = make_double2(s, q);
+}
+
+// dgamma[c] = sum_b sum(dz * xhat), dbeta[c] = sum_b sum(dz)
+__global__ void chgn_param_grad_kernel(const double2* __restrict__ tot, int B, int C, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < B; ++b) {
+    const double2 v = tot[(size_t)b * C + c];
+    s += v.x;
+    q += v.y;
+  }
+  dgamma[c] = (float)q;
+  dbeta[c] = (float)s;
+}
+
+// MODE 0: y = gelu(xhat * gamma + beta)
+// MODE 1: dx = rstd * (dz * gamma - cA - xhat * cB)
+template <int MODE>
+__global__ __launch_bounds__(NT) void chgn_apply_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                        int T, int C, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta,
+                                                        const float2* __restrict__ coef, bf16* __restrict__ out) {
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int tpr = C / 8;
+  const int rows = NT / tpr;
+  const int cg = threadIdx.x % tpr, r0 = threadIdx.x / tpr;
+  const int c0 = cg * 8;
+  float mu[8], rs[8], g[8], be[8], ca[8], cb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mu[i] = mean[(size_t)b * C + c0 + i];
+    rs[i] = rstd[(size_t)b * C + c0 + i];
+    g[i] = gamma[c0 + i];
+    be[i] = beta[c0 + i];
+    if (MODE == 1) {
+      const float2 k = coef[(size_t)b * C + c0 + i];
+      ca[i] = k.x;
+      cb[i] = k.y;
+    }
+  }
+  const int t1 = min(T, (chunk + 1) * CHUNK);
+  for (int t = chunk * CHUNK + r0; t < t1; t += rows) {
+    const size_t off = ((size_t)b * T + t) * C + c0;
+    const V8 xv = load8(x + off);
+    V8 o;
+    if (MODE == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o.v[i] = gelu(fmaf((xv.v[i] - mu[i]) * rs[i], g[i], be[i]));
+    } else {
+      const V8 dv = load8(dy + off);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xh = (xv.v[i] - mu[i]) * rs[i];
+        const float dz = dv.v[i] * gelu_grad(fmaf(xh, g[i], be[i]));
+        o.v[i] = rs[i] * (dz * g[i] - ca[i] - xh * cb[i]);
+      }
+    }
+    store8(out + off, o);
+  }
+}
+
+bool shape_ok(int B, int T, int C) {
+  return B > 0 && T > 0 && C > 0 && C % 8 == 0 && NT % (C / 8) == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+long long triad_chgn_workspace_bytes(int B, int T, int C) {
+  const long long nchunk = (T + CHUNK - 1) / CHUNK;
+  // chunk partials (float2) + backward coefficients (float2) + per-(b, c) totals (double2)
+  return (long long)B * nchunk * C * 8 + (long long)B * C * 8 + (long long)B * C * 16;
+}
+
+int triad_chgn_gelu_fwd(const void* x, int B, int T, int C, const float* gamma, const float* beta, float eps,
+                        float* mean, float* rstd, void* ws, void* y, hipStream_t stream) {
+  if (!shape_ok(B, T, C)) return TRIAD_EINVAL;
+  const int nchunk = (T + CHUNK - 1) / CHUNK;
+  float2* part = (float2*)ws;
+  hipLaunchKernelGGL(chgn_sums_kernel<0>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)x, nullptr, T, C,
+                     nullptr, nullptr, nullptr, nullptr, part);
+  hipLaunchKernelGGL(chgn_stats_kernel, dim3((C + 255) / 256, B), dim3(256), 0, stream, part, nchunk, T, C, eps,
+                     mean, rstd);
+  hipLaunchKernelGGL(chgn_apply_kernel<0>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)x, nullptr, T, C,
+                     mean, rstd, gamma, beta, nullptr, (bf16*)y);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_chgn_gelu_bwd(const void* x, const void* dy, int B, int T, int C, const float* gamma, const float* beta,
+                        const float* mean, const float* rstd, void* ws, void* dx, float* dgamma, float* dbeta,
+                        hipStream_t stream) {
+  if (!shape_ok(B, T, C)) return TRIAD_EINVAL;
+  const int nchunk = (T + CHUNK - 1) / CHUNK;
+  float2* part = (float2*)ws;
+  float2* coef = part + (size_t)B * nchunk * C;
+  double2* tot = (double2*)(coef + (size_t)B * C);
+  hipLaunchKernelGGL(chgn_sums_kernel<1>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)x, (const bf16*)dy,
+                     T, C, mean, rstd, gamma, beta, part);
+  hipLaunchKernelGGL(chgn_bwd_coef_kernel, dim3((C + 255) / 256, B), dim3(256), 0, stream, part, nchunk, T, C, gamma,
+                     coef, tot);
+  hipLaunchKernelGGL(chgn_param_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, tot, B, C, dgamma, dbeta);
+  hipLaunchKernelGGL(chgn_apply_kernel<1>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)x, (const bf16*)dy, T,
+                     C, mean, rstd, gamma, beta, coef, (bf16*)dx);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+}  // extern "C"

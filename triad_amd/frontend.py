@@ -1,0 +1,255 @@
+"""Convolutional front-ends of the backbones, executed as GEMMs (no MIOpen).
+
+The reference's audio path (SajayR/TRIAD model.py:29-30,64-66) runs HuBERT's conv
+feature encoder -- 7 strided conv1d layers over the 64 000-sample waveform, layer 0
+followed by GroupNorm(512 groups) and GELU, the others by GELU -- and its visual path
+(model.py:218-227) a 14x14 / stride-14 patch-embedding conv. On MI355X these are
+re-expressed without changing their parameters or math:
+
+  * every conv layer is im2col + ONE hipBLASLt GEMM over channels-last (B, T, C) tensors
+    (`conv1d_gemm`; M = B*T_out rows, K = kernel*C_in): MIOpen, its NCHW<->NHWC transposes
+    and its per-shape kernel search / runtime compilation on a fresh box are gone;
+  * layer 0's GroupNorm + GELU is one fused HIP kernel pair over the channels-last conv
+    output (`triad_chgn_gelu_fwd/bwd`, csrc/frontend.hip), writing the bf16 value the next
+    conv reads instead of fp32 GroupNorm and GELU tensors;
+  * the patch embedding is a reshape (non-overlapping patches) + one GEMM.
+
+The GEMMs run in the autocast dtype (bf16) with fp32 accumulation, as autocast would run
+the convolutions. On a CPU tensor the original transformers modules run unchanged.
+"""
+from __future__ import annotations
+
+import types
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr
+
+
+def _compute_dtype(x):
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        return torch.get_autocast_dtype("cuda")
+    return x.dtype
+
+
+class _Conv1dGemm(torch.autograd.Function):
+    """y[b, t, o] = sum_{j, c} x[b, s*t + j, c] * w[o, c, j] (+ bias[o]): a 'valid' strided
+    conv1d over channels-last x (B, T, C), as im2col (cols[b, t, j, c]) + one GEMM with the
+    weight viewed as wr[o, j*C + c]."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, need_dx, cd):
+        B, T, C = x.shape
+        O, Cw, k = w.shape
+        if Cw != C:
+            raise ValueError(f"conv1d_gemm: weight expects {Cw} input channels, got {C}")
+        To = (T - k) // stride + 1
+        if To <= 0:
+            raise ValueError("conv1d_gemm: input shorter than the kernel")
+        xc = x.to(cd)
+        if C == 1:
+            cols = xc.reshape(B, T).unfold(1, k, stride).reshape(B * To, k)
+        else:
+            cols4 = torch.empty(B, To, k, C, dtype=cd, device=x.device)
+            span = stride * (To - 1) + 1
+            for j in range(k):
+                cols4[:, :, j].copy_(xc[:, j:j + span:stride])
+            cols = cols4.view(B * To, k * C)
+        wr = w.to(cd).permute(0, 2, 1).reshape(O, k * C)
+        if bias is None:
+            y = torch.mm(cols, wr.t())
+        else:
+            y = torch.addmm(bias.to(cd), cols, wr.t())
+        ctx.save_for_backward(cols, wr)
+        ctx.shape = (B, T, C, O, k, To, stride)
+        ctx.need_dx, ctx.has_bias, ctx.w_dtype, ctx.x_dtype = need_dx, bias is not None, w.dtype, x.dtype
+        ctx.b_dtype = bias.dtype if bias is not None else None
+        return y.view(B, To, O)
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, wr = ctx.saved_tensors
+        B, T, C, O, k, To, stride = ctx.shape
+        dy2 = dy.reshape(B * To, O).to(cols.dtype)
+        dw = torch.mm(dy2.t(), cols).view(O, k, C).permute(0, 2, 1).to(ctx.w_dtype)
+        acc = torch.float32 if dy2.dtype in (torch.bfloat16, torch.float16) else dy2.dtype
+        db = torch.sum(dy2, 0, dtype=acc).to(ctx.b_dtype) if ctx.has_bias else None
+        dx = None
+        if ctx.need_dx:
+            dcols = torch.mm(dy2, wr).view(B, To, k, C)
+            dx = torch.zeros(B, T, C, dtype=cols.dtype, device=cols.device)
+            span = stride * (To - 1) + 1
+            for j in range(k):
+                dx[:, j:j + span:stride] += dcols[:, :, j]
+            dx = dx.to(ctx.x_dtype)
+        return dx, dw, db, None, None, None
+
+
+def conv1d_gemm(x, weight, bias, stride, need_dx=True):
+    """Channels-last strided conv1d (no padding, dilation 1, groups 1) as im2col + GEMM."""
+    return _Conv1dGemm.apply(x, weight, bias, int(stride), bool(need_dx), _compute_dtype(x))
+
+
+class _ChannelGroupNormGelu(torch.autograd.Function):
+    """gelu(GroupNorm(num_groups=C)(x)) over channels-last x (B, T, C) bf16 -> bf16 (HIP)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        B, T, C = x.shape
+        xc = x.contiguous()
+        dev = x.device
+        g = gamma.detach().float().contiguous()
+        b = beta.detach().float().contiguous()
+        mean = torch.empty(B, C, dtype=torch.float32, device=dev)
+        rstd = torch.empty(B, C, dtype=torch.float32, device=dev)
+        ws = torch.empty(int(call("triad_chgn_workspace_bytes", B, T, C)), dtype=torch.uint8, device=dev)
+        y = torch.empty_like(xc)
+        call("triad_chgn_gelu_fwd", ptr(xc), B, T, C, ptr(g), ptr(b), float(eps), ptr(mean), ptr(rstd), ptr(ws),
+             ptr(y), stream_ptr(dev))
+        ctx.save_for_backward(xc, g, b, mean, rstd)
+        ctx.dtypes = (gamma.dtype, beta.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, g, b, mean, rstd = ctx.saved_tensors
+        B, T, C = xc.shape
+        dev = xc.device
+        dyc = dy.to(xc.dtype).contiguous()
+        dx = torch.empty_like(xc)
+        dg = torch.empty(C, dtype=torch.float32, device=dev)
+        db = torch.empty(C, dtype=torch.float32, device=dev)
+        ws = torch.empty(int(call("triad_chgn_workspace_bytes", B, T, C)), dtype=torch.uint8, device=dev)
+        call("triad_chgn_gelu_bwd", ptr(xc), ptr(dyc), B, T, C, ptr(g), ptr(b), ptr(mean), ptr(rstd), ptr(ws),
+             ptr(dx), ptr(dg), ptr(db), stream_ptr(dev))
+        return dx, dg.to(ctx.dtypes[0]), db.to(ctx.dtypes[1]), None
+
+
+def channel_group_norm_gelu(x, gamma, beta, eps):
+    """GroupNorm(C groups, affine) + exact GELU, channels-last bf16 on the HIP device."""
+    if not x.is_cuda or x.dtype != torch.bfloat16:
+        raise _lib.TriadError("channel_group_norm_gelu runs on a HIP device over bf16 input")
+    return _ChannelGroupNormGelu.apply(x, gamma, beta, float(eps))
+
+
+def _hubert_feature_encoder_forward(self, input_values):
+    """transformers HubertFeatureEncoder.forward in channels-last GEMM form. Returns the
+    (B, C, T) feature map as a transposed view of (B, T, C) storage (HubertModel transposes it
+    straight back). The waveform gets no gradient (the reference only marks it for gradient
+    checkpointing)."""
+    if not input_values.is_cuda:
+        return self._triad_hf_forward(input_values)
+    h = input_values.unsqueeze(-1)
+    cd = _compute_dtype(h)
+    for i, layer in enumerate(self.conv_layers):
+        conv = layer.conv
+        y = conv1d_gemm(h, conv.weight, conv.bias, conv.stride[0], need_dx=i > 0)
+        norm = getattr(layer, "layer_norm", None)
+        if isinstance(norm, nn.GroupNorm) and cd == torch.bfloat16:
+            h = channel_group_norm_gelu(y, norm.weight, norm.bias, norm.eps)
+        elif isinstance(norm, nn.GroupNorm):
+            h = layer.activation(F.group_norm(y.transpose(1, 2), norm.num_groups, norm.weight, norm.bias,
+                                              norm.eps).transpose(1, 2))
+        elif isinstance(norm, nn.LayerNorm):
+            h = layer.activation(F.layer_norm(y, norm.normalized_shape, norm.weight, norm.bias, norm.eps))
+        else:
+            h = layer.activation(y)
+    return h.transpose(1, 2)
+
+
+class _PosConv(torch.autograd.Function):
+    """Grouped conv1d(C, C, K=128, padding=pad, groups) over channels-last x (B, T, C), first T
+    outputs (HubertSamePadLayer drops the last): forward and input gradient by the implicit-GEMM
+    HIP kernel (triad_posconv), weight gradient by aten.convolution_backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, groups, pad):
+        B, T, C = x.shape
+        Co, Cg, K = w.shape
+        if Co != C or Cg * groups != C or K != 128:
+            raise _lib.TriadError("posconv: expects Conv1d(C, C, 128, groups) weights")
+        xb = x.to(torch.bfloat16).contiguous()
+        wb = w.to(torch.bfloat16)
+        wt = wb.view(groups, Cg, Cg, K).permute(0, 1, 3, 2).reshape(groups, Cg, K * Cg).contiguous()
+        bf = None if bias is None else bias.detach().float().contiguous()
+        y = torch.empty_like(xb)
+        call("triad_posconv", ptr(xb), ptr(wt), ptr(bf), ptr(y), B, T, C, groups, pad, stream_ptr(x.device))
+        ctx.save_for_backward(xb, wb)
+        ctx.groups, ctx.pad, ctx.has_bias = groups, pad, bias is not None
+        ctx.dtypes = (x.dtype, w.dtype, None if bias is None else bias.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb = ctx.saved_tensors
+        B, T, C = xb.shape
+        G, pad = ctx.groups, ctx.pad
+        Co, Cg, K = wb.shape
+        dyb = dy.to(torch.bfloat16).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wtb = wb.view(G, Cg, Cg, K).flip(-1).permute(0, 2, 3, 1).reshape(G, Cg, K * Cg).contiguous()
+            dx = torch.empty_like(dyb)
+            call("triad_posconv", ptr(dyb), ptr(wtb), None, ptr(dx), B, T, C, G, K - 1 - pad, stream_ptr(xb.device))
+            dx = dx.to(ctx.dtypes[0])
+        if ctx.needs_input_grad[1]:
+            # the conv's full output has T_full = T + 2*pad - K + 1 steps; the dropped tail gets 0
+            t_full = T + 2 * pad - K + 1
+            dy_full = torch.zeros(B, t_full, C, dtype=torch.bfloat16, device=dyb.device)
+            dy_full[:, :T] = dyb
+            x4 = xb.transpose(1, 2).unsqueeze(2)          # (B, C, 1, T), channels-last storage
+            dy4 = dy_full.transpose(1, 2).unsqueeze(2)
+            dw = torch.ops.aten.convolution_backward(dy4, x4, wb.unsqueeze(2), None, [1, 1], [0, pad], [1, 1],
+                                                     False, [0, 0], G, [False, True, False])[1]
+            dw = dw.squeeze(2).to(ctx.dtypes[1])
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = torch.sum(dyb.view(B * T, C), 0, dtype=torch.float32).to(ctx.dtypes[2])
+        return dx, dw, db, None, None
+
+
+def _hubert_pos_conv_forward(self, hidden_states):
+    """transformers HubertPositionalConvEmbedding.forward (conv -> SamePad -> GELU) on the
+    channels-last (B, T, C) hidden state, without the two transposes."""
+    conv = self.conv
+    if not hidden_states.is_cuda or getattr(self, "batch_norm", None) is not None \
+            or _compute_dtype(hidden_states) != torch.bfloat16 or conv.kernel_size[0] != 128 \
+            or getattr(self.padding, "num_pad_remove", 1) != 1:
+        return self._triad_hf_forward(hidden_states)
+    y = _PosConv.apply(hidden_states, conv.weight, conv.bias, conv.groups, conv.padding[0])
+    return self.activation(y)
+
+
+def install_hubert_frontend(hubert):
+    """Route a transformers HubertModel's conv feature encoder through the GEMM form above
+    (CUDA tensors only; parameters and state_dict unchanged)."""
+    fe = getattr(hubert, "feature_extractor", None)
+    if fe is None or not hasattr(fe, "conv_layers"):
+        return hubert
+    for layer in fe.conv_layers:
+        c = layer.conv
+        if c.padding[0] != 0 or c.dilation[0] != 1 or c.groups != 1:
+            return hubert  # not the HuBERT layout: leave it alone
+    fe._requires_grad = False
+    fe._triad_hf_forward = fe.forward
+    fe.forward = types.MethodType(_hubert_feature_encoder_forward, fe)
+    pce = getattr(getattr(hubert, "encoder", None), "pos_conv_embed", None)
+    if pce is not None and isinstance(getattr(pce, "conv", None), nn.Conv1d):
+        pce._triad_hf_forward = pce.forward
+        pce.forward = types.MethodType(_hubert_pos_conv_forward, pce)
+    return hubert
+
+
+def patch_embed(x, weight, bias, patch):
+    """Conv2d(C, dim, kernel=patch, stride=patch) over (B, C, H, W) -> (B, N, dim) tokens in
+    row-major patch order (= conv(x).flatten(2).transpose(1, 2)): non-overlapping patches are a
+    reshape, so the conv is one GEMM with the weight viewed as (dim, C*patch*patch)."""
+    B, C, H, W = x.shape
+    gh, gw = H // patch, W // patch
+    cd = _compute_dtype(x)
+    xc = x[:, :, :gh * patch, :gw * patch].to(cd)
+    cols = xc.reshape(B, C, gh, patch, gw, patch).permute(0, 2, 4, 1, 3, 5).reshape(B, gh * gw, C * patch * patch)
+    w = weight.reshape(weight.shape[0], -1).to(cd)
+    return F.linear(cols, w, None if bias is None else bias.to(cd))

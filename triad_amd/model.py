@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import ops
+from . import frontend, ops
 from .vit import DinoVisionTransformer, apply_lora, store_frozen_base_bf16
 
 warnings.filterwarnings("ignore", message=".*torch.cuda.amp.*")
@@ -101,38 +101,13 @@ def _project(emb, h):
     return ops.projection_head(h, emb.projection1, emb.layer_norm, emb.projection2)
 
 
-def _conv1d_channels_last_forward(self, x):
-    """nn.Conv1d.forward as conv2d over (B, C, 1, T) in channels-last memory format: MIOpen
-    then runs its NHWC kernels directly instead of transposing NCHW in and out around every
-    call. Same parameters, same math; returns a (B, C_out, T_out) view of NHWC storage."""
-    x4 = x.unsqueeze(2)
-    if not x4.is_contiguous(memory_format=torch.channels_last):
-        x4 = x4.contiguous(memory_format=torch.channels_last)
-    y = F.conv2d(x4, self.weight.unsqueeze(2), self.bias, stride=(1, self.stride[0]),
-                 padding=(0, self.padding[0]), dilation=(1, self.dilation[0]), groups=self.groups)
-    return y.squeeze(2)
-
-
 def hubert_execution_tweaks(hubert):
-    """Execution-only changes to the HF HuBERT feature encoder (results unchanged):
-    * HubertFeatureEncoder.forward marks the raw waveform requires_grad=True in training (a
-      gradient-checkpointing workaround, modeling_hubert.py): autograd then computes a
-      waveform gradient nobody reads -- a C_in = 1 backward-data convolution per step.
-      `_requires_grad = False` skips that marking (it has no other use);
-    * conv layers after the first (no GroupNorm between them) run channels-last;
-    * so does the encoder's positional convolution (k=128, 16 groups, weight-normalised): its
-      input is the (B, T, C) hidden state transposed, i.e. already channels-last in memory."""
-    fe = getattr(hubert, "feature_extractor", None)
-    if fe is None:
-        return hubert
-    fe._requires_grad = False
-    for i, layer in enumerate(getattr(fe, "conv_layers", [])):
-        if i > 0 and hasattr(layer, "conv") and not hasattr(layer, "layer_norm"):
-            layer.conv.forward = types.MethodType(_conv1d_channels_last_forward, layer.conv)
-    pce = getattr(getattr(hubert, "encoder", None), "pos_conv_embed", None)
-    if pce is not None and isinstance(getattr(pce, "conv", None), nn.Conv1d):
-        pce.conv.forward = types.MethodType(_conv1d_channels_last_forward, pce.conv)
-    return hubert
+    """Execution-only changes to the HF HuBERT model (results unchanged up to summation order):
+    the conv feature encoder runs as channels-last im2col + GEMM with a fused HIP GroupNorm +
+    GELU for layer 0, and the positional convolution as an implicit-GEMM HIP kernel
+    (triad_amd.frontend) -- no MIOpen; the raw waveform gets no gradient (HF marks it
+    requires_grad only as a gradient-checkpointing workaround)."""
+    return frontend.install_hubert_frontend(hubert)
 
 
 class AudioEmbedder(nn.Module):

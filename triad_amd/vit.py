@@ -19,6 +19,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .frontend import patch_embed
+
 ARCHS = {
     # name: (embed_dim, depth, heads)
     "dinov2_vits14_reg": (384, 12, 6),
@@ -103,7 +105,8 @@ class PatchEmbed(nn.Module):
         self.proj = nn.Conv2d(3, dim, kernel_size=patch, stride=patch)
 
     def forward(self, x):
-        return self.proj(x).flatten(2).transpose(1, 2)
+        # = self.proj(x).flatten(2).transpose(1, 2), as one GEMM over the reshaped patches
+        return patch_embed(x, self.proj.weight, self.proj.bias, self.proj.stride[0])
 
 
 class DinoVisionTransformer(nn.Module):
