@@ -164,3 +164,55 @@ def test_gemm_layouts_vs_torch(kcontig, bk):
          stream_ptr())
     torch.cuda.synchronize()
     np.testing.assert_allclose(C.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("temp", [-0.8, 0.35])
+def test_tv_head_any_temperature_sign(temp):
+    """The forward folds sgn(temp) into the query fragments and works on |temp|-scaled values
+    (pairsim_fwd.hip): negative temperatures turn max into min of the raw dot products."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(300)
+    B, Nt, Nv = 8, 16, 40
+    T = _rand_feats(g, (B, Nt, 512))
+    V = _rand_feats(g, (B, Nv, 512))
+    mask = (torch.arange(Nt)[None, :] < torch.randint(1, Nt + 1, (B, 1), generator=g)).long()
+    thr, w = 0.005, 0.3
+    Tr, Vr = T.double().requires_grad_(True), V.double().requires_grad_(True)
+    tr = torch.tensor(temp, dtype=torch.float64, requires_grad=True)
+    total, stats = ref_cpu.tv_loss(Tr, Vr, mask, tr, thr, w)
+    total.backward()
+    Tg = T.to(dev, torch.bfloat16).requires_grad_(True)
+    Vg = V.to(dev, torch.bfloat16).requires_grad_(True)
+    tg = torch.tensor(temp, device=dev, requires_grad=True)
+    losses, st, clip = ops.contrastive_head(ops.TV, Tg, Vg, tg, q_mask=mask.to(dev), threshold=thr,
+                                            sparsity_weight=w)
+    losses[0].backward()
+    assert _scalar_close(float(losses[0]), float(total))
+    _check_grad(Tg.grad, Tr.grad.numpy())
+    _check_grad(Vg.grad, Vr.grad.numpy())
+    assert _scalar_close(float(tg.grad), float(tr.grad), 2e-3, 1e-5)
+
+
+def test_av_head_below_clamp_window():
+    """Large features: many S < -60, so the forward's fast unit-gradient form is corrected on
+    most tiles (epi_fixup) -- losses, gradients and d/dtemp still match the oracle."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(400)
+    B, Na, Nv = 6, 49, 64
+    A = (torch.randn(B, Na, 512, generator=g) * 1.4).to(torch.bfloat16).float()
+    V = (torch.randn(B, Nv, 512, generator=g) * 1.4).to(torch.bfloat16).float()
+    Ar, Vr = A.double().requires_grad_(True), V.double().requires_grad_(True)
+    tr = torch.tensor(1.5, dtype=torch.float64, requires_grad=True)
+    total, ce, reg, sm, stats = ref_cpu.av_loss(Ar, Vr, tr)
+    total.backward()
+    Ag = A.to(dev, torch.bfloat16).requires_grad_(True)
+    Vg = V.to(dev, torch.bfloat16).requires_grad_(True)
+    tg = torch.tensor(1.5, device=dev, requires_grad=True)
+    losses, st, clip = ops.contrastive_head(ops.AV, Ag, Vg, tg)
+    losses[0].backward()
+    lv = torch.stack([x.detach() for x in losses]).cpu().double().numpy()
+    for got, want in zip(lv, (total, ce, reg, sm)):
+        assert _scalar_close(float(got), float(want)), (got, float(want))
+    _check_grad(Ag.grad, Ar.grad.numpy())
+    _check_grad(Vg.grad, Vr.grad.numpy())
+    assert _scalar_close(float(tg.grad), float(tr.grad), 2e-3, 1e-5)

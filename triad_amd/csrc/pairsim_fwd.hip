@@ -21,15 +21,32 @@ namespace {
 
 constexpr int D = 512;
 constexpr int NS = D / 16;  // 32 k-steps
-constexpr int WAVES = 8;
-constexpr int ROWS_PER_WG = 32 * WAVES;  // 256, as pairsim_kernel (same grid / partial arrays)
+#ifndef FWD_WAVES
+#define FWD_WAVES 8  // waves per workgroup (8: one workgroup per CU; 4: two, NBUF must be 2)
+#endif
+#ifndef FWD_NBUF
+#define FWD_NBUF 3   // key-tile LDS ring slots (prefetch distance NBUF - 1)
+#endif
+#ifndef FWD_LDSPF
+#define FWD_LDSPF 2  // key fragments read from LDS ahead of their MFMA
+#endif
+#ifndef FWD_NT
+#define FWD_NT 0     // 1: dS stores non-temporal
+#endif
+constexpr int WAVES = FWD_WAVES;
+constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 at 8 waves, as pairsim_kernel (same grid / partial arrays)
 constexpr int KT_ELEMS = 32 * D;
-constexpr int NBUF = 3;
+constexpr int NBUF = FWD_NBUF;
+static_assert(NBUF == 2 || NBUF == 3, "ring of 2 or 3 key tiles");
 constexpr int GLDS_PER_TILE = 32 / WAVES;  // 1-KB LDS-DMA pieces per wave per key tile (4)
 
 // tuning knobs (A/B builds, tools/build_variants.py)
 #ifndef FWD_SETPRIO
 #define FWD_SETPRIO 0  // 1: waves 4-7 at s_setprio 1 (MI355X_MICROARCH.md "two waves per SIMD" item 4)
+#endif
+#ifndef FWD_EXPERIMENT
+#define FWD_EXPERIMENT 0  // A/B timing only (results wrong): 1 = no key DMA after the prologue,
+                          // 2 = no epilogue elements, 4 = no dS stores
 #endif
 #ifndef FWD_REGION
 #define FWD_REGION 2  // k-steps per scheduling region (sched_barrier spacing; 2 measured best)
@@ -90,7 +107,11 @@ __device__ __forceinline__ void stage_tile(i32x4 kr, const FwdArgs& a, bf16* dst
 // s_nop 1 covers the store-data read (cdna_hip_programming.md §5.7). Counted in sync_tile.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void store16(void* p, u32x4 v) {
+#if FWD_NT
+  asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#else
   asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#endif
 }
 
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {  // one v_cvt_pk_bf16_f32
@@ -99,37 +120,106 @@ __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {  // one v_
   return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
 }
 
+// The epilogue works on u = sgn(temp) * <q, k> (the sign folded into the query fragments
+// once per launch) so that S = su * u with su = |temp| > 0 (su = 1, u = 0 when temp == 0):
+// max / argmax of S are those of u (rounding is monotone: rowmax = su * max u exactly), and
+// clamp(S, lo, 0) = su * clamp(u, lo / su, 0). Per element that leaves compare + 2 selects
+// (max / argmax), one med3 and half a packed FMA / multiply / convert -- no temperature
+// multiply, no per-element SGPR-to-VGPR key moves (argmax within a tile is an inline
+// constant, merged once per tile).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 struct Epi {  // per-lane epilogue state (one 32-row block)
-  float m;
-  int am;   // argmax within the sample, without the 4h lane part (added at the sample's end)
-  int lim;  // masked tiles: valid keys of the tile minus 4h
-  float nn, st;
-  float prev;  // previous element's unit dS (pairs into one bf16x2)
+  float m;    // running max of u over the current key sample
+  float m0;   // m when the current tile's epilogue started
+  int am;     // argmax within the sample, without the 4h lane part (added at the sample's end)
+  int at;     // vkey of the tile's best element (valid when m > m0)
+  int lim;    // masked tiles: valid keys of the tile minus 4h
+  f32x2 nn2;  // sum of c^2 over the tile, c = clamp(u, lo/su, 0) (pairs of elements)
+  float mn;   // min u over the tile: any u < lo/su sends the tile through epi_fixup
+  float prev;  // previous element's c (pairs into one packed op)
   unsigned pk[8];
 };
 
 // key offset of accumulator element v inside a 32-key tile, without the 4h lane part
 __device__ __forceinline__ constexpr int vkey(int v) { return (v & 3) + 8 * (v >> 2); }
 
-// One element of a tile's epilogue (~9 VALU). FULL: every key of the tile is valid (no mask;
-// padded query rows are zero vectors, S = 0, and add nothing). key = 32 kb + vkey(v), uniform.
+// One element of a tile's epilogue. FULL: every key of the tile is valid (no mask; padded
+// query rows are zero vectors, u = 0, and add nothing). Fast form of the unit l_nonneg
+// gradient: d = su * c, exact unless some u < lo/su (then c = lo/su but d = 0) -- the tile
+// minimum tracked here detects that and epi_fixup redoes d for such (rare) tiles.
+// Plain VALU ops as asm: the compiler canonicalises NaNs around fminf/fmaxf/med3-with-inf
+// (extra v_max x, x per operand) and splits the packed f32 ops into scalar ones.
+__device__ __forceinline__ float min3f(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float maxf(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f32x2 pk_fma_sq(f32x2 c, f32x2 acc) {  // acc + c * c
+  asm("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(acc) : "v"(c));
+  return acc;
+}
+__device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) {
+  f32x2 r;
+  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Empty volatile asm that "modifies" v: the value is computed before this point and stays in
+// place (keeps the epilogue interleaved with the MFMA chain instead of sunk past it).
+#define PIN(v) asm volatile("" : "+v"(v))
+
 template <bool TRAIN, bool FULL>
-__device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, float temp, float lo, int key) {
-  if constexpr (!FULL) asm volatile("" : "+v"(e.lim));  // keep the 16 masks from being hoisted
-  const float raw = p[v];
-  const float s = raw * temp;
-  const bool better = (FULL || vkey(v) < e.lim) && s > e.m;  // keys ascend with v: strict >
-  e.m = better ? s : e.m;                                     // keeps the first index
-  e.am = better ? key : e.am;
-  // padded keys are zero vectors (s = 0): they add nothing below without a mask
-  const float c = __builtin_amdgcn_fmed3f(s, lo, 0.f);
-  e.nn = fmaf(c, c, e.nn);
-  if constexpr (TRAIN) {
-    const float d = (c == s) ? s : 0.f;  // S on [lo, 0]: unit grad of the l_nonneg term
-    e.st = fmaf(d, raw, e.st);
-    if (v & 1) e.pk[v >> 1] = pack_bf16x2(e.prev, d);
-    else e.prev = d;
+__device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 su2, float lo) {
+  const float u = p[v];
+  if constexpr (FULL) {
+    e.at = u > e.m ? vkey(v) : e.at;  // keys ascend with v: strict > keeps the first index
+    e.m = maxf(u, e.m);
+  } else {
+    PIN(e.lim);  // keep the 16 masks from being hoisted
+    const bool better = vkey(v) < e.lim && u > e.m;
+    e.m = better ? u : e.m;
+    e.at = better ? vkey(v) : e.at;
   }
+  // padded keys are zero vectors (u = 0): they add nothing below without a mask
+  const float c = __builtin_amdgcn_fmed3f(u, lo, 0.f);
+  if (v & 1) {
+    const f32x2 cc = {e.prev, c};
+    e.nn2 = pk_fma_sq(cc, e.nn2);
+    PIN(e.nn2);
+    if constexpr (TRAIN) {
+      e.mn = min3f(e.mn, p[v - 1], u);
+      const f32x2 d = pk_mul(cc, su2);
+      e.pk[v >> 1] = pack_bf16x2(d.x, d.y);
+      PIN(e.mn);
+      PIN(e.pk[v >> 1]);
+    }
+  } else {
+    e.prev = c;
+    PIN(e.prev);
+  }
+  PIN(e.m);
+  PIN(e.at);
+}
+
+// Slow form for a tile with some u < lo/su: d = su * u on [lo/su, 0], else 0; returns the
+// tile's sum of d^2 / su^2 (the fast form's sum of c^2 over-counts the clamped elements).
+__device__ __forceinline__ float epi_fixup(Epi& e, const f32x16& p, float su, float lo) {
+  float st = 0.f, dp = 0.f;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const float u = p[v];
+    const float d = (u >= lo && u <= 0.f) ? u : 0.f;
+    st = fmaf(d, d, st);
+    if (v & 1) e.pk[v >> 1] = pack_bf16x2(dp * su, d * su);
+    else dp = d;
+  }
+  return st;
 }
 
 struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in the walk
@@ -142,7 +232,7 @@ struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in 
 };
 
 template <bool TRAIN>
-__global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
+__global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 kbuf[NBUF * KT_ELEMS + 16 * WAVES];
   double* red = (double*)(kbuf + NBUF * KT_ELEMS);
 
@@ -176,13 +266,14 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
   int fslot = 0, cslot = 0;
   auto prefetch = [&](int b2) {
-    if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j, fc.kb, wave, lane);
+    if (b2 < nblocks && (!(FWD_EXPERIMENT & 1) || b2 < 2))
+      stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j, fc.kb, wave, lane);
     fc.next(nkb);
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
   };
-  // prologue: two tiles in flight
+  // prologue: NBUF - 1 tiles in flight
   prefetch(0);
-  prefetch(1);
+  if (NBUF == 3) prefetch(1);
 
   bf16x8 qf[NS];
   {
@@ -192,7 +283,20 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   }
   // uniform (SGPR) temperature: the load completes here, not at a wait inside the loop
   const float temp = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, *a.temp)));
-  const float lo = a.clamp_lo;
+  // u = sgn(temp) <q, k>: fold the sign into the query fragments (exact bf16 sign flips; zeros
+  // for temp == 0, where S == 0 everywhere and su = 1)
+  const float su = temp != 0.f ? fabsf(temp) : 1.f;
+  if (!(temp > 0.f)) {
+    const unsigned flip = temp < 0.f ? 0x80008000u : 0u, keep = temp == 0.f ? 0u : 0xffffffffu;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      u32x4 w = __builtin_bit_cast(u32x4, qf[s]);
+      w = (w & keep) ^ flip;
+      qf[s] = __builtin_bit_cast(bf16x8, w);
+    }
+  }
+  const f32x2 su2 = {su, su};
+  const float lo = a.clamp_lo / su;  // clamp window of u
   double accd = 0.0, accd2 = 0.0;
   // lane part of the swizzled LDS fragment offsets (bytes), k-step s reads chunk 2(s&7)+h
   int xo[8];
@@ -204,31 +308,37 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   Epi e;
   e.m = -INFINITY;
   e.am = 0;
+  e.at = 0;
 
   f32x16 cA, cB;
 
   auto sync_tile = [&](int b) {
     // VMEM ops younger than tile b's DMA, at least: tile b+1's 4 pieces (if any) and, in
     // training, one epilogue's 2 dS stores (b >= 2); vmcnt counts both, in issue order
-    const bool more = b + 1 < nblocks;
-    if (TRAIN && b >= 2) {
-      if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // (3-slot ring; a 2-slot ring has no younger tile in flight)
+    const bool more = NBUF == 3 && b + 1 < nblocks;
+    const bool st = TRAIN && !(FWD_EXPERIMENT & 4) && b >= 2;
+    if (more && st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_TILE + 2) : "memory");
+    else if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_TILE) : "memory");
+    else if (st) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  auto epi_end = [&]() {
-    accd += (double)e.nn;
+  auto epi_end = [&](const f32x16& p) {
+    if (e.m > e.m0) e.am = ec.kb * 32 + e.at;  // the tile raised the running max
+    const float nn = e.nn2.x + e.nn2.y;
+    accd += (double)nn;
     if (TRAIN) {
-      accd2 += (double)e.st;
+      // some u below the window in this wave's tile: redo d (wave-uniform branch)
+      const float st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup(e, p, su, lo) : nn;
+      accd2 += (double)st;
       bf16* d = dS_w + ((long long)ec.j * nkb + ec.kb) * 1024 + lane * 16;
-      store16(d, (u32x4){e.pk[0], e.pk[1], e.pk[2], e.pk[3]});
-      store16(d + 8, (u32x4){e.pk[4], e.pk[5], e.pk[6], e.pk[7]});
+      if (!(FWD_EXPERIMENT & 4)) {
+        store16(d, (u32x4){e.pk[0], e.pk[1], e.pk[2], e.pk[3]});
+        store16(d + 8, (u32x4){e.pk[4], e.pk[5], e.pk[6], e.pk[7]});
+      }
     }
     if (ec.kb == nkb - 1) {  // end of a key sample: combine the half-waves' max / argmax
       float m = e.m;
@@ -237,7 +347,7 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
       const int am2 = __shfl_xor(am, 32);
       if (m2 > m || (m2 == m && am2 < am)) { m = m2; am = am2; }
       if (h == 0 && rok) {
-        a.rowmax[(size_t)ec.j * a.R_pad + row] = m;
+        a.rowmax[(size_t)ec.j * a.R_pad + row] = su * m;  // max S = su * max u (monotone rounding)
         a.argmax[(size_t)ec.j * a.R_pad + row] = am;
       }
       e.m = -INFINITY;
@@ -250,22 +360,22 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   // FULL or masked), one element per two k-steps
   auto iter = [&](auto CH, auto EP, auto FULLT, int b, f32x16& c, const f32x16& p) {
     constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value, full = decltype(FULLT)::value;
-    const int kbase = ec.kb * 32;
     if constexpr (ch) {
       sync_tile(b);
-      prefetch(b + 2);
+      prefetch(b + NBUF - 1);
       const char* kt = (const char*)kbuf + cslot * (KT_ELEMS * 2);
       cslot = __builtin_amdgcn_readfirstlane(cslot == NBUF - 1 ? 0 : cslot + 1);
-      bf16x8 af[3];
-      af[0] = *(const bf16x8*)(kt + xo[0]);
-      af[1] = *(const bf16x8*)(kt + xo[1]);
+      constexpr int P = FWD_LDSPF;
+      bf16x8 af[P + 1];
+#pragma unroll
+      for (int s = 0; s < P; ++s) af[s] = *(const bf16x8*)(kt + xo[s & 7] + (s >> 3) * 256);
       c = (f32x16){};
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        if (s + 2 < NS) af[(s + 2) % 3] = *(const bf16x8*)(kt + xo[(s + 2) & 7] + ((s + 2) >> 3) * 256);
-        c = mfma32(af[s % 3], qf[s], c);
-        if constexpr (ep) {
-          if (s & 1) epi_elem<TRAIN, full>(e, p, s >> 1, temp, lo, kbase + vkey(s >> 1));
+        if (s + P < NS) af[(s + P) % (P + 1)] = *(const bf16x8*)(kt + xo[(s + P) & 7] + ((s + P) >> 3) * 256);
+        c = mfma32(af[s % (P + 1)], qf[s], c);
+        if constexpr (ep && !(FWD_EXPERIMENT & 2)) {
+          if (s & 1) epi_elem<TRAIN, full>(e, p, s >> 1, su2, lo);
         }
         // scheduling regions of 4 k-steps: two epilogue elements interleave and fill each
         // other's VALU->SGPR-mask wait states
@@ -273,9 +383,9 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
       }
     } else if constexpr (ep) {
 #pragma unroll
-      for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full>(e, p, v, temp, lo, kbase + vkey(v));
+      for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full>(e, p, v, su2, lo);
     }
-    if constexpr (ep) epi_end();
+    if constexpr (ep) epi_end(p);
   };
   using T = std::true_type;
   using F = std::false_type;
@@ -283,8 +393,9 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   auto tile_full = [&]() {
     const int nk = a.klen ? min(a.klen[ec.j], a.Nk_eff) : a.Nk_eff;
     const int nv = __builtin_amdgcn_readfirstlane(nk - ec.kb * 32);
-    e.nn = 0.f;
-    e.st = 0.f;
+    e.nn2 = (f32x2){0.f, 0.f};
+    e.mn = INFINITY;
+    e.m0 = e.m;
     e.lim = (rok ? min(32, nv) : 0) - 4 * h;
     return nv >= 32;
   };
@@ -308,8 +419,9 @@ __global__ __launch_bounds__(512, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   if (threadIdx.x == 0) {
     double t = 0.0, t2 = 0.0;
     for (int w = 0; w < WAVES; ++w) { t += red[w]; t2 += red[WAVES + w]; }
-    a.part[blockIdx.y * gridDim.x + blockIdx.x] = t;
-    if (a.part2) a.part2[blockIdx.y * gridDim.x + blockIdx.x] = t2;
+    // sum clamp(S, lo, 0)^2 = su^2 sum c^2; sum S^2/temp over [lo, 0] = temp sum u^2 there
+    a.part[blockIdx.y * gridDim.x + blockIdx.x] = t * (double)su * (double)su;
+    if (a.part2) a.part2[blockIdx.y * gridDim.x + blockIdx.x] = t2 * (double)temp;
   }
 }
 
@@ -362,8 +474,9 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
   a.j_per_wg = jpw; a.temp = temp; a.clamp_lo = clamp_lo;
   a.rowmax = rowmax; a.argmax = argmax; a.part = nn_part;
   a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part; a.klen = k_len;
-  if (dS) hipLaunchKernelGGL(pairsim_fwd2_kernel<true>, dim3(xb, ys), dim3(512), 0, stream, a);
-  else hipLaunchKernelGGL(pairsim_fwd2_kernel<false>, dim3(xb, ys), dim3(512), 0, stream, a);
+  const int xw = xb * (256 / ROWS_PER_WG);  // xb counts 256-row blocks
+  if (dS) hipLaunchKernelGGL(pairsim_fwd2_kernel<true>, dim3(xw, ys), dim3(64 * WAVES), 0, stream, a);
+  else hipLaunchKernelGGL(pairsim_fwd2_kernel<false>, dim3(xw, ys), dim3(64 * WAVES), 0, stream, a);
   TRIAD_CHECK_LAUNCH();
   if (diagS && diag) {
     hipLaunchKernelGGL(diag_sim_kernel, dim3((Nq + 31) / 32, Bq), dim3(256), 0, stream, (const bf16*)Q,
