@@ -65,9 +65,11 @@ def synthetic(B, rank, device):
     g = torch.Generator(device=device).manual_seed(1234 + rank)
     frames = torch.randn(B, 3, 224, 224, generator=g, device=device)
     audio = torch.randn(B, 64000, generator=g, device=device) * 0.1
-    ids = torch.randint(1000, 30522, (B, 32), generator=g, device=device)
-    mask = torch.ones(B, 32, dtype=torch.long, device=device)
-    return frames, audio, {"input_ids": ids, "attention_mask": mask}
+    # token ids / mask stay on the host like the reference tokenizer's output (model.py:102-112);
+    # the text embedder moves them with a pinned async copy each step
+    ids = torch.randint(1000, 30522, (B, 32), generator=torch.Generator().manual_seed(1234 + rank))
+    mask = torch.ones(B, 32, dtype=torch.long)
+    return frames, audio, {"input_ids": ids.pin_memory(), "attention_mask": mask.pin_memory()}
 
 
 def pmc_traffic(kernel_prefix, grid):

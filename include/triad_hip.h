@@ -196,6 +196,20 @@ int triad_chgn_gelu_bwd(const void* x, const void* dy, int B, int T, int C, cons
 int triad_posconv(const void* x, const void* wt, const float* bias, void* y, int B, int T, int C, int groups,
                   int pad, hipStream_t stream);
 
+/* Backbone self-attention (the DINOv2 / HuBERT / DistilBERT encoders of model.py:29-30,79-80,
+ * 218-227; no dropout, no mask): O = softmax(Q K^T * scale) V per (sample, head), head dim D = 64,
+ * N <= 320. Tensors are (B, N, H, 64) bf16 in memory with the head dim contiguous: element
+ * (b, n, h, c) at b*sB + n*sN + h*64 + c. lse: [B*H][N] f32 log-sum-exp (forward output, backward
+ * input); delta: [B*H][N] f32 scratch. */
+int triad_attn_fwd(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB, long long k_sN,
+                   const void* v, long long v_sB, long long v_sN, int B, int H, int N, int D, float scale, void* out,
+                   long long out_sB, long long out_sN, float* lse, hipStream_t stream);
+int triad_attn_bwd(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB, long long k_sN,
+                   const void* v, long long v_sB, long long v_sN, const void* o, long long o_sB, long long o_sN,
+                   const void* dout, long long do_sB, long long do_sN, const float* lse, int B, int H, int N, int D,
+                   float scale, void* dq, long long dq_sB, long long dq_sN, void* dk, long long dk_sB,
+                   long long dk_sN, void* dv, long long dv_sB, long long dv_sN, float* delta, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,6 +48,9 @@ SIGNATURES = {
     "triad_chgn_gelu_fwd": [vp, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp],
     "triad_chgn_gelu_bwd": [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "triad_posconv": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
+    "triad_attn_fwd": [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, f32, vp, i64, i64, vp, vp],
+    "triad_attn_bwd": [vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i32, i32, i32,
+                       i32, f32, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, vp],
 }
 # entry points returning a value rather than a status
 RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_longlong}
@@ -106,6 +109,17 @@ def call(name, *args):
 def ptr(t):
     """Device pointer of a tensor (None -> NULL)."""
     return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def h2d(t, device):
+    """Host tensor -> device tensor without a host synchronisation: staged through pinned
+    memory (the caching host allocator keeps the block alive until the async copy is done).
+    A pageable copy would block the host until the device queue drained."""
+    import torch
+    device = torch.device(device)
+    if device.type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
 
 
 def stream_ptr(device=None):

@@ -1,0 +1,138 @@
+"""Backbone self-attention on the HIP kernels of csrc/attention.hip.
+
+The reference's encoders (SajayR/TRIAD model.py:29-30,79-80,218-227: DINOv2, HuBERT,
+DistilBERT) run softmax(Q K^T * scale) V over short sequences -- 261 visual tokens, 199 audio
+frames, 32 text tokens -- with head dim 64. PyTorch-ROCm's flash-attention kernels are tuned for
+long sequences; here each (sample, head) sequence sits in LDS and a wave keeps a whole 32-row
+tile of scores in registers (exact softmax, no online rescaling). Used for dropout-free,
+mask-free attention with N <= 320 and head dim 64 in bf16; anything else goes to
+F.scaled_dot_product_attention.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ._lib import call, ptr, stream_ptr
+
+HEAD_DIM = 64
+MAX_TOKENS = 320
+
+
+def supported(x: torch.Tensor, n: int, head_dim: int) -> bool:
+    return x.is_cuda and x.dtype == torch.bfloat16 and head_dim == HEAD_DIM and 0 < n <= MAX_TOKENS
+
+
+def _rows(t):
+    """(B, N, H, 64) view with the head dim contiguous and heads adjacent -> (sB, sN)."""
+    return t.stride(0), t.stride(1)
+
+
+def _as_bnhd(t):
+    if t.stride(3) != 1 or t.stride(2) != HEAD_DIM:
+        t = t.contiguous()
+    return t
+
+
+def _fwd(q, k, v, scale):
+    B, N, H, D = q.shape
+    out = torch.empty(B, N, H, D, dtype=torch.bfloat16, device=q.device)
+    lse = torch.empty(B * H, N, dtype=torch.float32, device=q.device)
+    call("triad_attn_fwd", ptr(q), *_rows(q), ptr(k), *_rows(k), ptr(v), *_rows(v), B, H, N, D, float(scale),
+         ptr(out), *_rows(out), ptr(lse), stream_ptr(q.device))
+    return out, lse
+
+
+def _bwd(q, k, v, out, lse, dout, scale):
+    """-> (B, N, 3, H, 64) buffer holding dq, dk, dv (a fused qkv projection's gradient layout)."""
+    B, N, H, D = q.shape
+    do = _as_bnhd(dout.to(torch.bfloat16))
+    g = torch.empty(B, N, 3, H, D, dtype=torch.bfloat16, device=q.device)
+    dq, dk, dv = g[:, :, 0], g[:, :, 1], g[:, :, 2]
+    delta = torch.empty(B * H, N, dtype=torch.float32, device=q.device)
+    call("triad_attn_bwd", ptr(q), *_rows(q), ptr(k), *_rows(k), ptr(v), *_rows(v), ptr(out), *_rows(out),
+         ptr(do), *_rows(do), ptr(lse), B, H, N, D, float(scale), ptr(dq), *_rows(dq), ptr(dk), *_rows(dk), ptr(dv),
+         *_rows(dv), ptr(delta), stream_ptr(q.device))
+    return g
+
+
+class _Attention(torch.autograd.Function):
+    """q, k, v: (B, N, H, 64) bf16 views (head dim contiguous, heads adjacent) -> O (B, N, H, 64)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        q, k, v = _as_bnhd(q), _as_bnhd(k), _as_bnhd(v)
+        out, lse = _fwd(q, k, v, scale)
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.scale = float(scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse = ctx.saved_tensors
+        g = _bwd(q, k, v, out, lse, dout, ctx.scale)
+        return g[:, :, 0], g[:, :, 1], g[:, :, 2], None
+
+
+class _AttentionQKV(torch.autograd.Function):
+    """qkv: (B, N, 3*H*64) bf16 output of a fused projection (q | k | v, heads inside each) ->
+    O (B, N, H*64); the backward returns d qkv as one tensor."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads, scale):
+        B, N, C3 = qkv.shape
+        x = qkv.contiguous().view(B, N, 3, heads, HEAD_DIM)
+        q, k, v = x[:, :, 0], x[:, :, 1], x[:, :, 2]
+        out, lse = _fwd(q, k, v, scale)
+        ctx.save_for_backward(x, out, lse)
+        ctx.scale = float(scale)
+        return out.view(B, N, heads * HEAD_DIM)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, out, lse = ctx.saved_tensors
+        B, N = x.shape[0], x.shape[1]
+        g = _bwd(x[:, :, 0], x[:, :, 1], x[:, :, 2], out, lse, dout.view(out.shape), ctx.scale)
+        return g.view(B, N, -1), None, None
+
+
+def attention_qkv(qkv, heads, scale=None):
+    """Fused-projection attention: qkv (B, N, 3*heads*64) bf16 -> (B, N, heads*64)."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(HEAD_DIM)
+    return _AttentionQKV.apply(qkv, heads, scale)
+
+
+def attention_bnhd(q, k, v, scale=None):
+    """softmax(q k^T * scale) v over (B, N, H, 64) bf16 views -> (B, N, H, 64)."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    return _Attention.apply(q, k, v, scale)
+
+
+def sdpa(q, k, v, scale=None):
+    """F.scaled_dot_product_attention(q, k, v) (no mask / dropout) for (B, H, N, d) inputs: the
+    HIP kernels when supported, else PyTorch."""
+    B, H, N, d = q.shape
+    if not supported(q, N, d) or k.shape != q.shape or v.shape != q.shape:
+        return F.scaled_dot_product_attention(q, k, v, scale=scale)
+    o = attention_bnhd(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale)
+    return o.transpose(1, 2)
+
+
+def hf_attention_forward(module, query, key, value, attention_mask, dropout=0.0, scaling=None, is_causal=None,
+                         **kwargs):
+    """transformers attention-interface function ("triad"): the HIP kernels for unmasked,
+    dropout-free attention over <= 320 tokens, else the stock sdpa implementation. Returns
+    (B, N, H, d) as the interface requires."""
+    from transformers.integrations.sdpa_attention import sdpa_attention_forward
+    B, H, N, d = query.shape
+    if (attention_mask is not None or (dropout and module.training) or kwargs.get("output_attentions")
+            or key.shape != query.shape or value.shape != query.shape or not supported(query, N, d)
+            or getattr(module, "is_causal", False)):
+        return sdpa_attention_forward(module, query, key, value, attention_mask, dropout=dropout, scaling=scaling,
+                                      is_causal=is_causal, **kwargs)
+    o = attention_bnhd(query.transpose(1, 2), key.transpose(1, 2), value.transpose(1, 2), scaling)
+    return o, None

@@ -1,0 +1,405 @@
+// Backbone self-attention for short sequences (DINOv2 / HuBERT / DistilBERT under SajayR/TRIAD
+// model.py:29-30,79-80,218-227: softmax(Q K^T * scale) V per (sample, head), head dim 64,
+// N <= 320 tokens), forward and backward, bf16 in / fp32 accumulate.
+//
+// A whole (sample, head) sequence fits in LDS, so there is no online softmax: each wave owns a
+// 32-token tile and holds all of its scores in registers.
+//   forward : wave = query tile; S^T = K Q^T (query on the lane, 10 key tiles max in VGPRs),
+//             exact row max / sum (lane-local + one half-wave exchange), O^T = V^T P^T with P^T
+//             taken straight from the score registers: the MFMA's k-index is permuted to the
+//             keys each lane already holds (k = 8h + i <-> key 16c + 4h + (i & 3) + 8 (i >> 2)),
+//             and V^T fragments are transposed LDS reads (ds_read_b64_tr_b16) of row-major V in
+//             the same key order. Writes O and the log-sum-exp per query.
+//   backward: dq kernel (wave = query tile, same orientation: recompute S, P, dP = dO V^T,
+//             dS = P (dP - D), dQ^T += K^T dS^T) and dkv kernel (wave = key tile, key on the
+//             lane: S = Q K^T, dP = dO V^T, dV += P^T dO, dK += dS^T Q), D = rowsum(dO * O).
+// LDS rows of 64 bf16 (128 B) are stored with the 16-byte chunk swizzle chunk ^ g((row >> 1) & 7),
+// g(k) = (k >> 1) | ((k & 1) << 2): conflict-free for 32-row ds_read_b128 at one chunk and for the
+// 4-row transposed reads.
+// Tensors are (B, N, H, 64) in memory with the head dimension contiguous: element (b, n, h, c)
+// at b * sB + n * sN + h * 64 + c (fused qkv projections and HF's transposed views alike).
+#include "common.h"
+
+namespace {
+
+constexpr int HD = 64;            // head dim
+constexpr int MAX_KT = 10;        // key / query tiles of 32 (N <= 320)
+constexpr float LOG2E = 1.4426950408889634f;
+
+struct AttnArgs {
+  const bf16 *q, *k, *v, *o, *dout;
+  long long q_sB, q_sN, k_sB, k_sN, v_sB, v_sN, o_sB, o_sN, do_sB, do_sN;
+  bf16 *out, *dq, *dk, *dv;
+  long long out_sB, out_sN, dq_sB, dq_sN, dk_sB, dk_sN, dv_sB, dv_sN;
+  float* lse;       // [B*H][N] natural-log log-sum-exp of the scaled scores
+  float* delta;     // [B*H][N] rowsum(dO * O)
+  int B, H, N;
+  float scale;
+};
+
+__device__ __forceinline__ int swz(int row) {
+  const int k = (row >> 1) & 7;
+  return (k >> 1) | ((k & 1) << 2);
+}
+// byte offset of (row, dim d) in a swizzled [rows][64] bf16 LDS array
+__device__ __forceinline__ int lds_off(int row, int d) { return row * 128 + (((d >> 3) ^ swz(row)) << 4) + ((d & 7) << 1); }
+
+// rows [0, 32 NT) of two (b, h) slices into swizzled LDS, zero rows >= N. Every global load is
+// issued before the first LDS write (one latency, not one per row).
+template <int NT>
+__device__ __forceinline__ void load_rows2(char* l0, const bf16* b0, long long s0, char* l1, const bf16* b1,
+                                           long long s1, int N) {
+  static_assert((NT * 32 * 8) % 256 == 0, "256 threads");
+  constexpr int PER = NT * 32 * 8 / 256;
+  bf16x8 r0[PER], r1[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = threadIdx.x + 256 * i, r = e >> 3, c = e & 7;
+    r0[i] = r < N ? *(const bf16x8*)(b0 + (long long)r * s0 + c * 8) : (bf16x8){};
+    r1[i] = r < N ? *(const bf16x8*)(b1 + (long long)r * s1 + c * 8) : (bf16x8){};
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = threadIdx.x + 256 * i, r = e >> 3, c = e & 7;
+    const int off = r * 128 + ((c ^ swz(r)) << 4);
+    *(bf16x8*)(l0 + off) = r0[i];
+    *(bf16x8*)(l1 + off) = r1[i];
+  }
+}
+
+__device__ __forceinline__ bf16x8 lds_b128(const char* lds, int row, int chunk) {
+  return *(const bf16x8*)(lds + row * 128 + ((chunk ^ swz(row)) << 4));
+}
+
+// Transposed fragment: lane l of each 16-lane group receives column (colbase + (l & 15)) of rows
+// rowbase .. rowbase + 3 (the lane supplies row rowbase + ((l & 15) >> 2), columns 4 (l & 3) ..).
+__device__ __forceinline__ s16x4 lds_tr(const char* lds, int rowbase, int colbase, int lane) {
+  const int g = lane & 15;
+  return lds_tr16(lds + lds_off(rowbase + (g >> 2), colbase + 4 * (g & 3)));
+}
+
+// A/B fragment for k = 16 permuted keys (rows) of chunk c: {rows 16c+4h .. +3, 16c+4h+8 .. +11}, column
+// colbase + (lane & 15) (+16 for lanes 16-31 of each half)
+__device__ __forceinline__ bf16x8 frag_tr(const char* lds, int c, int dimbase, int lane) {
+  const int h = lane >> 5;
+  const int col = dimbase + 16 * ((lane >> 4) & 1);
+  const s16x4 lo = lds_tr(lds, 16 * c + 4 * h, col, lane);
+  const s16x4 hi = lds_tr(lds, 16 * c + 4 * h + 8, col, lane);
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& a, int half) {
+  bf16x8 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = (bf16)a[8 * half + i];
+  return r;
+}
+
+// 16 values of accumulator element order (row (v&3) + 8(v>>2) + 4h) written as 4 runs of 4
+__device__ __forceinline__ void store_cols(bf16* dst, const f32x16& a, float mul, int h) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bf16x4 w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (bf16)(a[4 * j + i] * mul);
+    *(bf16x4*)(dst + 8 * j + 4 * h) = w;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int NKT>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * NKT * 32 * 128];
+  char* kl = lds;
+  char* vl = lds + NKT * 32 * 128;
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, ql = lane & 31;
+  load_rows2<NKT>(kl, a.k + b * a.k_sB + hh * HD, a.k_sN, vl, a.v + b * a.v_sB + hh * HD, a.v_sN, a.N);
+  __syncthreads();
+  const int qt = blockIdx.x * 4 + wave;
+  if (qt * 32 >= a.N) return;
+  const int q = qt * 32 + ql;
+  const bool qok = q < a.N;
+
+  bf16x8 qf[4];
+  {
+    const bf16* qp = a.q + b * a.q_sB + (long long)(qok ? q : 0) * a.q_sN + hh * HD + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = *(const bf16x8*)(qp + 16 * s);
+      if (!qok) qf[s] = (bf16x8){};
+    }
+  }
+  f32x16 acc[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    acc[kt] = (f32x16){};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc[kt] = mfma32(lds_b128(kl, kt * 32 + ql, 2 * s + h), qf[s], acc[kt]);
+  }
+  // keys >= N only in the last tile
+  const int nlast = a.N - (NKT - 1) * 32;
+  if (nlast < 32) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      if ((v & 3) + 8 * (v >> 2) + 4 * h >= nlast) acc[NKT - 1][v] = -INFINITY;
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) m = fmaxf(m, acc[kt][v]);
+  m = fmaxf(m, __shfl_xor(m, 32));
+  const float c2 = a.scale * LOG2E;
+  const float mo = m * c2;
+  float l = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const float p = exp2f(fmaf(acc[kt][v], c2, -mo));
+      acc[kt][v] = p;
+      l += p;
+    }
+  l += __shfl_xor(l, 32);
+
+  f32x16 o0 = {}, o1 = {};
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int c = 2 * kt + half;
+      const bf16x8 pf = pack8(acc[kt], half);
+      o0 = mfma32(frag_tr(vl, c, 0, lane), pf, o0);
+      o1 = mfma32(frag_tr(vl, c, 32, lane), pf, o1);
+    }
+  if (!qok) return;
+  const float inv = 1.f / l;
+  bf16* op = a.out + b * a.out_sB + (long long)q * a.out_sN + hh * HD;
+  store_cols(op, o0, inv, h);
+  store_cols(op + 32, o1, inv, h);
+  if (h == 0) a.lse[(long long)bh * a.N + q] = m * a.scale + logf(l);
+}
+
+// D[bh][n] = sum_c dO[b][n][h][c] * O[b][n][h][c]
+__global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a) {
+  const long long total = (long long)a.B * a.H * a.N;
+  const long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= total) return;
+  const int lane = threadIdx.x & 63;
+  const int n = (int)(e % a.N);
+  const long long bh = e / a.N;
+  const int b = (int)(bh / a.H), hh = (int)(bh % a.H);
+  const float x = (float)a.dout[b * a.do_sB + (long long)n * a.do_sN + hh * HD + lane] *
+                  (float)a.o[b * a.o_sB + (long long)n * a.o_sN + hh * HD + lane];
+  const float s = wave_sum(x);
+  if (lane == 0) a.delta[e] = s;
+}
+
+// dQ: wave = query tile, query on the lane (the forward's orientation)
+template <int NKT>
+__global__ __launch_bounds__(256, 2) void attn_dq_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * NKT * 32 * 128];
+  char* kl = lds;
+  char* vl = lds + NKT * 32 * 128;
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, ql = lane & 31;
+  load_rows2<NKT>(kl, a.k + b * a.k_sB + hh * HD, a.k_sN, vl, a.v + b * a.v_sB + hh * HD, a.v_sN, a.N);
+  __syncthreads();
+  const int qt = blockIdx.x * 4 + wave;
+  if (qt * 32 >= a.N) return;
+  const int q = qt * 32 + ql;
+  const bool qok = q < a.N;
+  bf16x8 qf[4], df[4];
+  {
+    const long long qq = qok ? q : 0;
+    const bf16* qp = a.q + b * a.q_sB + qq * a.q_sN + hh * HD + 8 * h;
+    const bf16* dp = a.dout + b * a.do_sB + qq * a.do_sN + hh * HD + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = qok ? *(const bf16x8*)(qp + 16 * s) : (bf16x8){};
+      df[s] = qok ? *(const bf16x8*)(dp + 16 * s) : (bf16x8){};
+    }
+  }
+  const float c2 = a.scale * LOG2E;
+  const float lse2 = qok ? a.lse[(long long)bh * a.N + q] * LOG2E : 0.f;
+  const float dl = qok ? a.delta[(long long)bh * a.N + q] : 0.f;
+  f32x16 g0 = {}, g1 = {};
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    f32x16 s = {}, dp = {};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      s = mfma32(lds_b128(kl, kt * 32 + ql, 2 * st + h), qf[st], s);
+      dp = mfma32(lds_b128(vl, kt * 32 + ql, 2 * st + h), df[st], dp);
+    }
+    const int nv = a.N - kt * 32;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const bool ok = qok && (v & 3) + 8 * (v >> 2) + 4 * h < nv;
+      const float p = ok ? exp2f(fmaf(s[v], c2, -lse2)) : 0.f;
+      s[v] = p * (dp[v] - dl);  // dS
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int c = 2 * kt + half;
+      const bf16x8 sf = pack8(s, half);
+      g0 = mfma32(frag_tr(kl, c, 0, lane), sf, g0);
+      g1 = mfma32(frag_tr(kl, c, 32, lane), sf, g1);
+    }
+  }
+  if (!qok) return;
+  bf16* gp = a.dq + b * a.dq_sB + (long long)q * a.dq_sN + hh * HD;
+  store_cols(gp, g0, a.scale, h);
+  store_cols(gp + 32, g1, a.scale, h);
+}
+
+// dK, dV: wave = key tile, key on the lane
+template <int NQT>
+__global__ __launch_bounds__(256, 2) void attn_dkv_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * NQT * 32 * 128];
+  __shared__ float stat[2][NQT * 32];
+  char* ql_ = lds;
+  char* dl_ = lds + NQT * 32 * 128;
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, kl = lane & 31;
+  load_rows2<NQT>(ql_, a.q + b * a.q_sB + hh * HD, a.q_sN, dl_, a.dout + b * a.do_sB + hh * HD, a.do_sN, a.N);
+  for (int i = threadIdx.x; i < NQT * 32; i += blockDim.x) {
+    const bool ok = i < a.N;
+    stat[0][i] = ok ? a.lse[(long long)bh * a.N + i] * LOG2E : INFINITY;  // p = 0 past N
+    stat[1][i] = ok ? a.delta[(long long)bh * a.N + i] : 0.f;
+  }
+  __syncthreads();
+  const int kt = blockIdx.x * 4 + wave;
+  if (kt * 32 >= a.N) return;
+  const int key = kt * 32 + kl;
+  const bool kok = key < a.N;
+  bf16x8 kf[4], vf[4];
+  {
+    const long long kk = kok ? key : 0;
+    const bf16* kp = a.k + b * a.k_sB + kk * a.k_sN + hh * HD + 8 * h;
+    const bf16* vp = a.v + b * a.v_sB + kk * a.v_sN + hh * HD + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = kok ? *(const bf16x8*)(kp + 16 * s) : (bf16x8){};
+      vf[s] = kok ? *(const bf16x8*)(vp + 16 * s) : (bf16x8){};
+    }
+  }
+  const float c2 = a.scale * LOG2E;
+  f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
+#pragma unroll 1
+  for (int qt = 0; qt < NQT; ++qt) {
+    f32x16 s = {}, dp = {};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      s = mfma32(lds_b128(ql_, qt * 32 + kl, 2 * st + h), kf[st], s);   // S[q][key]: C[row=q][col=key]
+      dp = mfma32(lds_b128(dl_, qt * 32 + kl, 2 * st + h), vf[st], dp);
+    }
+    // rows of this lane's accumulator: queries qt*32 + (v&3) + 8(v>>2) + 4h (4 runs of 4)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q0 = qt * 32 + 8 * j + 4 * h;
+      const f32x4 ls = *(const f32x4*)&stat[0][q0];
+      const f32x4 de = *(const f32x4*)&stat[1][q0];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int v = 4 * j + i;
+        const float p = kok ? exp2f(fmaf(s[v], c2, -ls[i])) : 0.f;
+        s[v] = p;
+        dp[v] = p * (dp[v] - de[i]);  // dS
+      }
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int c = 2 * qt + half;
+      const bf16x8 pf = pack8(s, half);
+      const bf16x8 sf = pack8(dp, half);
+      const bf16x8 d0 = frag_tr(dl_, c, 0, lane), d1 = frag_tr(dl_, c, 32, lane);
+      const bf16x8 q0 = frag_tr(ql_, c, 0, lane), q1 = frag_tr(ql_, c, 32, lane);
+      dv0 = mfma32(pf, d0, dv0);  // dV[key][dim]: A = P^T (key rows), B = dO (query k, dim cols)
+      dv1 = mfma32(pf, d1, dv1);
+      dk0 = mfma32(sf, q0, dk0);
+      dk1 = mfma32(sf, q1, dk1);
+    }
+  }
+  // C[row = key (v&3)+8(v>>2)+4h][col = dim (lane&31)]
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const int kr = kt * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+    if (kr < a.N) {
+      bf16* dkp = a.dk + b * a.dk_sB + (long long)kr * a.dk_sN + hh * HD + kl;
+      bf16* dvp = a.dv + b * a.dv_sB + (long long)kr * a.dv_sN + hh * HD + kl;
+      dkp[0] = (bf16)(dk0[v] * a.scale);
+      dkp[32] = (bf16)(dk1[v] * a.scale);
+      dvp[0] = (bf16)dv0[v];
+      dvp[32] = (bf16)dv1[v];
+    }
+  }
+}
+
+#define ATTN_SWITCH(KERNEL, NT, GRID, ARGS)                                                     \
+  switch (NT) {                                                                                \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, stream, ARGS); break;             \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, stream, ARGS); break;             \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, stream, ARGS); break;             \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, stream, ARGS); break;             \
+    case 5: hipLaunchKernelGGL(KERNEL<5>, GRID, dim3(256), 0, stream, ARGS); break;             \
+    case 6: hipLaunchKernelGGL(KERNEL<6>, GRID, dim3(256), 0, stream, ARGS); break;             \
+    case 7: hipLaunchKernelGGL(KERNEL<7>, GRID, dim3(256), 0, stream, ARGS); break;             \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(256), 0, stream, ARGS); break;             \
+    case 9: hipLaunchKernelGGL(KERNEL<9>, GRID, dim3(256), 0, stream, ARGS); break;             \
+    default: hipLaunchKernelGGL(KERNEL<10>, GRID, dim3(256), 0, stream, ARGS); break;           \
+  }
+
+bool attn_ok(int B, int H, int N, int D) { return B > 0 && H > 0 && N > 0 && N <= MAX_KT * 32 && D == HD; }
+
+}  // namespace
+
+extern "C" {
+
+int triad_attn_fwd(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB, long long k_sN,
+                   const void* v, long long v_sB, long long v_sN, int B, int H, int N, int D, float scale, void* out,
+                   long long out_sB, long long out_sN, float* lse, hipStream_t stream) {
+  if (!attn_ok(B, H, N, D)) return TRIAD_EINVAL;
+  AttnArgs a = {};
+  a.q = (const bf16*)q; a.q_sB = q_sB; a.q_sN = q_sN;
+  a.k = (const bf16*)k; a.k_sB = k_sB; a.k_sN = k_sN;
+  a.v = (const bf16*)v; a.v_sB = v_sB; a.v_sN = v_sN;
+  a.out = (bf16*)out; a.out_sB = out_sB; a.out_sN = out_sN;
+  a.lse = lse; a.B = B; a.H = H; a.N = N; a.scale = scale;
+  const int nt = (N + 31) / 32;
+  const dim3 grid((nt + 3) / 4, B * H);
+  ATTN_SWITCH(attn_fwd_kernel, nt, grid, a)
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_attn_bwd(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB, long long k_sN,
+                   const void* v, long long v_sB, long long v_sN, const void* o, long long o_sB, long long o_sN,
+                   const void* dout, long long do_sB, long long do_sN, const float* lse, int B, int H, int N, int D,
+                   float scale, void* dq, long long dq_sB, long long dq_sN, void* dk, long long dk_sB,
+                   long long dk_sN, void* dv, long long dv_sB, long long dv_sN, float* delta, hipStream_t stream) {
+  if (!attn_ok(B, H, N, D)) return TRIAD_EINVAL;
+  AttnArgs a = {};
+  a.q = (const bf16*)q; a.q_sB = q_sB; a.q_sN = q_sN;
+  a.k = (const bf16*)k; a.k_sB = k_sB; a.k_sN = k_sN;
+  a.v = (const bf16*)v; a.v_sB = v_sB; a.v_sN = v_sN;
+  a.o = (const bf16*)o; a.o_sB = o_sB; a.o_sN = o_sN;
+  a.dout = (const bf16*)dout; a.do_sB = do_sB; a.do_sN = do_sN;
+  a.dq = (bf16*)dq; a.dq_sB = dq_sB; a.dq_sN = dq_sN;
+  a.dk = (bf16*)dk; a.dk_sB = dk_sB; a.dk_sN = dk_sN;
+  a.dv = (bf16*)dv; a.dv_sB = dv_sB; a.dv_sN = dv_sN;
+  a.lse = (float*)lse; a.delta = delta; a.B = B; a.H = H; a.N = N; a.scale = scale;
+  const long long rows = (long long)B * H * N;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, a);
+  const int nt = (N + 31) / 32;
+  const dim3 grid((nt + 3) / 4, B * H);
+  ATTN_SWITCH(attn_dq_kernel, nt, grid, a)
+  ATTN_SWITCH(attn_dkv_kernel, nt, grid, a)
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+}  // extern "C"

@@ -222,6 +222,34 @@ def _hubert_pos_conv_forward(self, hidden_states):
     return self.activation(y)
 
 
+def _hubert_mask_hidden_states(self, hidden_states, mask_time_indices=None, attention_mask=None):
+    """transformers HubertModel._mask_hidden_states (SpecAugment in training) without host syncs:
+    the numpy-drawn masks go up through pinned memory and are applied with torch.where instead of
+    boolean-mask assignment (which needs a device->host count). Same masks, same values."""
+    if not hidden_states.is_cuda:
+        return self._triad_hf_mask(hidden_states, mask_time_indices=mask_time_indices, attention_mask=attention_mask)
+    from transformers.models.hubert.modeling_hubert import _compute_mask_indices
+    cfg = self.config
+    if not getattr(cfg, "apply_spec_augment", True):
+        return hidden_states
+    B, T, C = hidden_states.shape
+    dev = hidden_states.device
+    emb = self.masked_spec_embed.to(hidden_states.dtype)
+    if mask_time_indices is not None:
+        hidden_states = torch.where(mask_time_indices[..., None].to(dev), emb, hidden_states)
+    elif cfg.mask_time_prob > 0 and self.training:
+        m = _compute_mask_indices((B, T), mask_prob=cfg.mask_time_prob, mask_length=cfg.mask_time_length,
+                                  attention_mask=attention_mask, min_masks=cfg.mask_time_min_masks)
+        m = _lib.h2d(torch.from_numpy(m).to(torch.bool), dev)
+        hidden_states = torch.where(m[..., None], emb, hidden_states)
+    if cfg.mask_feature_prob > 0 and self.training:
+        mf = _compute_mask_indices((B, C), mask_prob=cfg.mask_feature_prob, mask_length=cfg.mask_feature_length,
+                                   min_masks=cfg.mask_feature_min_masks)
+        mf = _lib.h2d(torch.from_numpy(mf).to(torch.bool), dev)
+        hidden_states = hidden_states.masked_fill(mf[:, None, :], 0)
+    return hidden_states
+
+
 def install_hubert_frontend(hubert):
     """Route a transformers HubertModel's conv feature encoder through the GEMM form above
     (CUDA tensors only; parameters and state_dict unchanged)."""
@@ -232,6 +260,9 @@ def install_hubert_frontend(hubert):
         c = layer.conv
         if c.padding[0] != 0 or c.dilation[0] != 1 or c.groups != 1:
             return hubert  # not the HuBERT layout: leave it alone
+    if hasattr(hubert, "_mask_hidden_states"):
+        hubert._triad_hf_mask = hubert._mask_hidden_states
+        hubert._mask_hidden_states = types.MethodType(_hubert_mask_hidden_states, hubert)
     fe._requires_grad = False
     fe._triad_hf_forward = fe.forward
     fe.forward = types.MethodType(_hubert_feature_encoder_forward, fe)

@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import frontend, ops
+from . import _lib, attention, frontend, ops
 from .vit import DinoVisionTransformer, apply_lora, store_frozen_base_bf16
 
 warnings.filterwarnings("ignore", message=".*torch.cuda.amp.*")
@@ -82,10 +82,20 @@ def _hf_model(kind, name, config_overrides=None):
     cfg_cls = {"HubertModel": transformers.HubertConfig, "DistilBertModel": transformers.DistilBertConfig}[kind]
     cfg = cfg_cls(**(config_overrides or {}))
     try:
-        cfg._attn_implementation = "sdpa"
+        cfg._attn_implementation = _register_attention()
     except Exception:
         pass
     return getattr(transformers, kind)(cfg)
+
+
+def _register_attention():
+    """transformers attention-interface entry "triad": the HIP attention kernels for dropout-free,
+    unmasked short sequences, the stock sdpa function otherwise (triad_amd.attention)."""
+    from transformers import AttentionInterface
+    from transformers.masking_utils import ALL_MASK_ATTENTION_FUNCTIONS, AttentionMaskInterface
+    AttentionInterface.register("triad", attention.hf_attention_forward)
+    AttentionMaskInterface.register("triad", ALL_MASK_ATTENTION_FUNCTIONS["sdpa"])  # same masks as sdpa
+    return "triad"
 
 
 _HUBERT_LARGE = dict(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16, intermediate_size=4096,
@@ -190,8 +200,14 @@ class TextEmbedder(nn.Module):
         Returns (text_feats (B,Nt,512), attention_mask (B,Nt))."""
         inputs = dict(text_list) if isinstance(text_list, Mapping) else self.tokenize(text_list)
         device = next(self.parameters()).device
-        inputs = {k: v.to(device, non_blocking=True) for k, v in inputs.items()}
-        h = self.encoder(input_ids=inputs["input_ids"], attention_mask=inputs["attention_mask"]).last_hidden_state
+        mask = inputs["attention_mask"]
+        # A host-side mask with no padding is dropped before the encoder (identical math): HF
+        # would otherwise test it on the device (`mask.all()`, a host sync) every step.
+        no_pad = not mask.is_cuda and bool(mask.all())
+        inputs = {k: (_lib.h2d(v, device) if not v.is_cuda and device.type == "cuda" else v.to(device))
+                  for k, v in inputs.items()}
+        h = self.encoder(input_ids=inputs["input_ids"],
+                         attention_mask=None if no_pad else inputs["attention_mask"]).last_hidden_state
         return _project(self, h), inputs["attention_mask"]
 
 

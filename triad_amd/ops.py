@@ -466,8 +466,8 @@ def patch_dropout(x: torch.Tensor, keep_mask: torch.Tensor, n_out: Optional[int]
     n_out overrides the padded length (global negatives pad to the global maximum)."""
     _check_device(x)
     idx, inv, n_out = dropout_indices(keep_mask, n_out)
-    idx_d = idx.to(x.device, non_blocking=True)
-    inv_d = inv.to(x.device, non_blocking=True)
+    idx_d = _lib.h2d(idx.contiguous(), x.device)
+    inv_d = _lib.h2d(inv.contiguous(), x.device)
     return _GatherRows.apply(x.contiguous(), idx_d, inv_d)
 
 

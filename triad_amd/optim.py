@@ -26,6 +26,7 @@ from typing import Dict, Iterable, List, Sequence
 import numpy as np
 import torch
 
+from . import _lib
 from ._lib import TriadError, call, ptr, stream_ptr
 
 CHUNK = 16384
@@ -84,6 +85,7 @@ class FlatParamSpace:
         self.shadow_base = (torch.from_numpy(shadow_base.view(np.int64)).to(self.device)
                             if self.shadowed.any() else None)
         self._chunk_cache: Dict[tuple, tuple] = {}
+        self._index_cache: Dict[tuple, torch.Tensor] = {}
 
     def _mark(self, i):
         def hook(_p):
@@ -105,13 +107,25 @@ class FlatParamSpace:
             for s in range(0, n, CHUNK):
                 rows.append((self.offsets[i] + s, min(CHUNK, n - s), i))
         arr = np.array(rows, dtype=_CHUNK_DT) if rows else np.zeros(0, dtype=_CHUNK_DT)
-        dev = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device) if rows else None
-        owner = torch.tensor([r[2] for r in rows], dtype=torch.long, device=self.device) if rows else None
+        dev = _lib.h2d(torch.from_numpy(arr.view(np.uint8).copy()), self.device) if rows else None
+        owner = _lib.h2d(torch.tensor([r[2] for r in rows], dtype=torch.long), self.device) if rows else None
         out = (dev, len(rows), owner)
         if len(self._chunk_cache) > 64:
             self._chunk_cache.clear()
         self._chunk_cache[key] = out
         return out
+
+    def index_tensor(self, ids: Sequence[int]) -> torch.Tensor:
+        """Device int64 tensor of parameter ids (cached: the same few id sets recur every step,
+        and each fresh host->device copy would be a host sync)."""
+        key = tuple(ids)
+        t = self._index_cache.get(key)
+        if t is None:
+            if len(self._index_cache) > 64:
+                self._index_cache.clear()
+            t = _lib.h2d(torch.tensor(list(key), dtype=torch.long), self.device)
+            self._index_cache[key] = t
+        return t
 
     def touched_ids(self, ids: Sequence[int]):
         return [i for i in ids if self.touched[i]]
@@ -176,7 +190,7 @@ class FlatParamSpace:
             s = e + 1
         if ids:
             self.touched[ids] = False
-            self.scale.index_fill_(0, torch.tensor(ids, device=self.device), 1.0)
+            self.scale.index_fill_(0, self.index_tensor(ids), 1.0)
             for i in ids:
                 if self.shadowed[i]:
                     self.params[i].grad = None
@@ -284,7 +298,7 @@ def grad_norms(space: FlatParamSpace, groups: Dict[str, Sequence[torch.nn.Parame
     for name, params in groups.items():
         ids = [i for i in space.param_ids(params) if space.touched[i]]
         if ids:
-            out[name] = sq[torch.tensor(ids, device=space.device)].sum().sqrt().float()
+            out[name] = sq[space.index_tensor(ids)].sum().sqrt().float()
         else:
             out[name] = torch.zeros((), device=space.device)
     return out, sq
@@ -299,7 +313,7 @@ def clip_grad_norm_(space: FlatParamSpace, params, max_norm: float, sq: torch.Te
         return torch.zeros((), device=space.device)
     if sq is None:
         sq = space.param_sumsq(ids)
-    idx = torch.tensor(ids, device=space.device)
+    idx = space.index_tensor(ids)
     total = sq[idx].sum().sqrt().float()
     coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
     space.scale[idx] = space.scale[idx] * coef

@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import attention
 from .frontend import patch_embed
 
 ARCHS = {
@@ -60,7 +61,10 @@ class Attention(nn.Module):
 
     def forward(self, x):
         B, N, C = x.shape
-        qkv = self.qkv(x).reshape(B, N, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
+        qkv = self.qkv(x)
+        if attention.supported(qkv, N, C // self.heads):  # HIP kernels (triad_amd.attention)
+            return self.proj(attention.attention_qkv(qkv, self.heads))
+        qkv = qkv.reshape(B, N, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
         o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
         return self.proj(o.transpose(1, 2).reshape(B, N, C))
 
