@@ -93,3 +93,33 @@ def test_hubert_pos_conv_matches_transformers(C, G, T):
     assert _rel(xd.grad, xr.grad) < 2e-2
     for (n, p), (_, q) in zip(m.named_parameters(), ref_m.named_parameters()):
         assert _rel(p.grad, q.grad) < 3e-2, n
+
+
+@pytest.mark.parametrize("M,K,O", [(66 * 261, 768, 2304), (5 * 37, 768, 768), (3, 384, 1152)])
+def test_lora_linear_matches_reference_chain(M, K, O):
+    """ViT LoRA (triad_amd.vit._LoRALinear: rows_nt / rows_tn HIP kernels + one base GEMM and an
+    in-place rank-8 update) against the reference chain base(x) + B(A(x)) * s under bf16 autocast."""
+    from triad_amd.vit import LoRALinear
+    torch.manual_seed(M)
+    base = torch.nn.Linear(K, O).to(dev)
+    base.weight.data = base.weight.data.to(torch.bfloat16)
+    base.bias.data = base.bias.data.to(torch.bfloat16)
+    for p in base.parameters():
+        p.requires_grad = False
+    m = LoRALinear(base, 8, 16).to(dev)
+    with torch.no_grad():
+        m.lora_B.normal_(0, 0.05)
+    x = torch.randn(M, K, device=dev)
+    xr = x.clone().requires_grad_(True)
+    xd = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ref = base(xr) + torch.nn.functional.linear(torch.nn.functional.linear(xr, m.lora_A), m.lora_B) * m.scaling
+        got = m(xd)
+    assert got.dtype == torch.bfloat16 and got.shape == ref.shape
+    assert _rel(got.float(), ref.float()) < 1e-2
+    gy = torch.randn(M, O, device=dev)
+    rx, gA, gB = torch.autograd.grad((ref.float() * gy).sum(), (xr, m.lora_A, m.lora_B))
+    dx, dA, dB = torch.autograd.grad((got.float() * gy).sum(), (xd, m.lora_A, m.lora_B))
+    assert _rel(dx, rx) < 2e-2
+    assert _rel(dA, gA) < 2e-2
+    assert _rel(dB, gB) < 2e-2

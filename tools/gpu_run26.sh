@@ -1,0 +1,12 @@
+# LoRA skinny kernels + attention delta fusion: tests, bench, steady profile
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_frontend_gpu.py tests/test_attention_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/fe_tests.log 2>&1 || exit 1
+timeout -k 10 300 python tools/attn_micro.py > gpurun_out/attn_micro.log 2>&1 || exit 1
+timeout -k 10 600 python bench.py --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 1
+TRIAD_PROFILE_MARK=1 timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_bench -o bench -- python bench.py --steps 3 --warmup 2 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1 && \
+python tools/trace_summary.py gpurun_out/prof_bench/bench_kernel_trace.csv 3 gpurun_out/bench_steady_kernels.csv > gpurun_out/trace_summary.log 2>&1
+rm -f gpurun_out/prof_bench/bench_kernel_trace.csv
+echo "all done"

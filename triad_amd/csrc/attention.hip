@@ -12,7 +12,8 @@
 //             the same key order. Writes O and the log-sum-exp per query.
 //   backward: dq kernel (wave = query tile, same orientation: recompute S, P, dP = dO V^T,
 //             dS = P (dP - D), dQ^T += K^T dS^T) and dkv kernel (wave = key tile, key on the
-//             lane: S = Q K^T, dP = dO V^T, dV += P^T dO, dK += dS^T Q), D = rowsum(dO * O).
+//             lane: S = Q K^T, dP = dO V^T, dV += P^T dO, dK += dS^T Q); D = rowsum(dO * O) is
+//             formed by the dq kernel (which reads O anyway) and handed to the dkv kernel.
 // LDS rows of 64 bf16 (128 B) are stored with the 16-byte chunk swizzle chunk ^ g((row >> 1) & 7),
 // g(k) = (k >> 1) | ((k & 1) << 2): conflict-free for 32-row ds_read_b128 at one chunk and for the
 // 4-row transposed reads.
@@ -183,21 +184,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
   if (h == 0) a.lse[(long long)bh * a.N + q] = m * a.scale + logf(l);
 }
 
-// D[bh][n] = sum_c dO[b][n][h][c] * O[b][n][h][c]
-__global__ __launch_bounds__(256) void attn_delta_kernel(AttnArgs a) {
-  const long long total = (long long)a.B * a.H * a.N;
-  const long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (e >= total) return;
-  const int lane = threadIdx.x & 63;
-  const int n = (int)(e % a.N);
-  const long long bh = e / a.N;
-  const int b = (int)(bh / a.H), hh = (int)(bh % a.H);
-  const float x = (float)a.dout[b * a.do_sB + (long long)n * a.do_sN + hh * HD + lane] *
-                  (float)a.o[b * a.o_sB + (long long)n * a.o_sN + hh * HD + lane];
-  const float s = wave_sum(x);
-  if (lane == 0) a.delta[e] = s;
-}
-
 // dQ: wave = query tile, query on the lane (the forward's orientation)
 template <int NKT>
 __global__ __launch_bounds__(256, 2) void attn_dq_kernel(AttnArgs a) {
@@ -213,19 +199,25 @@ __global__ __launch_bounds__(256, 2) void attn_dq_kernel(AttnArgs a) {
   const int q = qt * 32 + ql;
   const bool qok = q < a.N;
   bf16x8 qf[4], df[4];
+  float dl = 0.f;  // D = rowsum(dO * O) of this query: the lane's 32 dims + the other half's
   {
     const long long qq = qok ? q : 0;
     const bf16* qp = a.q + b * a.q_sB + qq * a.q_sN + hh * HD + 8 * h;
     const bf16* dp = a.dout + b * a.do_sB + qq * a.do_sN + hh * HD + 8 * h;
+    const bf16* op = a.o + b * a.o_sB + qq * a.o_sN + hh * HD + 8 * h;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       qf[s] = qok ? *(const bf16x8*)(qp + 16 * s) : (bf16x8){};
       df[s] = qok ? *(const bf16x8*)(dp + 16 * s) : (bf16x8){};
+      const bf16x8 ov = qok ? *(const bf16x8*)(op + 16 * s) : (bf16x8){};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dl = fmaf((float)df[s][i], (float)ov[i], dl);
     }
   }
+  dl += __shfl_xor(dl, 32);
+  if (qok && h == 0) a.delta[(long long)bh * a.N + q] = dl;  // for the dkv kernel (launched after)
   const float c2 = a.scale * LOG2E;
   const float lse2 = qok ? a.lse[(long long)bh * a.N + q] * LOG2E : 0.f;
-  const float dl = qok ? a.delta[(long long)bh * a.N + q] : 0.f;
   f32x16 g0 = {}, g1 = {};
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
@@ -392,8 +384,6 @@ int triad_attn_bwd(const void* q, long long q_sB, long long q_sN, const void* k,
   a.dk = (bf16*)dk; a.dk_sB = dk_sB; a.dk_sN = dk_sN;
   a.dv = (bf16*)dv; a.dv_sB = dv_sB; a.dv_sN = dv_sN;
   a.lse = (float*)lse; a.delta = delta; a.B = B; a.H = H; a.N = N; a.scale = scale;
-  const long long rows = (long long)B * H * N;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, a);
   const int nt = (N + 31) / 32;
   const dim3 grid((nt + 3) / 4, B * H);
   ATTN_SWITCH(attn_dq_kernel, nt, grid, a)

@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import attention
+from ._lib import call, ptr, stream_ptr
 from .frontend import patch_embed
 
 ARCHS = {
@@ -31,6 +32,58 @@ ARCHS = {
     "dinov2_vitb14": (768, 12, 12),
     "dinov2_vitl14": (1024, 24, 16),
 }
+
+
+class _LoRALinear(torch.autograd.Function):
+    """y = x W^T + b + (s B)(A x) for a frozen base under bf16 autocast, as ONE base GEMM plus an
+    in-place rank-8 update, with the skinny products on the HIP kernels of csrc/lora.hip
+    (t = x A^T and dt = dy (s B) by triad_rows_nt; dB = s dy^T t and dA = dt^T x by
+    triad_rows_tn). Same operands and roundings class as autocast's F.linear chain; the LoRA
+    gradients accumulate in fp32."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, A, B, scaling):
+        lead, K = x.shape[:-1], x.shape[-1]
+        O, r = B.shape
+        xb = x.reshape(-1, K).to(torch.bfloat16).contiguous()
+        M = xb.shape[0]
+        dev = x.device
+        Ab = A.detach().to(torch.bfloat16).contiguous()
+        sB = (B.detach() * scaling).to(torch.bfloat16)
+        y = F.linear(xb, w.to(torch.bfloat16), None if b is None else b.to(torch.bfloat16))
+        t = torch.empty(M, r, dtype=torch.bfloat16, device=dev)
+        call("triad_rows_nt", ptr(xb), K, M, K, ptr(Ab), r, ptr(t), stream_ptr(dev))
+        y.addmm_(t, sB.t())
+        ctx.save_for_backward(xb, w, Ab, sB, t)
+        ctx.meta = (lead, x.dtype, float(scaling), A.dtype, B.dtype)
+        return y.view(*lead, O)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, w, Ab, sB, t = ctx.saved_tensors
+        lead, x_dtype, scaling, a_dtype, b_dtype = ctx.meta
+        M, K = xb.shape
+        O, r = sB.shape
+        dev = xb.device
+        dy2 = dy.reshape(M, O).to(torch.bfloat16).contiguous()
+        st = stream_ptr(dev)
+        dt = torch.empty(M, r, dtype=torch.bfloat16, device=dev)
+        call("triad_rows_nt", ptr(dy2), O, M, O, ptr(sB.t().contiguous()), r, ptr(dt), st)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2, w.to(torch.bfloat16))
+            dx.addmm_(dt, Ab)
+            dx = dx.view(*lead, K).to(x_dtype)
+        slabs = torch.empty(call("triad_rows_tn_slabs", M) * max(O, K) * r, dtype=torch.float32, device=dev)
+        dB = torch.empty(O, r, dtype=torch.float32, device=dev)
+        call("triad_rows_tn", ptr(dy2), O, M, O, ptr(t), r, scaling, ptr(slabs), ptr(dB), st)
+        dAt = torch.empty(K, r, dtype=torch.float32, device=dev)
+        call("triad_rows_tn", ptr(xb), K, M, K, ptr(dt), r, 1.0, ptr(slabs), ptr(dAt), st)
+        return dx, None, None, dAt.t().to(a_dtype), dB.to(b_dtype), None
+
+
+def lora_linear(x, w, b, A, B, scaling):
+    return _LoRALinear.apply(x, w, b, A, B, scaling)
 
 
 class LoRALinear(nn.Module):
@@ -49,6 +102,9 @@ class LoRALinear(nn.Module):
         return self.base.weight
 
     def forward(self, x):
+        if x.is_cuda and torch.is_autocast_enabled("cuda") and not self.base.weight.requires_grad \
+                and (self.base.bias is None or not self.base.bias.requires_grad) and self.lora_A.shape[0] == 8:
+            return lora_linear(x, self.base.weight, self.base.bias, self.lora_A, self.lora_B, self.scaling)
         return self.base(x) + F.linear(F.linear(x, self.lora_A), self.lora_B) * self.scaling
 
 
