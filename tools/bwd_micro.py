@@ -1,0 +1,59 @@
+"""Microbench of the backward tile GEMMs alone (triad_tile_gemm dQ = dS K and dK = dS^T Q) at
+the c3 AV / TV shapes over a random tiled dS. Loads TRIAD_LIB_VARIANT if set
+(tools/build_variants.py). Prints one JSON line per case: average ms over `iters` launches
+(HIP events) and algorithmic TFLOP/s (2 R Bk Nk_eff 512 per GEMM)."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from triad_amd import ops  # noqa: E402
+from triad_amd._lib import call, ptr, stream_ptr  # noqa: E402
+
+
+def run(B, Nq, Nk, dk, iters):
+    g = ops.Geometry(B, Nq, B, Nk)
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    q = (torch.randn(B, Nq, 512, device="cuda", generator=gen) * 0.58).to(torch.bfloat16)
+    k = (torch.randn(B, Nk, 512, device="cuda", generator=gen) * 0.58).to(torch.bfloat16)
+    Qb, Kb = ops.pack_queries(q, g), ops.pack_keys(k, g)
+    CT = ops._rup(g.C_pad // 32, 4)
+    dS = (torch.randn((g.R_pad // 32) * CT * 1024, device="cuda", generator=gen) * 1e-3).to(torch.bfloat16)
+    alpha = torch.tensor([1.5], device="cuda")
+    if dk:
+        M, nkt, Bm = CT * 32, g.R_pad // 32, Qb
+    else:
+        M, nkt, Bm = g.R_pad, g.C_pad // 32, Kb
+    sp = ops._gemm_splits(M // 128, nkt)
+    slabs = torch.empty(sp * M * 512, dtype=torch.float32, device="cuda") if sp > 1 else None
+    out = torch.empty(M, 512, dtype=torch.bfloat16, device="cuda")
+
+    def launch():
+        call("triad_tile_gemm", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream_ptr())
+    for _ in range(3):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = 2.0 * g.R * g.Bk * g.Nk_eff * 512
+    return ms, flops / ms / 1e9, sp
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tag", default=os.environ.get("TRIAD_LIB_VARIANT", "default"))
+    a = ap.parse_args()
+    for name, Nq, Nk in (("AV", 199, 212), ("TV", 32, 212)):
+        for dk in (0, 1):
+            ms, tf, sp = run(256, Nq, Nk, dk, a.iters)
+            print(json.dumps({"tag": os.path.basename(a.tag), "head": name, "gemm": "dK" if dk else "dQ",
+                              "splits": sp, "ms": round(ms, 4), "algo_TFLOPs": round(tf, 1)}), flush=True)

@@ -159,7 +159,129 @@ __global__ __launch_bounds__(512, 2) void tile_gemm_kernel(const bf16* __restric
     }
 }
 
+// Ring form of the same GEMM: stage = ONE 32-deep k tile (A 4 tiles = 8 KB, B 32 rows x 512 =
+// 32 KB), a 4-slot LDS ring (the full 160 KB) with the DMA issued three tiles ahead. Each wave
+// issues exactly RING_PIECES LDS-DMA pieces per tile, so the wait for tile `it` is a counted
+// `s_waitcnt vmcnt(RING_PIECES * younger)` (tiles it+1, it+2 stay in flight across it) followed by
+// the workgroup barrier; the slot refilled after the barrier is the one every wave finished
+// reading before it.
+constexpr int RING_NB = 4;
+constexpr int RING_ST = 4 * 1024 + TBK * TBN;  // 40 KB
+constexpr int RING_PIECES = 1 + TBK / 8;       // per wave per tile: 1 A piece + 4 B rows
+
+template <bool DK>
+__device__ __forceinline__ void stage_ring(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ B,
+                                           int mt0, int kt, bf16* dst, int wave, int lane) {
+  {
+    const int t = wave >> 1, half = wave & 1;
+    const int pos = half * 64 + lane;
+    const int c = DK ? swz_k(pos) : swz_q(pos);
+    const long long tile = DK ? ((long long)kt * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + kt);
+    glds16(Dt + tile * 1024 + c * 8, dst + t * 1024 + half * 512);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k = wave * 4 + u;
+    const int c = lane ^ ((k & 3) << 2);
+    glds16(B + ((long long)kt * TBK + k) * TBN + c * 8, dst + 4096 + k * TBN);
+  }
+}
+
+template <bool DK, bool SLAB>
+__global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __restrict__ Dt, long long CT,
+                                                                const bf16* __restrict__ B, int M, int nkt_total,
+                                                                int kt_per_split, const float* __restrict__ alpha_p,
+                                                                void* __restrict__ Cout) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[RING_NB * RING_ST];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  const int m0 = swz * TBM, mt0 = m0 / 32;
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int nkt = __builtin_amdgcn_readfirstlane(min(kt_per_split, nkt_total - kt0));
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[t][n] = (f32x16){};
+
+#pragma unroll
+  for (int p = 0; p < RING_NB - 1; ++p)
+    if (p < nkt) stage_ring<DK>(Dt, CT, B, mt0, kt0 + p, lds + p * RING_ST, wave, lane);
+  for (int it = 0; it < nkt; ++it) {
+    const int younger = min(RING_NB - 2, nkt - 1 - it);  // uniform
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RING_PIECES) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING_PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (it + RING_NB - 1 < nkt)
+      stage_ring<DK>(Dt, CT, B, mt0, kt0 + it + RING_NB - 1, lds + ((it + RING_NB - 1) % RING_NB) * RING_ST, wave,
+                     lane);
+    const bf16* As = lds + (it % RING_NB) * RING_ST;
+    const bf16* Bs = As + 4096;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[4], bf[2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16* tile = As + t * 1024;
+        if (!DK) {
+          af[t] = *(const bf16x8*)(tile + swz_q(2 * l32 + 64 * h + s) * 8);
+        } else {
+          const int a = 2 * (g & 1) + (p4 >> 1), hh = p4 & 1;
+          s16x4* rp = (s16x4*)&af[t];
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) {
+            const int qry = 16 * s + 8 * h + 4 * tt + q4;
+            const int c = (qry + 32 * hh) * 2 + (a >> 1);
+            rp[tt] = lds_tr16(tile + swz_k(c) * 8 + 4 * (a & 1));
+          }
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int n0 = wave * 64 + n * 32;
+        bf[n] = DK ? bfrag(Bs, 16 * s + 8 * h + q4, 4, n0, lane) : bfrag(Bs, 16 * s + 4 * h + q4, 8, n0, lane);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[t][n] = mfma32(af[t], bf[n], acc[t][n]);
+    }
+  }
+
+  const float alpha = SLAB ? 1.f : *alpha_p;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int col = wave * 64 + n * 32 + l32;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int m = m0 + t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        const float val = alpha * acc[t][n][v];
+        if (SLAB) ((float*)Cout)[((size_t)blockIdx.y * M + m) * TBN + col] = val;
+        else ((bf16*)Cout)[(size_t)m * TBN + col] = (bf16)val;
+      }
+    }
+}
+
 }  // namespace
+
+#ifndef TG_RING
+#define TG_RING 1  // 1: tile_gemm_ring_kernel (one k tile per stage, 4-slot ring); 0: 2-stage form
+#endif
+#if TG_RING
+#define TG_KERNEL tile_gemm_ring_kernel
+#define TG_KPS 1
+#else
+#define TG_KERNEL tile_gemm_kernel
+#define TG_KPS KPS
+#endif
 
 extern "C" {
 
@@ -170,18 +292,18 @@ int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, 
                     int splits, float* slabs, void* C, hipStream_t stream) {
   if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
   int kps = (nkt + splits - 1) / splits;
-  kps = (kps + KPS - 1) / KPS * KPS;  // whole stages per split
+  kps = (kps + TG_KPS - 1) / TG_KPS * TG_KPS;  // whole stages per split
   dim3 grid(M / TBM, splits);
   const bf16* d = (const bf16*)Dt;
   const bf16* b = (const bf16*)B;
   if (splits == 1) {
-    if (dk) hipLaunchKernelGGL((tile_gemm_kernel<true, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
-    else hipLaunchKernelGGL((tile_gemm_kernel<false, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
+    if (dk) hipLaunchKernelGGL((TG_KERNEL<true, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
+    else hipLaunchKernelGGL((TG_KERNEL<false, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
-  if (dk) hipLaunchKernelGGL((tile_gemm_kernel<true, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
-  else hipLaunchKernelGGL((tile_gemm_kernel<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
+  if (dk) hipLaunchKernelGGL((TG_KERNEL<true, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
+  else hipLaunchKernelGGL((TG_KERNEL<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
   TRIAD_CHECK_LAUNCH();
   return triad_sum_slabs(slabs, splits, (long long)M * TBN, alpha, 1, C, stream);
 }
