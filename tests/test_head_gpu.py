@@ -216,3 +216,37 @@ def test_av_head_below_clamp_window():
     _check_grad(Ag.grad, Ar.grad.numpy())
     _check_grad(Vg.grad, Vr.grad.numpy())
     assert _scalar_close(float(tg.grad), float(tr.grad), 2e-3, 1e-5)
+
+
+def _untile_dS(dS, R_pad, CT):
+    """Tiled dS ([R_pad/32][CT][1024], lane L = query L&31 / half L>>5, value v = key
+    (v&3) + 8(v>>2) + 4(L>>5), the 32x32x16 accumulator order) -> dense [R_pad][CT*32] fp32."""
+    t = dS.float().view(R_pad // 32, CT, 2, 32, 4, 4)  # rt, ct, hh, q, v>>2, v&3
+    t = t.permute(0, 3, 1, 4, 2, 5)                     # rt, q, ct, v>>2, hh, v&3 -> key 8(v>>2)+4hh+(v&3)
+    return t.reshape(R_pad, CT * 32)
+
+
+@pytest.mark.parametrize("panels,ct", [(16, 64), (7, 36), (400, 24), (3, 4)])
+def test_tile_gemm_vs_torch(panels, ct):
+    """triad_tile_gemm (ring kernel, split-K slabs where chosen) against fp32 torch matmuls of the
+    untiled dS: dQ = alpha dS K, dK = alpha dS^T Q."""
+    from triad_amd._lib import stream_ptr
+    ops = _ops()
+    g = torch.Generator(device=dev).manual_seed(panels * 100 + ct)
+    R_pad, CT = panels * 128, ct
+    dS = (torch.randn(R_pad // 32 * CT * 1024, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    K = torch.randn(CT * 32, 512, device=dev, generator=g).to(torch.bfloat16)
+    Q = torch.randn(R_pad, 512, device=dev, generator=g).to(torch.bfloat16)
+    alpha = torch.tensor([0.75], device=dev)
+    dense = _untile_dS(dS, R_pad, CT)
+    dQ = torch.empty(R_pad, 512, dtype=torch.bfloat16, device=dev)
+    ops.tile_gemm(dS, CT, 0, K, R_pad, CT, alpha, dQ, stream_ptr())
+    dK = torch.empty(CT * 32, 512, dtype=torch.bfloat16, device=dev)
+    if CT % 4 == 0:
+        ops.tile_gemm(dS, CT, 1, Q, CT * 32, R_pad // 32, alpha, dK, stream_ptr())
+    torch.cuda.synchronize()
+    refQ = 0.75 * dense @ K.float()
+    assert _rel(dQ.float().cpu(), refQ.cpu()) < 5e-3
+    if CT % 4 == 0:
+        refK = 0.75 * dense.t() @ Q.float()
+        assert _rel(dK.float().cpu(), refK.cpu()) < 5e-3

@@ -28,11 +28,10 @@ def run(B, Nq, Nk, dk, iters):
     else:
         M, nkt, Bm = g.R_pad, g.C_pad // 32, Kb
     sp = ops._gemm_splits(M // 128, nkt)
-    slabs = torch.empty(sp * M * 512, dtype=torch.float32, device="cuda") if sp > 1 else None
     out = torch.empty(M, 512, dtype=torch.bfloat16, device="cuda")
 
     def launch():
-        call("triad_tile_gemm", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream_ptr())
+        ops.tile_gemm(dS, CT, dk, Bm, M, nkt, alpha, out, stream_ptr())
     for _ in range(3):
         launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -85,6 +85,16 @@ def pack_keys(k: torch.Tensor, g: Geometry) -> torch.Tensor:
     return out
 
 
+def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream):
+    """dQ = alpha dS K (dk=0) / dK = alpha dS^T Q (dk=1) over the tiled dS (triad_tile_gemm),
+    split-K over the CUs when the row panels alone leave them idle. (A stream-K form -- one run
+    of (row panel, k tile) units per CU, no slab round trip -- measured slower: runs start at
+    different k offsets, so CUs of one XCD no longer share the streamed B panel in L2.)"""
+    sp = _gemm_splits(M // 128, nkt)
+    slabs = torch.empty(sp * M * D, dtype=torch.float32, device=out.device) if sp > 1 else None
+    call("triad_tile_gemm", ptr(dS), CT, dk, ptr(B), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream)
+
+
 def _gemm_splits(wgs, nkt, cus=256, max_splits=8):
     """Split-K factor that best fills `cus` one-workgroup-per-CU slots (ties -> fewer splits)."""
     best, best_eff = 1, 0.0
@@ -242,20 +252,14 @@ class _ContrastiveHead(torch.autograd.Function):
         gq = gk = gt = None
         if ctx.needs_input_grad[0]:
             dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
-            nkt = g.C_pad // 32
-            sp = _gemm_splits(g.R_pad // 128, nkt)
-            slabs = torch.empty(sp * g.R_pad * D, dtype=f32, device=dev) if sp > 1 else None
             _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dQ")
-            call("triad_tile_gemm", ptr(dS), CT, 0, ptr(Kb), g.R_pad, nkt, ptr(alpha), sp, ptr(slabs), ptr(dQ), st)
+            tile_gemm(dS, CT, 0, Kb, g.R_pad, g.C_pad // 32, alpha, dQ, st)
             gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(ctx.q_dtype)
         if ctx.needs_input_grad[1]:
             Mk = CT * 32
             dK = torch.empty(Mk, D, dtype=torch.bfloat16, device=dev)
-            nkt = g.R_pad // 32
-            sp = _gemm_splits(Mk // 128, nkt)
-            slabs = torch.empty(sp * Mk * D, dtype=f32, device=dev) if sp > 1 else None
             _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dK")
-            call("triad_tile_gemm", ptr(dS), CT, 1, ptr(Qb), Mk, nkt, ptr(alpha), sp, ptr(slabs), ptr(dK), st)
+            tile_gemm(dS, CT, 1, Qb, Mk, g.R_pad // 32, alpha, dK, st)
             Nk_pad = g.Nk_pad
             if W > 1:
                 from . import dist as tdist
