@@ -169,23 +169,34 @@ constexpr int RING_NB = 4;
 constexpr int RING_ST = 4 * 1024 + TBK * TBN;  // 40 KB
 constexpr int RING_PIECES = 1 + TBK / 8;       // per wave per tile: 1 A piece + 4 B rows
 
+// one of a wave's RING_PIECES pieces of k tile kt: piece 0 = its A piece, 1..4 = its B rows
 template <bool DK>
-__device__ __forceinline__ void stage_ring(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ B,
-                                           int mt0, int kt, bf16* dst, int wave, int lane) {
-  {
+__device__ __forceinline__ void ring_piece(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ B,
+                                           int mt0, int kt, bf16* dst, int wave, int lane, int piece) {
+  if (piece == 0) {
     const int t = wave >> 1, half = wave & 1;
     const int pos = half * 64 + lane;
     const int c = DK ? swz_k(pos) : swz_q(pos);
     const long long tile = DK ? ((long long)kt * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + kt);
     glds16(Dt + tile * 1024 + c * 8, dst + t * 1024 + half * 512);
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int k = wave * 4 + u;
+  } else {
+    const int k = wave * 4 + piece - 1;
     const int c = lane ^ ((k & 3) << 2);
     glds16(B + ((long long)kt * TBK + k) * TBN + c * 8, dst + 4096 + k * TBN);
   }
 }
+
+template <bool DK>
+__device__ __forceinline__ void stage_ring(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ B,
+                                           int mt0, int kt, bf16* dst, int wave, int lane) {
+#pragma unroll
+  for (int u = 0; u < RING_PIECES; ++u) ring_piece<DK>(Dt, CT, B, mt0, kt, dst, wave, lane, u);
+}
+
+#ifndef TG_SPREAD
+#define TG_SPREAD 1  // 1: the next tile's DMA pieces issued between the MFMAs (one per 3) instead of in a burst
+                     // after the barrier (A/B: dQ/dK 3-4 % faster)
+#endif
 
 template <bool DK, bool SLAB>
 __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __restrict__ Dt, long long CT,
@@ -218,9 +229,9 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __re
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING_PIECES) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (it + RING_NB - 1 < nkt)
-      stage_ring<DK>(Dt, CT, B, mt0, kt0 + it + RING_NB - 1, lds + ((it + RING_NB - 1) % RING_NB) * RING_ST, wave,
-                     lane);
+    const bool pf = it + RING_NB - 1 < nkt;
+    bf16* const pdst = lds + ((it + RING_NB - 1) % RING_NB) * RING_ST;
+    if (!TG_SPREAD && pf) stage_ring<DK>(Dt, CT, B, mt0, kt0 + it + RING_NB - 1, pdst, wave, lane);
     const bf16* As = lds + (it % RING_NB) * RING_ST;
     const bf16* Bs = As + 4096;
 #pragma unroll
@@ -250,7 +261,15 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __re
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int n = 0; n < 2; ++n) acc[t][n] = mfma32(af[t], bf[n], acc[t][n]);
+        for (int n = 0; n < 2; ++n) {
+          acc[t][n] = mfma32(af[t], bf[n], acc[t][n]);
+          const int m = s * 8 + t * 2 + n;
+          if (TG_SPREAD && m % 3 == 0 && m / 3 < RING_PIECES) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (pf) ring_piece<DK>(Dt, CT, B, mt0, kt0 + it + RING_NB - 1, pdst, wave, lane, m / 3);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
     }
   }
 

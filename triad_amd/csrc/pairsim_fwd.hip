@@ -48,6 +48,12 @@ constexpr int GLDS_PER_TILE = 32 / WAVES;  // 1-KB LDS-DMA pieces per wave per k
 #define FWD_EXPERIMENT 0  // A/B timing only (results wrong): 1 = no key DMA after the prologue,
                           // 2 = no epilogue elements, 4 = no dS stores
 #endif
+#ifndef FWD_SPREAD
+#define FWD_SPREAD 0  // 1: the key-tile DMA pieces issued between the chain's MFMAs
+#endif
+#ifndef FWD_PK
+#define FWD_PK 0  // 1: packed v_pk_fma_f32 / v_pk_mul_f32 in the epilogue; 0: scalar pairs
+#endif
 #ifndef FWD_REGION
 #define FWD_REGION 2  // k-steps per scheduling region (sched_barrier spacing; 2 measured best)
 #endif
@@ -88,18 +94,22 @@ __device__ __forceinline__ void dma16(i32x4 rsrc, unsigned lds_addr, unsigned vo
 }
 
 // One key tile (32 rows x 1 KB) into an LDS slot: 1-KB pieces, the row offset in soffset
-// (uniform), the source-side swizzle chunk ^ (row & 15) in voffset.
-__device__ __forceinline__ void stage_tile(i32x4 kr, const FwdArgs& a, bf16* dst, int j, int kb, int wave,
-                                           int lane) {
+// (uniform), the source-side swizzle chunk ^ (row & 15) in voffset. Piece u of this wave's
+// GLDS_PER_TILE.
+__device__ __forceinline__ void stage_piece(i32x4 kr, const FwdArgs& a, bf16* dst, int j, int kb, int wave,
+                                            int lane, int u) {
   const unsigned row0 = (unsigned)(j * a.Nk_pad + kb * 32 + wave * GLDS_PER_TILE);
   const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) bf16*)dst;
   asm volatile("" : "+v"(lane));  // recompute the lane offsets here, do not keep them live
+  const int t = wave * GLDS_PER_TILE + u;
+  dma16(kr, __builtin_amdgcn_readfirstlane(lds0 + t * D * 2), (unsigned)((lane ^ (t & 15)) * 16),
+        __builtin_amdgcn_readfirstlane((row0 + u) * (D * 2)));
+}
+
+__device__ __forceinline__ void stage_tile(i32x4 kr, const FwdArgs& a, bf16* dst, int j, int kb, int wave,
+                                           int lane) {
 #pragma unroll
-  for (int u = 0; u < GLDS_PER_TILE; ++u) {
-    const int t = wave * GLDS_PER_TILE + u;
-    dma16(kr, __builtin_amdgcn_readfirstlane(lds0 + t * D * 2), (unsigned)((lane ^ (t & 15)) * 16),
-          __builtin_amdgcn_readfirstlane((row0 + u) * (D * 2)));
-  }
+  for (int u = 0; u < GLDS_PER_TILE; ++u) stage_piece(kr, a, dst, j, kb, wave, lane, u);
 }
 
 // 16-byte store hidden from hipcc's waitcnt bookkeeping (it would otherwise drain vmcnt(0) --
@@ -164,6 +174,17 @@ __device__ __forceinline__ f32x2 pk_fma_sq(f32x2 c, f32x2 acc) {  // acc + c * c
   asm("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(acc) : "v"(c));
   return acc;
 }
+// scalar forms (FWD_PK 0): beside MFMAs a packed f32 op costs ~22 issue cycles more than two
+// scalar ones (MI355X_MICROARCH.md, 'price of one filler beside MFMAs')
+__device__ __forceinline__ float fma_sq(float c, float acc) {  // acc + c * c
+  asm("v_fmac_f32 %0, %1, %1" : "+v"(acc) : "v"(c));
+  return acc;
+}
+__device__ __forceinline__ float mulf(float a, float b) {
+  float r;
+  asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) {
   f32x2 r;
   asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -190,11 +211,20 @@ __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 s
   const float c = __builtin_amdgcn_fmed3f(u, lo, 0.f);
   if (v & 1) {
     const f32x2 cc = {e.prev, c};
+#if FWD_PK
     e.nn2 = pk_fma_sq(cc, e.nn2);
+#else
+    e.nn2.x = fma_sq(cc.x, e.nn2.x);
+    e.nn2.y = fma_sq(cc.y, e.nn2.y);
+#endif
     PIN(e.nn2);
     if constexpr (TRAIN) {
       e.mn = min3f(e.mn, p[v - 1], u);
+#if FWD_PK
       const f32x2 d = pk_mul(cc, su2);
+#else
+      const f32x2 d = {mulf(cc.x, su2.x), mulf(cc.y, su2.y)};
+#endif
       e.pk[v >> 1] = pack_bf16x2(d.x, d.y);
       PIN(e.mn);
       PIN(e.pk[v >> 1]);
@@ -268,6 +298,15 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) 
   auto prefetch = [&](int b2) {
     if (b2 < nblocks && (!(FWD_EXPERIMENT & 1) || b2 < 2))
       stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j, fc.kb, wave, lane);
+    fc.next(nkb);
+    fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
+  };
+  // FWD_SPREAD: piece u of tile b2 issued inside the chain; the cursor advances after the last
+  auto prefetch_piece = [&](int b2, int u) {
+    if (b2 < nblocks && (!(FWD_EXPERIMENT & 1) || b2 < 2))
+      stage_piece(kr, a, kbuf + fslot * KT_ELEMS, fc.j, fc.kb, wave, lane, u);
+  };
+  auto prefetch_done = [&]() {
     fc.next(nkb);
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
   };
@@ -362,7 +401,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) 
     constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value, full = decltype(FULLT)::value;
     if constexpr (ch) {
       sync_tile(b);
-      prefetch(b + NBUF - 1);
+      if (!FWD_SPREAD) prefetch(b + NBUF - 1);
       const char* kt = (const char*)kbuf + cslot * (KT_ELEMS * 2);
       cslot = __builtin_amdgcn_readfirstlane(cslot == NBUF - 1 ? 0 : cslot + 1);
       constexpr int P = FWD_LDSPF;
@@ -380,7 +419,15 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) 
         // scheduling regions of 4 k-steps: two epilogue elements interleave and fill each
         // other's VALU->SGPR-mask wait states
         if (s % FWD_REGION == FWD_REGION - 1) __builtin_amdgcn_sched_barrier(0);
+        // next-but-one tile's DMA pieces between the MFMAs, one per 8 k-steps (not a burst
+        // right after the barrier, where every wave of the SIMD would issue them at once)
+        if (FWD_SPREAD && s % (NS / GLDS_PER_TILE) == 3) {
+          __builtin_amdgcn_sched_barrier(0);
+          prefetch_piece(b + NBUF - 1, s / (NS / GLDS_PER_TILE));
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
+      if (FWD_SPREAD) prefetch_done();
     } else if constexpr (ep) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full>(e, p, v, su2, lo);
