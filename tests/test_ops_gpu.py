@@ -240,3 +240,35 @@ def test_trainer_bf16_model_weights_track_fp32_masters():
     name = "audio_embedder.hubert.encoder.layers.0.attention.q_proj.weight"
     i = sp.index[id(dict(m.named_parameters())[name])]
     assert sd[name].dtype == torch.float32 and torch.equal(sd[name].cpu(), sp.master(i).cpu())
+
+
+@pytest.mark.parametrize("M,K,O,bias", [(50944 // 4, 768, 2304, True), (16384, 3072, 768, False),
+                                        (20480, 512, 768, True)])
+def test_triad_linear_matches_autocast_linear(M, K, O, bias):
+    """TriadLinear (dW on the HIP split-K GEMM) against nn.Linear under bf16 autocast: same output,
+    dX, dW, db to bf16 tolerance (different fp32 summation order only)."""
+    from triad_amd.linear import TriadLinear
+    torch.manual_seed(M + K)
+    ref = torch.nn.Linear(K, O, bias=bias).to(dev).to(torch.bfloat16)
+    fast = torch.nn.Linear(K, O, bias=bias).to(dev).to(torch.bfloat16)
+    fast.load_state_dict(ref.state_dict())
+    fast.__class__ = TriadLinear
+    x = torch.randn(4, M // 4, K, device=dev)
+    gy = torch.randn(4, M // 4, O, device=dev)
+    xr = x.clone().requires_grad_(True)
+    xf = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yr = ref(xr)
+        yf = fast(xf)
+    assert yf.dtype == yr.dtype == torch.bfloat16
+    assert torch.equal(yf, yr)
+    (yr.float() * gy).sum().backward()
+    (yf.float() * gy).sum().backward()
+
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / b.float().norm())
+    assert rel(xf.grad, xr.grad) < 1e-6
+    assert fast.weight.grad.dtype == torch.bfloat16
+    assert rel(fast.weight.grad, ref.weight.grad) < 1e-2
+    if bias:
+        assert rel(fast.bias.grad, ref.bias.grad) < 1e-2

@@ -31,6 +31,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib, attention, frontend, ops
+from .linear import install_fast_linear
 from .vit import DinoVisionTransformer, apply_lora, store_frozen_base_bf16
 
 warnings.filterwarnings("ignore", message=".*torch.cuda.amp.*")
@@ -76,7 +77,7 @@ def _hf_model(kind, name, config_overrides=None):
     """Load `name` from a local HF cache if present, else random-init its architecture."""
     import transformers
     try:
-        return getattr(transformers, kind).from_pretrained(name, local_files_only=True)
+        return install_fast_linear(getattr(transformers, kind).from_pretrained(name, local_files_only=True))
     except Exception:
         pass
     cfg_cls = {"HubertModel": transformers.HubertConfig, "DistilBertModel": transformers.DistilBertConfig}[kind]
@@ -85,7 +86,7 @@ def _hf_model(kind, name, config_overrides=None):
         cfg._attn_implementation = _register_attention()
     except Exception:
         pass
-    return getattr(transformers, kind)(cfg)
+    return install_fast_linear(getattr(transformers, kind)(cfg))
 
 
 def _register_attention():
