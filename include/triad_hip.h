@@ -219,6 +219,15 @@ int triad_rows_nt(const void* X, long long ldx, int M, int K, const void* W, int
 int triad_rows_tn_slabs(int M);
 int triad_rows_tn(const void* Y, long long ldy, int M, int O, const void* T, int J, float alpha, float* slabs,
                   float* out, hipStream_t stream);
+/* triad_lora_update: Y[m][o] += sum_j T[m][j] Bs[o][j] in place (Y [M][ldy] bf16, T [M][8], Bs [O][8] bf16;
+ *                    y += t (sB)^T after the base GEMM, dx += dt A in the backward).
+ * triad_lora_tn:     out[o][j] = alpha sum_m Y[m][o] T[m][j] (f32 [O][8]) and, if Wt != NULL,
+ *                    dt[m][j] = sum_o Y[m][o] Wt[j][o] (Wt [16][O] bf16, rows 8..15 zero; dt [M][8] bf16),
+ *                    in ONE pass over Y; O / 256 in {1,2,3,4,6,8,9,12}; slabs: triad_lora_tn_blocks(M) * O * 8. */
+int triad_lora_update(void* Y, long long ldy, int M, int O, const void* T, const void* Bs, hipStream_t stream);
+int triad_lora_tn_blocks(int M);
+int triad_lora_tn(const void* Y, long long ldy, int M, int O, const void* T, const void* Wt, void* dt, float alpha,
+                  float* slabs, float* out, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -88,7 +88,8 @@ def _rand_feats(g, shape):
 
 
 @pytest.mark.parametrize("B,Na,Nv,pad,mix", [(8, 199, 256, False, False), (6, 199, 200, True, False),
-                                             (16, 50, 96, True, False), (6, 40, 70, True, True)])
+                                             (16, 50, 96, True, False), (6, 40, 70, True, True),
+                                             (5, 499, 1369, True, False)])  # c5: 10 s audio, 518 px
 def test_av_head_vs_oracle_random(B, Na, Nv, pad, mix):
     ops = _ops()
     g = torch.Generator().manual_seed(100 + B)
@@ -119,7 +120,8 @@ def test_av_head_vs_oracle_random(B, Na, Nv, pad, mix):
     assert _scalar_close(float(tg.grad), float(tr.grad), 2e-3, 1e-5)
 
 
-@pytest.mark.parametrize("B,Nt,Nv,mix", [(16, 32, 205, False), (12, 16, 64, False), (8, 12, 40, True)])
+@pytest.mark.parametrize("B,Nt,Nv,mix", [(16, 32, 205, False), (12, 16, 64, False), (8, 12, 40, True),
+                                         (5, 32, 1369, False)])  # c5: 518 px frames
 def test_tv_head_vs_oracle_random(B, Nt, Nv, mix):
     ops = _ops()
     g = torch.Generator().manual_seed(200 + B)

@@ -51,13 +51,16 @@ SIGNATURES = {
     "triad_rows_nt": [vp, i64, i32, i32, vp, i32, vp, vp],
     "triad_rows_tn_slabs": [i32],
     "triad_rows_tn": [vp, i64, i32, i32, vp, i32, f32, vp, vp, vp],
+    "triad_lora_update": [vp, i64, i32, i32, vp, vp, vp],
+    "triad_lora_tn_blocks": [i32],
+    "triad_lora_tn": [vp, i64, i32, i32, vp, vp, vp, f32, vp, vp, vp],
     "triad_attn_fwd": [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, f32, vp, i64, i64, vp, vp],
     "triad_attn_bwd": [vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i32, i32, i32,
                        i32, f32, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, vp],
 }
 # entry points returning a value rather than a status
 RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_longlong,
-            "triad_rows_tn_slabs": C.c_int}
+            "triad_rows_tn_slabs": C.c_int, "triad_lora_tn_blocks": C.c_int}
 
 _lock = threading.Lock()
 _lib = None

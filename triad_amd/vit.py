@@ -36,10 +36,11 @@ ARCHS = {
 
 class _LoRALinear(torch.autograd.Function):
     """y = x W^T + b + (s B)(A x) for a frozen base under bf16 autocast, as ONE base GEMM plus an
-    in-place rank-8 update, with the skinny products on the HIP kernels of csrc/lora.hip
-    (t = x A^T and dt = dy (s B) by triad_rows_nt; dB = s dy^T t and dA = dt^T x by
-    triad_rows_tn). Same operands and roundings class as autocast's F.linear chain; the LoRA
-    gradients accumulate in fp32."""
+    in-place rank-8 update, with the skinny products on the HIP kernels of csrc/lora.hip:
+    forward t = x A^T (triad_rows_nt) and y += t (sB)^T (triad_lora_update); backward ONE pass
+    over dy for both dt = dy (sB) and dB = s dy^T t (triad_lora_tn), dX = dy W on the library
+    GEMM plus dx += dt A (triad_lora_update), and one pass over x for dA = dt^T x. Same
+    operands and rounding class as autocast's F.linear chain; LoRA gradients accumulate in fp32."""
 
     @staticmethod
     def forward(ctx, x, w, b, A, B, scaling):
@@ -48,12 +49,13 @@ class _LoRALinear(torch.autograd.Function):
         xb = x.reshape(-1, K).to(torch.bfloat16).contiguous()
         M = xb.shape[0]
         dev = x.device
+        st = stream_ptr(dev)
         Ab = A.detach().to(torch.bfloat16).contiguous()
-        sB = (B.detach() * scaling).to(torch.bfloat16)
+        sB = (B.detach() * scaling).to(torch.bfloat16).contiguous()
         y = F.linear(xb, w.to(torch.bfloat16), None if b is None else b.to(torch.bfloat16))
         t = torch.empty(M, r, dtype=torch.bfloat16, device=dev)
-        call("triad_rows_nt", ptr(xb), K, M, K, ptr(Ab), r, ptr(t), stream_ptr(dev))
-        y.addmm_(t, sB.t())
+        call("triad_rows_nt", ptr(xb), K, M, K, ptr(Ab), r, ptr(t), st)
+        call("triad_lora_update", ptr(y), O, M, O, ptr(t), ptr(sB), st)
         ctx.save_for_backward(xb, w, Ab, sB, t)
         ctx.meta = (lead, x.dtype, float(scaling), A.dtype, B.dtype)
         return y.view(*lead, O)
@@ -68,17 +70,20 @@ class _LoRALinear(torch.autograd.Function):
         dy2 = dy.reshape(M, O).to(torch.bfloat16).contiguous()
         st = stream_ptr(dev)
         dt = torch.empty(M, r, dtype=torch.bfloat16, device=dev)
-        call("triad_rows_nt", ptr(dy2), O, M, O, ptr(sB.t().contiguous()), r, ptr(dt), st)
+        G = call("triad_lora_tn_blocks", M)
+        slabs = torch.empty(G * max(O, K) * r, dtype=torch.float32, device=dev)
+        # dt = dy (sB) and dB = s dy^T t in one pass over dy
+        wt = torch.zeros(16, O, dtype=torch.bfloat16, device=dev)
+        wt[:r].copy_(sB.t())
+        dB = torch.empty(O, r, dtype=torch.float32, device=dev)
+        call("triad_lora_tn", ptr(dy2), O, M, O, ptr(t), ptr(wt), ptr(dt), scaling, ptr(slabs), ptr(dB), st)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy2, w.to(torch.bfloat16))
-            dx.addmm_(dt, Ab)
+            call("triad_lora_update", ptr(dx), K, M, K, ptr(dt), ptr(Ab.t().contiguous()), st)
             dx = dx.view(*lead, K).to(x_dtype)
-        slabs = torch.empty(call("triad_rows_tn_slabs", M) * max(O, K) * r, dtype=torch.float32, device=dev)
-        dB = torch.empty(O, r, dtype=torch.float32, device=dev)
-        call("triad_rows_tn", ptr(dy2), O, M, O, ptr(t), r, scaling, ptr(slabs), ptr(dB), st)
         dAt = torch.empty(K, r, dtype=torch.float32, device=dev)
-        call("triad_rows_tn", ptr(xb), K, M, K, ptr(dt), r, 1.0, ptr(slabs), ptr(dAt), st)
+        call("triad_lora_tn", ptr(xb), K, M, K, ptr(dt), None, None, 1.0, ptr(slabs), ptr(dAt), st)
         return dx, None, None, dAt.t().to(a_dtype), dB.to(b_dtype), None
 
 
@@ -103,7 +108,8 @@ class LoRALinear(nn.Module):
 
     def forward(self, x):
         if x.is_cuda and torch.is_autocast_enabled("cuda") and not self.base.weight.requires_grad \
-                and (self.base.bias is None or not self.base.bias.requires_grad) and self.lora_A.shape[0] == 8:
+                and (self.base.bias is None or not self.base.bias.requires_grad) and self.lora_A.shape[0] == 8 \
+                and self.lora_A.shape[1] % 256 == 0 and self.lora_B.shape[0] % 256 == 0:
             return lora_linear(x, self.base.weight, self.base.bias, self.lora_A, self.lora_B, self.scaling)
         return self.base(x) + F.linear(F.linear(x, self.lora_A), self.lora_B) * self.scaling
 
