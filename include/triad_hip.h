@@ -212,13 +212,9 @@ int triad_attn_bwd(const void* q, long long q_sB, long long q_sN, const void* k,
 
 /* LoRA skinny products (model.py:223-266, peft LoRA r = 8 on the ViT's attn.qkv / attn.proj):
  * triad_rows_nt: out[m][j] = sum_k X[m][k] * W[j][k], X [M][ldx] bf16, W [J][K] bf16, J <= 16,
- *                K % 32 == 0, out [M][J] bf16 (t = x A^T, dt = dy (sB)).
- * triad_rows_tn: out[o][j] = alpha * sum_m Y[m][o] * T[m][j], Y [M][ldy] bf16, T [M][8] bf16 (J = 8),
- *                O % 8 == 0, out [O][8] f32 (dB, dA^T); slabs: triad_rows_tn_slabs(M) * O * 8 floats. */
+ *                K % 32 == 0, out [M][J] bf16 (t = x A^T).
+ */
 int triad_rows_nt(const void* X, long long ldx, int M, int K, const void* W, int J, void* out, hipStream_t stream);
-int triad_rows_tn_slabs(int M);
-int triad_rows_tn(const void* Y, long long ldy, int M, int O, const void* T, int J, float alpha, float* slabs,
-                  float* out, hipStream_t stream);
 /* triad_lora_update: Y[m][o] += sum_j T[m][j] Bs[o][j] in place (Y [M][ldy] bf16, T [M][8], Bs [O][8] bf16;
  *                    y += t (sB)^T after the base GEMM, dx += dt A in the backward).
  * triad_lora_tn:     out[o][j] = alpha sum_m Y[m][o] T[m][j] (f32 [O][8]) and, if Wt != NULL,

@@ -98,7 +98,7 @@ def test_hubert_pos_conv_matches_transformers(C, G, T):
 @pytest.mark.parametrize("M,K,O", [(66 * 261, 768, 2304), (5 * 37, 768, 768), (3, 384, 1152), (1001, 1024, 3072),
                                    (33, 768, 768), (256 * 261, 768, 2304)])
 def test_lora_linear_matches_reference_chain(M, K, O):
-    """ViT LoRA (triad_amd.vit._LoRALinear: rows_nt / rows_tn HIP kernels + one base GEMM and an
+    """ViT LoRA (triad_amd.vit._LoRALinear: rows_nt / lora_update / lora_tn HIP kernels + one base GEMM and an
     in-place rank-8 update) against the reference chain base(x) + B(A(x)) * s under bf16 autocast."""
     from triad_amd.vit import LoRALinear
     torch.manual_seed(M)

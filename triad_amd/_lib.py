@@ -49,8 +49,6 @@ SIGNATURES = {
     "triad_chgn_gelu_bwd": [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "triad_posconv": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "triad_rows_nt": [vp, i64, i32, i32, vp, i32, vp, vp],
-    "triad_rows_tn_slabs": [i32],
-    "triad_rows_tn": [vp, i64, i32, i32, vp, i32, f32, vp, vp, vp],
     "triad_lora_update": [vp, i64, i32, i32, vp, vp, vp],
     "triad_lora_tn_blocks": [i32],
     "triad_lora_tn": [vp, i64, i32, i32, vp, vp, vp, f32, vp, vp, vp],
@@ -60,7 +58,7 @@ SIGNATURES = {
 }
 # entry points returning a value rather than a status
 RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_longlong,
-            "triad_rows_tn_slabs": C.c_int, "triad_lora_tn_blocks": C.c_int}
+            "triad_lora_tn_blocks": C.c_int}
 
 _lock = threading.Lock()
 _lib = None

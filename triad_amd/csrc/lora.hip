@@ -3,12 +3,10 @@
 //
 // With M = B*N tokens (66 816 at c3) and rank r = 8 these products are HBM-bound streams over
 // one (M, K) activation, which the library GEMMs run at a fraction of bandwidth:
-//   triad_rows_nt: out[m][j] = sum_k X[m][k] W[j][k]      (t = x A^T, dt = dy (sB))   MFMA 16x16x32,
-//                  rows of X straight from HBM, W fragments from L2, j < J <= 16;
-//   triad_rows_tn: out[o][j] = alpha sum_m Y[m][o] T[m][j] (dB = s dy^T t, dA^T = x^T dt)  fp32 VALU,
-//                  one pass over Y split into row slabs, partials reduced by a second kernel;
-//   triad_lora_tn: the same product on MFMA (Y tiles transposed by ds_read_b64_tr_b16 out of LDS),
-//                  fused with dt[m][j] = sum_o Y[m][o] Wt[j][o] over the same tiles: ONE pass over
+//   triad_rows_nt: out[m][j] = sum_k X[m][k] W[j][k]  (t = x A^T)  MFMA 16x16x32, rows of X
+//                  straight from HBM, W fragments from L2, j < J <= 16;
+//   triad_lora_tn: out[o][j] = alpha sum_m Y[m][o] T[m][j]  (dB = s dy^T t, dA^T = x^T dt)  MFMA,
+//                  Y tiles transposed by ds_read_b64_tr_b16 out of LDS, fused with dt[m][j] = sum_o Y[m][o] Wt[j][o] over the same tiles: ONE pass over
 //                  dy gives both dB and dt; a second pass over x gives dA;
 //   triad_lora_update: Y[m][o] += sum_j T[m][j] Bs[o][j] in place (the rank-8 update of the base
 //                  GEMM's output / of dX), one read + one write of Y.
@@ -56,36 +54,7 @@ __global__ __launch_bounds__(256) void rows_nt_kernel(const bf16* __restrict__ X
   }
 }
 
-// thread = 8 consecutive columns o of Y; grid.y = row slabs. slab[s][o][j] (fp32).
-constexpr int TJ = 8;
-__global__ __launch_bounds__(256) void rows_tn_kernel(const bf16* __restrict__ Y, long long ldy, int M, int O,
-                                                      const bf16* __restrict__ T, int rows_per_slab,
-                                                      float* __restrict__ slab) {
-  const int c8 = blockIdx.x * blockDim.x + threadIdx.x;
-  if (8 * c8 >= O) return;
-  const int m0 = blockIdx.y * rows_per_slab, m1 = min(M, m0 + rows_per_slab);
-  float acc[8][TJ];
-#pragma unroll
-  for (int c = 0; c < 8; ++c)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[c][j] = 0.f;
-  const bf16* yp = Y + 8 * c8;
-#pragma unroll 4
-  for (int m = m0; m < m1; ++m) {
-    const bf16x8 y = *(const bf16x8*)(yp + (long long)m * ldy);
-    const bf16x8 t = *(const bf16x8*)(T + (long long)m * TJ);
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) acc[c][j] = fmaf((float)y[c], (float)t[j], acc[c][j]);
-  }
-  float* sp = slab + ((long long)blockIdx.y * O + 8 * c8) * TJ;
-#pragma unroll
-  for (int c = 0; c < 8; ++c)
-#pragma unroll
-    for (int j = 0; j < TJ; j += 4)
-      *(f32x4_t*)(sp + c * TJ + j) = (f32x4_t){acc[c][j], acc[c][j + 1], acc[c][j + 2], acc[c][j + 3]};
-}
+constexpr int TJ = 8;  // LoRA rank
 
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int S, long long n, float alpha,
                                                        float* __restrict__ out) {
@@ -259,24 +228,6 @@ int triad_rows_nt(const void* X, long long ldx, int M, int K, const void* W, int
   const int blocks = (M + 63) / 64;
   hipLaunchKernelGGL(rows_nt_kernel, dim3(blocks), dim3(256), 0, stream, (const bf16*)X, ldx, M, K, (const bf16*)W, J,
                      (bf16*)out);
-  TRIAD_CHECK_LAUNCH();
-  return TRIAD_OK;
-}
-
-int triad_rows_tn_slabs(int M) { return M >= 32768 ? 256 : (M + 127) / 128; }
-
-int triad_rows_tn(const void* Y, long long ldy, int M, int O, const void* T, int J, float alpha, float* slabs,
-                  float* out, hipStream_t stream) {
-  if (M <= 0 || O <= 0 || O % 8 || J != TJ || ldy < O || ldy % 8) return TRIAD_EINVAL;
-  const int S = triad_rows_tn_slabs(M);
-  const int rows = (M + S - 1) / S;
-  const int threads = O / 8 >= 256 ? 256 : ((O / 8 + 63) / 64) * 64;
-  const dim3 grid((O / 8 + threads - 1) / threads, S);
-  hipLaunchKernelGGL(rows_tn_kernel, grid, dim3(threads), 0, stream, (const bf16*)Y, ldy, M, O, (const bf16*)T, rows,
-                     slabs);
-  const long long n = (long long)O * TJ;
-  hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, slabs, S, n, alpha,
-                     out);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
