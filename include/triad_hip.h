@@ -225,6 +225,16 @@ int triad_lora_tn_blocks(int M);
 int triad_lora_tn(const void* Y, long long ldy, int M, int O, const void* T, const void* Wt, void* dt, float alpha,
                   float* slabs, float* out, hipStream_t stream);
 
+/* ViT residual + LayerScale + LayerNorm (model.py:207-266, DINOv2 blocks; csrc/resid_ln.hip):
+ * triad_addln_fwd: xn = x + g * y (y bf16, may be NULL: LN of x alone, xn not written), ln = LN(xn) w + b
+ *                  as bf16 (out_f32 = 0) or fp32, per-row mean / rstd; x, xn, w, b, g fp32; D % 256 == 0.
+ * triad_addln_bwd: dx = dres (may be NULL) + LN backward of dln (bf16 / fp32) at xn, dy = bf16(g dx). */
+int triad_addln_fwd(const float* x, const void* y, const float* g, const float* w, const float* b, float eps, int M,
+                    int D, float* xn, void* ln, int out_f32, float* mean, float* rstd, hipStream_t stream);
+int triad_addln_bwd(const void* dln, int dln_f32, const float* dres, const float* xn, const float* mean,
+                    const float* rstd, const float* w, const float* g, int M, int D, float* dx, void* dy,
+                    hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -124,3 +124,39 @@ def test_lora_linear_matches_reference_chain(M, K, O):
     assert _rel(dx, rx) < 2e-2
     assert _rel(dA, gA) < 2e-2
     assert _rel(dB, gB) < 2e-2
+
+
+def test_vit_fused_residual_ln_matches_unfused(monkeypatch):
+    """DINOv2-B/14-reg + LoRA blocks with the fused residual + LayerScale + LayerNorm passes
+    (vit._AddScaleLN, csrc/resid_ln.hip) against the unfused autocast chain: same features and
+    LoRA gradients to bf16 tolerance."""
+    from triad_amd import vit as V
+    torch.manual_seed(0)
+    m = V.apply_lora(V.DinoVisionTransformer("dinov2_vitb14_reg"), 8, 16).to(dev)
+    V.store_frozen_base_bf16(m)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "lora_B" in n:
+                p.normal_(0, 0.02)
+        for blk in m.blocks:  # LayerScale 1e-5 would make every block near-identity
+            blk.ls1.gamma.fill_(0.3)
+            blk.ls2.gamma.fill_(0.3)
+    x = torch.randn(2, 3, 98, 98, device=dev)
+    gy = torch.randn(2, 49, 768, device=dev)
+
+    def run(fused):
+        monkeypatch.setattr(V.DinoVisionTransformer, "_fused_ok",
+                            (lambda self, t, n, norm: True) if fused else (lambda self, t, n, norm: False))
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = m.get_intermediate_layers(x, n=1)[0]
+        (out.float() * gy).sum().backward()
+        return out.detach().float(), {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    o_ref, g_ref = run(False)
+    o_fus, g_fus = run(True)
+    assert o_fus.shape == o_ref.shape == (2, 49, 768) and o_fus.dtype == o_ref.dtype
+    assert _rel(o_fus, o_ref) < 1e-2
+    assert set(g_fus) == set(g_ref) and len(g_ref) == 48
+    for n in g_ref:
+        assert _rel(g_fus[n], g_ref[n]) < 3e-2, n

@@ -50,6 +50,8 @@ SIGNATURES = {
     "triad_posconv": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "triad_rows_nt": [vp, i64, i32, i32, vp, i32, vp, vp],
     "triad_lora_update": [vp, i64, i32, i32, vp, vp, vp],
+    "triad_addln_fwd": [vp, vp, vp, vp, vp, f32, i32, i32, vp, vp, i32, vp, vp, vp],
+    "triad_addln_bwd": [vp, i32, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, vp],
     "triad_lora_tn_blocks": [i32],
     "triad_lora_tn": [vp, i64, i32, i32, vp, vp, vp, f32, vp, vp, vp],
     "triad_attn_fwd": [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, f32, vp, i64, i64, vp, vp],

@@ -56,13 +56,24 @@ __global__ __launch_bounds__(256) void rows_nt_kernel(const bf16* __restrict__ X
 
 constexpr int TJ = 8;  // LoRA rank
 
-__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int S, long long n, float alpha,
-                                                       float* __restrict__ out) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  float s = 0.f;
-  for (int i = 0; i < S; ++i) s += slab[i * n + e];
-  out[e] = alpha * s;
+// out[e] = alpha * sum_s slab[s][e]: block = 64 consecutive elements x 16 slab lanes (coalesced
+// 256-B rows per slab, 16 independent load chains per element), LDS tree over the lanes
+__global__ __launch_bounds__(1024) void slab_sum_kernel(const float* __restrict__ slab, int S, long long n, float alpha,
+                                                        float* __restrict__ out) {
+  __shared__ float part[16][64];
+  const int el = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const long long e = (long long)blockIdx.x * 64 + el;
+  float acc = 0.f;
+  if (e < n)
+    for (int i = sl; i < S; i += 16) acc += slab[i * n + e];
+  part[sl][el] = acc;
+  __syncthreads();
+  if (sl == 0 && e < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += part[i][el];
+    out[e] = alpha * t;
+  }
 }
 
 // ---- rank-8 update -------------------------------------------------------------------------
@@ -271,7 +282,7 @@ int triad_lora_tn(const void* Y, long long ldy, int M, int O, const void* T, con
   }
 #undef TN_CASE
   const long long n = (long long)O * TJ;
-  hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, slabs, G, n, alpha,
+  hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, stream, slabs, G, n, alpha,
                      out);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;

@@ -150,6 +150,55 @@ class Mlp(nn.Module):
         return self.fc2(F.gelu(self.fc1(x)))
 
 
+class _AddScaleLN(torch.autograd.Function):
+    """(xn, ln) = (x + g * y, LayerNorm(x + g * y)) for the frozen DINOv2 blocks under bf16
+    autocast, as one HIP row pass each way (csrc/resid_ln.hip): y is the bf16 branch output
+    (attention proj / fc2), g the LayerScale gamma, ln bf16 (the next GEMM's operand) or fp32
+    (the final norm). Backward: dx = dxn + LN'(dln), dy = bf16(g dx); LayerNorm / LayerScale
+    parameters are frozen (model.py:223-224) and get no gradient."""
+
+    @staticmethod
+    def forward(ctx, x, y, g, w, b, eps, out_f32):
+        M, D = x.numel() // x.shape[-1], x.shape[-1]
+        dev = x.device
+        # the kernels index x / xn as fp32 and y as bf16 rows of D: check before launching
+        if not (x.dtype == torch.float32 and y.dtype == torch.bfloat16 and y.shape == x.shape
+                and all(p.dtype == torch.float32 and p.numel() == D for p in (g, w, b))):
+            raise TypeError(f"add_scale_ln: x {x.dtype} {tuple(x.shape)}, y {y.dtype} {tuple(y.shape)}")
+        x = x.contiguous()
+        y = y.contiguous()
+        xn = torch.empty_like(x)
+        ln = torch.empty(x.shape, dtype=torch.float32 if out_f32 else torch.bfloat16, device=dev)
+        mean = torch.empty(M, dtype=torch.float32, device=dev)
+        rstd = torch.empty(M, dtype=torch.float32, device=dev)
+        call("triad_addln_fwd", ptr(x), ptr(y), ptr(g), ptr(w), ptr(b), eps, M, D, ptr(xn), ptr(ln), int(out_f32),
+             ptr(mean), ptr(rstd), stream_ptr(dev))
+        ctx.save_for_backward(xn, mean, rstd, w, g)
+        return xn, ln
+
+    @staticmethod
+    def backward(ctx, dxn, dln):
+        xn, mean, rstd, w, g = ctx.saved_tensors
+        M, D = xn.numel() // xn.shape[-1], xn.shape[-1]
+        dev = xn.device
+        if dln is None:
+            dln = torch.zeros_like(xn)
+        dln = dln.contiguous()
+        if dln.shape != xn.shape or dln.dtype not in (torch.float32, torch.bfloat16) or \
+                (dxn is not None and (dxn.shape != xn.shape or dxn.dtype != torch.float32)):
+            raise TypeError("add_scale_ln backward: unexpected gradient layout")
+        dxn = None if dxn is None else dxn.contiguous()
+        dx = torch.empty_like(xn)
+        dy = torch.empty(xn.shape, dtype=torch.bfloat16, device=dev)
+        call("triad_addln_bwd", ptr(dln), int(dln.dtype == torch.float32), ptr(dxn), ptr(xn), ptr(mean), ptr(rstd),
+             ptr(w), ptr(g), M, D, ptr(dx), ptr(dy), stream_ptr(dev))
+        return dx, dy, None, None, None, None, None
+
+
+def add_scale_ln(x, y, ls, norm, out_f32=False):
+    return _AddScaleLN.apply(x, y, ls.gamma, norm.weight, norm.bias, norm.eps, out_f32)
+
+
 class Block(nn.Module):
     def __init__(self, dim, heads, mlp_ratio=4.0, ls_init=1e-5):
         super().__init__()
@@ -235,9 +284,34 @@ class DinoVisionTransformer(nn.Module):
             t = torch.cat([t[:, :1], self.register_tokens.expand(B, -1, -1).to(t.dtype), t[:, 1:]], dim=1)
         return t
 
+    def _fused_ok(self, t, n, norm):
+        return (t.is_cuda and n == 1 and norm and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16 and self.embed_dim % 256 == 0
+                and self.embed_dim <= 1536
+                and not any(p.requires_grad for blk in self.blocks
+                            for m in (blk.norm1, blk.norm2, blk.ls1, blk.ls2) for p in m.parameters())
+                and not any(p.requires_grad for p in self.norm.parameters()))
+
+    def _blocks_fused(self, t):
+        """The blocks with every residual + LayerScale + LayerNorm step as one HIP row pass
+        (_AddScaleLN); attention and MLP branches unchanged. Returns the final norm (fp32).
+        The token embedding comes out of the patch GEMM in bf16; autocast's first residual add
+        promotes it to fp32 exactly, as t.float() does here."""
+        t = t.float()
+        ln = F.layer_norm(t, (self.embed_dim,), self.blocks[0].norm1.weight, self.blocks[0].norm1.bias,
+                          self.blocks[0].norm1.eps)
+        last = len(self.blocks) - 1
+        for i, blk in enumerate(self.blocks):
+            t, ln = add_scale_ln(t, blk.attn(ln), blk.ls1, blk.norm2)
+            nxt = self.norm if i == last else self.blocks[i + 1].norm1
+            t, ln = add_scale_ln(t, blk.mlp(ln), blk.ls2, nxt, out_f32=i == last)
+        return ln
+
     def get_intermediate_layers(self, x, n=1, norm=True):
         """Hub semantics for an int n: outputs of the last n blocks, normed, patch tokens only."""
         t = self.prepare_tokens(x)
+        if self._fused_ok(t, n, norm):
+            return (self._blocks_fused(t)[:, 1 + self.num_register_tokens:],)
         outs = []
         start = len(self.blocks) - n
         for i, blk in enumerate(self.blocks):
