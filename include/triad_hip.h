@@ -235,6 +235,24 @@ int triad_addln_bwd(const void* dln, int dln_f32, const float* dres, const float
                     const float* rstd, const float* w, const float* g, int M, int D, float* dx, void* dy,
                     hipStream_t stream);
 
+/* HuBERT post-LN layer passes (transformers HubertEncoderLayer under bf16 autocast; csrc/postln.hip).
+ * Dropout keep bits: counter hash of (seed, element pair), keep iff 16-bit uniform >= round(p * 65536).
+ * triad_dropaddln_fwd: h = LN(res + bf16(y keep / (1-p))) fp32 and hb = bf16(h), mean / rstd per row (D % 256 == 0).
+ * triad_dropaddln_bwd: dres = LN'(dh + dhb) (either NULL), dy = bf16(bf16(dres) keep / (1-p)); part:
+ *                      triad_dropaddln_bwd_blocks(M) x 2 x D fp32 dgamma / dbeta partials.
+ * triad_geludrop_fwd / _bwd: v = bf16(bf16(gelu(u)) keep / (1-p)) over n bf16 (n % 8 == 0) and its gradient.
+ * triad_dropout_keep: the keep bits (u8) for n elements (tests). */
+int triad_dropaddln_fwd(const float* res, const void* y, const float* w, const float* b, float eps, int M, int D,
+                        float p, unsigned seed, float* h, void* hb, float* mean, float* rstd, hipStream_t stream);
+int triad_dropaddln_bwd_blocks(int M);
+int triad_dropaddln_bwd(const float* dh, const void* dhb, const float* res, const void* y, const float* mean,
+                        const float* rstd, const float* w, int M, int D, float p, unsigned seed, float* dres, void* dy,
+                        float* part, hipStream_t stream);
+int triad_geludrop_fwd(const void* u, long long n, float p, unsigned seed, void* v, hipStream_t stream);
+int triad_geludrop_bwd(const void* u, const void* dv, long long n, float p, unsigned seed, void* du,
+                       hipStream_t stream);
+int triad_dropout_keep(long long n, float p, unsigned seed, void* out, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

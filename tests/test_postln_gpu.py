@@ -1,0 +1,124 @@
+"""GPU parity of the fused HuBERT post-LN passes (triad_amd.postln, csrc/postln.hip) against
+torch on the SAME dropout masks (the kernels' keep bits exposed by triad_dropout_keep), and of
+the fused encoder against the stock transformers encoder with dropout off."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+@pytest.mark.parametrize("M,D,p", [(1000, 768, 0.1), (333, 1024, 0.1), (64, 768, 0.0), (5, 256, 0.3)])
+def test_drop_add_ln_matches_torch_on_same_mask(M, D, p):
+    from triad_amd import postln
+    g = torch.Generator(device=dev).manual_seed(M + D)
+    res = torch.randn(M, D, device=dev, generator=g)
+    y = torch.randn(M, D, device=dev, generator=g).to(torch.bfloat16)
+    w = 1 + 0.1 * torch.randn(D, device=dev, generator=g)
+    b = 0.1 * torch.randn(D, device=dev, generator=g)
+    norm = torch.nn.LayerNorm(D, eps=1e-5).to(dev)
+    with torch.no_grad():
+        norm.weight.copy_(w)
+        norm.bias.copy_(b)
+    seed = 12345 + M
+    keep = postln.dropout_keep(M * D, p, seed, dev).view(M, D).float()
+    dh = torch.randn(M, D, device=dev, generator=g)
+    dhb = torch.randn(M, D, device=dev, generator=g).to(torch.bfloat16)
+
+    rr = res.clone().requires_grad_(True)
+    yr = y.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yd = (yr.float() * keep * (1.0 / (1.0 - p))).to(torch.bfloat16)
+    hr = F.layer_norm(rr + yd.float(), (D,), wr, br, 1e-5)
+    hbr = hr.to(torch.bfloat16)
+    ((hr * dh).sum() + (hbr.float() * dhb.float()).sum()).backward()
+
+    rf = res.clone().requires_grad_(True)
+    yf = y.clone().requires_grad_(True)
+    h, hb = postln.drop_add_ln(rf, yf, norm, p, seed)
+    ((h * dh).sum() + (hb.float() * dhb.float()).sum()).backward()
+    assert _rel(h, hr) < 1e-5
+    assert (hb.float() - hbr.float()).abs().max() <= 2 ** -7 * hbr.float().abs().max()
+    assert _rel(rf.grad, rr.grad) < 1e-4
+    assert _rel(yf.grad, yr.grad) < 1e-2
+    assert _rel(norm.weight.grad, wr.grad) < 1e-4
+    assert _rel(norm.bias.grad, br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("n,p", [(256 * 199 * 48, 0.1), (4096, 0.5), (8, 0.0)])
+def test_gelu_drop_matches_torch_on_same_mask(n, p):
+    from triad_amd import postln
+    g = torch.Generator(device=dev).manual_seed(n)
+    u = (2 * torch.randn(n, device=dev, generator=g)).to(torch.bfloat16)
+    dv = torch.randn(n, device=dev, generator=g).to(torch.bfloat16)
+    seed = 777
+    keep = postln.dropout_keep(n, p, seed, dev).float()
+    ur = u.clone().requires_grad_(True)
+    vr = (F.gelu(ur).float() * keep * (1.0 / (1.0 - p))).to(torch.bfloat16)
+    vr.backward(dv)
+    uf = u.clone().requires_grad_(True)
+    vf = postln.gelu_drop(uf, p, seed)
+    vf.backward(dv)
+    assert _rel(vf, vr) < 1e-3
+    assert _rel(uf.grad, ur.grad) < 1e-2
+
+
+def test_dropout_keep_bits_statistics():
+    from triad_amd import postln
+    n = 1 << 22
+    k1 = postln.dropout_keep(n, 0.1, 1, dev).float()
+    k2 = postln.dropout_keep(n, 0.1, 2, dev).float()
+    for k in (k1, k2):
+        assert abs(float(k.mean()) - 0.9) < 2e-3
+        a, b = k[:-1] - 0.9, k[1:] - 0.9  # neighbouring elements (same / adjacent hash pairs)
+        assert abs(float((a * b).mean()) / 0.09) < 5e-3
+    assert abs(float(((k1 - 0.9) * (k2 - 0.9)).mean()) / 0.09) < 5e-3  # seeds decorrelate
+    assert float(postln.dropout_keep(n, 0.0, 3, dev).float().mean()) == 1.0
+
+
+def test_fused_hubert_encoder_matches_stock_without_dropout():
+    """Fused encoder vs the stock HubertEncoder (transformers) with every dropout and LayerDrop
+    off: same last_hidden_state and parameter gradients to bf16 tolerance."""
+    from triad_amd import model as Mdl
+    torch.manual_seed(0)
+    over = dict(hidden_size=768, num_hidden_layers=2, num_attention_heads=12, intermediate_size=3072,
+                hidden_dropout=0.0, activation_dropout=0.0, attention_dropout=0.0, layerdrop=0.0,
+                feat_proj_dropout=0.0, mask_time_prob=0.0)  # SpecAugment draws fresh masks per call
+    hub = Mdl.hubert_execution_tweaks(Mdl._hf_model("HubertModel", "none/none", over)).to(dev)
+    hub.train()
+    enc = hub.encoder
+    assert hasattr(enc, "_triad_stock_forward")
+    x = 0.1 * torch.randn(2, 16000, device=dev)
+
+    def run(fwd):
+        hub.zero_grad(set_to_none=True)
+        enc.forward = fwd
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = hub(x).last_hidden_state
+        gy = torch.linspace(-1, 1, out.numel(), device=dev).view_as(out)
+        (out.float() * gy).sum().backward()
+        return out.detach().float(), {n: q.grad.float().clone() for n, q in hub.named_parameters()
+                                      if q.grad is not None}
+
+    fused_fwd = enc.forward
+    try:
+        o_f, g_f = run(fused_fwd)
+        o_s, g_s = run(enc._triad_stock_forward)
+    finally:
+        enc.forward = fused_fwd
+    assert o_f.shape == o_s.shape and o_f.dtype == o_s.dtype == torch.float32
+    assert _rel(o_f, o_s) < 1e-2
+    assert set(g_f) == set(g_s)
+    for n in g_s:
+        if n.endswith("k_proj.bias"):  # exactly 0 in exact arithmetic (softmax shift invariance): noise
+            assert float(g_f[n].norm()) < 1e-3 * float(g_s[n.replace("bias", "weight")].norm()) + 1e-6
+            continue
+        assert _rel(g_f[n], g_s[n]) < 3e-2, (n, _rel(g_f[n], g_s[n]))

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libtriad_hip.so")
 # the default is the in-tree build above
 LIB_PATH = os.environ.get("TRIAD_LIB_VARIANT", LIB_PATH)
 
-vp, i32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_double
+vp, i32, u32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_uint, C.c_longlong, C.c_float, C.c_double
 
 # name -> argtypes (restype is always int status). Keep in sync with include/triad_hip.h.
 SIGNATURES = {
@@ -50,6 +50,12 @@ SIGNATURES = {
     "triad_posconv": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "triad_rows_nt": [vp, i64, i32, i32, vp, i32, vp, vp],
     "triad_lora_update": [vp, i64, i32, i32, vp, vp, vp],
+    "triad_dropaddln_fwd": [vp, vp, vp, vp, f32, i32, i32, f32, u32, vp, vp, vp, vp, vp],
+    "triad_dropaddln_bwd_blocks": [i32],
+    "triad_dropaddln_bwd": [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, u32, vp, vp, vp, vp],
+    "triad_geludrop_fwd": [vp, i64, f32, u32, vp, vp],
+    "triad_geludrop_bwd": [vp, vp, i64, f32, u32, vp, vp],
+    "triad_dropout_keep": [i64, f32, u32, vp, vp],
     "triad_addln_fwd": [vp, vp, vp, vp, vp, f32, i32, i32, vp, vp, i32, vp, vp, vp],
     "triad_addln_bwd": [vp, i32, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, vp],
     "triad_lora_tn_blocks": [i32],
@@ -60,7 +66,7 @@ SIGNATURES = {
 }
 # entry points returning a value rather than a status
 RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_longlong,
-            "triad_lora_tn_blocks": C.c_int}
+            "triad_lora_tn_blocks": C.c_int, "triad_dropaddln_bwd_blocks": C.c_int}
 
 _lock = threading.Lock()
 _lib = None

@@ -1,0 +1,308 @@
+// HuBERT post-LN encoder layer passes (SajayR/TRIAD model.py:29-30, 79-80: HubertModel trained
+// end to end after unfreeze, bf16 autocast; transformers HubertEncoderLayer / HubertFeedForward):
+//   h1 = LN1(res + dropout(attn(res)));  h2 = LN2(h1 + dropout(fc2(dropout(gelu(fc1(h1))))))
+//
+// Under autocast each residual step is four to six HBM passes (dropout with its stored mask, add,
+// LayerNorm, casts of the fp32 result for the q / k / v / fc1 GEMMs) and twice that backward.
+// Here each is one row pass:
+//   dropaddln_fwd: z = res + bf16(y * keep / (1 - p)); h = LN(z) (fp32 residual) and hb = bf16(h)
+//                  (the next GEMMs' operand), per-row mean / rstd;
+//   dropaddln_bwd: dl = dh + dhb; dz = LN'(dl) at z (z recomputed from res, y and the mask);
+//                  dres = dz, dy = bf16(bf16(dz) * keep / (1 - p)); per-block dgamma / dbeta partials;
+//   geludrop_fwd / _bwd: v = bf16(bf16(gelu(u)) * keep / (1 - p)) and its gradient, no mask tensor.
+// Dropout keep bits come from a counter-based hash of (seed, element pair): 16-bit uniform per
+// element, keep iff >= round(p * 65536); forward and backward regenerate the same bits
+// (triad_dropout_keep exposes them for tests). The roundings follow the autocast chain
+// (bf16 dropout output, fp32 add / LayerNorm, bf16 GELU output).
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ unsigned hash32(unsigned x) {  // lowbias32
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// keep bits of elements 2q and 2q+1 (bit 0 / bit 1)
+__device__ __forceinline__ unsigned keep_pair(unsigned long long q, unsigned seed, unsigned thr) {
+  const unsigned h = hash32((unsigned)q * 0x9E3779B9u + seed + hash32((unsigned)(q >> 32) ^ 0x85ebca6bu));
+  return ((h & 0xffffu) >= thr ? 1u : 0u) | ((h >> 16) >= thr ? 2u : 0u);
+}
+
+__device__ __forceinline__ float drop(float v, bool keep, float scale) { return keep ? (float)(bf16)(v * scale) : 0.f; }
+
+template <int NB>
+__device__ __forceinline__ void stats(const float (&v)[NB][4], float eps, float& mean, float& rstd) {
+  constexpr int D = NB * 256;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s += v[i][c];
+  mean = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float d = v[i][c] - mean;
+      q = fmaf(d, d, q);
+    }
+  rstd = rsqrtf(wave_sum(q) / D + eps);
+}
+
+// z for one lane's 4 x NB elements (row-major index e = row * D + c0 + c, pairs q = e / 2)
+template <int NB>
+__device__ __forceinline__ void load_z(const float* __restrict__ res, const bf16* __restrict__ y, long long row,
+                                       int lane, unsigned seed, unsigned thr, float scale, float (&v)[NB][4]) {
+  constexpr int D = NB * 256;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int c0 = i * 256 + lane * 4;
+    const long long e = row * D + c0;
+    const f32x4 r = *(const f32x4*)(res + e);
+    const bf16x4 yv = *(const bf16x4*)(y + e);
+    const unsigned k = keep_pair((unsigned long long)e >> 1, seed, thr) | (keep_pair(((unsigned long long)e >> 1) + 1, seed, thr) << 2);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[i][c] = r[c] + drop((float)yv[c], (k >> c) & 1u, scale);
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(256) void dropaddln_fwd_kernel(const float* __restrict__ res, const bf16* __restrict__ y,
+                                                            const float* __restrict__ w, const float* __restrict__ b,
+                                                            float eps, int M, unsigned seed, unsigned thr, float scale,
+                                                            float* __restrict__ h, bf16* __restrict__ hb,
+                                                            float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int D = NB * 256;
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[NB][4];
+  load_z<NB>(res, y, row, lane, seed, thr, scale, v);
+  float mean, rstd;
+  stats<NB>(v, eps, mean, rstd);
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int c0 = i * 256 + lane * 4;
+    const f32x4 wv = *(const f32x4*)(w + c0);
+    const f32x4 bv = *(const f32x4*)(b + c0);
+    f32x4 o;
+    bf16x4 ob;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      o[c] = (v[i][c] - mean) * rstd * wv[c] + bv[c];
+      ob[c] = (bf16)o[c];
+    }
+    *(f32x4*)(h + row * D + c0) = o;
+    *(bf16x4*)(hb + row * D + c0) = ob;
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// grid-stride over rows (wave = row); dgamma / dbeta partials per block: part[blk][0 / 1][D]
+template <int NB>
+__global__ __launch_bounds__(256) void dropaddln_bwd_kernel(const float* __restrict__ dh, const bf16* __restrict__ dhb,
+                                                            const float* __restrict__ res, const bf16* __restrict__ y,
+                                                            const float* __restrict__ mean_in,
+                                                            const float* __restrict__ rstd_in, const float* __restrict__ w,
+                                                            int M, unsigned seed, unsigned thr, float scale,
+                                                            float* __restrict__ dres, bf16* __restrict__ dy,
+                                                            float* __restrict__ part) {
+  constexpr int D = NB * 256;
+  __shared__ float red[4][2][D];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float gw[NB][4] = {}, gb[NB][4] = {};
+  for (long long row = (long long)blockIdx.x * 4 + wave; row < M; row += (long long)gridDim.x * 4) {
+    float z[NB][4];
+    load_z<NB>(res, y, row, lane, seed, thr, scale, z);
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NB][4], wd[NB][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int c0 = i * 256 + lane * 4;
+      const long long e = row * D + c0;
+      f32x4 d = dh ? *(const f32x4*)(dh + e) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (dhb) {
+        const bf16x4 t = *(const bf16x4*)(dhb + e);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d[c] += (float)t[c];
+      }
+      const f32x4 wv = *(const f32x4*)(w + c0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        xh[i][c] = (z[i][c] - mean) * rstd;
+        gw[i][c] = fmaf(d[c], xh[i][c], gw[i][c]);
+        gb[i][c] += d[c];
+        wd[i][c] = wv[c] * d[c];
+        s1 += wd[i][c];
+        s2 = fmaf(wd[i][c], xh[i][c], s2);
+      }
+    }
+    const float c1 = wave_sum(s1) / D, c2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int c0 = i * 256 + lane * 4;
+      const long long e = row * D + c0;
+      const unsigned k = keep_pair((unsigned long long)e >> 1, seed, thr) | (keep_pair(((unsigned long long)e >> 1) + 1, seed, thr) << 2);
+      f32x4 dz;
+      bf16x4 yb;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        dz[c] = rstd * (wd[i][c] - c1 - xh[i][c] * c2);
+        yb[c] = (bf16)drop((float)(bf16)dz[c], (k >> c) & 1u, scale);
+      }
+      *(f32x4*)(dres + e) = dz;
+      *(bf16x4*)(dy + e) = yb;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      red[wave][0][i * 256 + lane * 4 + c] = gw[i][c];
+      red[wave][1][i * 256 + lane * 4 + c] = gb[i][c];
+    }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * D; t += 256) {
+    const int which = t / D, col = t % D;
+    part[((long long)blockIdx.x * 2 + which) * D + col] =
+        red[0][which][col] + red[1][which][col] + red[2][which][col] + red[3][which][col];
+  }
+}
+
+constexpr float kAlpha = 0.70710678118654752440f;                 // M_SQRT1_2
+constexpr float kBeta = 1.12837916709551257390f * 0.70710678118654752440f * 0.5f;  // M_2_SQRTPI * M_SQRT1_2 / 2
+
+// thread = 8 consecutive elements (4 pairs)
+__global__ __launch_bounds__(256) void geludrop_fwd_kernel(const bf16* __restrict__ u, long long n, unsigned seed,
+                                                           unsigned thr, float scale, bf16* __restrict__ v) {
+  const long long e0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (e0 >= n) return;
+  const bf16x8 x = *(const bf16x8*)(u + e0);
+  bf16x8 o;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const unsigned k = keep_pair((unsigned long long)(e0 >> 1) + p, seed, thr);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float xf = (float)x[2 * p + c];
+      const float g = (float)(bf16)(0.5f * xf * (1.0f + erff(xf * kAlpha)));
+      o[2 * p + c] = (bf16)drop(g, (k >> c) & 1u, scale);
+    }
+  }
+  *(bf16x8*)(v + e0) = o;
+}
+
+__global__ __launch_bounds__(256) void geludrop_bwd_kernel(const bf16* __restrict__ u, const bf16* __restrict__ dv,
+                                                           long long n, unsigned seed, unsigned thr, float scale,
+                                                           bf16* __restrict__ du) {
+  const long long e0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (e0 >= n) return;
+  const bf16x8 x = *(const bf16x8*)(u + e0);
+  const bf16x8 d = *(const bf16x8*)(dv + e0);
+  bf16x8 o;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const unsigned k = keep_pair((unsigned long long)(e0 >> 1) + p, seed, thr);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float xf = (float)x[2 * p + c];
+      const float dg = drop((float)d[2 * p + c], (k >> c) & 1u, scale);  // dropout backward (bf16)
+      const float cdf = 0.5f * (1.0f + erff(xf * kAlpha));
+      const float pdf = expf(-0.5f * xf * xf) * kBeta;
+      o[2 * p + c] = (bf16)(dg * (cdf + xf * pdf));
+    }
+  }
+  *(bf16x8*)(du + e0) = o;
+}
+
+__global__ __launch_bounds__(256) void dropout_keep_kernel(long long n, unsigned seed, unsigned thr,
+                                                           unsigned char* __restrict__ out) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  out[e] = (keep_pair((unsigned long long)e >> 1, seed, thr) >> (e & 1)) & 1u;
+}
+
+unsigned drop_thr(float p) { return (unsigned)(p * 65536.f + 0.5f); }
+
+}  // namespace
+
+extern "C" {
+
+// h = LN(res + dropout(y)) fp32 and hb = bf16(h); res fp32 [M][D], y bf16 [M][D]; D % 256 == 0.
+int triad_dropaddln_fwd(const float* res, const void* y, const float* w, const float* b, float eps, int M, int D,
+                        float p, unsigned seed, float* h, void* hb, float* mean, float* rstd, hipStream_t stream) {
+  if (M <= 0 || D % 256 || D > 1024 || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
+  const float scale = 1.f / (1.f - p);
+  const dim3 grid((M + 3) / 4);
+#define DAL_F(NB)                                                                                                  \
+  if (D == NB * 256) {                                                                                             \
+    hipLaunchKernelGGL(dropaddln_fwd_kernel<NB>, grid, dim3(256), 0, stream, res, (const bf16*)y, w, b, eps, M, seed, \
+                       drop_thr(p), scale, h, (bf16*)hb, mean, rstd);                                              \
+    TRIAD_CHECK_LAUNCH();                                                                                          \
+    return TRIAD_OK;                                                                                               \
+  }
+  DAL_F(1) DAL_F(2) DAL_F(3) DAL_F(4)
+#undef DAL_F
+  return TRIAD_EINVAL;
+}
+
+int triad_dropaddln_bwd_blocks(int M) { return M < 4 * 1024 ? (M + 3) / 4 : 1024; }
+
+// dres = LN'(dh + dhb) (either may be NULL), dy = dropout'(bf16(dres)); part: blocks x 2 x D
+// fp32 dgamma / dbeta partials (triad_dropaddln_bwd_blocks(M) blocks).
+int triad_dropaddln_bwd(const float* dh, const void* dhb, const float* res, const void* y, const float* mean,
+                        const float* rstd, const float* w, int M, int D, float p, unsigned seed, float* dres, void* dy,
+                        float* part, hipStream_t stream) {
+  if (M <= 0 || D % 256 || D > 1024 || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
+  const float scale = 1.f / (1.f - p);
+  const dim3 grid(triad_dropaddln_bwd_blocks(M));
+#define DAL_B(NB)                                                                                                  \
+  if (D == NB * 256) {                                                                                             \
+    hipLaunchKernelGGL(dropaddln_bwd_kernel<NB>, grid, dim3(256), 0, stream, dh, (const bf16*)dhb, res,             \
+                       (const bf16*)y, mean, rstd, w, M, seed, drop_thr(p), scale, dres, (bf16*)dy, part);         \
+    TRIAD_CHECK_LAUNCH();                                                                                          \
+    return TRIAD_OK;                                                                                               \
+  }
+  DAL_B(1) DAL_B(2) DAL_B(3) DAL_B(4)
+#undef DAL_B
+  return TRIAD_EINVAL;
+}
+
+// v = dropout(gelu(u)) over n bf16 elements (n % 8 == 0)
+int triad_geludrop_fwd(const void* u, long long n, float p, unsigned seed, void* v, hipStream_t stream) {
+  if (n <= 0 || n % 8 || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(geludrop_fwd_kernel, dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, stream,
+                     (const bf16*)u, n, seed, drop_thr(p), 1.f / (1.f - p), (bf16*)v);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_geludrop_bwd(const void* u, const void* dv, long long n, float p, unsigned seed, void* du,
+                       hipStream_t stream) {
+  if (n <= 0 || n % 8 || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(geludrop_bwd_kernel, dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, stream,
+                     (const bf16*)u, (const bf16*)dv, n, seed, drop_thr(p), 1.f / (1.f - p), (bf16*)du);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+// keep bit of each of n elements (u8 0 / 1) for the given seed and p (test / debug view of the masks)
+int triad_dropout_keep(long long n, float p, unsigned seed, void* out, hipStream_t stream) {
+  if (n <= 0 || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(dropout_keep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, seed,
+                     drop_thr(p), (unsigned char*)out);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+}  // extern "C"

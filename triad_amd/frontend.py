@@ -234,10 +234,11 @@ def _hubert_mask_hidden_states(self, hidden_states, mask_time_indices=None, atte
         return hidden_states
     B, T, C = hidden_states.shape
     dev = hidden_states.device
-    emb = self.masked_spec_embed.to(hidden_states.dtype)
     if mask_time_indices is not None:
+        emb = self.masked_spec_embed.to(hidden_states.dtype)
         hidden_states = torch.where(mask_time_indices[..., None].to(dev), emb, hidden_states)
     elif cfg.mask_time_prob > 0 and self.training:
+        emb = self.masked_spec_embed.to(hidden_states.dtype)  # exists only when masking is configured
         m = _compute_mask_indices((B, T), mask_prob=cfg.mask_time_prob, mask_length=cfg.mask_time_length,
                                   attention_mask=attention_mask, min_masks=cfg.mask_time_min_masks)
         m = _lib.h2d(torch.from_numpy(m).to(torch.bool), dev)

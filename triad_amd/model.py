@@ -32,6 +32,7 @@ import torch.nn.functional as F
 
 from . import _lib, attention, frontend, ops
 from .linear import install_fast_linear
+from .postln import install_fused_encoder
 from .vit import DinoVisionTransformer, apply_lora, store_frozen_base_bf16
 
 warnings.filterwarnings("ignore", message=".*torch.cuda.amp.*")
@@ -117,8 +118,9 @@ def hubert_execution_tweaks(hubert):
     the conv feature encoder runs as channels-last im2col + GEMM with a fused HIP GroupNorm +
     GELU for layer 0, and the positional convolution as an implicit-GEMM HIP kernel
     (triad_amd.frontend) -- no MIOpen; the raw waveform gets no gradient (HF marks it
-    requires_grad only as a gradient-checkpointing workaround)."""
-    return frontend.install_hubert_frontend(hubert)
+    requires_grad only as a gradient-checkpointing workaround); the post-LN encoder layers run
+    their residual / dropout / LayerNorm / GELU passes fused (triad_amd.postln)."""
+    return install_fused_encoder(frontend.install_hubert_frontend(hubert))
 
 
 class AudioEmbedder(nn.Module):
