@@ -45,10 +45,17 @@ def main(which, B=256):
         step()
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+    shapes = "--shapes" in sys.argv
+    acts = [ProfilerActivity.CUDA] + ([ProfilerActivity.CPU] if shapes else [])
+    with profile(activities=acts, record_shapes=shapes) as prof:
         for _ in range(3):
             step()
         torch.cuda.synchronize()
+    if shapes:  # aten ops by input shape, by device time (attribute copies / adds to their callers)
+        print(prof.key_averages(group_by_input_shape=True).table(sort_by="device_time_total", row_limit=45,
+                                                                 max_name_column_width=40,
+                                                                 max_shapes_column_width=90))
+        return
     rows = []
     for e in prof.key_averages():
         t = getattr(e, "device_time_total", None) or getattr(e, "cuda_time_total", 0)
