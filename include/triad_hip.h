@@ -175,17 +175,18 @@ int triad_l2norm_rows(const void* x, int rows, int D, float eps, void* y, hipStr
 
 /* Audio front-end (model.py:29-30,66: the HuBERT conv feature encoder's layer 0,
  * transformers HubertGroupNormConvLayer = conv -> GroupNorm(C groups) -> GELU), fused
- * GroupNorm + exact GELU over channels-last x[B][T][C] bf16 (C % 8 == 0, 256 % (C/8) == 0).
- * fwd: y = bf16(gelu((x - mean[b][c]) * rstd[b][c] * gamma[c] + beta[c])), statistics over t
+ * GroupNorm + exact GELU over channels-last x[B][Tp][C] bf16 (C % 8 == 0, 256 % (C/8) == 0); the
+ * first T frames of each sample are valid, frames T .. Tp-1 padding (outputs written as 0).
+ * fwd: y = bf16(gelu((x - mean[b][c]) * rstd[b][c] * gamma[c] + beta[c])), statistics over t < T
  *      in fp32/fp64, mean / rstd (B*C floats) saved for the backward.
  * bwd: dx (bf16) and dgamma / dbeta (C floats, overwritten) from dy (bf16).
  * ws: triad_chgn_workspace_bytes(B, T, C) bytes of scratch. */
 long long triad_chgn_workspace_bytes(int B, int T, int C);
-int triad_chgn_gelu_fwd(const void* x, int B, int T, int C, const float* gamma, const float* beta, float eps,
-                        float* mean, float* rstd, void* ws, void* y, hipStream_t stream);
-int triad_chgn_gelu_bwd(const void* x, const void* dy, int B, int T, int C, const float* gamma, const float* beta,
-                        const float* mean, const float* rstd, void* ws, void* dx, float* dgamma, float* dbeta,
-                        hipStream_t stream);
+int triad_chgn_gelu_fwd(const void* x, int B, int T, int Tp, int C, const float* gamma, const float* beta,
+                        float eps, float* mean, float* rstd, void* ws, void* y, hipStream_t stream);
+int triad_chgn_gelu_bwd(const void* x, const void* dy, int B, int T, int Tp, int C, const float* gamma,
+                        const float* beta, const float* mean, const float* rstd, void* ws, void* dx, float* dgamma,
+                        float* dbeta, hipStream_t stream);
 
 /* HuBERT positional convolution (model.py:29-30,66: transformers HubertPositionalConvEmbedding,
  * Conv1d(C, C, 128, padding 64, groups) + SamePad) as an implicit GEMM over channels-last bf16:

@@ -41,7 +41,11 @@ def test_channel_group_norm_gelu(B, T, C):
     assert _rel(beta.grad, br.grad) < 1e-4
 
 
-def test_hubert_feature_encoder_gemm_matches_transformers():
+@pytest.mark.parametrize("B,L", [(3, 16000), (4, 16000), (8, 64000), (2, 16400)])
+def test_hubert_feature_encoder_gemm_matches_transformers(B, L):
+    """Padded-frame conv stack (HIP overlapping-row GEMMs where the row counts allow, the same
+    products through torch otherwise) and, for lengths whose frame chain turns odd (16400), the
+    im2col path -- against transformers' nn.Conv1d stack under autocast."""
     import transformers
     from triad_amd import frontend
     torch.manual_seed(0)
@@ -49,7 +53,8 @@ def test_hubert_feature_encoder_gemm_matches_transformers():
     m = transformers.HubertModel(transformers.HubertConfig()).to(dev).train()
     m.load_state_dict(ref_m.state_dict())
     frontend.install_hubert_frontend(m)
-    x = torch.randn(3, 16000, device=dev) * 0.5
+    x = torch.randn(B, L, device=dev) * 0.5
+    assert (frontend._frame_stack_plan(m.feature_extractor, x.to(torch.bfloat16)) is None) == (L == 16400)
     with torch.autocast("cuda", dtype=torch.bfloat16):
         ref = ref_m.feature_extractor(x)
         got = m.feature_extractor(x)

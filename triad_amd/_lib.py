@@ -45,8 +45,8 @@ SIGNATURES = {
     "triad_gather_rows": [vp, i64, vp, i32, i32, i32, vp, vp],
     "triad_l2norm_rows": [vp, i32, i32, f32, vp, vp],
     "triad_chgn_workspace_bytes": [i32, i32, i32],
-    "triad_chgn_gelu_fwd": [vp, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp],
-    "triad_chgn_gelu_bwd": [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "triad_chgn_gelu_fwd": [vp, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp],
+    "triad_chgn_gelu_bwd": [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "triad_posconv": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "triad_rows_nt": [vp, i64, i32, i32, vp, i32, vp, vp],
     "triad_lora_update": [vp, i64, i32, i32, vp, vp, vp],

@@ -47,7 +47,7 @@ __device__ __forceinline__ float gelu_grad(float z) {
 // MODE 1: (dz, dz * xhat) with dz = dy * gelu'(xhat * gamma + beta) (backward sums)
 template <int MODE>
 __global__ __launch_bounds__(NT) void chgn_sums_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                       int T, int C, const float* __restrict__ mean,
+                                                       int T, int Tp, int C, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, float2* __restrict__ part) {
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(NT) void chgn_sums_kernel(const bf16* __restrict__ 
   }
   const int t1 = min(T, (chunk + 1) * CHUNK);
   for (int t = chunk * CHUNK + r0; t < t1; t += rows) {
-    const size_t off = ((size_t)b * T + t) * C + c0;
+    const size_t off = ((size_t)b * Tp + t) * C + c0;
     const V8 xv = load8(x + off);
     if (MODE == 0) {
 #pragma unroll
@@ -161,7 +161,7 @@ __global__ void chgn_param_grad_kernel(const double2* __restrict__ tot, int B, i
 // MODE 1: dx = rstd * (dz * gamma - cA - xhat * cB)
 template <int MODE>
 __global__ __launch_bounds__(NT) void chgn_apply_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                        int T, int C, const float* __restrict__ mean,
+                                                        int T, int Tp, int C, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
@@ -185,8 +185,14 @@ __global__ __launch_bounds__(NT) void chgn_apply_kernel(const bf16* __restrict__
     }
   }
   const int t1 = min(T, (chunk + 1) * CHUNK);
+  if (chunk == gridDim.x - 1) {  // padding frames T .. Tp-1 of the sample: zeros (finite, no gradient)
+    V8 z;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z.v[i] = 0.f;
+    for (int t = T + r0; t < Tp; t += rows) store8(out + ((size_t)b * Tp + t) * C + c0, z);
+  }
   for (int t = chunk * CHUNK + r0; t < t1; t += rows) {
-    const size_t off = ((size_t)b * T + t) * C + c0;
+    const size_t off = ((size_t)b * Tp + t) * C + c0;
     const V8 xv = load8(x + off);
     V8 o;
     if (MODE == 0) {
@@ -219,36 +225,36 @@ long long triad_chgn_workspace_bytes(int B, int T, int C) {
   return (long long)B * nchunk * C * 8 + (long long)B * C * 8 + (long long)B * C * 16;
 }
 
-int triad_chgn_gelu_fwd(const void* x, int B, int T, int C, const float* gamma, const float* beta, float eps,
-                        float* mean, float* rstd, void* ws, void* y, hipStream_t stream) {
-  if (!shape_ok(B, T, C)) return TRIAD_EINVAL;
+int triad_chgn_gelu_fwd(const void* x, int B, int T, int Tp, int C, const float* gamma, const float* beta,
+                        float eps, float* mean, float* rstd, void* ws, void* y, hipStream_t stream) {
+  if (!shape_ok(B, T, C) || Tp < T) return TRIAD_EINVAL;
   const int nchunk = (T + CHUNK - 1) / CHUNK;
   float2* part = (float2*)ws;
-  hipLaunchKernelGGL(chgn_sums_kernel<0>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)x, nullptr, T, C,
+  hipLaunchKernelGGL(chgn_sums_kernel<0>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)x, nullptr, T, Tp, C,
                      nullptr, nullptr, nullptr, nullptr, part);
   hipLaunchKernelGGL(chgn_stats_kernel, dim3((C + 255) / 256, B), dim3(256), 0, stream, part, nchunk, T, C, eps,
                      mean, rstd);
-  hipLaunchKernelGGL(chgn_apply_kernel<0>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)x, nullptr, T, C,
+  hipLaunchKernelGGL(chgn_apply_kernel<0>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)x, nullptr, T, Tp, C,
                      mean, rstd, gamma, beta, nullptr, (bf16*)y);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
 
-int triad_chgn_gelu_bwd(const void* x, const void* dy, int B, int T, int C, const float* gamma, const float* beta,
-                        const float* mean, const float* rstd, void* ws, void* dx, float* dgamma, float* dbeta,
-                        hipStream_t stream) {
-  if (!shape_ok(B, T, C)) return TRIAD_EINVAL;
+int triad_chgn_gelu_bwd(const void* x, const void* dy, int B, int T, int Tp, int C, const float* gamma,
+                        const float* beta, const float* mean, const float* rstd, void* ws, void* dx, float* dgamma,
+                        float* dbeta, hipStream_t stream) {
+  if (!shape_ok(B, T, C) || Tp < T) return TRIAD_EINVAL;
   const int nchunk = (T + CHUNK - 1) / CHUNK;
   float2* part = (float2*)ws;
   float2* coef = part + (size_t)B * nchunk * C;
   double2* tot = (double2*)(coef + (size_t)B * C);
   hipLaunchKernelGGL(chgn_sums_kernel<1>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)x, (const bf16*)dy,
-                     T, C, mean, rstd, gamma, beta, part);
+                     T, Tp, C, mean, rstd, gamma, beta, part);
   hipLaunchKernelGGL(chgn_bwd_coef_kernel, dim3((C + 255) / 256, B), dim3(256), 0, stream, part, nchunk, T, C, gamma,
                      coef, tot);
   hipLaunchKernelGGL(chgn_param_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, tot, B, C, dgamma, dbeta);
   hipLaunchKernelGGL(chgn_apply_kernel<1>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)x, (const bf16*)dy, T,
-                     C, mean, rstd, gamma, beta, coef, (bf16*)dx);
+                     Tp, C, mean, rstd, gamma, beta, coef, (bf16*)dx);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

@@ -20,6 +20,7 @@ the convolutions. On a CPU tensor the original transformers modules run unchange
 from __future__ import annotations
 
 import types
+from ctypes import c_void_p as C_void_p
 
 import torch
 import torch.nn as nn
@@ -94,11 +95,19 @@ def conv1d_gemm(x, weight, bias, stride, need_dx=True):
 
 
 class _ChannelGroupNormGelu(torch.autograd.Function):
-    """gelu(GroupNorm(num_groups=C)(x)) over channels-last x (B, T, C) bf16 -> bf16 (HIP)."""
+    """gelu(GroupNorm(num_groups=C)(x)) over channels-last x (B, T, C) bf16 -> bf16 (HIP). With
+    `frames` = (B, T, Tp), x is a flat padded frame buffer (sample b's valid frames at rows
+    b*Tp .. b*Tp+T-1; padding frames come out 0 and get no gradient)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps):
-        B, T, C = x.shape
+    def forward(ctx, x, gamma, beta, eps, frames=None):
+        if frames is None:
+            B, T, C = x.shape
+            Tp = T
+        else:
+            (B, T, Tp), C = frames, x.shape[-1]
+            if x.dim() != 2 or x.shape[0] < B * Tp:
+                raise _lib.TriadError("channel_group_norm_gelu: frame buffer smaller than B * Tp rows")
         xc = x.contiguous()
         dev = x.device
         g = gamma.detach().float().contiguous()
@@ -107,25 +116,145 @@ class _ChannelGroupNormGelu(torch.autograd.Function):
         rstd = torch.empty(B, C, dtype=torch.float32, device=dev)
         ws = torch.empty(int(call("triad_chgn_workspace_bytes", B, T, C)), dtype=torch.uint8, device=dev)
         y = torch.empty_like(xc)
-        call("triad_chgn_gelu_fwd", ptr(xc), B, T, C, ptr(g), ptr(b), float(eps), ptr(mean), ptr(rstd), ptr(ws),
+        if y.shape[0] > B * Tp and frames is not None:
+            y[B * Tp:].zero_()
+        call("triad_chgn_gelu_fwd", ptr(xc), B, T, Tp, C, ptr(g), ptr(b), float(eps), ptr(mean), ptr(rstd), ptr(ws),
              ptr(y), stream_ptr(dev))
         ctx.save_for_backward(xc, g, b, mean, rstd)
         ctx.dtypes = (gamma.dtype, beta.dtype)
+        ctx.frames = (B, T, Tp, C)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         xc, g, b, mean, rstd = ctx.saved_tensors
-        B, T, C = xc.shape
+        B, T, Tp, C = ctx.frames
         dev = xc.device
         dyc = dy.to(xc.dtype).contiguous()
         dx = torch.empty_like(xc)
+        if dx.dim() == 2 and dx.shape[0] > B * Tp:
+            dx[B * Tp:].zero_()
         dg = torch.empty(C, dtype=torch.float32, device=dev)
         db = torch.empty(C, dtype=torch.float32, device=dev)
         ws = torch.empty(int(call("triad_chgn_workspace_bytes", B, T, C)), dtype=torch.uint8, device=dev)
-        call("triad_chgn_gelu_bwd", ptr(xc), ptr(dyc), B, T, C, ptr(g), ptr(b), ptr(mean), ptr(rstd), ptr(ws),
+        call("triad_chgn_gelu_bwd", ptr(xc), ptr(dyc), B, T, Tp, C, ptr(g), ptr(b), ptr(mean), ptr(rstd), ptr(ws),
              ptr(dx), ptr(dg), ptr(db), stream_ptr(dev))
-        return dx, dg.to(ctx.dtypes[0]), db.to(ctx.dtypes[1]), None
+        return dx, dg.to(ctx.dtypes[0]), db.to(ctx.dtypes[1]), None, None
+
+
+# ---- HuBERT conv stack over padded frame buffers ---------------------------------------------
+# Activations of the feature encoder live in flat channels-last frame buffers [B*Tp + 2, C]
+# (bf16): sample b's frames at rows b*Tp .. b*Tp+Tp-1 with Tp EVEN (the valid T frames, then one
+# padding frame when T is odd), plus two spare zero frames at the end. Pairs of frames are then
+# rows of a [B*Tp/2 + 1, 2C] matrix with a uniform stride, so a kernel-3 / stride-2 conv is ONE
+# GEMM whose A operand has OVERLAPPING rows (row r = frames 2r .. 2r+2: lda = 2C < K = 3C) and a
+# kernel-2 / stride-2 conv a plain GEMM over the pair rows -- no im2col copy; and the input
+# gradient of the kernel-3 conv is one GEMM over overlapping rows of dY (row q = dY[q-1], dY[q]).
+# Each layer produces B*Tp/2 rows of which the last per sample straddles the next sample: it is
+# the padding frame of the next layer (finite, never read by a valid output, zero gradient).
+
+def _addr(t, row, ld):
+    return C_void_p(t.data_ptr() + 2 * row * ld)
+
+
+def _gemm_rows(a, a_row, lda, M, K, b, out, out_row, ldc):
+    """out[out_row + m][:N] = sum_k A[m][k] b[n][k] (bf16, fp32 accumulate) with A[m][k] =
+    a.flat[(a_row + m) * lda + k] (rows may overlap), b [N][K] contiguous bf16."""
+    N = b.shape[0]
+    if M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and lda % 8 == 0 and ldc % 8 == 0:
+        call("triad_gemm_bf16", _addr(a, a_row, lda), lda, 1, ptr(b), K, 1, M, N, K, None, _addr(out, out_row, ldc), ldc,
+             1, stream_ptr(a.device))
+    else:  # same product through torch (it copies the overlapping operand)
+        A = a.as_strided((M, K), (lda, 1), a.storage_offset() + a_row * lda)
+        out.as_strided((M, N), (ldc, 1), out.storage_offset() + out_row * ldc).copy_(torch.mm(A, b.t()))
+
+
+def _weight_grad_rows(dy, M, x, ldx, N):
+    """fp32 [O][N] = sum_r dy[r][o] X[r][n] over r < M, X[r][n] = x.flat[r * ldx + n] (overlapping)."""
+    O = dy.shape[1]
+    if M % 64 == 0 and O % 128 == 0 and N % 128 == 0 and ldx % 8 == 0:
+        sp = 8
+        slabs = torch.empty(sp * O * N, dtype=torch.float32, device=dy.device)
+        out = torch.empty(O, N, dtype=torch.float32, device=dy.device)
+        call("triad_gemm_bf16_splitk", ptr(dy), O, 0, ptr(x), ldx, 0, O, N, M, sp, None, ptr(slabs), ptr(out), 0,
+             stream_ptr(dy.device))
+        return out
+    X = x.as_strided((M, N), (ldx, 1), x.storage_offset())
+    return torch.mm(dy[:M].t(), X, out_dtype=torch.float32)
+
+
+class _FrameConv0(torch.autograd.Function):
+    """HuBERT conv layer 0 (1 -> O channels, kernel k, stride s, no bias) from the (B, L)
+    waveform into a padded frame buffer; the padding frame is computed from zero-padded
+    samples. The waveform gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, wave, w, stride, Tp):
+        B, L = wave.shape
+        O, _, k = w.shape
+        need = (Tp - 1) * stride + k
+        xw = F.pad(wave.to(torch.bfloat16), (0, max(0, need - L)))
+        cols = xw.unfold(1, k, stride)[:, :Tp].reshape(B * Tp, k)
+        wr = w.to(torch.bfloat16).reshape(O, k)
+        y = torch.empty(B * Tp + 2, O, dtype=torch.bfloat16, device=wave.device)
+        torch.mm(cols, wr.t(), out=y[:B * Tp])
+        y[B * Tp:].zero_()
+        ctx.save_for_backward(cols)
+        ctx.meta = (B, Tp, w.shape, w.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (cols,) = ctx.saved_tensors
+        B, Tp, wshape, wdt = ctx.meta
+        dw = torch.mm(dy[:B * Tp].t().to(torch.bfloat16), cols, out_dtype=torch.float32)
+        return None, dw.view(wshape).to(wdt), None, None
+
+
+class _FrameConvS2(torch.autograd.Function):
+    """Kernel-k (2 or 3), stride-2 conv (C -> O, no bias) between padded frame buffers:
+    x [B*Tp + 2, C] -> y [B*Tp/2 + 2, O]."""
+
+    @staticmethod
+    def forward(ctx, x, w, B, Tp):
+        Cin = x.shape[1]
+        O, Cw, k = w.shape
+        if Cw != Cin or k not in (2, 3) or Tp % 2 or x.shape[0] != B * Tp + 2:
+            raise _lib.TriadError("frame conv: expects a [B*Tp + 2, C] buffer, even Tp, kernel 2 or 3")
+        M = B * Tp // 2
+        wr = w.to(torch.bfloat16).permute(0, 2, 1).reshape(O, k * Cin).contiguous()
+        y = torch.empty(M + 2, O, dtype=torch.bfloat16, device=x.device)
+        _gemm_rows(x, 0, 2 * Cin, M, k * Cin, wr, y, 0, O)
+        y[M:].zero_()
+        ctx.save_for_backward(x, w)
+        ctx.meta = (B, Tp, w.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        B, Tp, wdt = ctx.meta
+        Cin = x.shape[1]
+        O, _, k = w.shape
+        M = B * Tp // 2
+        dy = dy.to(torch.bfloat16).contiguous()
+        wb = w.to(torch.bfloat16)
+        wj = [wb[:, :, j] for j in range(k)]  # [O][C] each
+        dx = torch.empty(M + 1, 2 * Cin, dtype=torch.bfloat16, device=x.device)  # = B*Tp + 2 frames
+        if k == 3:
+            # even frames 2q: dY[q-1] W2 + dY[q] W0 -- rows q = 1..M over overlapping dY rows
+            be = torch.cat([wj[2].t(), wj[0].t()], dim=1).contiguous()  # [C][2O]
+            _gemm_rows(dy, 0, O, M, 2 * O, be, dx, 1, 2 * Cin)
+            dx[0, :Cin] = (dy[0:1] @ wj[0])[0]
+            # odd frames 2q+1: dY[q] W1
+            _gemm_rows(dy, 0, O, M, O, wj[1].t().contiguous(), dx[:, Cin:], 0, 2 * Cin)
+        else:
+            bk = torch.cat([wj[0].t(), wj[1].t()], dim=0).contiguous()  # [2C][O]
+            _gemm_rows(dy, 0, O, M, O, bk, dx, 0, 2 * Cin)
+        dx[M].zero_()  # spare frames: constants
+        dwr = _weight_grad_rows(dy, M, x, 2 * Cin, k * Cin)  # [O][k*C], column j*C + c
+        dw = dwr.view(O, k, Cin).permute(0, 2, 1).to(wdt)
+        return dx.view(2 * M + 2, Cin), dw, None, None
 
 
 def channel_group_norm_gelu(x, gamma, beta, eps):
@@ -135,13 +264,53 @@ def channel_group_norm_gelu(x, gamma, beta, eps):
     return _ChannelGroupNormGelu.apply(x, gamma, beta, float(eps))
 
 
+def _frame_stack_plan(self, input_values):
+    """[(T, Tp)] of layer 0's output and every later layer's input when HuBERT's layout runs
+    over padded frame buffers (every Tp even), else None."""
+    layers = self.conv_layers
+    if len(layers) < 2 or _compute_dtype(input_values) != torch.bfloat16 or input_values.dim() != 2:
+        return None
+    c0 = layers[0].conv
+    if c0.in_channels != 1 or c0.bias is not None or not isinstance(getattr(layers[0], "layer_norm", None),
+                                                                     nn.GroupNorm):
+        return None
+    T = (input_values.shape[1] - c0.kernel_size[0]) // c0.stride[0] + 1
+    Tp = T + (T & 1)
+    plan = [(T, Tp)]
+    for layer in layers[1:]:
+        c = layer.conv
+        if c.bias is not None or c.stride[0] != 2 or c.kernel_size[0] not in (2, 3) \
+                or getattr(layer, "layer_norm", None) is not None or Tp % 2:
+            return None
+        T = (T - c.kernel_size[0]) // 2 + 1
+        Tp //= 2
+        if T <= 0:
+            return None
+        plan.append((T, Tp))
+    return plan
+
+
 def _hubert_feature_encoder_forward(self, input_values):
     """transformers HubertFeatureEncoder.forward in channels-last GEMM form. Returns the
     (B, C, T) feature map as a transposed view of (B, T, C) storage (HubertModel transposes it
     straight back). The waveform gets no gradient (the reference only marks it for gradient
-    checkpointing)."""
+    checkpointing). HuBERT's own layout (conv0 + GroupNorm, then bias-free stride-2 convs)
+    runs over padded frame buffers (_FrameConv0 / _FrameConvS2); any other layout through
+    conv1d_gemm."""
     if not input_values.is_cuda:
         return self._triad_hf_forward(input_values)
+    plan = _frame_stack_plan(self, input_values)
+    if plan is not None:
+        B = input_values.shape[0]
+        l0 = self.conv_layers[0]
+        T, Tp = plan[0]
+        y = _FrameConv0.apply(input_values, l0.conv.weight, l0.conv.stride[0], Tp)
+        norm = l0.layer_norm
+        h = _ChannelGroupNormGelu.apply(y, norm.weight, norm.bias, float(norm.eps), (B, T, Tp))
+        for layer, (T, Tp_out) in zip(self.conv_layers[1:], plan[1:]):
+            h = layer.activation(_FrameConvS2.apply(h, layer.conv.weight, B, Tp))
+            Tp = Tp_out
+        return h[:B * Tp].view(B, Tp, -1)[:, :T].transpose(1, 2)
     h = input_values.unsqueeze(-1)
     cd = _compute_dtype(h)
     for i, layer in enumerate(self.conv_layers):
