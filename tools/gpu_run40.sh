@@ -1,0 +1,16 @@
+# generic GEMM: 256x128 ring form (spread / burst) vs the 128x128 form; parity of every GEMM user
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_frontend_gpu.py tests/test_ops_gpu.py tests/test_head_gpu.py tests/test_postln_gpu.py -x -q --timeout 250 --timeout-method thread > gpurun_out/tests_gbig.log 2>&1 || exit 1
+: > gpurun_out/ab.log
+for v in default gbigburst gold; do
+  if [ $v = default ]; then unset TRIAD_LIB_VARIANT; else export TRIAD_LIB_VARIANT=tools/variants/lib_$v.so; fi
+  echo "== $v" >> gpurun_out/ab.log
+  timeout -k 10 300 python tools/conv_micro.py >> gpurun_out/ab.log 2>&1 || exit 1
+  timeout -k 10 120 python tools/dw_variants.py 50944 2>&1 | grep triad >> gpurun_out/ab.log || exit 1
+done
+unset TRIAD_LIB_VARIANT
+timeout -k 10 600 python bench.py --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 1
+echo "all done"

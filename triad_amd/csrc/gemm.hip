@@ -25,29 +25,32 @@ __device__ __forceinline__ int nc_off(int k, int col) {
   return k * BN + ((((col >> 3) ^ ((k & 3) << 2))) << 3) + (col & 7);
 }
 
+// piece u (0..3) of this wave's share of an A stage (one 16-byte LDS-DMA wave-instruction)
+template <bool A_KCONTIG>
+__device__ __forceinline__ void stage_a_piece(const bf16* __restrict__ A, long long lda, int m0, int k0, bf16* dst,
+                                              int wave, int lane, int u) {
+  const int inst = wave * 4 + u;
+  if (A_KCONTIG) {  // 16 wave-instructions of 8 rows x 128 B
+    const int m = inst * 8 + (lane >> 3), cp = lane & 7;
+    const int c = cp ^ ((m >> 1) & 7);
+    glds16(A + (size_t)(m0 + m) * lda + k0 + c * 8, dst + inst * 512);
+  } else {  // A stored [k][m]: 16 wave-instructions of 4 k-rows x 256 B
+    const int k = inst * 4 + (lane >> 4), cp = lane & 15;
+    const int c = cp ^ ((k & 3) << 2);
+    glds16(A + (size_t)(k0 + k) * lda + m0 + c * 8, dst + inst * 512);
+  }
+}
+
 template <bool A_KCONTIG>
 __device__ __forceinline__ void stage_a(const bf16* __restrict__ A, long long lda, int m0, int k0, bf16* dst,
                                         int wave, int lane) {
-  if (A_KCONTIG) {
-    // 16 wave-instructions of 8 rows x 128 B
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int inst = wave * 4 + u;
-      const int m = inst * 8 + (lane >> 3), cp = lane & 7;
-      const int c = cp ^ ((m >> 1) & 7);
-      glds16(A + (size_t)(m0 + m) * lda + k0 + c * 8, dst + inst * 512);
-    }
-  } else {
-    // A stored [k][m]: 16 wave-instructions of 4 k-rows x 256 B
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int inst = wave * 4 + u;
-      const int k = inst * 4 + (lane >> 4), cp = lane & 15;
-      const int c = cp ^ ((k & 3) << 2);
-      glds16(A + (size_t)(k0 + k) * lda + m0 + c * 8, dst + inst * 512);
-    }
-  }
+  for (int u = 0; u < 4; ++u) stage_a_piece<A_KCONTIG>(A, lda, m0, k0, dst, wave, lane, u);
 }
+
+#ifndef GEMM_SPREAD
+#define GEMM_SPREAD 0  // 1: next stage's 8 DMA pieces issued between the 16 MFMAs, not in a burst
+#endif
 
 // B is [k][n] (B_KCONTIG=0, n-contiguous) or [n][k] (B_KCONTIG=1) -- the same two
 // images as A with the roles of m and n swapped.
@@ -107,8 +110,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
   }
   for (int kt = 0; kt < nk; ++kt) {
     lds_dma_barrier();
-    if (kt + 1 < nk) {
-      bf16* nb = lds + ((kt + 1) & 1) * (A_ELEMS + B_ELEMS);
+    bf16* const nb = lds + ((kt + 1) & 1) * (A_ELEMS + B_ELEMS);
+    const bool pf = kt + 1 < nk;
+    if (!GEMM_SPREAD && pf) {
       stage_a<A_KCONTIG>(A, lda, m0, kbeg + (kt + 1) * BK, nb, wave, lane);
       stage_b<B_KCONTIG>(B, ldb, n0, kbeg + (kt + 1) * BK, nb + A_ELEMS, wave, lane);
     }
@@ -136,7 +140,17 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[a], bfr[b], acc[a][b]);
+        for (int b = 0; b < 2; ++b) {
+          acc[a][b] = mfma32(af[a], bfr[b], acc[a][b]);
+          if (GEMM_SPREAD && (a * 2 + b) % 2 == 1) {  // 2 pieces per k-step: A piece s, B piece s
+            __builtin_amdgcn_sched_barrier(0);
+            if (pf) {
+              if (a == 0) stage_a_piece<A_KCONTIG>(A, lda, m0, kbeg + (kt + 1) * BK, nb, wave, lane, s);
+              else stage_a_piece<B_KCONTIG>(B, ldb, n0, kbeg + (kt + 1) * BK, nb + A_ELEMS, wave, lane, s);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
     }
   }
 
@@ -154,12 +168,154 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
     }
 }
 
+// ---- 256 x 128 ring form ----------------------------------------------------------------------
+// Workgroup = 8 waves (4 x 2, each 64 x 64 as above), tile 256 (M) x 128 (N) x 64 (K) per stage,
+// a 3-slot LDS ring (3 x 48 KB) with the next-but-one stage's LDS-DMA issued while the current
+// one computes; each wave issues exactly 6 pieces per stage, so the wait for stage kt is a
+// counted `s_waitcnt vmcnt(6)` (stage kt+1 stays in flight) + the barrier. Twice the B reuse
+// of the 128 x 128 form. The A image is [256][64] (k-contiguous A) or two [64][128] halves.
+constexpr int GB_M = 256, GB_NB = 3;
+constexpr int GB_A = GB_M * BK, GB_ST = GB_A + B_ELEMS;  // elements per stage (48 KB)
+constexpr int GB_PIECES = 6;
+
+#ifndef GBIG_SPREAD
+#define GBIG_SPREAD 1  // 1: the 6 pieces between the 16 MFMAs of a stage (one per 2); 0: burst
+#endif
+
+template <bool A_KCONTIG, bool B_KCONTIG>
+__device__ __forceinline__ void gb_piece(const bf16* __restrict__ A, long long lda, const bf16* __restrict__ B,
+                                         long long ldb, int m0, int n0, int k0, bf16* dst, int wave, int lane,
+                                         int u) {
+  if (u < 4) {  // A: 32 pieces, 4 per wave
+    const int inst = wave * 4 + u;
+    if (A_KCONTIG) {  // 8 rows x 128 B
+      const int m = inst * 8 + (lane >> 3), cp = lane & 7;
+      const int c = cp ^ ((m >> 1) & 7);
+      glds16(A + (size_t)(m0 + m) * lda + k0 + c * 8, dst + inst * 512);
+    } else {  // half inst >> 4, 4 k-rows x 256 B
+      const int half = inst >> 4, ii = inst & 15;
+      const int k = ii * 4 + (lane >> 4), cp = lane & 15;
+      const int c = cp ^ ((k & 3) << 2);
+      glds16(A + (size_t)(k0 + k) * lda + m0 + half * 128 + c * 8, dst + half * (BK * 128) + ii * 512);
+    }
+  } else {  // B: 16 pieces, 2 per wave
+    const int inst = wave * 2 + (u - 4);
+    bf16* bd = dst + GB_A;
+    if (B_KCONTIG) {
+      const int n = inst * 8 + (lane >> 3), cp = lane & 7;
+      const int c = cp ^ ((n >> 1) & 7);
+      glds16(B + (size_t)(n0 + n) * ldb + k0 + c * 8, bd + inst * 512);
+    } else {
+      const int k = inst * 4 + (lane >> 4), cp = lane & 15;
+      const int c = cp ^ ((k & 3) << 2);
+      glds16(B + (size_t)(k0 + k) * ldb + n0 + c * 8, bd + inst * 512);
+    }
+  }
+}
+
+template <bool A_KCONTIG, bool B_KCONTIG, typename OutT>
+__global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict__ A, long long lda,
+                                                          const bf16* __restrict__ B, long long ldb, int M, int N,
+                                                          int Kd, const float* __restrict__ alpha_p,
+                                                          OutT* __restrict__ C, long long ldc, int k_per_split,
+                                                          long long slab_stride) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[GB_NB * GB_ST];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  const int ntn = N / BN;
+  const int m0 = (swz / ntn) * GB_M, n0 = (swz % ntn) * BN;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){};
+
+  const int kbeg = blockIdx.y * k_per_split;
+  const int nk = __builtin_amdgcn_readfirstlane(max(0, min(k_per_split, Kd - kbeg)) / BK);
+  C += (size_t)blockIdx.y * slab_stride;
+#pragma unroll
+  for (int p = 0; p < GB_NB - 1; ++p)
+    if (p < nk)
+#pragma unroll
+      for (int u = 0; u < GB_PIECES; ++u)
+        gb_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kbeg + p * BK, lds + p * GB_ST, wave, lane, u);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB_PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool pf = kt + GB_NB - 1 < nk;
+    bf16* const nb = lds + ((kt + GB_NB - 1) % GB_NB) * GB_ST;
+    const int kn = kbeg + (kt + GB_NB - 1) * BK;
+    if (!GBIG_SPREAD && pf)
+#pragma unroll
+      for (int u = 0; u < GB_PIECES; ++u) gb_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, u);
+    const bf16* ai = lds + (kt % GB_NB) * GB_ST;
+    const bf16* bi = ai + GB_A;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int mrow = wm * 64 + t * 32;
+        if (A_KCONTIG) af[t] = *(const bf16x8*)(ai + kc_off(mrow + (lane & 31), 2 * s + h));
+        else af[t] = frag_tr(ai + (mrow >> 7) * (BK * 128), mrow & 127, s, lane);
+        const int ncol = wn * 64 + t * 32;
+        if (B_KCONTIG) bfr[t] = *(const bf16x8*)(bi + kc_off(ncol + (lane & 31), 2 * s + h));
+        else bfr[t] = frag_tr(bi, ncol, s, lane);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          acc[a][b] = mfma32(af[a], bfr[b], acc[a][b]);
+          const int mi = s * 4 + a * 2 + b;
+          if (GBIG_SPREAD && (mi & 1) && mi / 2 < GB_PIECES) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (pf) gb_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, mi / 2);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+    }
+  }
+
+  const float alpha = alpha_p ? *alpha_p : 1.f;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int n = n0 + wn * 64 + b * 32 + (lane & 31);
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int m = m0 + wm * 64 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v]);
+      }
+    }
+}
+
+#ifndef GEMM_BIG
+#define GEMM_BIG 1  // 1: gemm_big_kernel where it measured faster (see launch)
+#endif
+
 template <bool AK, bool BK_, typename OutT>
 int launch(const void* A, long long lda, const void* B, long long ldb, int M, int N, int Kd, const float* alpha,
            void* C, long long ldc, hipStream_t st, int splits = 1, long long slab_stride = 0) {
   if (M % BM || N % BN || Kd % BK || lda % 8 || ldb % 8 || splits < 1) return TRIAD_EINVAL;
-  const int nwg = (M / BM) * (N / BN);
   const int kps = ((Kd / BK + splits - 1) / splits) * BK;
+  // the 256-row ring pays off on long k loops or many row tiles (conv / projection GEMMs);
+  // the short split-K weight-gradient loops keep the 128 x 128 form (measured, tools/dw_variants.py)
+  if (GEMM_BIG && M % GB_M == 0 && (M >= 8192 || Kd / splits >= 32768)) {
+    const int nwg = (M / GB_M) * (N / BN);
+    hipLaunchKernelGGL((gemm_big_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
+                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride);
+    TRIAD_CHECK_LAUNCH();
+    return TRIAD_OK;
+  }
+  const int nwg = (M / BM) * (N / BN);
   hipLaunchKernelGGL((gemm_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(256), 0, st, (const bf16*)A, lda,
                      (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride);
   TRIAD_CHECK_LAUNCH();
