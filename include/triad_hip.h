@@ -210,6 +210,23 @@ int triad_attn_bwd(const void* q, long long q_sB, long long q_sN, const void* k,
                    const void* dout, long long do_sB, long long do_sN, const float* lse, int B, int H, int N, int D,
                    float scale, void* dq, long long dq_sB, long long dq_sN, void* dk, long long dk_sB,
                    long long dk_sN, void* dv, long long dv_sB, long long dv_sN, float* delta, hipStream_t stream);
+/* Attention-probability dropout (HuBERT / DistilBERT attention_dropout, transformers' sdpa path):
+ * O = (softmax(Q K^T scale) * keep / (1 - p)) V, lse of the undropped scores. Keep bits from the
+ * common.h hash of element (bh N + q) N + key, stored by triad_attn_dropmask in two layouts of
+ * ceil(N/32) words per row: wq[(bh N + q) nkt + kt] (bit j = key 32 kt + j) and wk[(bh N + key) nkt + qt]
+ * (bit j = query 32 qt + j); B*H*N*nkt u32 each. NULL masks = no dropout. */
+int triad_attn_dropmask(int B, int H, int N, float p, unsigned seed, unsigned* wq, unsigned* wk, hipStream_t stream);
+int triad_attn_fwd_dropout(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB,
+                           long long k_sN, const void* v, long long v_sB, long long v_sN, int B, int H, int N, int D,
+                           float scale, const unsigned* wq, float p, void* out, long long out_sB, long long out_sN,
+                           float* lse, hipStream_t stream);
+int triad_attn_bwd_dropout(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB,
+                           long long k_sN, const void* v, long long v_sB, long long v_sN, const void* o,
+                           long long o_sB, long long o_sN, const void* dout, long long do_sB, long long do_sN,
+                           const float* lse, int B, int H, int N, int D, float scale, const unsigned* wq,
+                           const unsigned* wk, float p, void* dq, long long dq_sB, long long dq_sN, void* dk,
+                           long long dk_sB, long long dk_sN, void* dv, long long dv_sB, long long dv_sN, float* delta,
+                           hipStream_t stream);
 
 /* LoRA skinny products (model.py:223-266, peft LoRA r = 8 on the ViT's attn.qkv / attn.proj):
  * triad_rows_nt: out[m][j] = sum_k X[m][k] * W[j][k], X [M][ldx] bf16, W [J][K] bf16, J <= 16,

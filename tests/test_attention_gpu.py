@@ -67,3 +67,33 @@ def test_attention_fused_qkv_and_strided_views():
     o2 = attention.sdpa(qh, kh, vh)
     ref2 = torch.nn.functional.scaled_dot_product_attention(qh.float(), kh.float(), vh.float())
     assert _rel(o2.float(), ref2) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,N,p", [(2, 12, 199, 0.1), (3, 4, 261, 0.1), (2, 3, 33, 0.5), (4, 2, 32, 0.1),
+                                     (1, 2, 320, 0.3)])
+def test_attention_dropout_matches_fp32_on_same_mask(B, H, N, p, monkeypatch):
+    """Attention-probability dropout (HuBERT / DistilBERT attention_dropout) against torch fp32
+    softmax * keep / (1 - p) @ V on the SAME keep bits; the query- and key-major bit layouts the
+    forward and the two backward kernels read must describe one mask."""
+    from triad_amd import attention
+    seed = 4242 + N
+    monkeypatch.setattr(attention, "_SEEDS", lambda: seed)
+    keep_q, keep_k = attention.dropout_keep_dense(B, H, N, p, seed, dev)
+    assert torch.equal(keep_q, keep_k)
+    frac = float(keep_q.float().mean())
+    assert abs(frac - (1 - p)) < 0.02
+    g = torch.Generator(device=dev).manual_seed(N)
+    q, k, v = [(torch.randn(B, N, H, 64, device=dev, generator=g) * 1.5).to(torch.bfloat16) for _ in range(3)]
+    scale = 1.0 / math.sqrt(64)
+    qr, kr, vr = [t.float().requires_grad_(True) for t in (q, k, v)]
+    s = torch.einsum("bnhd,bmhd->bhnm", qr, kr) * scale
+    pr = torch.softmax(s, -1) * keep_q.float() / (1 - p)
+    ref = torch.einsum("bhnm,bmhd->bnhd", pr, vr)
+    qd, kd, vd = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    out = attention.attention_bnhd(qd, kd, vd, scale, dropout=p)
+    assert _rel(out.float(), ref) < 1e-2
+    go = torch.randn(B, N, H, 64, device=dev, generator=g)
+    ref.backward(go)
+    out.backward(go.to(torch.bfloat16))
+    for name, a, r in (("dq", qd.grad, qr.grad), ("dk", kd.grad, kr.grad), ("dv", vd.grad, vr.grad)):
+        assert _rel(a.float(), r) < 1e-2, (name, _rel(a.float(), r))

@@ -60,6 +60,11 @@ SIGNATURES = {
     "triad_addln_bwd": [vp, i32, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, vp],
     "triad_lora_tn_blocks": [i32],
     "triad_lora_tn": [vp, i64, i32, i32, vp, vp, vp, f32, vp, vp, vp],
+    "triad_attn_dropmask": [i32, i32, i32, f32, u32, vp, vp, vp],
+    "triad_attn_fwd_dropout": [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, f32, vp, f32, vp, i64,
+                               i64, vp, vp],
+    "triad_attn_bwd_dropout": [vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i32, i32,
+                               i32, i32, f32, vp, vp, f32, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, vp],
     "triad_attn_fwd": [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, f32, vp, i64, i64, vp, vp],
     "triad_attn_bwd": [vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i32, i32, i32,
                        i32, f32, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, vp],

@@ -4,9 +4,10 @@ The reference's encoders (SajayR/TRIAD model.py:29-30,79-80,218-227: DINOv2, HuB
 DistilBERT) run softmax(Q K^T * scale) V over short sequences -- 261 visual tokens, 199 audio
 frames, 32 text tokens -- with head dim 64. PyTorch-ROCm's flash-attention kernels are tuned for
 long sequences; here each (sample, head) sequence sits in LDS and a wave keeps a whole 32-row
-tile of scores in registers (exact softmax, no online rescaling). Used for dropout-free,
-mask-free attention with N <= 320 and head dim 64 in bf16; anything else goes to
-F.scaled_dot_product_attention.
+tile of scores in registers (exact softmax, no online rescaling). Used for mask-free attention
+with N <= 320 and head dim 64 in bf16, with or without dropout on the attention probabilities
+(keep bits from the common.h counter hash, stored as bit words for the backward); anything
+else goes to F.scaled_dot_product_attention.
 """
 from __future__ import annotations
 
@@ -36,44 +37,77 @@ def _as_bnhd(t):
     return t
 
 
-def _fwd(q, k, v, scale):
+def _dropmask(B, H, N, p, device):
+    """Keep bits of the attention-probability dropout in both layouts (triad_attn_dropmask)."""
+    nkt = (N + 31) // 32
+    wq = torch.empty(B * H * N * nkt, dtype=torch.int32, device=device)
+    wk = torch.empty_like(wq)
+    call("triad_attn_dropmask", B, H, N, float(p), _SEEDS(), ptr(wq), ptr(wk), stream_ptr(device))
+    return wq, wk
+
+
+def _fwd(q, k, v, scale, drop=None):
     B, N, H, D = q.shape
     out = torch.empty(B, N, H, D, dtype=torch.bfloat16, device=q.device)
     lse = torch.empty(B * H, N, dtype=torch.float32, device=q.device)
-    call("triad_attn_fwd", ptr(q), *_rows(q), ptr(k), *_rows(k), ptr(v), *_rows(v), B, H, N, D, float(scale),
-         ptr(out), *_rows(out), ptr(lse), stream_ptr(q.device))
+    wq, p = (drop[0], drop[2]) if drop is not None else (None, 0.0)
+    call("triad_attn_fwd_dropout", ptr(q), *_rows(q), ptr(k), *_rows(k), ptr(v), *_rows(v), B, H, N, D, float(scale),
+         ptr(wq), float(p), ptr(out), *_rows(out), ptr(lse), stream_ptr(q.device))
     return out, lse
 
 
-def _bwd(q, k, v, out, lse, dout, scale):
+def _bwd(q, k, v, out, lse, dout, scale, drop=None):
     """-> (B, N, 3, H, 64) buffer holding dq, dk, dv (a fused qkv projection's gradient layout)."""
     B, N, H, D = q.shape
     do = _as_bnhd(dout.to(torch.bfloat16))
     g = torch.empty(B, N, 3, H, D, dtype=torch.bfloat16, device=q.device)
     dq, dk, dv = g[:, :, 0], g[:, :, 1], g[:, :, 2]
     delta = torch.empty(B * H, N, dtype=torch.float32, device=q.device)
-    call("triad_attn_bwd", ptr(q), *_rows(q), ptr(k), *_rows(k), ptr(v), *_rows(v), ptr(out), *_rows(out),
-         ptr(do), *_rows(do), ptr(lse), B, H, N, D, float(scale), ptr(dq), *_rows(dq), ptr(dk), *_rows(dk), ptr(dv),
-         *_rows(dv), ptr(delta), stream_ptr(q.device))
+    wq, wk, p = drop if drop is not None else (None, None, 0.0)
+    call("triad_attn_bwd_dropout", ptr(q), *_rows(q), ptr(k), *_rows(k), ptr(v), *_rows(v), ptr(out), *_rows(out),
+         ptr(do), *_rows(do), ptr(lse), B, H, N, D, float(scale), ptr(wq), ptr(wk), float(p), ptr(dq), *_rows(dq),
+         ptr(dk), *_rows(dk), ptr(dv), *_rows(dv), ptr(delta), stream_ptr(q.device))
     return g
 
 
+class _Seeds:
+    """Per-call 32-bit dropout seeds from a host generator (no device sync)."""
+
+    def __init__(self):
+        self.gen = torch.Generator()
+        self.gen.manual_seed(torch.initial_seed() % (2 ** 63) + 1)
+
+    def __call__(self):
+        return int(torch.randint(0, 2 ** 32 - 1, (1,), generator=self.gen))
+
+
+_SEEDS = _Seeds()
+
+
 class _Attention(torch.autograd.Function):
-    """q, k, v: (B, N, H, 64) bf16 views (head dim contiguous, heads adjacent) -> O (B, N, H, 64)."""
+    """q, k, v: (B, N, H, 64) bf16 views (head dim contiguous, heads adjacent) -> O (B, N, H, 64);
+    dropout p > 0 drops attention probabilities (keep bits drawn per call, kept for the backward)."""
 
     @staticmethod
-    def forward(ctx, q, k, v, scale):
+    def forward(ctx, q, k, v, scale, p=0.0):
         q, k, v = _as_bnhd(q), _as_bnhd(k), _as_bnhd(v)
-        out, lse = _fwd(q, k, v, scale)
-        ctx.save_for_backward(q, k, v, out, lse)
+        drop = None
+        if p > 0.0:
+            B, N, H, _ = q.shape
+            drop = (*_dropmask(B, H, N, p, q.device), float(p))
+        out, lse = _fwd(q, k, v, scale, drop)
+        ctx.save_for_backward(q, k, v, out, lse, *(drop[:2] if drop else ()))
         ctx.scale = float(scale)
+        ctx.p = float(p)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        q, k, v, out, lse = ctx.saved_tensors
-        g = _bwd(q, k, v, out, lse, dout, ctx.scale)
-        return g[:, :, 0], g[:, :, 1], g[:, :, 2], None
+        saved = ctx.saved_tensors
+        q, k, v, out, lse = saved[:5]
+        drop = (saved[5], saved[6], ctx.p) if ctx.p > 0.0 else None
+        g = _bwd(q, k, v, out, lse, dout, ctx.scale, drop)
+        return g[:, :, 0], g[:, :, 1], g[:, :, 2], None, None
 
 
 class _AttentionQKV(torch.autograd.Function):
@@ -105,11 +139,26 @@ def attention_qkv(qkv, heads, scale=None):
     return _AttentionQKV.apply(qkv, heads, scale)
 
 
-def attention_bnhd(q, k, v, scale=None):
-    """softmax(q k^T * scale) v over (B, N, H, 64) bf16 views -> (B, N, H, 64)."""
+def attention_bnhd(q, k, v, scale=None, dropout=0.0):
+    """dropout(softmax(q k^T * scale)) v over (B, N, H, 64) bf16 views -> (B, N, H, 64)."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
-    return _Attention.apply(q, k, v, scale)
+    return _Attention.apply(q, k, v, scale, float(dropout))
+
+
+def dropout_keep_dense(B, H, N, p, seed, device):
+    """(B, H, N, N) keep mask (bool) of the attention dropout for a given seed, unpacked from both
+    stored layouts (tests: the two must agree)."""
+    nkt = (N + 31) // 32
+    wq = torch.empty(B * H * N * nkt, dtype=torch.int32, device=device)
+    wk = torch.empty_like(wq)
+    call("triad_attn_dropmask", B, H, N, float(p), seed, ptr(wq), ptr(wk), stream_ptr(device))
+    bits = torch.arange(32, device=device, dtype=torch.int32)
+
+    def unpack(w):
+        m = ((w.view(B, H, N, nkt, 1) >> bits) & 1).bool().view(B, H, N, nkt * 32)
+        return m[..., :N]
+    return unpack(wq), unpack(wk).transpose(-1, -2)
 
 
 def sdpa(q, k, v, scale=None):
@@ -124,15 +173,16 @@ def sdpa(q, k, v, scale=None):
 
 def hf_attention_forward(module, query, key, value, attention_mask, dropout=0.0, scaling=None, is_causal=None,
                          **kwargs):
-    """transformers attention-interface function ("triad"): the HIP kernels for unmasked,
-    dropout-free attention over <= 320 tokens, else the stock sdpa implementation. Returns
-    (B, N, H, d) as the interface requires."""
+    """transformers attention-interface function ("triad"): the HIP kernels for unmasked attention
+    over <= 320 tokens (attention dropout included), else the stock sdpa implementation.
+    Returns (B, N, H, d) as the interface requires."""
     from transformers.integrations.sdpa_attention import sdpa_attention_forward
     B, H, N, d = query.shape
-    if (attention_mask is not None or (dropout and module.training) or kwargs.get("output_attentions")
+    p = float(dropout) if module.training else 0.0
+    if (attention_mask is not None or kwargs.get("output_attentions") or not 0.0 <= p < 1.0
             or key.shape != query.shape or value.shape != query.shape or not supported(query, N, d)
             or getattr(module, "is_causal", False)):
         return sdpa_attention_forward(module, query, key, value, attention_mask, dropout=dropout, scaling=scaling,
                                       is_causal=is_causal, **kwargs)
-    o = attention_bnhd(query.transpose(1, 2), key.transpose(1, 2), value.transpose(1, 2), scaling)
+    o = attention_bnhd(query.transpose(1, 2), key.transpose(1, 2), value.transpose(1, 2), scaling, dropout=p)
     return o, None

@@ -36,7 +36,16 @@ struct AttnArgs {
   float* delta;     // [B*H][N] rowsum(dO * O)
   int B, H, N;
   float scale;
+  // dropout on the attention probabilities (DROP kernels): keep bits by query row
+  // wq[(bh * N + q) * nkt + kt] (bit j = key 32 kt + j) and by key row wk[(bh * N + key) * nkt + qt]
+  // (bit j = query 32 qt + j); kept probabilities scaled by drop_scale = 1 / (1 - p)
+  const unsigned *wq, *wk;
+  int nkt;
+  float drop_scale;
 };
+
+// bit of accumulator element v (row / column (v & 3) + 8 (v >> 2) + 4 h of a 32-wide tile)
+__device__ __forceinline__ bool tile_bit(unsigned w, int v, int h) { return (w >> ((v & 3) + 8 * (v >> 2) + 4 * h)) & 1u; }
 
 __device__ __forceinline__ int swz(int row) {
   const int k = (row >> 1) & 7;
@@ -110,7 +119,7 @@ __device__ __forceinline__ void store_cols(bf16* dst, const f32x16& a, float mul
 }
 
 // ---------------------------------------------------------------------------------------------
-template <int NKT>
+template <int NKT, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[2 * NKT * 32 * 128];
   char* kl = lds;
@@ -165,6 +174,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
       l += p;
     }
   l += __shfl_xor(l, 32);
+  if (DROP) {  // O = sum_k p_k keep_k / (1 - p) v_k; l (the normaliser) keeps every p_k
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const unsigned w = qok ? a.wq[((long long)bh * a.N + q) * NKT + kt] : 0u;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[kt][v] = tile_bit(w, v, h) ? acc[kt][v] : 0.f;
+    }
+  }
 
   f32x16 o0 = {}, o1 = {};
 #pragma unroll
@@ -177,7 +194,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
       o1 = mfma32(frag_tr(vl, c, 32, lane), pf, o1);
     }
   if (!qok) return;
-  const float inv = 1.f / l;
+  const float inv = (DROP ? a.drop_scale : 1.f) / l;
   bf16* op = a.out + b * a.out_sB + (long long)q * a.out_sN + hh * HD;
   store_cols(op, o0, inv, h);
   store_cols(op + 32, o1, inv, h);
@@ -185,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
 }
 
 // dQ: wave = query tile, query on the lane (the forward's orientation)
-template <int NKT>
+template <int NKT, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[2 * NKT * 32 * 128];
   char* kl = lds;
@@ -228,11 +245,13 @@ __global__ __launch_bounds__(256, 2) void attn_dq_kernel(AttnArgs a) {
       dp = mfma32(lds_b128(vl, kt * 32 + ql, 2 * st + h), df[st], dp);
     }
     const int nv = a.N - kt * 32;
+    const unsigned w = DROP && qok ? a.wq[((long long)bh * a.N + q) * NKT + kt] : 0u;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       const bool ok = qok && (v & 3) + 8 * (v >> 2) + 4 * h < nv;
       const float p = ok ? exp2f(fmaf(s[v], c2, -lse2)) : 0.f;
-      s[v] = p * (dp[v] - dl);  // dS
+      const float dpv = DROP ? (tile_bit(w, v, h) ? dp[v] * a.drop_scale : 0.f) : dp[v];
+      s[v] = p * (dpv - dl);  // dS
     }
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -249,7 +268,7 @@ __global__ __launch_bounds__(256, 2) void attn_dq_kernel(AttnArgs a) {
 }
 
 // dK, dV: wave = key tile, key on the lane
-template <int NQT>
+template <int NQT, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[2 * NQT * 32 * 128];
   __shared__ float stat[2][NQT * 32];
@@ -290,6 +309,7 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_kernel(AttnArgs a) {
       dp = mfma32(lds_b128(dl_, qt * 32 + kl, 2 * st + h), vf[st], dp);
     }
     // rows of this lane's accumulator: queries qt*32 + (v&3) + 8(v>>2) + 4h (4 runs of 4)
+    const unsigned w = DROP && kok ? a.wk[((long long)bh * a.N + key) * NQT + qt] : 0u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int q0 = qt * 32 + 8 * j + 4 * h;
@@ -299,8 +319,14 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_kernel(AttnArgs a) {
       for (int i = 0; i < 4; ++i) {
         const int v = 4 * j + i;
         const float p = kok ? exp2f(fmaf(s[v], c2, -ls[i])) : 0.f;
-        s[v] = p;
-        dp[v] = p * (dp[v] - de[i]);  // dS
+        if (DROP) {
+          const float m = tile_bit(w, v, h) ? a.drop_scale : 0.f;
+          s[v] = p * m;                 // dropped probability (dV operand)
+          dp[v] = p * (dp[v] * m - de[i]);  // dS
+        } else {
+          s[v] = p;
+          dp[v] = p * (dp[v] - de[i]);  // dS
+        }
       }
     }
 #pragma unroll
@@ -331,19 +357,60 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_kernel(AttnArgs a) {
   }
 }
 
-#define ATTN_SWITCH(KERNEL, NT, GRID, ARGS)                                                     \
+#define ATTN_SWITCH(KERNEL, DR, NT, GRID, ARGS)                                                 \
   switch (NT) {                                                                                \
-    case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, stream, ARGS); break;             \
-    case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, stream, ARGS); break;             \
-    case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, stream, ARGS); break;             \
-    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, stream, ARGS); break;             \
-    case 5: hipLaunchKernelGGL(KERNEL<5>, GRID, dim3(256), 0, stream, ARGS); break;             \
-    case 6: hipLaunchKernelGGL(KERNEL<6>, GRID, dim3(256), 0, stream, ARGS); break;             \
-    case 7: hipLaunchKernelGGL(KERNEL<7>, GRID, dim3(256), 0, stream, ARGS); break;             \
-    case 8: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(256), 0, stream, ARGS); break;             \
-    case 9: hipLaunchKernelGGL(KERNEL<9>, GRID, dim3(256), 0, stream, ARGS); break;             \
-    default: hipLaunchKernelGGL(KERNEL<10>, GRID, dim3(256), 0, stream, ARGS); break;           \
+    case 1: hipLaunchKernelGGL((KERNEL<1, DR>), GRID, dim3(256), 0, stream, ARGS); break;       \
+    case 2: hipLaunchKernelGGL((KERNEL<2, DR>), GRID, dim3(256), 0, stream, ARGS); break;       \
+    case 3: hipLaunchKernelGGL((KERNEL<3, DR>), GRID, dim3(256), 0, stream, ARGS); break;       \
+    case 4: hipLaunchKernelGGL((KERNEL<4, DR>), GRID, dim3(256), 0, stream, ARGS); break;       \
+    case 5: hipLaunchKernelGGL((KERNEL<5, DR>), GRID, dim3(256), 0, stream, ARGS); break;       \
+    case 6: hipLaunchKernelGGL((KERNEL<6, DR>), GRID, dim3(256), 0, stream, ARGS); break;       \
+    case 7: hipLaunchKernelGGL((KERNEL<7, DR>), GRID, dim3(256), 0, stream, ARGS); break;       \
+    case 8: hipLaunchKernelGGL((KERNEL<8, DR>), GRID, dim3(256), 0, stream, ARGS); break;       \
+    case 9: hipLaunchKernelGGL((KERNEL<9, DR>), GRID, dim3(256), 0, stream, ARGS); break;       \
+    default: hipLaunchKernelGGL((KERNEL<10, DR>), GRID, dim3(256), 0, stream, ARGS); break;     \
   }
+
+// keep bits of the attention-probability dropout in both layouts (AttnArgs::wq / wk): bit of
+// (bh, q, key) = element e = (bh N + q) N + key of the (B H, N, N) probability tensor.
+// Block = one 32 x 32 (query tile, key tile) of one (sample, head): 32 threads hash their query
+// row's pairs into its wq word, the words meet in LDS and 32 threads transpose them into wk.
+__global__ __launch_bounds__(64) void attn_dropmask_kernel(int N, int nkt, unsigned seed, unsigned thr,
+                                                           unsigned* __restrict__ wq, unsigned* __restrict__ wk) {
+  __shared__ unsigned words[32];
+  const int kt = blockIdx.x, qt = blockIdx.y;
+  const long long bh = blockIdx.z;
+  const int t = threadIdx.x;
+  if (t < 32) {
+    const int q = qt * 32 + t;
+    unsigned bits = 0u;
+    if (q < N) {
+      const unsigned long long e0 = (unsigned long long)((bh * N + q) * N + kt * 32);
+      const int ncol = min(32, N - kt * 32);
+      // pairs covering elements e0 .. e0 + ncol - 1
+      const unsigned long long p0 = e0 >> 1;
+      const int off = (int)(e0 & 1);
+      unsigned long long stream = 0ull;  // bit i = element e0 - off + i
+      const int npairs = (ncol + off + 1) >> 1;
+      for (int i = 0; i < npairs; ++i) stream |= (unsigned long long)keep_pair(p0 + i, seed, thr) << (2 * i);
+      bits = (unsigned)(stream >> off);
+      if (ncol < 32) bits &= (1u << ncol) - 1u;
+      wq[(bh * N + q) * nkt + kt] = bits;
+    }
+    words[t] = bits;
+  }
+  __syncthreads();
+  if (t >= 32) {
+    const int j = t - 32;  // key row kt * 32 + j: bit i = query qt * 32 + i
+    const int key = kt * 32 + j;
+    if (key < N) {
+      unsigned w = 0u;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) w |= ((words[i] >> j) & 1u) << i;
+      wk[(bh * N + key) * nkt + qt] = w;
+    }
+  }
+}
 
 bool attn_ok(int B, int H, int N, int D) { return B > 0 && H > 0 && N > 0 && N <= MAX_KT * 32 && D == HD; }
 
@@ -351,10 +418,21 @@ bool attn_ok(int B, int H, int N, int D) { return B > 0 && H > 0 && N > 0 && N <
 
 extern "C" {
 
-int triad_attn_fwd(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB, long long k_sN,
-                   const void* v, long long v_sB, long long v_sN, int B, int H, int N, int D, float scale, void* out,
-                   long long out_sB, long long out_sN, float* lse, hipStream_t stream) {
-  if (!attn_ok(B, H, N, D)) return TRIAD_EINVAL;
+int triad_attn_dropmask(int B, int H, int N, float p, unsigned seed, unsigned* wq, unsigned* wk, hipStream_t stream) {
+  if (B <= 0 || H <= 0 || N <= 0 || N > MAX_KT * 32 || p < 0.f || p >= 1.f || (long long)B * H > 65535)
+    return TRIAD_EINVAL;
+  const int nkt = (N + 31) / 32;
+  hipLaunchKernelGGL(attn_dropmask_kernel, dim3(nkt, nkt, B * H), dim3(64), 0, stream, N, nkt, seed,
+                     triad_drop_thr(p), wq, wk);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_attn_fwd_dropout(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB,
+                           long long k_sN, const void* v, long long v_sB, long long v_sN, int B, int H, int N, int D,
+                           float scale, const unsigned* wq, float p, void* out, long long out_sB, long long out_sN,
+                           float* lse, hipStream_t stream) {
+  if (!attn_ok(B, H, N, D) || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
   AttnArgs a = {};
   a.q = (const bf16*)q; a.q_sB = q_sB; a.q_sN = q_sN;
   a.k = (const bf16*)k; a.k_sB = k_sB; a.k_sN = k_sN;
@@ -362,18 +440,29 @@ int triad_attn_fwd(const void* q, long long q_sB, long long q_sN, const void* k,
   a.out = (bf16*)out; a.out_sB = out_sB; a.out_sN = out_sN;
   a.lse = lse; a.B = B; a.H = H; a.N = N; a.scale = scale;
   const int nt = (N + 31) / 32;
+  a.wq = wq; a.nkt = nt; a.drop_scale = 1.f / (1.f - p);
   const dim3 grid((nt + 3) / 4, B * H);
-  ATTN_SWITCH(attn_fwd_kernel, nt, grid, a)
+  if (wq) { ATTN_SWITCH(attn_fwd_kernel, true, nt, grid, a) }
+  else { ATTN_SWITCH(attn_fwd_kernel, false, nt, grid, a) }
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
 
-int triad_attn_bwd(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB, long long k_sN,
-                   const void* v, long long v_sB, long long v_sN, const void* o, long long o_sB, long long o_sN,
-                   const void* dout, long long do_sB, long long do_sN, const float* lse, int B, int H, int N, int D,
-                   float scale, void* dq, long long dq_sB, long long dq_sN, void* dk, long long dk_sB,
-                   long long dk_sN, void* dv, long long dv_sB, long long dv_sN, float* delta, hipStream_t stream) {
-  if (!attn_ok(B, H, N, D)) return TRIAD_EINVAL;
+int triad_attn_fwd(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB, long long k_sN,
+                   const void* v, long long v_sB, long long v_sN, int B, int H, int N, int D, float scale, void* out,
+                   long long out_sB, long long out_sN, float* lse, hipStream_t stream) {
+  return triad_attn_fwd_dropout(q, q_sB, q_sN, k, k_sB, k_sN, v, v_sB, v_sN, B, H, N, D, scale, nullptr, 0.f, out,
+                                out_sB, out_sN, lse, stream);
+}
+
+int triad_attn_bwd_dropout(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB,
+                           long long k_sN, const void* v, long long v_sB, long long v_sN, const void* o,
+                           long long o_sB, long long o_sN, const void* dout, long long do_sB, long long do_sN,
+                           const float* lse, int B, int H, int N, int D, float scale, const unsigned* wq,
+                           const unsigned* wk, float p, void* dq, long long dq_sB, long long dq_sN, void* dk,
+                           long long dk_sB, long long dk_sN, void* dv, long long dv_sB, long long dv_sN, float* delta,
+                           hipStream_t stream) {
+  if (!attn_ok(B, H, N, D) || p < 0.f || p >= 1.f || (!wq != !wk)) return TRIAD_EINVAL;
   AttnArgs a = {};
   a.q = (const bf16*)q; a.q_sB = q_sB; a.q_sN = q_sN;
   a.k = (const bf16*)k; a.k_sB = k_sB; a.k_sN = k_sN;
@@ -385,11 +474,27 @@ int triad_attn_bwd(const void* q, long long q_sB, long long q_sN, const void* k,
   a.dv = (bf16*)dv; a.dv_sB = dv_sB; a.dv_sN = dv_sN;
   a.lse = (float*)lse; a.delta = delta; a.B = B; a.H = H; a.N = N; a.scale = scale;
   const int nt = (N + 31) / 32;
+  a.wq = wq; a.wk = wk; a.nkt = nt; a.drop_scale = 1.f / (1.f - p);
   const dim3 grid((nt + 3) / 4, B * H);
-  ATTN_SWITCH(attn_dq_kernel, nt, grid, a)
-  ATTN_SWITCH(attn_dkv_kernel, nt, grid, a)
+  if (wq) {
+    ATTN_SWITCH(attn_dq_kernel, true, nt, grid, a)
+    ATTN_SWITCH(attn_dkv_kernel, true, nt, grid, a)
+  } else {
+    ATTN_SWITCH(attn_dq_kernel, false, nt, grid, a)
+    ATTN_SWITCH(attn_dkv_kernel, false, nt, grid, a)
+  }
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
+}
+
+int triad_attn_bwd(const void* q, long long q_sB, long long q_sN, const void* k, long long k_sB, long long k_sN,
+                   const void* v, long long v_sB, long long v_sN, const void* o, long long o_sB, long long o_sN,
+                   const void* dout, long long do_sB, long long do_sN, const float* lse, int B, int H, int N, int D,
+                   float scale, void* dq, long long dq_sB, long long dq_sN, void* dk, long long dk_sB,
+                   long long dk_sN, void* dv, long long dv_sB, long long dv_sN, float* delta, hipStream_t stream) {
+  return triad_attn_bwd_dropout(q, q_sB, q_sN, k, k_sB, k_sN, v, v_sB, v_sN, o, o_sB, o_sN, dout, do_sB, do_sN, lse,
+                                B, H, N, D, scale, nullptr, nullptr, 0.f, dq, dq_sB, dq_sN, dk, dk_sB, dk_sN, dv,
+                                dv_sB, dv_sN, delta, stream);
 }
 
 }  // extern "C"

@@ -16,6 +16,23 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
+// Dropout keep bits shared by every dropout kernel (postln.hip, attention.hip): a counter hash of
+// (seed, element pair q = e / 2) gives one 16-bit uniform per element; keep iff >= thr
+// (thr = round(p * 65536)). Bit 0 / bit 1 of keep_pair = elements 2q / 2q + 1.
+__device__ __forceinline__ unsigned hash32(unsigned x) {  // lowbias32
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ unsigned keep_pair(unsigned long long q, unsigned seed, unsigned thr) {
+  const unsigned h = hash32((unsigned)q * 0x9E3779B9u + seed + hash32((unsigned)(q >> 32) ^ 0x85ebca6bu));
+  return ((h & 0xffffu) >= thr ? 1u : 0u) | ((h >> 16) >= thr ? 2u : 0u);
+}
+inline unsigned triad_drop_thr(float p) { return (unsigned)(p * 65536.f + 0.5f); }
+
 // One 16-byte global->LDS DMA per lane (global_load_lds_dwordx4). The LDS
 // destination is the wave-uniform `lds_base` + lane*16; the global source is
 // per lane (CDNA4 LDS-DMA semantics).

@@ -18,20 +18,7 @@
 
 namespace {
 
-__device__ __forceinline__ unsigned hash32(unsigned x) {  // lowbias32
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
-}
-
-// keep bits of elements 2q and 2q+1 (bit 0 / bit 1)
-__device__ __forceinline__ unsigned keep_pair(unsigned long long q, unsigned seed, unsigned thr) {
-  const unsigned h = hash32((unsigned)q * 0x9E3779B9u + seed + hash32((unsigned)(q >> 32) ^ 0x85ebca6bu));
-  return ((h & 0xffffu) >= thr ? 1u : 0u) | ((h >> 16) >= thr ? 2u : 0u);
-}
+// hash32 / keep_pair: common.h
 
 __device__ __forceinline__ float drop(float v, bool keep, float scale) { return keep ? (float)(bf16)(v * scale) : 0.f; }
 
@@ -232,7 +219,7 @@ __global__ __launch_bounds__(256) void dropout_keep_kernel(long long n, unsigned
   out[e] = (keep_pair((unsigned long long)e >> 1, seed, thr) >> (e & 1)) & 1u;
 }
 
-unsigned drop_thr(float p) { return (unsigned)(p * 65536.f + 0.5f); }
+unsigned drop_thr(float p) { return triad_drop_thr(p); }
 
 }  // namespace
 

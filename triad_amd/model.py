@@ -91,8 +91,8 @@ def _hf_model(kind, name, config_overrides=None):
 
 
 def _register_attention():
-    """transformers attention-interface entry "triad": the HIP attention kernels for dropout-free,
-    unmasked short sequences, the stock sdpa function otherwise (triad_amd.attention)."""
+    """transformers attention-interface entry "triad": the HIP attention kernels (attention dropout
+    included) for unmasked short sequences, the stock sdpa function otherwise (triad_amd.attention)."""
     from transformers import AttentionInterface
     from transformers.masking_utils import ALL_MASK_ATTENTION_FUNCTIONS, AttentionMaskInterface
     AttentionInterface.register("triad", attention.hf_attention_forward)
