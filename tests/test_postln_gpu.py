@@ -122,3 +122,38 @@ def test_fused_hubert_encoder_matches_stock_without_dropout():
             assert float(g_f[n].norm()) < 1e-3 * float(g_s[n.replace("bias", "weight")].norm()) + 1e-6
             continue
         assert _rel(g_f[n], g_s[n]) < 3e-2, (n, _rel(g_f[n], g_s[n]))
+
+
+def test_fused_distilbert_matches_stock_without_dropout():
+    """Fused DistilBERT transformer (postln passes) vs the stock one with dropout off: same
+    last_hidden_state and parameter gradients to bf16 tolerance."""
+    from triad_amd import model as Mdl
+    from triad_amd import postln
+    torch.manual_seed(0)
+    enc = Mdl._hf_model("DistilBertModel", "none/none", dict(n_layers=2, dropout=0.0, attention_dropout=0.0))
+    enc = postln.install_fused_distilbert(enc).to(dev).train()
+    tr = enc.transformer
+    ids = torch.randint(1000, 30000, (4, 32), device=dev)
+
+    def run(fwd):
+        enc.zero_grad(set_to_none=True)
+        tr.forward = fwd
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = enc(input_ids=ids).last_hidden_state
+        gy = torch.linspace(-1, 1, out.numel(), device=dev).view_as(out)
+        (out.float() * gy).sum().backward()
+        return out.detach().float(), {n: q.grad.float().clone() for n, q in enc.named_parameters() if q.grad is not None}
+
+    fused_fwd = tr.forward
+    try:
+        o_f, g_f = run(fused_fwd)
+        o_s, g_s = run(tr._triad_stock_forward)
+    finally:
+        tr.forward = fused_fwd
+    assert o_f.shape == o_s.shape
+    assert _rel(o_f, o_s) < 1e-2
+    assert set(g_f) == set(g_s)
+    for n in g_s:
+        if n.endswith("k_lin.bias"):  # exactly 0 in exact arithmetic: noise
+            continue
+        assert _rel(g_f[n], g_s[n]) < 3e-2, (n, _rel(g_f[n], g_s[n]))

@@ -32,7 +32,7 @@ import torch.nn.functional as F
 
 from . import _lib, attention, frontend, ops
 from .linear import install_fast_linear
-from .postln import install_fused_encoder
+from .postln import install_fused_distilbert, install_fused_encoder
 from .vit import DinoVisionTransformer, apply_lora, store_frozen_base_bf16
 
 warnings.filterwarnings("ignore", message=".*torch.cuda.amp.*")
@@ -187,7 +187,7 @@ class TextEmbedder(nn.Module):
             self.tokenizer = AutoTokenizer.from_pretrained(model_name, local_files_only=True)
         except Exception:
             self.tokenizer = HashTokenizer()
-        self.encoder = _hf_model("DistilBertModel", model_name)
+        self.encoder = install_fused_distilbert(_hf_model("DistilBertModel", model_name))
         self.projection1 = nn.Linear(self.encoder.config.hidden_size, 512)
         self.layer_norm = nn.LayerNorm(512)
         self.projection2 = nn.Linear(512, embedding_dim)

@@ -177,3 +177,44 @@ def install_fused_encoder(hubert):
         enc._triad_seeds = _Seeds()
         enc.forward = types.MethodType(_encoder_forward, enc)
     return hubert
+
+
+# ---- DistilBERT (model.py:79-80, 102-116: DistilBertModel trained after unfreeze_text_step) ----
+# TransformerBlock: h1 = sa_LN(attn(h) + h); h2 = out_LN(dropout(lin2(gelu(lin1(h1)))) + h1),
+# the same passes with p = 0 where DistilBERT has no dropout.
+
+def fused_distilbert_block(block, res, res_b, seeds):
+    ffn = block.ffn
+    p = ffn.dropout.p if block.training else 0.0
+    a = block.attention(res_b)[0]
+    h1, h1b = drop_add_ln(res, a, block.sa_layer_norm, 0.0, 0)
+    v = gelu_drop(ffn.lin1(h1b), 0.0, 0)
+    return drop_add_ln(h1, ffn.lin2(v), block.output_layer_norm, p, seeds())
+
+
+def _distilbert_transformer_forward(self, hidden_states, attention_mask=None, **kwargs):
+    """transformers DistilBERT Transformer.forward with the fused residual / LayerNorm passes."""
+    cfg = self.config
+    if not (hidden_states.is_cuda and attention_mask is None and not kwargs.get("output_attentions")
+            and not kwargs.get("output_hidden_states") and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16 and cfg.dim % 256 == 0 and cfg.dim <= 1024
+            and cfg.activation == "gelu" and getattr(cfg, "chunk_size_feed_forward", 0) == 0
+            and (hidden_states.shape[0] * hidden_states.shape[1] * cfg.hidden_dim) % 8 == 0):
+        return self._triad_stock_forward(hidden_states, attention_mask, **kwargs)
+    from transformers.modeling_outputs import BaseModelOutput
+    res = hidden_states.float()
+    res_b = res.to(torch.bfloat16)
+    for block in self.layer:
+        res, res_b = fused_distilbert_block(block, res, res_b, self._triad_seeds)
+    return BaseModelOutput(last_hidden_state=res)
+
+
+def install_fused_distilbert(encoder):
+    """Swap a DistilBertModel's Transformer.forward for the fused one (per instance)."""
+    tr = getattr(encoder, "transformer", None)
+    if tr is not None and hasattr(tr, "layer") and not hasattr(tr, "_triad_stock_forward"):
+        tr._triad_stock_forward = tr.forward
+        tr._triad_seeds = _Seeds()
+        tr.config = encoder.config
+        tr.forward = types.MethodType(_distilbert_transformer_forward, tr)
+    return encoder
