@@ -134,9 +134,11 @@ int triad_projhead_fwd(const void* h, int M, int H, const void* W1, const float*
 int triad_ln_bwd(const float* dln, const void* y1, const float* mean, const float* rstd, const float* gamma, int M,
                  void* dy1, float* dgb_part, int nblocks, hipStream_t stream);
 
-/* part[s][c] = sum over row slice s of X[r][c] (bias gradients); X bf16 (x_bf16) or fp32. */
-int triad_colsum_partials(const void* X, int x_bf16, long long rows, int cols, long long ld, int nsplit, float* part,
-                          hipStream_t stream);
+/* out[c] = alpha * sum_r X[r][c] over bf16 X [rows][ld] (cols % 8 == 0), fp32 or bf16 out, at HBM rate:
+ * row slices x 8-column 16-byte loads, partials in part (triad_colsum_splits(rows, cols) * cols floats). */
+int triad_colsum_splits(long long rows, int cols);
+int triad_colsum(const void* X, long long rows, int cols, long long ld, float* part, float alpha, int out_bf16,
+                 void* out, hipStream_t stream);
 
 /* out[e] = alpha * sum_i slabs[i][e] (alpha may be NULL = 1), fp32 or bf16 out. */
 int triad_sum_slabs(const float* slabs, int nslab, long long n, const float* alpha, int out_bf16, void* out,

@@ -272,3 +272,16 @@ def test_triad_linear_matches_autocast_linear(M, K, O, bias):
     assert rel(fast.weight.grad, ref.weight.grad) < 1e-2
     if bias:
         assert rel(fast.bias.grad, ref.bias.grad) < 1e-2
+
+
+@pytest.mark.parametrize("rows,cols", [(50944, 768), (8192, 3072), (100, 8), (65536, 512), (7, 2304)])
+def test_colsum_matches_torch(rows, cols):
+    """triad_colsum (bias gradients) against an fp64 torch column sum of the same bf16 matrix."""
+    from triad_amd import ops
+    x = torch.randn(rows, cols, device=dev).to(torch.bfloat16)
+    ref = x.double().sum(0)
+    got = ops.colsum(x)
+    assert got.dtype == torch.float32
+    assert float((got.double() - ref).abs().max()) <= 1e-5 * float(x.double().abs().sum(0).max()) + 1e-6
+    gb = ops.colsum(x, torch.bfloat16)
+    assert gb.dtype == torch.bfloat16 and torch.allclose(gb.float(), got, rtol=8e-3, atol=1e-2)

@@ -36,8 +36,9 @@ SIGNATURES = {
     "triad_gemm_bf16_splitk": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp],
     "triad_projhead_fwd": [vp, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, i64, vp, vp, vp, vp, vp],
     "triad_ln_bwd": [vp, vp, vp, vp, vp, i32, vp, vp, i32, vp],
-    "triad_colsum_partials": [vp, i32, i64, i32, i64, i32, vp, vp],
     "triad_sum_slabs": [vp, i32, i64, vp, i32, vp, vp],
+    "triad_colsum_splits": [i64, i32],
+    "triad_colsum": [vp, i64, i32, i64, vp, f32, i32, vp, vp],
     "triad_global_znorm": [vp, i64, f32, vp, vp, i32, vp],
     "triad_grad_sumsq": [vp, vp, i32, vp, vp],
     "triad_adamw_step": [vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, vp, vp],
@@ -71,7 +72,8 @@ SIGNATURES = {
 }
 # entry points returning a value rather than a status
 RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_longlong,
-            "triad_lora_tn_blocks": C.c_int, "triad_dropaddln_bwd_blocks": C.c_int}
+            "triad_lora_tn_blocks": C.c_int, "triad_dropaddln_bwd_blocks": C.c_int,
+            "triad_colsum_splits": C.c_int}
 
 _lock = threading.Lock()
 _lib = None

@@ -70,18 +70,10 @@ def _bwd(q, k, v, out, lse, dout, scale, drop=None):
     return g
 
 
-class _Seeds:
-    """Per-call 32-bit dropout seeds from a host generator (no device sync)."""
-
-    def __init__(self):
-        self.gen = torch.Generator()
-        self.gen.manual_seed(torch.initial_seed() % (2 ** 63) + 1)
-
-    def __call__(self):
-        return int(torch.randint(0, 2 ** 32 - 1, (1,), generator=self.gen))
-
-
-_SEEDS = _Seeds()
+def _SEEDS():
+    """Per-call 32-bit dropout seed drawn from torch's default CPU generator (no device sync):
+    torch.manual_seed reproduces the masks, as it does for torch's own dropout kernels."""
+    return int(torch.randint(0, 2 ** 32 - 1, (1,)))
 
 
 class _Attention(torch.autograd.Function):

@@ -248,18 +248,56 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
   }
 }
 
-// out[c] = alpha * sum_{r<rows} X[r][c] (+ out if accumulate). X bf16 or f32, columns contiguous.
-template <typename T>
-__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ X, long long rows, int cols,
-                                                     long long ld, float* __restrict__ part) {
-  // grid (ceil(cols/256), nsplit); each thread one column over a row slice
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+// Column sums, HBM-rate form (bias gradients over 8-65 K token rows): thread = 8 consecutive
+// columns (one 16-byte load per row) x a strided set of rows of the block's row slice; the row
+// lanes meet in LDS; part[slice][cols] fp32. Then colsum_reduce_kernel: 64 columns x 16 slice
+// lanes per block, LDS tree, out = alpha * sum (fp32 or bf16).
+__global__ __launch_bounds__(256) void colsum8_kernel(const bf16* __restrict__ X, long long rows, int cols, long long ld,
+                                                      int cg, float* __restrict__ part) {
+  __shared__ float red[256 * 8];
+  const int t = threadIdx.x, g = t % cg, rl = t / cg, nrl = 256 / cg;
+  const int c8 = blockIdx.x * cg + g;
   const long long per = (rows + gridDim.y - 1) / gridDim.y;
   const long long a = blockIdx.y * per, b = min(rows, a + per);
-  float s = 0.f;
-  for (long long r = a; r < b; ++r) s += (float)X[r * ld + c];
-  part[(size_t)blockIdx.y * cols + c] = s;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c8 * 8 < cols && rl < nrl) {
+    for (long long r = a + rl; r < b; r += nrl) {
+      const bf16x8 v = *(const bf16x8*)(X + r * ld + c8 * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] += (float)v[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[t * 8 + i] = s[i];
+  __syncthreads();
+  if (rl == 0 && c8 * 8 < cols) {
+    for (int l = 1; l < nrl; ++l)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] += red[(l * cg + g) * 8 + i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) part[(size_t)blockIdx.y * cols + c8 * 8 + i] = s[i];
+  }
+}
+
+__global__ __launch_bounds__(1024) void colsum_reduce_kernel(const float* __restrict__ part, int S, long long cols,
+                                                             const float* __restrict__ alpha_p, float alpha,
+                                                             int out_bf16, void* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int el = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const long long c = (long long)blockIdx.x * 64 + el;
+  float acc = 0.f;
+  if (c < cols)
+    for (int i = sl; i < S; i += 16) acc += part[(size_t)i * cols + c];
+  red[sl][el] = acc;
+  __syncthreads();
+  if (sl == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][el];
+    t *= alpha_p ? *alpha_p : alpha;
+    if (out_bf16) ((bf16*)out)[c] = (bf16)t;
+    else ((float*)out)[c] = t;
+  }
 }
 
 __global__ __launch_bounds__(256) void sum_slabs_kernel(const float* __restrict__ slabs, int nslab, long long n,
@@ -299,25 +337,42 @@ int triad_ln_bwd(const float* dln, const void* y1, const float* mean, const floa
   return TRIAD_OK;
 }
 
-int triad_colsum_partials(const void* X, int x_bf16, long long rows, int cols, long long ld, int nsplit, float* part,
-                          hipStream_t stream) {
-  if (rows <= 0 || cols <= 0 || nsplit <= 0) return TRIAD_EINVAL;
-  dim3 grid((cols + 255) / 256, nsplit);
-  if (x_bf16)
-    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, stream, (const bf16*)X, rows, cols, ld, part);
-  else
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, stream, (const float*)X, rows, cols, ld, part);
-  TRIAD_CHECK_LAUNCH();
-  return TRIAD_OK;
-}
-
 int triad_sum_slabs(const float* slabs, int nslab, long long n, const float* alpha, int out_bf16, void* out,
                     hipStream_t stream) {
   if (nslab <= 0 || n <= 0) return TRIAD_EINVAL;
+  if (nslab >= 16 && n <= (1 << 20)) {  // many slabs of a short vector: 16 slab lanes per element
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, stream, slabs, nslab, n,
+                       alpha, 1.f, out_bf16, out);
+    TRIAD_CHECK_LAUNCH();
+    return TRIAD_OK;
+  }
   long long blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, slabs, nslab, n, alpha, out_bf16,
                      out);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+// out[c] = alpha * sum_{r < rows} X[r][c], X bf16 [rows][ld] (cols % 8 == 0, ld % 8 == 0); part:
+// triad_colsum_splits(rows, cols) * cols floats of scratch; out fp32 or bf16.
+int triad_colsum_splits(long long rows, int cols) {
+  const int cg = cols / 8 < 256 ? cols / 8 : 256;
+  const int gx = (cols / 8 + cg - 1) / cg;
+  long long s = 1024 / gx;
+  if (s > rows / 16) s = rows / 16;
+  return (int)(s < 1 ? 1 : s);
+}
+
+int triad_colsum(const void* X, long long rows, int cols, long long ld, float* part, float alpha, int out_bf16,
+                 void* out, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || cols % 8 || ld % 8 || ld < cols) return TRIAD_EINVAL;
+  const int cg = cols / 8 < 256 ? cols / 8 : 256;
+  const int S = triad_colsum_splits(rows, cols);
+  const dim3 grid((cols / 8 + cg - 1) / cg, S);
+  hipLaunchKernelGGL(colsum8_kernel, grid, dim3(256), 0, stream, (const bf16*)X, rows, cols, ld, cg, part);
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3((cols + 63) / 64), dim3(1024), 0, stream, part, S, (long long)cols,
+                     (const float*)nullptr, alpha, out_bf16, out);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

@@ -162,6 +162,7 @@ def _gemm_rows(a, a_row, lda, M, K, b, out, out_row, ldc):
     a.flat[(a_row + m) * lda + k] (rows may overlap), b [N][K] contiguous bf16."""
     N = b.shape[0]
     if M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and lda % 8 == 0 and ldc % 8 == 0:
+        _lib.META = dict(backbone=True)
         call("triad_gemm_bf16", _addr(a, a_row, lda), lda, 1, ptr(b), K, 1, M, N, K, None, _addr(out, out_row, ldc), ldc,
              1, stream_ptr(a.device))
     else:  # same product through torch (it copies the overlapping operand)
@@ -176,6 +177,7 @@ def _weight_grad_rows(dy, M, x, ldx, N):
         sp = 8
         slabs = torch.empty(sp * O * N, dtype=torch.float32, device=dy.device)
         out = torch.empty(O, N, dtype=torch.float32, device=dy.device)
+        _lib.META = dict(backbone=True)
         call("triad_gemm_bf16_splitk", ptr(dy), O, 0, ptr(x), ldx, 0, O, N, M, sp, None, ptr(slabs), ptr(out), 0,
              stream_ptr(dy.device))
         return out

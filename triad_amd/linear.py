@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _lib
 from ._lib import call, ptr, stream_ptr
 
 MIN_TOKENS = 4096  # DistilBERT at B=256 (8,192 tokens) still gains 1.1-1.8x
@@ -35,6 +36,7 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     sp = _splits(M, O, K)
     slabs = torch.empty(sp * O * K, dtype=torch.float32, device=dy2.device)
     dw = torch.empty(O, K, dtype=torch.bfloat16, device=dy2.device)
+    _lib.META = dict(backbone=True)
     call("triad_gemm_bf16_splitk", ptr(dy2), dy2.stride(0), 0, ptr(x2), x2.stride(0), 0, O, K, M, sp, None,
          ptr(slabs), ptr(dw), 1, stream_ptr(dy2.device))
     return dw
@@ -65,7 +67,8 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = weight_grad(dy2, x2).to(w_dtype)
         if b_dtype is not None and ctx.needs_input_grad[2]:
-            db = dy2.sum(0, dtype=torch.float32).to(b_dtype)
+            from .ops import colsum
+            db = colsum(dy2, torch.bfloat16 if b_dtype == torch.bfloat16 else torch.float32).to(b_dtype)
         return dx, dw, db
 
 

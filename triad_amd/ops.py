@@ -85,6 +85,16 @@ def pack_keys(k: torch.Tensor, g: Geometry) -> torch.Tensor:
     return out
 
 
+def colsum(x, out_dtype=torch.float32):
+    """Column sums of a bf16 [rows][cols] matrix (bias gradients) at HBM rate (triad_colsum)."""
+    rows, cols = x.shape
+    part = torch.empty(call("triad_colsum_splits", rows, cols) * cols, dtype=torch.float32, device=x.device)
+    out = torch.empty(cols, dtype=out_dtype, device=x.device)
+    call("triad_colsum", ptr(x), rows, cols, x.stride(0), ptr(part), 1.0, int(out_dtype == torch.bfloat16), ptr(out),
+         stream_ptr(x.device))
+    return out
+
+
 def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream):
     """dQ = alpha dS K (dk=0) / dK = alpha dS^T Q (dk=1) over the tiled dS (triad_tile_gemm),
     split-K over the CUs when the row panels alone leave them idle. (A stream-K form -- one run
@@ -383,11 +393,7 @@ class _ProjectionHead(torch.autograd.Function):
         dw2 = torch.empty(D, D, dtype=f32, device=dev)
         call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp, None, ptr(slabs), ptr(dw2), 0, st)
         # db2 = column sums of dy
-        ns = max(1, min(64, Mp // 512))
-        cpart = torch.empty(ns, D, dtype=f32, device=dev)
-        db2 = torch.empty(D, dtype=f32, device=dev)
-        call("triad_colsum_partials", ptr(dyp), 1, Mp, D, D, ns, ptr(cpart), st)
-        call("triad_sum_slabs", ptr(cpart), ns, D, None, 0, ptr(db2), st)
+        db2 = colsum(dyp, f32)
         # LayerNorm backward -> dy1 (bf16), dgamma, dbeta
         dy1 = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
         if Mp > M:
@@ -402,9 +408,7 @@ class _ProjectionHead(torch.autograd.Function):
         dw1 = torch.empty(D, H, dtype=f32, device=dev)
         call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), 0,
              st)
-        call("triad_colsum_partials", ptr(dy1), 1, Mp, D, D, ns, ptr(cpart), st)
-        db1 = torch.empty(D, dtype=f32, device=dev)
-        call("triad_sum_slabs", ptr(cpart), ns, D, None, 0, ptr(db1), st)
+        db1 = colsum(dy1, f32)
         # dh = dy1 . W1           [Mp][H] bf16
         dh = torch.empty(Mp, H, dtype=torch.bfloat16, device=dev)
         call("triad_gemm_bf16", ptr(dy1), D, 1, ptr(w1b), H, 0, Mp, H, D, None, ptr(dh), H, 1, st)
