@@ -190,6 +190,20 @@ int triad_chgn_gelu_bwd(const void* x, const void* dy, int B, int T, int Tp, int
                         const float* beta, const float* mean, const float* rstd, void* ws, void* dx, float* dgamma,
                         float* dbeta, hipStream_t stream);
 
+/* HuBERT conv layer 0 (1 -> C, kernel 10, stride 5, no bias) + GroupNorm(C groups) + GELU forward with
+ * conv0 recomputed from the bf16 waveform wave[b][Lp] (Lp >= 5 (Tp - 1) + 10) in both passes; writes the
+ * padded frame buffers out = bf16(gelu(gn(y0))) and y0out = y0 (frames T .. Tp-1 zero) and mean / rstd;
+ * the backward is triad_chgn_gelu_bwd over y0out. ws: triad_chgn_workspace_bytes(B, T, C) bytes. */
+int triad_c0gn_fwd(const void* wave, long long Lp, const void* w0, int B, int T, int Tp, int C, const float* gamma,
+                   const float* beta, float eps, float* mean, float* rstd, void* ws, void* out, void* y0out,
+                   hipStream_t stream);
+
+/* conv0's weight gradient dw0[c][j] (fp32) = sum_{b, t < T} dy0[b*Tp + t][c] * wave[b][5t + j] (bf16 inputs);
+ * ws: triad_conv0_dw_workspace_bytes(B, T, C) bytes. */
+long long triad_conv0_dw_workspace_bytes(int B, int T, int C);
+int triad_conv0_dw(const void* wave, long long Lp, const void* dy0, int B, int T, int Tp, int C, void* ws, float* dw0,
+                   hipStream_t stream);
+
 /* HuBERT positional convolution (model.py:29-30,66: transformers HubertPositionalConvEmbedding,
  * Conv1d(C, C, 128, padding 64, groups) + SamePad) as an implicit GEMM over channels-last bf16:
  * y[b][t][g*CG+n] = bias + sum_{j<128, c<CG} x[b][t+j-pad][g*CG+c] * wt[g][n][j*CG+c], t < T,

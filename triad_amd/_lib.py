@@ -48,6 +48,9 @@ SIGNATURES = {
     "triad_chgn_workspace_bytes": [i32, i32, i32],
     "triad_chgn_gelu_fwd": [vp, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp],
     "triad_chgn_gelu_bwd": [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "triad_conv0_dw_workspace_bytes": [i32, i32, i32],
+    "triad_conv0_dw": [vp, i64, vp, i32, i32, i32, i32, vp, vp, vp],
+    "triad_c0gn_fwd": [vp, i64, vp, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
     "triad_posconv": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
     "triad_rows_nt": [vp, i64, i32, i32, vp, i32, vp, vp],
     "triad_lora_update": [vp, i64, i32, i32, vp, vp, vp],
@@ -72,6 +75,7 @@ SIGNATURES = {
 }
 # entry points returning a value rather than a status
 RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_longlong,
+            "triad_conv0_dw_workspace_bytes": C.c_longlong,
             "triad_lora_tn_blocks": C.c_int, "triad_dropaddln_bwd_blocks": C.c_int,
             "triad_colsum_splits": C.c_int}
 

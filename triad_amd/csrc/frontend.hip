@@ -211,6 +211,163 @@ __global__ __launch_bounds__(NT) void chgn_apply_kernel(const bf16* __restrict__
   }
 }
 
+// ---- conv0 + GroupNorm + GELU forward with conv0 recomputed from the waveform ---------------
+// HuBERT's conv layer 0 (1 -> C channels, kernel 10, stride 5, no bias) has 10 taps per output:
+// recomputing y0[b][t][c] = bf16(sum_j w[c][j] s[b][5t + j]) from the (bf16) waveform costs 10
+// FMAs per element where reading y0 costs 2 bytes. The forward therefore never reads y0: MODE 0
+// = GroupNorm statistics (chunk partials, finalised by chgn_stats_kernel), MODE 1 = output
+// h = bf16(gelu(gn(y0))) plus y0 itself for the backward (chgn_*<1> over y0 and dy, which is
+// HBM-bound there; recomputing y0 and its GELU' twice made the backward VALU-bound -- measured).
+// The block stages its rows' waveform span in LDS (fp32).
+constexpr int C0_K = 10, C0_S = 5;
+
+template <int MODE>
+__global__ __launch_bounds__(NT) void c0gn_kernel(const bf16* __restrict__ wave, long long Lp,
+                                                  const bf16* __restrict__ w0, int T, int Tp, int C,
+                                                  const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                  bf16* __restrict__ out, bf16* __restrict__ y0out,
+                                                  float2* __restrict__ part) {
+  __shared__ float smp[C0_S * CHUNK + C0_K];
+  __shared__ float2 red[MODE == 0 ? NT * 8 : 1];
+  const int b = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
+  const int tpr = C / 8, rows = NT / tpr;
+  const int cg = threadIdx.x % tpr, r0 = threadIdx.x / tpr;
+  const int c0 = cg * 8;
+  const int t0 = blk * CHUNK, t1 = min(T, t0 + CHUNK);
+  const int nsmp = (t1 > t0) ? C0_S * (t1 - t0 - 1) + C0_K : 0;
+  for (int i = threadIdx.x; i < nsmp; i += NT) smp[i] = (float)wave[(long long)b * Lp + (long long)C0_S * t0 + i];
+  float w[8][C0_K];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < C0_K; ++j) w[i][j] = (float)w0[(c0 + i) * C0_K + j];
+  float mu[8], rs[8], g[8], be[8], s[8], q[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s[i] = 0.f;
+    q[i] = 0.f;
+    if (MODE == 1) {
+      mu[i] = mean[(size_t)b * C + c0 + i];
+      rs[i] = rstd[(size_t)b * C + c0 + i];
+      g[i] = gamma[c0 + i];
+      be[i] = beta[c0 + i];
+    }
+  }
+  __syncthreads();
+  if (MODE == 1 && blk == nblk - 1) {  // padding frames T .. Tp-1: zeros
+    bf16x8 z;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
+    for (int t = T + r0; t < Tp; t += rows) {
+      *(bf16x8*)(out + ((size_t)b * Tp + t) * C + c0) = z;
+      *(bf16x8*)(y0out + ((size_t)b * Tp + t) * C + c0) = z;
+    }
+  }
+  for (int t = t0 + r0; t < t1; t += rows) {
+    const float* sp = smp + C0_S * (t - t0);
+    float sv[C0_K];
+#pragma unroll
+    for (int j = 0; j < C0_K; ++j) sv[j] = sp[j];
+    float y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < C0_K; ++j) a = fmaf(w[i][j], sv[j], a);
+      y[i] = (float)(bf16)a;  // the bf16 conv output autocast's conv would store
+    }
+    if (MODE == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        s[i] += y[i];
+        q[i] = fmaf(y[i], y[i], q[i]);
+      }
+    } else {
+      const size_t off = ((size_t)b * Tp + t) * C + c0;
+      bf16x8 o, yb;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        o[i] = (bf16)gelu(fmaf((y[i] - mu[i]) * rs[i], g[i], be[i]));
+        yb[i] = (bf16)y[i];
+      }
+      *(bf16x8*)(out + off) = o;
+      *(bf16x8*)(y0out + off) = yb;
+    }
+  }
+  if (MODE == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[threadIdx.x * 8 + i] = make_float2(s[i], q[i]);
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += NT) {
+      const int g8 = c / 8, i = c % 8;
+      float2 acc = make_float2(0.f, 0.f);
+      for (int r = 0; r < rows; ++r) {
+        const float2 v = red[(r * tpr + g8) * 8 + i];
+        acc.x += v.x;
+        acc.y += v.y;
+      }
+      part[((size_t)b * nblk + blk) * C + c] = acc;
+    }
+  }
+}
+
+// dW0[c][j] = sum_{b, t < T} dy0[b][t][c] * s[b][5t + j]: conv0's weight gradient straight from the
+// waveform windows (a K = 3.3 M-row, 10-column contraction the library GEMM runs at < 1/3 of HBM
+// rate). Block = 1024 rows of one sample, waveform span in LDS, 8 channels x 10 taps per thread;
+// row lanes summed through LDS into per-block partials dwpart[b * nblk + blk][c * 10 + j].
+constexpr int C0_DW_ROWS = 1024;
+
+__global__ __launch_bounds__(NT) void c0dw_kernel(const bf16* __restrict__ wave, long long Lp, const bf16* __restrict__ dy,
+                                                  int T, int Tp, int C, float* __restrict__ dwpart) {
+  __shared__ float smp[C0_S * C0_DW_ROWS + C0_K];
+  __shared__ float red[NT * 8 * 2];
+  const int b = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
+  const int tpr = C / 8, rows = NT / tpr;
+  const int cg = threadIdx.x % tpr, r0 = threadIdx.x / tpr;
+  const int c0 = cg * 8;
+  const int t0 = blk * C0_DW_ROWS, t1 = min(T, t0 + C0_DW_ROWS);
+  const int nsmp = (t1 > t0) ? C0_S * (t1 - t0 - 1) + C0_K : 0;
+  for (int i = threadIdx.x; i < nsmp; i += NT) smp[i] = (float)wave[(long long)b * Lp + (long long)C0_S * t0 + i];
+  __syncthreads();
+  float dw[8][C0_K];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < C0_K; ++j) dw[i][j] = 0.f;
+  for (int t = t0 + r0; t < t1; t += rows) {
+    const V8 dv = load8(dy + ((size_t)b * Tp + t) * C + c0);
+    const float* sp = smp + C0_S * (t - t0);
+#pragma unroll
+    for (int j = 0; j < C0_K; ++j) {
+      const float sj = sp[j];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dw[i][j] = fmaf(dv.v[i], sj, dw[i][j]);
+    }
+  }
+  float* dst = dwpart + ((size_t)b * nblk + blk) * C * C0_K;
+#pragma unroll
+  for (int j0 = 0; j0 < C0_K; j0 += 2) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[(threadIdx.x * 8 + i) * 2] = dw[i][j0];
+      red[(threadIdx.x * 8 + i) * 2 + 1] = dw[i][j0 + 1];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += NT) {
+      const int g8 = c / 8, i = c % 8;
+      float a0 = 0.f, a1 = 0.f;
+      for (int r = 0; r < rows; ++r) {
+        a0 += red[((r * tpr + g8) * 8 + i) * 2];
+        a1 += red[((r * tpr + g8) * 8 + i) * 2 + 1];
+      }
+      dst[c * C0_K + j0] = a0;
+      dst[c * C0_K + j0 + 1] = a1;
+    }
+  }
+}
+
 bool shape_ok(int B, int T, int C) {
   return B > 0 && T > 0 && C > 0 && C % 8 == 0 && NT % (C / 8) == 0;
 }
@@ -259,4 +416,38 @@ int triad_chgn_gelu_bwd(const void* x, const void* dy, int B, int T, int Tp, int
   return TRIAD_OK;
 }
 
+// conv0 (1 -> C, kernel 10, stride 5, no bias) + GroupNorm(C groups) + GELU forward, conv0 recomputed
+// from the bf16 waveform wave[b][Lp] (Lp >= 5 (Tp - 1) + 10); writes the padded frame buffers
+// out = bf16(gelu(gn(y0))) and y0out = y0 ([b*Tp + t][c], frames T .. Tp-1 zero); mean / rstd for the
+// backward (triad_chgn_gelu_bwd over y0out). ws: triad_chgn_workspace_bytes(B, T, C) bytes.
+int triad_c0gn_fwd(const void* wave, long long Lp, const void* w0, int B, int T, int Tp, int C, const float* gamma,
+                   const float* beta, float eps, float* mean, float* rstd, void* ws, void* out, void* y0out,
+                   hipStream_t stream) {
+  if (!shape_ok(B, T, C) || Tp < T || Lp < (long long)C0_S * (Tp - 1) + C0_K) return TRIAD_EINVAL;
+  const int nchunk = (T + CHUNK - 1) / CHUNK;
+  float2* part = (float2*)ws;
+  hipLaunchKernelGGL(c0gn_kernel<0>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)wave, Lp, (const bf16*)w0, T,
+                     Tp, C, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, part);
+  hipLaunchKernelGGL(chgn_stats_kernel, dim3((C + 255) / 256, B), dim3(256), 0, stream, part, nchunk, T, C, eps,
+                     mean, rstd);
+  hipLaunchKernelGGL(c0gn_kernel<1>, dim3(nchunk, B), dim3(NT), 0, stream, (const bf16*)wave, Lp, (const bf16*)w0, T,
+                     Tp, C, mean, rstd, gamma, beta, (bf16*)out, (bf16*)y0out, nullptr);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+// dw0[c][j] (fp32) = sum_{b, t < T} dy0[b*Tp + t][c] * wave[b][5t + j]; ws: triad_conv0_dw_workspace_bytes.
+long long triad_conv0_dw_workspace_bytes(int B, int T, int C) {
+  return (long long)B * ((T + C0_DW_ROWS - 1) / C0_DW_ROWS) * C * C0_K * 4;
+}
+
+int triad_conv0_dw(const void* wave, long long Lp, const void* dy0, int B, int T, int Tp, int C, void* ws, float* dw0,
+                   hipStream_t stream) {
+  if (!shape_ok(B, T, C) || Tp < T || Lp < (long long)C0_S * (T - 1) + C0_K) return TRIAD_EINVAL;
+  const int nblk = (T + C0_DW_ROWS - 1) / C0_DW_ROWS;
+  hipLaunchKernelGGL(c0dw_kernel, dim3(nblk, B), dim3(NT), 0, stream, (const bf16*)wave, Lp, (const bf16*)dy0, T, Tp,
+                     C, (float*)ws);
+  TRIAD_CHECK_LAUNCH();
+  return triad_sum_slabs((const float*)ws, B * nblk, (long long)C * C0_K, nullptr, 0, dw0, stream);
+}
 }  // extern "C"

@@ -213,6 +213,55 @@ class _FrameConv0(torch.autograd.Function):
         return None, dw.view(wshape).to(wdt), None, None
 
 
+class _Conv0GNGelu(torch.autograd.Function):
+    """HuBERT conv layer 0 (1 -> C, kernel 10, stride 5, no bias) + GroupNorm(C groups) + GELU into
+    a padded frame buffer. Forward: conv0 recomputed from the waveform in the statistics and the
+    output pass (csrc/frontend.hip c0gn; neither pass reads conv0's output), which is written
+    once for the backward; backward: the fused GroupNorm+GELU backward over it and dW0 contracted
+    with the waveform windows (triad_conv0_dw). The waveform gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, wave, w, gamma, beta, eps, Tp):
+        B, L = wave.shape
+        O = w.shape[0]
+        T = (L - 10) // 5 + 1
+        need = (Tp - 1) * 5 + 10
+        xw = F.pad(wave.to(torch.bfloat16), (0, max(0, need - L))).contiguous()
+        w0 = w.to(torch.bfloat16).reshape(O, 10).contiguous()
+        g = gamma.detach().float().contiguous()
+        b = beta.detach().float().contiguous()
+        dev = wave.device
+        mean = torch.empty(B, O, dtype=torch.float32, device=dev)
+        rstd = torch.empty(B, O, dtype=torch.float32, device=dev)
+        ws = torch.empty(int(call("triad_chgn_workspace_bytes", B, T, O)), dtype=torch.uint8, device=dev)
+        out = torch.empty(B * Tp + 2, O, dtype=torch.bfloat16, device=dev)
+        y0 = torch.empty(B * Tp, O, dtype=torch.bfloat16, device=dev)
+        out[B * Tp:].zero_()
+        call("triad_c0gn_fwd", ptr(xw), xw.shape[1], ptr(w0), B, T, Tp, O, ptr(g), ptr(b), float(eps), ptr(mean),
+             ptr(rstd), ptr(ws), ptr(out), ptr(y0), stream_ptr(dev))
+        ctx.save_for_backward(xw, y0, g, b, mean, rstd)
+        ctx.meta = (B, T, Tp, w.shape, w.dtype, gamma.dtype, beta.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        xw, y0, g, b, mean, rstd = ctx.saved_tensors
+        B, T, Tp, wshape, wdt, gdt, bdt = ctx.meta
+        O = y0.shape[1]
+        dev = xw.device
+        dy = dout[:B * Tp].to(torch.bfloat16).contiguous()
+        ws = torch.empty(int(call("triad_chgn_workspace_bytes", B, T, O)), dtype=torch.uint8, device=dev)
+        dy0 = torch.empty_like(y0)
+        dg = torch.empty(O, dtype=torch.float32, device=dev)
+        db = torch.empty(O, dtype=torch.float32, device=dev)
+        call("triad_chgn_gelu_bwd", ptr(y0), ptr(dy), B, T, Tp, O, ptr(g), ptr(b), ptr(mean), ptr(rstd), ptr(ws),
+             ptr(dy0), ptr(dg), ptr(db), stream_ptr(dev))
+        dw = torch.empty(O, 10, dtype=torch.float32, device=dev)
+        ws2 = torch.empty(int(call("triad_conv0_dw_workspace_bytes", B, T, O)), dtype=torch.uint8, device=dev)
+        call("triad_conv0_dw", ptr(xw), xw.shape[1], ptr(dy0), B, T, Tp, O, ptr(ws2), ptr(dw), stream_ptr(dev))
+        return None, dw.view(wshape).to(wdt), dg.to(gdt), db.to(bdt), None, None
+
+
 class _FrameConvS2(torch.autograd.Function):
     """Kernel-k (2 or 3), stride-2 conv (C -> O, no bias) between padded frame buffers:
     x [B*Tp + 2, C] -> y [B*Tp/2 + 2, O]."""
@@ -306,9 +355,13 @@ def _hubert_feature_encoder_forward(self, input_values):
         B = input_values.shape[0]
         l0 = self.conv_layers[0]
         T, Tp = plan[0]
-        y = _FrameConv0.apply(input_values, l0.conv.weight, l0.conv.stride[0], Tp)
         norm = l0.layer_norm
-        h = _ChannelGroupNormGelu.apply(y, norm.weight, norm.bias, float(norm.eps), (B, T, Tp))
+        if l0.conv.kernel_size[0] == 10 and l0.conv.stride[0] == 5 and l0.conv.out_channels % 8 == 0 \
+                and 256 % (l0.conv.out_channels // 8) == 0:
+            h = _Conv0GNGelu.apply(input_values, l0.conv.weight, norm.weight, norm.bias, float(norm.eps), Tp)
+        else:
+            y = _FrameConv0.apply(input_values, l0.conv.weight, l0.conv.stride[0], Tp)
+            h = _ChannelGroupNormGelu.apply(y, norm.weight, norm.bias, float(norm.eps), (B, T, Tp))
         for layer, (T, Tp_out) in zip(self.conv_layers[1:], plan[1:]):
             h = layer.activation(_FrameConvS2.apply(h, layer.conv.weight, B, Tp))
             Tp = Tp_out
