@@ -157,3 +157,19 @@ def test_fused_distilbert_matches_stock_without_dropout():
         if n.endswith("k_lin.bias"):  # exactly 0 in exact arithmetic: noise
             continue
         assert _rel(g_f[n], g_s[n]) < 3e-2, (n, _rel(g_f[n], g_s[n]))
+
+
+@pytest.mark.parametrize("shape", [(66 * 261, 3072), (3, 7, 8), (1 << 20,)])
+def test_gelu_matches_aten_bit_exact(shape):
+    """postln.gelu (geludrop kernels at p = 0, used for the ViT MLP, the HuBERT conv stack and the
+    positional conv) against aten gelu / gelu_backward on bf16: identical values and gradients."""
+    from triad_amd.postln import gelu
+    g = torch.Generator(device=dev).manual_seed(len(shape))
+    u = (torch.randn(shape, device=dev, generator=g) * 3).to(torch.bfloat16)
+    dv = torch.randn(shape, device=dev, generator=g).to(torch.bfloat16)
+    ud = u.clone().requires_grad_(True)
+    v = gelu(ud)
+    assert v.grad_fn is not None and "GeluDrop" in type(v.grad_fn).__name__
+    torch.testing.assert_close(v, torch.nn.functional.gelu(u), rtol=0, atol=0)
+    v.backward(dv)
+    torch.testing.assert_close(ud.grad, torch.ops.aten.gelu_backward(dv, u), rtol=0, atol=0)

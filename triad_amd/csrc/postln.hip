@@ -169,7 +169,8 @@ __global__ __launch_bounds__(256) void dropaddln_bwd_kernel(const float* __restr
 constexpr float kAlpha = 0.70710678118654752440f;                 // M_SQRT1_2
 constexpr float kBeta = 1.12837916709551257390f * 0.70710678118654752440f * 0.5f;  // M_2_SQRTPI * M_SQRT1_2 / 2
 
-// thread = 8 consecutive elements (4 pairs)
+// thread = 8 consecutive elements (4 pairs); DROP = false: p = 0 (plain GELU, no hash)
+template <bool DROP>
 __global__ __launch_bounds__(256) void geludrop_fwd_kernel(const bf16* __restrict__ u, long long n, unsigned seed,
                                                            unsigned thr, float scale, bf16* __restrict__ v) {
   const long long e0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
@@ -178,17 +179,18 @@ __global__ __launch_bounds__(256) void geludrop_fwd_kernel(const bf16* __restric
   bf16x8 o;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    const unsigned k = keep_pair((unsigned long long)(e0 >> 1) + p, seed, thr);
+    const unsigned k = DROP ? keep_pair((unsigned long long)(e0 >> 1) + p, seed, thr) : 3u;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const float xf = (float)x[2 * p + c];
       const float g = (float)(bf16)(0.5f * xf * (1.0f + erff(xf * kAlpha)));
-      o[2 * p + c] = (bf16)drop(g, (k >> c) & 1u, scale);
+      o[2 * p + c] = DROP ? (bf16)drop(g, (k >> c) & 1u, scale) : (bf16)g;
     }
   }
   *(bf16x8*)(v + e0) = o;
 }
 
+template <bool DROP>
 __global__ __launch_bounds__(256) void geludrop_bwd_kernel(const bf16* __restrict__ u, const bf16* __restrict__ dv,
                                                            long long n, unsigned seed, unsigned thr, float scale,
                                                            bf16* __restrict__ du) {
@@ -199,11 +201,11 @@ __global__ __launch_bounds__(256) void geludrop_bwd_kernel(const bf16* __restric
   bf16x8 o;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    const unsigned k = keep_pair((unsigned long long)(e0 >> 1) + p, seed, thr);
+    const unsigned k = DROP ? keep_pair((unsigned long long)(e0 >> 1) + p, seed, thr) : 3u;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const float xf = (float)x[2 * p + c];
-      const float dg = drop((float)d[2 * p + c], (k >> c) & 1u, scale);  // dropout backward (bf16)
+      const float dg = DROP ? drop((float)d[2 * p + c], (k >> c) & 1u, scale) : (float)d[2 * p + c];  // dropout bwd
       const float cdf = 0.5f * (1.0f + erff(xf * kAlpha));
       const float pdf = expf(-0.5f * xf * xf) * kBeta;
       o[2 * p + c] = (bf16)(dg * (cdf + xf * pdf));
@@ -265,11 +267,12 @@ int triad_dropaddln_bwd(const float* dh, const void* dhb, const float* res, cons
   return TRIAD_EINVAL;
 }
 
-// v = dropout(gelu(u)) over n bf16 elements (n % 8 == 0)
+// v = dropout(gelu(u)) over n bf16 elements (n % 8 == 0); p = 0: plain exact-erf GELU (aten's roundings)
 int triad_geludrop_fwd(const void* u, long long n, float p, unsigned seed, void* v, hipStream_t stream) {
   if (n <= 0 || n % 8 || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
-  hipLaunchKernelGGL(geludrop_fwd_kernel, dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, stream,
-                     (const bf16*)u, n, seed, drop_thr(p), 1.f / (1.f - p), (bf16*)v);
+  hipLaunchKernelGGL(p > 0.f ? geludrop_fwd_kernel<true> : geludrop_fwd_kernel<false>,
+                     dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, stream, (const bf16*)u, n, seed, drop_thr(p),
+                     1.f / (1.f - p), (bf16*)v);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
@@ -277,8 +280,9 @@ int triad_geludrop_fwd(const void* u, long long n, float p, unsigned seed, void*
 int triad_geludrop_bwd(const void* u, const void* dv, long long n, float p, unsigned seed, void* du,
                        hipStream_t stream) {
   if (n <= 0 || n % 8 || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
-  hipLaunchKernelGGL(geludrop_bwd_kernel, dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, stream,
-                     (const bf16*)u, (const bf16*)dv, n, seed, drop_thr(p), 1.f / (1.f - p), (bf16*)du);
+  hipLaunchKernelGGL(p > 0.f ? geludrop_bwd_kernel<true> : geludrop_bwd_kernel<false>,
+                     dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, stream, (const bf16*)u, (const bf16*)dv, n,
+                     seed, drop_thr(p), 1.f / (1.f - p), (bf16*)du);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

@@ -315,6 +315,14 @@ def channel_group_norm_gelu(x, gamma, beta, eps):
     return _ChannelGroupNormGelu.apply(x, gamma, beta, float(eps))
 
 
+def _hip_act(act):
+    """transformers' exact-erf GELUActivation -> postln.gelu (the same function and roundings as
+    one HIP pass each way); any other activation unchanged."""
+    from transformers.activations import GELUActivation
+    from .postln import gelu
+    return gelu if isinstance(act, GELUActivation) and act.act is F.gelu else act
+
+
 def _frame_stack_plan(self, input_values):
     """[(T, Tp)] of layer 0's output and every later layer's input when HuBERT's layout runs
     over padded frame buffers (every Tp even), else None."""
@@ -363,7 +371,7 @@ def _hubert_feature_encoder_forward(self, input_values):
             y = _FrameConv0.apply(input_values, l0.conv.weight, l0.conv.stride[0], Tp)
             h = _ChannelGroupNormGelu.apply(y, norm.weight, norm.bias, float(norm.eps), (B, T, Tp))
         for layer, (T, Tp_out) in zip(self.conv_layers[1:], plan[1:]):
-            h = layer.activation(_FrameConvS2.apply(h, layer.conv.weight, B, Tp))
+            h = _hip_act(layer.activation)(_FrameConvS2.apply(h, layer.conv.weight, B, Tp))
             Tp = Tp_out
         return h[:B * Tp].view(B, Tp, -1)[:, :T].transpose(1, 2)
     h = input_values.unsqueeze(-1)
@@ -443,7 +451,7 @@ def _hubert_pos_conv_forward(self, hidden_states):
             or getattr(self.padding, "num_pad_remove", 1) != 1:
         return self._triad_hf_forward(hidden_states)
     y = _PosConv.apply(hidden_states, conv.weight, conv.bias, conv.groups, conv.padding[0])
-    return self.activation(y)
+    return _hip_act(self.activation)(y)
 
 
 def _hubert_mask_hidden_states(self, hidden_states, mask_time_indices=None, attention_mask=None):

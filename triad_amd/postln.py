@@ -115,6 +115,15 @@ def gelu_drop(u, p, seed):
     return _GeluDrop.apply(u, p, seed)
 
 
+def gelu(u):
+    """Exact-erf GELU of a bf16 CUDA tensor on the geludrop kernels with p = 0 (same value and
+    gradient roundings as aten gelu / gelu_backward, one pass each way at HBM rate); anything
+    else through F.gelu."""
+    if u.is_cuda and u.dtype == torch.bfloat16 and u.numel() % 8 == 0 and u.numel() > 0:
+        return _GeluDrop.apply(u, 0.0, 0)
+    return torch.nn.functional.gelu(u)
+
+
 def dropout_keep(n, p, seed, device):
     """The keep bits (u8) the kernels use for `n` elements at (p, seed): test view."""
     out = torch.empty(n, dtype=torch.uint8, device=device)

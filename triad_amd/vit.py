@@ -22,6 +22,7 @@ import torch.nn.functional as F
 from . import attention
 from ._lib import call, ptr, stream_ptr
 from .frontend import patch_embed
+from .postln import gelu
 
 ARCHS = {
     # name: (embed_dim, depth, heads)
@@ -147,7 +148,7 @@ class Mlp(nn.Module):
         self.fc2 = nn.Linear(hidden, dim)
 
     def forward(self, x):
-        return self.fc2(F.gelu(self.fc1(x)))
+        return self.fc2(gelu(self.fc1(x)))
 
 
 class _AddScaleLN(torch.autograd.Function):
