@@ -282,8 +282,14 @@ int triad_dropaddln_bwd_blocks(int M);
 int triad_dropaddln_bwd(const float* dh, const void* dhb, const float* res, const void* y, const float* mean,
                         const float* rstd, const float* w, int M, int D, float p, unsigned seed, float* dres, void* dy,
                         float* part, hipStream_t stream);
-int triad_geludrop_fwd(const void* u, long long n, float p, unsigned seed, void* v, hipStream_t stream);
-int triad_geludrop_bwd(const void* u, const void* dv, long long n, float p, unsigned seed, void* du,
+/* GELU table for the two passes below: triad_gelu_table_bytes() bytes of device memory built once by
+ * triad_gelu_table (value and slope of every bf16 argument with |x| in [2^-40, 2^6)); table = NULL
+ * makes the passes evaluate the formula. */
+long long triad_gelu_table_bytes(void);
+int triad_gelu_table(void* table, hipStream_t stream);
+int triad_geludrop_fwd(const void* u, long long n, float p, unsigned seed, const void* table, void* v,
+                       hipStream_t stream);
+int triad_geludrop_bwd(const void* u, const void* dv, long long n, float p, unsigned seed, const void* table, void* du,
                        hipStream_t stream);
 int triad_dropout_keep(long long n, float p, unsigned seed, void* out, hipStream_t stream);
 

@@ -173,3 +173,25 @@ def test_gelu_matches_aten_bit_exact(shape):
     torch.testing.assert_close(v, torch.nn.functional.gelu(u), rtol=0, atol=0)
     v.backward(dv)
     torch.testing.assert_close(ud.grad, torch.ops.aten.gelu_backward(dv, u), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gelu_table_every_bf16_pattern(p):
+    """The table-driven GELU passes (triad_gelu_table: |x| in [2^-40, 2^6) from the table, every
+    other pattern by the formula) over ALL 65536 bf16 bit patterns, against aten gelu /
+    gelu_backward on the same dropout mask: identical values (NaN where aten gives NaN)."""
+    from triad_amd import postln
+    bits = torch.arange(65536, dtype=torch.int32, device=dev).to(torch.int16)
+    u = bits.view(torch.bfloat16).repeat(2)  # 131072 elements: every pattern at even and odd positions
+    u = torch.cat([u[1:], u[:1]])
+    g = torch.Generator(device=dev).manual_seed(7)
+    dv = torch.randn(u.shape, device=dev, generator=g).to(torch.bfloat16)
+    keep = postln.dropout_keep(u.numel(), p, 1234, dev).bool()
+    ud = u.clone().requires_grad_(True)
+    v = postln.gelu_drop(ud, p, 1234)
+    s = 1.0 / (1.0 - p)
+    ref = torch.where(keep, (torch.nn.functional.gelu(u).float() * s).to(torch.bfloat16), torch.zeros_like(u))
+    torch.testing.assert_close(v, ref, rtol=0, atol=0, equal_nan=True)
+    v.backward(dv)
+    dg = torch.where(keep, (dv.float() * s).to(torch.bfloat16), torch.zeros_like(dv))
+    torch.testing.assert_close(ud.grad, torch.ops.aten.gelu_backward(dg, u), rtol=0, atol=0, equal_nan=True)

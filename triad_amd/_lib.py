@@ -57,8 +57,10 @@ SIGNATURES = {
     "triad_dropaddln_fwd": [vp, vp, vp, vp, f32, i32, i32, f32, u32, vp, vp, vp, vp, vp],
     "triad_dropaddln_bwd_blocks": [i32],
     "triad_dropaddln_bwd": [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, u32, vp, vp, vp, vp],
-    "triad_geludrop_fwd": [vp, i64, f32, u32, vp, vp],
-    "triad_geludrop_bwd": [vp, vp, i64, f32, u32, vp, vp],
+    "triad_gelu_table_bytes": [],
+    "triad_gelu_table": [vp, vp],
+    "triad_geludrop_fwd": [vp, i64, f32, u32, vp, vp, vp],
+    "triad_geludrop_bwd": [vp, vp, i64, f32, u32, vp, vp, vp],
     "triad_dropout_keep": [i64, f32, u32, vp, vp],
     "triad_addln_fwd": [vp, vp, vp, vp, vp, f32, i32, i32, vp, vp, i32, vp, vp, vp],
     "triad_addln_bwd": [vp, i32, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp, vp],
@@ -75,7 +77,7 @@ SIGNATURES = {
 }
 # entry points returning a value rather than a status
 RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_longlong,
-            "triad_conv0_dw_workspace_bytes": C.c_longlong,
+            "triad_conv0_dw_workspace_bytes": C.c_longlong, "triad_gelu_table_bytes": C.c_longlong,
             "triad_lora_tn_blocks": C.c_int, "triad_dropaddln_bwd_blocks": C.c_int,
             "triad_colsum_splits": C.c_int}
 

@@ -169,49 +169,111 @@ __global__ __launch_bounds__(256) void dropaddln_bwd_kernel(const float* __restr
 constexpr float kAlpha = 0.70710678118654752440f;                 // M_SQRT1_2
 constexpr float kBeta = 1.12837916709551257390f * 0.70710678118654752440f * 0.5f;  // M_2_SQRTPI * M_SQRT1_2 / 2
 
-// thread = 8 consecutive elements (4 pairs); DROP = false: p = 0 (plain GELU, no hash)
-template <bool DROP>
-__global__ __launch_bounds__(256) void geludrop_fwd_kernel(const bf16* __restrict__ u, long long n, unsigned seed,
-                                                           unsigned thr, float scale, bf16* __restrict__ v) {
-  const long long e0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
-  if (e0 >= n) return;
-  const bf16x8 x = *(const bf16x8*)(u + e0);
-  bf16x8 o;
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const unsigned k = DROP ? keep_pair((unsigned long long)(e0 >> 1) + p, seed, thr) : 3u;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const float xf = (float)x[2 * p + c];
-      const float g = (float)(bf16)(0.5f * xf * (1.0f + erff(xf * kAlpha)));
-      o[2 * p + c] = DROP ? (bf16)drop(g, (k >> c) & 1u, scale) : (bf16)g;
-    }
-  }
-  *(bf16x8*)(v + e0) = o;
+__device__ __forceinline__ float gelu_val(float x) { return 0.5f * x * (1.0f + erff(x * kAlpha)); }
+__device__ __forceinline__ float gelu_slope(float x) {  // aten gelu_backward's factor: cdf + x * pdf
+  const float cdf = 0.5f * (1.0f + erff(x * kAlpha));
+  const float pdf = expf(-0.5f * x * x) * kBeta;
+  return cdf + x * pdf;
 }
 
-template <bool DROP>
-__global__ __launch_bounds__(256) void geludrop_bwd_kernel(const bf16* __restrict__ u, const bf16* __restrict__ dv,
-                                                           long long n, unsigned seed, unsigned thr, float scale,
-                                                           bf16* __restrict__ du) {
-  const long long e0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
-  if (e0 >= n) return;
-  const bf16x8 x = *(const bf16x8*)(u + e0);
-  const bf16x8 d = *(const bf16x8*)(dv + e0);
-  bf16x8 o;
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const unsigned k = DROP ? keep_pair((unsigned long long)(e0 >> 1) + p, seed, thr) : 3u;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const float xf = (float)x[2 * p + c];
-      const float dg = DROP ? drop((float)d[2 * p + c], (k >> c) & 1u, scale) : (float)d[2 * p + c];  // dropout bwd
-      const float cdf = 0.5f * (1.0f + erff(xf * kAlpha));
-      const float pdf = expf(-0.5f * xf * xf) * kBeta;
-      o[2 * p + c] = (bf16)(dg * (cdf + xf * pdf));
-    }
+// GELU of a bf16 input has only 65536 possible arguments, so the erf / exp work (~28 VALU
+// instructions per element, which made the pass VALU-bound at ~60 % of HBM rate) is done once
+// into a table: entry i covers the bf16 pattern with exponent field GL_E0 + i / 256, sign
+// (i >> 7) & 1, mantissa i & 127, i.e. every finite |x| in [2^-40, 2^6); other patterns (zero,
+// tiny, huge, inf / NaN) take the direct formula. Values are computed by the same device code,
+// so table and formula agree bit for bit. Layout: GL_N fp32 slopes, then GL_N bf16 values.
+constexpr int GL_E0 = 127 - 40, GL_NE = 46, GL_N = GL_NE * 256;
+constexpr int GL_BYTES = GL_N * 4 + GL_N * 2;
+
+__device__ __forceinline__ int gl_index(unsigned bits) {
+  const int idx = (int)((bits >> 7) & 255u) - GL_E0;
+  return (unsigned)idx < (unsigned)GL_NE ? (idx << 8) | (int)(bits >> 8 & 128u) | (int)(bits & 127u) : -1;
+}
+
+__global__ __launch_bounds__(256) void gelu_table_kernel(float* __restrict__ slope, bf16* __restrict__ val) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= GL_N) return;
+  const unsigned bits = ((unsigned)(i >> 7 & 1) << 15) | ((unsigned)(GL_E0 + (i >> 8)) << 7) | (unsigned)(i & 127);
+  const float x = __uint_as_float(bits << 16);
+  slope[i] = gelu_slope(x);
+  val[i] = (bf16)gelu_val(x);
+}
+
+__device__ __forceinline__ unsigned bf16_bits(bf16 v) { return (unsigned)__builtin_bit_cast(unsigned short, v); }
+
+// Persistent passes (grid ~ a few blocks per CU, table staged in LDS once per block), thread =
+// 8 consecutive elements (4 pairs) per iteration; DROP = false: p = 0 (plain GELU, no hash).
+// TABLE = false: the direct formula (no table buffer given).
+constexpr int GL_NT = 512;
+
+template <bool DROP, bool TABLE>
+__global__ __launch_bounds__(GL_NT) void geludrop_fwd_kernel(const bf16* __restrict__ u, long long n, unsigned seed,
+                                                             unsigned thr, float scale, const bf16* __restrict__ tval,
+                                                             bf16* __restrict__ v) {
+  __shared__ bf16 tab[TABLE ? GL_N : 1];
+  if constexpr (TABLE) {
+    for (int i = threadIdx.x * 8; i < GL_N; i += GL_NT * 8) *(bf16x8*)(tab + i) = *(const bf16x8*)(tval + i);
+    __syncthreads();
   }
-  *(bf16x8*)(du + e0) = o;
+  for (long long e0 = ((long long)blockIdx.x * GL_NT + threadIdx.x) * 8; e0 < n; e0 += (long long)gridDim.x * GL_NT * 8) {
+    const bf16x8 x = *(const bf16x8*)(u + e0);
+    bf16x8 o;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const unsigned k = DROP ? keep_pair((unsigned long long)(e0 >> 1) + p, seed, thr) : 3u;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const bf16 xb = x[2 * p + c];
+        bf16 g;
+        const int idx = TABLE ? gl_index(bf16_bits(xb)) : -1;
+        if (idx >= 0) g = tab[idx];
+        else g = (bf16)gelu_val((float)xb);
+        o[2 * p + c] = DROP ? (bf16)drop((float)g, (k >> c) & 1u, scale) : g;
+      }
+    }
+    *(bf16x8*)(v + e0) = o;
+  }
+}
+
+template <bool DROP, bool TABLE>
+__global__ __launch_bounds__(GL_NT) void geludrop_bwd_kernel(const bf16* __restrict__ u, const bf16* __restrict__ dv,
+                                                             long long n, unsigned seed, unsigned thr, float scale,
+                                                             const float* __restrict__ tslope, bf16* __restrict__ du) {
+  __shared__ float tab[TABLE ? GL_N : 1];
+  if constexpr (TABLE) {
+    for (int i = threadIdx.x * 4; i < GL_N; i += GL_NT * 4) *(f32x4*)(tab + i) = *(const f32x4*)(tslope + i);
+    __syncthreads();
+  }
+  for (long long e0 = ((long long)blockIdx.x * GL_NT + threadIdx.x) * 8; e0 < n; e0 += (long long)gridDim.x * GL_NT * 8) {
+    const bf16x8 x = *(const bf16x8*)(u + e0);
+    const bf16x8 d = *(const bf16x8*)(dv + e0);
+    bf16x8 o;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const unsigned k = DROP ? keep_pair((unsigned long long)(e0 >> 1) + p, seed, thr) : 3u;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const bf16 xb = x[2 * p + c];
+        const float dg = DROP ? drop((float)d[2 * p + c], (k >> c) & 1u, scale) : (float)d[2 * p + c];  // dropout bwd
+        const int idx = TABLE ? gl_index(bf16_bits(xb)) : -1;
+        const float sl = idx >= 0 ? tab[idx] : gelu_slope((float)xb);
+        o[2 * p + c] = (bf16)(dg * sl);
+      }
+    }
+    *(bf16x8*)(du + e0) = o;
+  }
+}
+
+int gl_blocks(long long n) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const long long need = (n / 8 + GL_NT - 1) / GL_NT;
+  return (int)(need < 2LL * cus ? need : 2LL * cus);
 }
 
 __global__ __launch_bounds__(256) void dropout_keep_kernel(long long n, unsigned seed, unsigned thr,
@@ -267,22 +329,38 @@ int triad_dropaddln_bwd(const float* dh, const void* dhb, const float* res, cons
   return TRIAD_EINVAL;
 }
 
-// v = dropout(gelu(u)) over n bf16 elements (n % 8 == 0); p = 0: plain exact-erf GELU (aten's roundings)
-int triad_geludrop_fwd(const void* u, long long n, float p, unsigned seed, void* v, hipStream_t stream) {
-  if (n <= 0 || n % 8 || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
-  hipLaunchKernelGGL(p > 0.f ? geludrop_fwd_kernel<true> : geludrop_fwd_kernel<false>,
-                     dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, stream, (const bf16*)u, n, seed, drop_thr(p),
-                     1.f / (1.f - p), (bf16*)v);
+// Table for the GELU passes below (caller-owned device buffer of triad_gelu_table_bytes() bytes,
+// built once per device by triad_gelu_table; a NULL table makes the passes use the formula).
+long long triad_gelu_table_bytes(void) { return GL_BYTES; }
+
+int triad_gelu_table(void* table, hipStream_t stream) {
+  if (!table) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(gelu_table_kernel, dim3((GL_N + 255) / 256), dim3(256), 0, stream, (float*)table,
+                     (bf16*)((char*)table + GL_N * 4));
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
 
-int triad_geludrop_bwd(const void* u, const void* dv, long long n, float p, unsigned seed, void* du,
+// v = dropout(gelu(u)) over n bf16 elements (n % 8 == 0); p = 0: plain exact-erf GELU (aten's roundings)
+int triad_geludrop_fwd(const void* u, long long n, float p, unsigned seed, const void* table, void* v,
                        hipStream_t stream) {
   if (n <= 0 || n % 8 || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
-  hipLaunchKernelGGL(p > 0.f ? geludrop_bwd_kernel<true> : geludrop_bwd_kernel<false>,
-                     dim3((unsigned)((n / 8 + 255) / 256)), dim3(256), 0, stream, (const bf16*)u, (const bf16*)dv, n,
-                     seed, drop_thr(p), 1.f / (1.f - p), (bf16*)du);
+  const bf16* tv = table ? (const bf16*)((const char*)table + GL_N * 4) : nullptr;
+  auto kern = p > 0.f ? (table ? geludrop_fwd_kernel<true, true> : geludrop_fwd_kernel<true, false>)
+                      : (table ? geludrop_fwd_kernel<false, true> : geludrop_fwd_kernel<false, false>);
+  hipLaunchKernelGGL(kern, dim3(gl_blocks(n)), dim3(GL_NT), 0, stream, (const bf16*)u, n, seed, drop_thr(p),
+                     1.f / (1.f - p), tv, (bf16*)v);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_geludrop_bwd(const void* u, const void* dv, long long n, float p, unsigned seed, const void* table, void* du,
+                       hipStream_t stream) {
+  if (n <= 0 || n % 8 || p < 0.f || p >= 1.f) return TRIAD_EINVAL;
+  auto kern = p > 0.f ? (table ? geludrop_bwd_kernel<true, true> : geludrop_bwd_kernel<true, false>)
+                      : (table ? geludrop_bwd_kernel<false, true> : geludrop_bwd_kernel<false, false>);
+  hipLaunchKernelGGL(kern, dim3(gl_blocks(n)), dim3(GL_NT), 0, stream, (const bf16*)u, (const bf16*)dv, n, seed,
+                     drop_thr(p), 1.f / (1.f - p), (const float*)table, (bf16*)du);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

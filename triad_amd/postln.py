@@ -83,6 +83,20 @@ class _DropAddLN(torch.autograd.Function):
         return dres, dy, gwb[:D], gwb[D:], None, None, None
 
 
+_GELU_TABLES = {}
+
+
+def gelu_table(device):
+    """Per-device GELU value / slope table (triad_gelu_table), built once."""
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    t = _GELU_TABLES.get(key)
+    if t is None:
+        t = torch.empty(int(call("triad_gelu_table_bytes")), dtype=torch.uint8, device=device)
+        call("triad_gelu_table", ptr(t), stream_ptr(device))
+        _GELU_TABLES[key] = t
+    return t
+
+
 class _GeluDrop(torch.autograd.Function):
     """v = dropout(gelu(u)) on bf16 u (exact erf GELU, as ACT2FN['gelu'])."""
 
@@ -92,7 +106,8 @@ class _GeluDrop(torch.autograd.Function):
             raise TypeError(f"gelu_drop: u {u.dtype} {tuple(u.shape)}")
         u = u.contiguous()
         v = torch.empty_like(u)
-        call("triad_geludrop_fwd", ptr(u), u.numel(), p, seed, ptr(v), stream_ptr(u.device))
+        call("triad_geludrop_fwd", ptr(u), u.numel(), p, seed, ptr(gelu_table(u.device)), ptr(v),
+             stream_ptr(u.device))
         ctx.save_for_backward(u)
         ctx.meta = (p, seed)
         return v
@@ -103,7 +118,8 @@ class _GeluDrop(torch.autograd.Function):
         p, seed = ctx.meta
         dv = dv.to(torch.bfloat16).contiguous()
         du = torch.empty_like(u)
-        call("triad_geludrop_bwd", ptr(u), ptr(dv), u.numel(), p, seed, ptr(du), stream_ptr(u.device))
+        call("triad_geludrop_bwd", ptr(u), ptr(dv), u.numel(), p, seed, ptr(gelu_table(u.device)), ptr(du),
+             stream_ptr(u.device))
         return du, None, None
 
 
