@@ -121,6 +121,11 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
                            int M, int N, int Kd, int splits, const float* alpha, float* slabs, void* C,
                            int out_bf16, hipStream_t stream);
 
+/* Select the form the two GEMM entry points above use from now on (process-wide tuning / test
+ * knob): 0 = size policy (default), 1 = 128 x 128 tiles, 2 = 256 x 128 LDS ring, 3 = 256 x 256
+ * four-wave tiles (M, N multiples of 256). */
+int triad_gemm_set_form(int form);
+
 /* Fused projection head forward (model.py:32-34,68 / 81-83,116 / 253-255,326 under bf16
  * autocast): y = bf16(LN(bf16(h W1^T + b1)) W2^T + b2) for M rows of H features; also
  * saves y1 = bf16(h W1^T + b1), ln = bf16(LN(y1)), mean/rstd per row for the backward.

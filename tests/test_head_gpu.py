@@ -148,12 +148,15 @@ def test_tv_head_vs_oracle_random(B, Nt, Nv, mix):
     assert _scalar_close(float(tg.grad), float(tr.grad), 2e-3, 1e-5)
 
 
+@pytest.mark.parametrize("form", [0, 1, 2, 3])
 @pytest.mark.parametrize("kcontig,bk", [(1, 0), (0, 0), (1, 1), (0, 1)])
-def test_gemm_layouts_vs_torch(kcontig, bk):
-    """triad_gemm_bf16 against a plain fp32 torch matmul of the same bf16 operands."""
+def test_gemm_layouts_vs_torch(kcontig, bk, form):
+    """triad_gemm_bf16 in each tile form (triad_gemm_set_form: size policy, 128 x 128, 256 x 128
+    ring, 256 x 256 four-wave) against a plain fp32 torch matmul of the same bf16 operands."""
     from triad_amd._lib import call, ptr, stream_ptr
     g = torch.Generator().manual_seed(7)
-    M, N, K = 256, 512, 384
+    M, N, K = 512, 768, 384
+    call("triad_gemm_set_form", form)
     A = torch.randn(M, K, generator=g).to(torch.bfloat16)
     B = torch.randn(K, N, generator=g).to(torch.bfloat16)
     ref = 0.7 * (A.float() @ B.float())
@@ -165,6 +168,7 @@ def test_gemm_layouts_vs_torch(kcontig, bk):
          ptr(C), N, 0,
          stream_ptr())
     torch.cuda.synchronize()
+    call("triad_gemm_set_form", 0)
     np.testing.assert_allclose(C.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-3)
 
 

@@ -297,6 +297,135 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
     }
 }
 
+// ---- 256 x 256 four-wave form ------------------------------------------------------------------
+// Workgroup = 4 waves (2 x 2), each owning a 128 x 128 output (4 x 4 tiles of 32 x 32, 256 fp32
+// accumulators per lane in AGPRs), tile 256 x 256 x 64 per stage, two 64 KB LDS slots. Per
+// 16-deep k step a wave reads 8 fragments for 16 MFMAs (the 64 x 64-per-wave forms read 4 for 4),
+// halving the LDS bytes per MFMA -- the limit of the smaller forms, most of all on the transposed
+// (ds_read_b64_tr_b16) operand reads of the weight-gradient GEMMs. Each wave issues 16 DMA
+// pieces for the next stage, one after every 4th of its 64 MFMAs; the wait at the top of a
+// stage is vmcnt(0) + barrier (one stage of lead, ~2 K MFMA cycles).
+constexpr int GW_M = 256, GW_N = 256;
+constexpr int GW_A = GW_M * BK, GW_ST = GW_A + GW_N * BK;  // elements per stage (64 KB)
+constexpr int GW_PIECES = 16;
+
+template <bool KCONTIG>
+__device__ __forceinline__ void gw_piece_one(const bf16* __restrict__ X, long long ld, int r0, int k0, bf16* img,
+                                             int inst, int lane) {
+  if (KCONTIG) {  // image [256][64]: 8 rows x 128 B per wave-instruction
+    const int m = inst * 8 + (lane >> 3), cp = lane & 7;
+    const int c = cp ^ ((m >> 1) & 7);
+    glds16(X + (size_t)(r0 + m) * ld + k0 + c * 8, img + inst * 512);
+  } else {  // X stored [k][rows]: two [64][128] halves, 4 k-rows x 256 B per wave-instruction
+    const int half = inst >> 4, ii = inst & 15;
+    const int k = ii * 4 + (lane >> 4), cp = lane & 15;
+    const int c = cp ^ ((k & 3) << 2);
+    glds16(X + (size_t)(k0 + k) * ld + r0 + half * 128 + c * 8, img + half * (BK * 128) + ii * 512);
+  }
+}
+
+template <bool A_KCONTIG, bool B_KCONTIG>
+__device__ __forceinline__ void gw_piece(const bf16* __restrict__ A, long long lda, const bf16* __restrict__ B,
+                                         long long ldb, int m0, int n0, int k0, bf16* dst, int wave, int lane,
+                                         int u) {
+  if (u < 8) gw_piece_one<A_KCONTIG>(A, lda, m0, k0, dst, wave * 8 + u, lane);
+  else gw_piece_one<B_KCONTIG>(B, ldb, n0, k0, dst + GW_A, wave * 8 + (u - 8), lane);
+}
+
+template <bool KCONTIG>
+__device__ __forceinline__ bf16x8 gw_frag(const bf16* img, int row, int s, int lane) {
+  if (KCONTIG) return *(const bf16x8*)(img + kc_off(row + (lane & 31), 2 * s + (lane >> 5)));
+  return frag_tr(img + (row >> 7) * (BK * 128), row & 127, s, lane);
+}
+
+template <bool A_KCONTIG, bool B_KCONTIG, typename OutT>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict__ A, long long lda,
+                                                         const bf16* __restrict__ B, long long ldb, int M, int N,
+                                                         int Kd, const float* __restrict__ alpha_p,
+                                                         OutT* __restrict__ C, long long ldc, int k_per_split,
+                                                         long long slab_stride) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * GW_ST];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  const int ntn = N / GW_N;
+  const int m0 = (swz / ntn) * GW_M, n0 = (swz % ntn) * GW_N;
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x16){};
+
+  const int kbeg = blockIdx.y * k_per_split;
+  const int nk = __builtin_amdgcn_readfirstlane(max(0, min(k_per_split, Kd - kbeg)) / BK);
+  C += (size_t)blockIdx.y * slab_stride;
+  if (nk > 0)
+#pragma unroll
+    for (int u = 0; u < GW_PIECES; ++u)
+      gw_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kbeg, lds, wave, lane, u);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool pf = kt + 1 < nk;
+    bf16* const nb = lds + ((kt + 1) & 1) * GW_ST;
+    const int kn = kbeg + (kt + 1) * BK;
+    const bf16* ai = lds + (kt & 1) * GW_ST;
+    const bf16* bi = ai + GW_A;
+    // fragments double-buffered across the four 16-deep steps: step s + 1's 8 LDS reads are
+    // issued between step s's first 8 MFMAs (only step 0's reads are exposed per stage)
+    bf16x8 af[2][4], bfr[2][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      af[0][t] = gw_frag<A_KCONTIG>(ai, wm * 128 + t * 32, 0, lane);
+      bfr[0][t] = gw_frag<B_KCONTIG>(bi, wn * 128 + t * 32, 0, lane);
+    }
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const int cur = s & 1;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          acc[a][b] = mfma32(af[cur][a], bfr[cur][b], acc[a][b]);
+          const int j = a * 4 + b, mi = s * 16 + j;
+          if (s + 1 < BK / 16 && j < 8) {
+            __builtin_amdgcn_sched_barrier(0);
+            const int t = j >> 1;
+            if (j & 1) bfr[cur ^ 1][t] = gw_frag<B_KCONTIG>(bi, wn * 128 + t * 32, s + 1, lane);
+            else af[cur ^ 1][t] = gw_frag<A_KCONTIG>(ai, wm * 128 + t * 32, s + 1, lane);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if ((mi & 3) == 3) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (pf) gw_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, mi >> 2);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+    }
+  }
+
+  const float alpha = alpha_p ? *alpha_p : 1.f;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int n = n0 + wn * 128 + b * 32 + (lane & 31);
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int m = m0 + wm * 128 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v]);
+      }
+    }
+}
+
+// Form override for measurement and tests (triad_gemm_set_form): 0 = the size policy in
+// launch(), 1 = 128 x 128, 2 = 256 x 128 ring, 3 = 256 x 256 four-wave (when the shape allows).
+int g_gemm_form = 0;
+
 #ifndef GEMM_BIG
 #define GEMM_BIG 1  // 1: gemm_big_kernel where it measured faster (see launch)
 #endif
@@ -308,7 +437,20 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
   const int kps = ((Kd / BK + splits - 1) / splits) * BK;
   // the 256-row ring pays off on long k loops or many row tiles (conv / projection GEMMs);
   // the short split-K weight-gradient loops keep the 128 x 128 form (measured, tools/dw_variants.py)
-  if (GEMM_BIG && M % GB_M == 0 && (M >= 8192 || Kd / splits >= 32768)) {
+  const bool w4_ok = M % GW_M == 0 && N % GW_N == 0;
+  // the four-wave form measured faster on the long conv-stack GEMMs (tools/gemm_forms.py:
+  // 2.94 -> 2.67 ms at M = 1.6 M, N = 512, K = 1536); the split-K weight gradients and the
+  // shorter forward shapes keep the smaller tiles
+  const bool w4_auto = AK && BK_ && splits == 1 && M >= 65536 && Kd >= 1024;
+  if (w4_ok && (g_gemm_form == 3 || (g_gemm_form == 0 && w4_auto))) {
+    const int nwg = (M / GW_M) * (N / GW_N);
+    hipLaunchKernelGGL((gemm_w4_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(256), 0, st, (const bf16*)A, lda,
+                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride);
+    TRIAD_CHECK_LAUNCH();
+    return TRIAD_OK;
+  }
+  if (g_gemm_form != 1 && M % GB_M == 0 &&
+      (g_gemm_form == 2 || (GEMM_BIG && (M >= 8192 || Kd / splits >= 32768)))) {
     const int nwg = (M / GB_M) * (N / BN);
     hipLaunchKernelGGL((gemm_big_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
                        (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride);
@@ -361,6 +503,14 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
 #undef TRIAD_GEMM_SK
   if (rc) return rc;
   return triad_sum_slabs(slabs, splits, slab, alpha, out_bf16, C, stream);
+}
+
+// Select the GEMM form for later calls (0 = size policy, 1 = 128 x 128, 2 = 256 x 128 ring,
+// 3 = 256 x 256 four-wave). Process-wide tuning / test knob.
+int triad_gemm_set_form(int form) {
+  if (form < 0 || form > 3) return TRIAD_EINVAL;
+  g_gemm_form = form;
+  return TRIAD_OK;
 }
 
 }  // extern "C"
