@@ -301,10 +301,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
 // Workgroup = 4 waves (2 x 2), each owning a 128 x 128 output (4 x 4 tiles of 32 x 32, 256 fp32
 // accumulators per lane in AGPRs), tile 256 x 256 x 64 per stage, two 64 KB LDS slots. Per
 // 16-deep k step a wave reads 8 fragments for 16 MFMAs (the 64 x 64-per-wave forms read 4 for 4),
-// halving the LDS bytes per MFMA -- the limit of the smaller forms, most of all on the transposed
-// (ds_read_b64_tr_b16) operand reads of the weight-gradient GEMMs. Each wave issues 16 DMA
-// pieces for the next stage, one after every 4th of its 64 MFMAs; the wait at the top of a
-// stage is vmcnt(0) + barrier (one stage of lead, ~2 K MFMA cycles).
+// halving the LDS bytes per MFMA. Each wave issues the 16 DMA pieces of the next stage in the
+// first half of the current one (one after every 2nd MFMA; every 4th measured 5 % slower), and
+// waits with vmcnt(0) + barrier at the top of the next. Measured bounds (tools/gemm_forms.py,
+// profiles/r01_gemm_w4_bounds.log): without the fragment reads the conv GEMM runs 3 % faster,
+// without the DMA 25 % faster -- the LDS-DMA fill rate (~64 KB per CU per stage), not the LDS
+// reads, is what holds it under the MFMA rate; a 32-deep 4-slot ring with more lead was slower.
 constexpr int GW_M = 256, GW_N = 256;
 constexpr int GW_A = GW_M * BK, GW_ST = GW_A + GW_N * BK;  // elements per stage (64 KB)
 constexpr int GW_PIECES = 16;
@@ -399,9 +401,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
             else af[cur ^ 1][t] = gw_frag<A_KCONTIG>(ai, wm * 128 + t * 32, s + 1, lane);
             __builtin_amdgcn_sched_barrier(0);
           }
-          if ((mi & 3) == 3) {
+          if (mi % 2 == 1 && mi / 2 < GW_PIECES) {  // all 16 pieces in the stage's first 32 MFMAs
             __builtin_amdgcn_sched_barrier(0);
-            if (pf) gw_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, mi >> 2);
+            if (pf) gw_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, mi / 2);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
