@@ -218,6 +218,14 @@ int triad_conv0_dw(const void* wave, long long Lp, const void* dy0, int B, int T
 int triad_posconv(const void* x, const void* wt, const float* bias, void* y, int B, int T, int C, int groups,
                   int pad, hipStream_t stream);
 
+/* Weight gradient of the same conv (C / groups == 48): fp32 partials part[s][g][j][n][c] over
+ * `splits` contiguous sample ranges, dW[g*48 + n][c][j] = sum_s part[...]; part holds
+ * triad_posconv_dw_part_bytes(C, groups, splits) bytes. Replaces aten's grouped-conv weight
+ * gradient (transformers HubertPositionalConvEmbedding backward). */
+long long triad_posconv_dw_part_bytes(int C, int groups, int splits);
+int triad_posconv_dw(const void* x, const void* dy, int B, int T, int C, int groups, int pad, int splits, float* part,
+                     hipStream_t stream);
+
 /* Backbone self-attention (the DINOv2 / HuBERT / DistilBERT encoders of model.py:29-30,79-80,
  * 218-227; no dropout, no mask): O = softmax(Q K^T * scale) V per (sample, head), head dim D = 64,
  * N <= 320. Tensors are (B, N, H, 64) bf16 in memory with the head dim contiguous: element

@@ -165,3 +165,21 @@ def test_vit_fused_residual_ln_matches_unfused(monkeypatch):
     assert set(g_fus) == set(g_ref) and len(g_ref) == 48
     for n in g_ref:
         assert _rel(g_fus[n], g_ref[n]) < 3e-2, n
+
+
+@pytest.mark.parametrize("B,T,splits", [(5, 199, 2), (3, 300, 3), (2, 37, 1)])
+def test_posconv_weight_grad_vs_fp32(B, T, splits):
+    """triad_posconv_dw (groups of 48 channels, 128 taps, padding 64, first T outputs) against the
+    fp32 grouped-conv weight gradient of the same bf16 operands (fp32 accumulation both ways)."""
+    from triad_amd._lib import call, ptr, stream_ptr
+    C, G, K, pad = 768, 16, 128, 64
+    g = torch.Generator(device=dev).manual_seed(T)
+    x = torch.randn(B, T, C, device=dev, generator=g).to(torch.bfloat16)
+    dy = torch.randn(B, T, C, device=dev, generator=g).to(torch.bfloat16)
+    part = torch.empty(int(call("triad_posconv_dw_part_bytes", C, G, splits)) // 4, device=dev)
+    call("triad_posconv_dw", ptr(x), ptr(dy), B, T, C, G, pad, splits, ptr(part), stream_ptr(x.device))
+    dw = part.view(splits, -1).sum(0).view(G, K, 48, 48).permute(0, 2, 3, 1).reshape(C, 48, K)
+    # full conv output has T + 1 steps; the dropped last one gets zero gradient
+    dy_full = torch.cat([dy.float(), torch.zeros(B, 1, C, device=dev)], 1).transpose(1, 2)
+    ref = torch.nn.grad.conv1d_weight(x.float().transpose(1, 2), (C, 48, K), dy_full, padding=pad, groups=G)
+    assert _rel(dw, ref) < 1e-5

@@ -53,6 +53,8 @@ SIGNATURES = {
     "triad_conv0_dw": [vp, i64, vp, i32, i32, i32, i32, vp, vp, vp],
     "triad_c0gn_fwd": [vp, i64, vp, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
     "triad_posconv": [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
+    "triad_posconv_dw_part_bytes": [i32, i32, i32],
+    "triad_posconv_dw": [vp, vp, i32, i32, i32, i32, i32, i32, vp, vp],
     "triad_rows_nt": [vp, i64, i32, i32, vp, i32, vp, vp],
     "triad_lora_update": [vp, i64, i32, i32, vp, vp, vp],
     "triad_dropaddln_fwd": [vp, vp, vp, vp, f32, i32, i32, f32, u32, vp, vp, vp, vp, vp],
@@ -79,6 +81,7 @@ SIGNATURES = {
 # entry points returning a value rather than a status
 RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_longlong,
             "triad_conv0_dw_workspace_bytes": C.c_longlong, "triad_gelu_table_bytes": C.c_longlong,
+            "triad_posconv_dw_part_bytes": C.c_longlong,
             "triad_lora_tn_blocks": C.c_int, "triad_dropaddln_bwd_blocks": C.c_int,
             "triad_colsum_splits": C.c_int}
 

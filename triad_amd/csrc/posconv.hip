@@ -104,6 +104,101 @@ __global__ __launch_bounds__(256) void posconv_kernel(const bf16* __restrict__ x
   }
 }
 
+// ---- weight gradient ----------------------------------------------------------------------------
+// dW[g*CG + n][c][j] = sum_{b, t < T} dy[b, t, g*CG + n] * x[b, t + j - pad, g*CG + c]: per (group,
+// tap) a CG x CG GEMM contracted over every (sample, time) row. Workgroup = (group, 16 taps,
+// sample range); wave w owns taps j0 + 4w .. + 3 (4 x (CG/16)^2 accumulator tiles of
+// v_mfma_f32_16x16x32_bf16). Per (sample, 224-row time block) dy and the x window (224 + 15
+// rows, the 16 taps' shifts of each other) are staged in LDS; both operands are k(=time)-major,
+// so their fragments are transposed LDS reads (ds_read_b64_tr_b16) and a tap's B fragment is the
+// window read one row further down. Partials per sample range: part[s][g][j][n][c] (fp32).
+constexpr int DW_TP = 224;   // time rows per block step
+constexpr int DW_TAPS = 16;  // taps per workgroup (4 per wave)
+
+template <int CG>
+__device__ __forceinline__ bf16x8 dw_frag(const bf16* img, int row0, int col0, int lane) {
+  // 8 consecutive rows (row0 + 8 (lane >> 4) ..) of column col0 + (lane & 15)
+  const int g = lane & 15, q = lane >> 4;
+  const bf16* p = img + (row0 + 8 * q + (g >> 2)) * CG + col0 + 4 * (g & 3);
+  const s16x4 lo = lds_tr16(p);
+  const s16x4 hi = lds_tr16(p + 4 * CG);
+  bf16x8 r;
+  s16x4* rp = (s16x4*)&r;
+  rp[0] = lo;
+  rp[1] = hi;
+  return r;
+}
+
+template <int CG>
+__global__ __launch_bounds__(256, 2) void posconv_dw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                            int B, int T, int C, int pad, int spb,
+                                                            float* __restrict__ part) {
+  constexpr int NTL = CG / 16;
+  constexpr int XW = DW_TP + DW_TAPS - 1;
+  __shared__ __attribute__((aligned(16))) bf16 dyl[DW_TP * CG];
+  __shared__ __attribute__((aligned(16))) bf16 xl[XW * CG];
+  const int g = blockIdx.x, j0 = blockIdx.y * DW_TAPS, sidx = blockIdx.z;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int G = gridDim.x;
+
+  f32x4_t acc[4][NTL][NTL];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+    for (int a = 0; a < NTL; ++a)
+#pragma unroll
+      for (int b = 0; b < NTL; ++b) acc[tt][a][b] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  constexpr int PIECES = CG / 8;
+  const int b_lo = sidx * spb, b_hi = min(B, b_lo + spb);
+  for (int b = b_lo; b < b_hi; ++b)
+    for (int tb = 0; tb < T; tb += DW_TP) {
+      __syncthreads();  // previous step's reads done
+      for (int e = threadIdx.x; e < DW_TP * PIECES; e += 256) {
+        const int w = e / PIECES, p = e - w * PIECES, t = tb + w;
+        bf16x8 v = {};
+        if (t < T) v = *(const bf16x8*)(dy + ((size_t)b * T + t) * C + g * CG + p * 8);
+        *(bf16x8*)(dyl + w * CG + p * 8) = v;
+      }
+      for (int e = threadIdx.x; e < XW * PIECES; e += 256) {
+        const int w = e / PIECES, p = e - w * PIECES, t = tb + w + j0 - pad;
+        bf16x8 v = {};
+        if (t >= 0 && t < T) v = *(const bf16x8*)(x + ((size_t)b * T + t) * C + g * CG + p * 8);
+        *(bf16x8*)(xl + w * CG + p * 8) = v;
+      }
+      __syncthreads();
+      const int nks = (min(DW_TP, T - tb) + 31) / 32;
+      for (int ks = 0; ks < nks; ++ks) {
+        bf16x8 af[NTL];
+#pragma unroll
+        for (int a = 0; a < NTL; ++a) af[a] = dw_frag<CG>(dyl, ks * 32, a * 16, lane);
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+          for (int b2 = 0; b2 < NTL; ++b2) {
+            const bf16x8 bf = dw_frag<CG>(xl, ks * 32 + wave * 4 + tt, b2 * 16, lane);
+#pragma unroll
+            for (int a = 0; a < NTL; ++a)
+              acc[tt][a][b2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bf, acc[tt][a][b2], 0, 0, 0);
+          }
+      }
+    }
+
+  // C/D layout: col = lane & 15, row = 4 * (lane >> 4) + v
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    const int j = j0 + wave * 4 + tt;
+    float* dst = part + (((size_t)sidx * G + g) * KT + j) * CG * CG;
+#pragma unroll
+    for (int a = 0; a < NTL; ++a)
+#pragma unroll
+      for (int b2 = 0; b2 < NTL; ++b2)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) dst[(a * 16 + 4 * q + v) * CG + b2 * 16 + r] = acc[tt][a][b2][v];
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -121,6 +216,26 @@ int triad_posconv(const void* x, const void* wt, const float* bias, void* y, int
                        (bf16*)y, T, C, pad);
   else
     return TRIAD_EINVAL;
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+// Weight-gradient partials of the positional conv (C / groups == 48, HuBERT-base):
+// part[s][g][j][n][c] (fp32, s < splits) with
+// dW[g*CG + n][c][j] = sum_s part[s][g][j][n][c]; samples split into `splits` contiguous ranges.
+long long triad_posconv_dw_part_bytes(int C, int groups, int splits) {
+  return groups > 0 && C % groups == 0 ? (long long)splits * groups * KT * (C / groups) * (C / groups) * 4 : -1;
+}
+
+int triad_posconv_dw(const void* x, const void* dy, int B, int T, int C, int groups, int pad, int splits, float* part,
+                     hipStream_t stream) {
+  if (B <= 0 || T <= 0 || groups <= 0 || C % groups || pad < 0 || pad >= KT || splits <= 0 || splits > 65535)
+    return TRIAD_EINVAL;
+  const int cg = C / groups, spb = (B + splits - 1) / splits;
+  const dim3 grid(groups, KT / DW_TAPS, splits);
+  if (cg != 48) return TRIAD_EINVAL;  // 4 taps x 9 tiles per wave fit the registers at CG = 48 only
+  hipLaunchKernelGGL(posconv_dw_kernel<48>, grid, dim3(256), 0, stream, (const bf16*)x, (const bf16*)dy, B, T, C, pad,
+                     spb, part);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

@@ -395,7 +395,8 @@ def _hubert_feature_encoder_forward(self, input_values):
 class _PosConv(torch.autograd.Function):
     """Grouped conv1d(C, C, K=128, padding=pad, groups) over channels-last x (B, T, C), first T
     outputs (HubertSamePadLayer drops the last): forward and input gradient by the implicit-GEMM
-    HIP kernel (triad_posconv), weight gradient by aten.convolution_backward."""
+    HIP kernel (triad_posconv), weight gradient by triad_posconv_dw (48 channels per group;
+    aten.convolution_backward otherwise)."""
 
     @staticmethod
     def forward(ctx, x, w, bias, groups, pad):
@@ -427,7 +428,16 @@ class _PosConv(torch.autograd.Function):
             dx = torch.empty_like(dyb)
             call("triad_posconv", ptr(dyb), ptr(wtb), None, ptr(dx), B, T, C, G, K - 1 - pad, stream_ptr(xb.device))
             dx = dx.to(ctx.dtypes[0])
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and C // G == 48:
+            # HIP weight gradient: fp32 partials over sample ranges, summed, then [g][j][n][c] -> [g*48+n][c][j]
+            splits = max(1, min(B, 16))
+            part = torch.empty(int(call("triad_posconv_dw_part_bytes", C, G, splits)) // 4, dtype=torch.float32,
+                               device=dyb.device)
+            call("triad_posconv_dw", ptr(xb), ptr(dyb), B, T, C, G, pad, splits, ptr(part), stream_ptr(dyb.device))
+            cg = C // G
+            dw = part.view(splits, -1).sum(0).view(G, K, cg, cg).permute(0, 2, 3, 1).reshape(C, cg, K)
+            dw = dw.to(ctx.dtypes[1])
+        elif ctx.needs_input_grad[1]:
             # the conv's full output has T_full = T + 2*pad - K + 1 steps; the dropped tail gets 0
             t_full = T + 2 * pad - K + 1
             dy_full = torch.zeros(B, t_full, C, dtype=torch.bfloat16, device=dyb.device)
