@@ -14,9 +14,9 @@
 //
 // Workgroup = (group, sample, 208-row time block); 4 waves; wave w owns the 16-row time tiles
 // w, w+4, w+8, w+12 and all CG/16 channel tiles (v_mfma_f32_16x16x32_bf16, fp32 accumulate).
-// B fragments (Wt[g][n][k], k contiguous) come straight from L2, prefetched one k-step ahead:
-// blockIdx.x = group, so consecutive workgroups (dealt round-robin to the 8 XCDs) put only
-// G/8 groups' weights into each XCD's L2.
+// B fragments (Wt[g][n][k], k contiguous) come from 256-deep chunks of the group's weights staged
+// in LDS (two slots, LDS-DMA): blockIdx.x = group, so consecutive workgroups (dealt round-robin
+// to the 8 XCDs) put only G/8 groups' weights into each XCD's L2.
 #include "common.h"
 
 namespace {
@@ -26,6 +26,7 @@ constexpr int MT = 13;        // 16-row time tiles per workgroup (208 rows >= T 
 constexpr int ROWS = MT * 16;
 constexpr int NWAVE = 4;
 constexpr int MT_PER_WAVE = (MT + NWAVE - 1) / NWAVE;  // 4
+constexpr int PC_KC = 256;  // W chunk depth (8 k-steps)
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
@@ -38,6 +39,7 @@ __global__ __launch_bounds__(256) void posconv_kernel(const bf16* __restrict__ x
   constexpr int NKS = KTOT / 32;         // k-steps
   constexpr int WIN = ROWS + KT - 1;     // window rows
   __shared__ __attribute__((aligned(16))) bf16 xwin[WIN * CG];
+  __shared__ __attribute__((aligned(16))) bf16 wl[2 * CG * PC_KC];
 
   const int g = blockIdx.x, b = blockIdx.y, t0 = blockIdx.z * ROWS;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -56,8 +58,6 @@ __global__ __launch_bounds__(256) void posconv_kernel(const bf16* __restrict__ x
   const int r = lane & 15, q = lane >> 4;
   // A fragment of time tile m at k-step s: xwin[(16 m + r) * CG + 32 s + 8 q .. +7]
   const bf16* abase = xwin + r * CG + 8 * q;
-  // B fragment of channel tile n at k-step s: wt[g][16 n + r][32 s + 8 q .. +7]
-  const bf16* bbase = wt + ((size_t)g * CG + r) * KTOT + 8 * q;
 
   f32x4_t acc[MT_PER_WAVE][NT];
 #pragma unroll
@@ -65,25 +65,44 @@ __global__ __launch_bounds__(256) void posconv_kernel(const bf16* __restrict__ x
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[i][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 bcur[NT], bnext[NT];
+  // W chunks (CG rows x PC_KC k, 512-B rows, 16-B chunk c stored at c ^ (row & 15): each
+  // 16-lane group of a ds_read_b128 hits 16 distinct bank slots) stream through two LDS slots
+  // by LDS-DMA, one chunk ahead, shared by the four waves (each wave fetching its own B
+  // fragments from L2 moved 4x the bytes and ran at ~1/5 of the MFMA rate).
+  constexpr int NCH = KTOT / PC_KC, CH_PIECES = CG * PC_KC * 2 / 1024 / NWAVE;  // per wave
+  const bf16* wg = wt + (size_t)g * CG * KTOT;
+  auto stage = [&](int ch, bf16* dst) {
 #pragma unroll
-  for (int n = 0; n < NT; ++n) bcur[n] = *(const bf16x8*)(bbase + (size_t)n * 16 * KTOT);
-  for (int s = 0; s < NKS; ++s) {
-    if (s + 1 < NKS) {
-#pragma unroll
-      for (int n = 0; n < NT; ++n) bnext[n] = *(const bf16x8*)(bbase + (size_t)n * 16 * KTOT + (s + 1) * 32);
+    for (int u = 0; u < CH_PIECES; ++u) {
+      const int piece = wave * CH_PIECES + u, row = piece * 2 + (lane >> 5), pc = lane & 31;
+      glds16(wg + (size_t)row * KTOT + ch * PC_KC + ((pc ^ (row & 15)) << 3), dst + piece * 512);
     }
+  };
+  stage(0, wl);
+  for (int ch = 0; ch < NCH; ++ch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ch + 1 < NCH) stage(ch + 1, wl + ((ch + 1) & 1) * CG * PC_KC);
+    const bf16* wc = wl + (ch & 1) * CG * PC_KC;
+#pragma unroll 2
+    for (int ss = 0; ss < PC_KC / 32; ++ss) {
+      const int s = ch * (PC_KC / 32) + ss;
+      bf16x8 bc[NT];
 #pragma unroll
-    for (int i = 0; i < MT_PER_WAVE; ++i) {
-      const int m = wave + NWAVE * i;
-      if (m < MT) {
-        const bf16x8 a = *(const bf16x8*)(abase + m * 16 * CG + s * 32);
+      for (int n = 0; n < NT; ++n) {
+        const int row = 16 * n + r, c = 4 * ss + q;
+        bc[n] = *(const bf16x8*)(wc + row * PC_KC + ((c ^ (row & 15)) << 3));
+      }
 #pragma unroll
-        for (int n = 0; n < NT; ++n) acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bcur[n], acc[i][n], 0, 0, 0);
+      for (int i = 0; i < MT_PER_WAVE; ++i) {
+        const int m = wave + NWAVE * i;
+        if (m < MT) {
+          const bf16x8 a = *(const bf16x8*)(abase + m * 16 * CG + s * 32);
+#pragma unroll
+          for (int n = 0; n < NT; ++n) acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bc[n], acc[i][n], 0, 0, 0);
+        }
       }
     }
-#pragma unroll
-    for (int n = 0; n < NT; ++n) bcur[n] = bnext[n];
   }
 
   // C/D layout: col = lane & 15, row = 4 * (lane >> 4) + v
