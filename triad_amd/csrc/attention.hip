@@ -14,6 +14,9 @@
 //             dS = P (dP - D), dQ^T += K^T dS^T) and dkv kernel (wave = key tile, key on the
 //             lane: S = Q K^T, dP = dO V^T, dV += P^T dO, dK += dS^T Q); D = rowsum(dO * O) is
 //             formed by the dq kernel (which reads O anyway) and handed to the dkv kernel.
+// Probabilities use the raw v_exp_f32 (__builtin_amdgcn_exp2f; arguments are <= 0 up to rounding,
+// results below 2^-126 flush to 0 -- exp2f's denormal scaling cost 4 more VALU per score in
+// kernels that are VALU-bound on the softmax).
 // LDS rows of 64 bf16 (128 B) are stored with the 16-byte chunk swizzle chunk ^ g((row >> 1) & 7),
 // g(k) = (k >> 1) | ((k & 1) << 2): conflict-free for 32-row ds_read_b128 at one chunk and for the
 // 4-row transposed reads.
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
   for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
-      const float p = exp2f(fmaf(acc[kt][v], c2, -mo));
+      const float p = __builtin_amdgcn_exp2f(fmaf(acc[kt][v], c2, -mo));  // raw v_exp_f32 (arg <= 0)
       acc[kt][v] = p;
       l += p;
     }
@@ -249,7 +252,8 @@ __global__ __launch_bounds__(256, 2) void attn_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       const bool ok = qok && (v & 3) + 8 * (v >> 2) + 4 * h < nv;
-      const float p = ok ? exp2f(fmaf(s[v], c2, -lse2)) : 0.f;
+      const float e = __builtin_amdgcn_exp2f(fmaf(s[v], c2, -lse2));
+      const float p = ok ? e : 0.f;
       const float dpv = DROP ? (tile_bit(w, v, h) ? dp[v] * a.drop_scale : 0.f) : dp[v];
       s[v] = p * (dpv - dl);  // dS
     }
@@ -318,7 +322,8 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_kernel(AttnArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int v = 4 * j + i;
-        const float p = kok ? exp2f(fmaf(s[v], c2, -ls[i])) : 0.f;
+        const float e = __builtin_amdgcn_exp2f(fmaf(s[v], c2, -ls[i]));
+        const float p = kok ? e : 0.f;
         if (DROP) {
           const float m = tile_bit(w, v, h) ? a.drop_scale : 0.f;
           s[v] = p * m;                 // dropped probability (dV operand)
