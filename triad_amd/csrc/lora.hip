@@ -63,10 +63,18 @@ __global__ __launch_bounds__(1024) void slab_sum_kernel(const float* __restrict_
   __shared__ float part[16][64];
   const int el = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const long long e = (long long)blockIdx.x * 64 + el;
-  float acc = 0.f;
-  if (e < n)
-    for (int i = sl; i < S; i += 16) acc += slab[i * n + e];
-  part[sl][el] = acc;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // independent chains: loads in flight together
+  if (e < n) {
+    int i = sl;
+    for (; i + 48 < S; i += 64) {
+      a0 += slab[i * n + e];
+      a1 += slab[(i + 16) * n + e];
+      a2 += slab[(i + 32) * n + e];
+      a3 += slab[(i + 48) * n + e];
+    }
+    for (; i < S; i += 16) a0 += slab[i * n + e];
+  }
+  part[sl][el] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (sl == 0 && e < n) {
     float t = 0.f;

@@ -285,10 +285,20 @@ __global__ __launch_bounds__(1024) void colsum_reduce_kernel(const float* __rest
   __shared__ float red[16][64];
   const int el = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const long long c = (long long)blockIdx.x * 64 + el;
-  float acc = 0.f;
-  if (c < cols)
-    for (int i = sl; i < S; i += 16) acc += part[(size_t)i * cols + c];
-  red[sl][el] = acc;
+  // four independent partial sums: the loads of a thread's slices are in flight together
+  // (one dependent chain of S / 16 loads made this a latency-bound 16 us launch)
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < cols) {
+    int i = sl;
+    for (; i + 48 < S; i += 64) {
+      a0 += part[(size_t)i * cols + c];
+      a1 += part[(size_t)(i + 16) * cols + c];
+      a2 += part[(size_t)(i + 32) * cols + c];
+      a3 += part[(size_t)(i + 48) * cols + c];
+    }
+    for (; i < S; i += 16) a0 += part[(size_t)i * cols + c];
+  }
+  red[sl][el] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (sl == 0 && c < cols) {
     float t = 0.f;
@@ -305,9 +315,16 @@ __global__ __launch_bounds__(256) void sum_slabs_kernel(const float* __restrict_
                                                         void* __restrict__ out) {
   const float alpha = alpha_p ? *alpha_p : 1.f;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int i = 0; i < nslab; ++i) s += slabs[(size_t)i * n + e];
-    s *= alpha;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // independent chains: loads in flight together
+    int i = 0;
+    for (; i + 3 < nslab; i += 4) {
+      s0 += slabs[(size_t)i * n + e];
+      s1 += slabs[(size_t)(i + 1) * n + e];
+      s2 += slabs[(size_t)(i + 2) * n + e];
+      s3 += slabs[(size_t)(i + 3) * n + e];
+    }
+    for (; i < nslab; ++i) s0 += slabs[(size_t)i * n + e];
+    float s = ((s0 + s1) + (s2 + s3)) * alpha;
     if (out_bf16) ((bf16*)out)[e] = (bf16)s;
     else ((float*)out)[e] = s;
   }
