@@ -195,3 +195,37 @@ def test_gelu_table_every_bf16_pattern(p):
     v.backward(dv)
     dg = torch.where(keep, (dv.float() * s).to(torch.bfloat16), torch.zeros_like(dv))
     torch.testing.assert_close(ud.grad, torch.ops.aten.gelu_backward(dg, u), rtol=0, atol=0, equal_nan=True)
+
+
+def test_fused_qkv_self_attention_matches_module():
+    """postln.self_attention (q / k / v as one projection GEMM, linear._QKVFn, and the fused-qkv
+    HIP attention with dropout) against the HubertAttention module itself (three projections,
+    the same HIP attention kernels via the 'triad' interface) on the same dropout masks: values
+    and gradients of the input and of every projection parameter."""
+    from triad_amd import model as Mdl, postln
+    torch.manual_seed(0)
+    over = dict(hidden_size=768, num_hidden_layers=1, num_attention_heads=12, intermediate_size=3072,
+                attention_dropout=0.1, mask_time_prob=0.0)
+    hub = Mdl.hubert_execution_tweaks(Mdl._hf_model("HubertModel", "none/none", over)).to(dev)
+    attn = hub.encoder.layers[0].attention.train()
+    x0 = (torch.randn(64, 128, 768, device=dev)).to(torch.bfloat16)
+    gy = torch.randn(64, 128, 768, device=dev)
+
+    def run(fn):
+        attn.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        torch.manual_seed(5)  # attention-dropout seeds come from torch's generator
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = fn(x)
+        (y.float() * gy).sum().backward()
+        return y.detach().float(), x.grad.float(), {n: p.grad.float().clone() for n, p in attn.named_parameters()}
+
+    y_m, gx_m, g_m = run(lambda x: attn(x)[0])
+    y_f, gx_f, g_f = run(lambda x: postln.self_attention(attn, x))
+    assert _rel(y_f, y_m) < 1e-2
+    assert _rel(gx_f, gx_m) < 2e-2
+    assert set(g_f) == set(g_m) and len(g_m) == 8
+    for n in g_m:
+        if n == "k_proj.bias":  # softmax shift invariance: exactly 0 up to rounding noise
+            continue
+        assert _rel(g_f[n], g_m[n]) < 2e-2, (n, _rel(g_f[n], g_m[n]))

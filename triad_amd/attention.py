@@ -104,31 +104,36 @@ class _Attention(torch.autograd.Function):
 
 class _AttentionQKV(torch.autograd.Function):
     """qkv: (B, N, 3*H*64) bf16 output of a fused projection (q | k | v, heads inside each) ->
-    O (B, N, H*64); the backward returns d qkv as one tensor."""
+    O (B, N, H*64); dropout p > 0 on the probabilities as in _Attention; the backward returns
+    d qkv as one tensor (the fused projection's gradient, no per-view scatter)."""
 
     @staticmethod
-    def forward(ctx, qkv, heads, scale):
+    def forward(ctx, qkv, heads, scale, p=0.0):
         B, N, C3 = qkv.shape
         x = qkv.contiguous().view(B, N, 3, heads, HEAD_DIM)
         q, k, v = x[:, :, 0], x[:, :, 1], x[:, :, 2]
-        out, lse = _fwd(q, k, v, scale)
-        ctx.save_for_backward(x, out, lse)
+        drop = (*_dropmask(B, heads, N, p, qkv.device), float(p)) if p > 0.0 else None
+        out, lse = _fwd(q, k, v, scale, drop)
+        ctx.save_for_backward(x, out, lse, *(drop[:2] if drop else ()))
         ctx.scale = float(scale)
+        ctx.p = float(p)
         return out.view(B, N, heads * HEAD_DIM)
 
     @staticmethod
     def backward(ctx, dout):
-        x, out, lse = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        x, out, lse = saved[:3]
+        drop = (saved[3], saved[4], ctx.p) if ctx.p > 0.0 else None
         B, N = x.shape[0], x.shape[1]
-        g = _bwd(x[:, :, 0], x[:, :, 1], x[:, :, 2], out, lse, dout.view(out.shape), ctx.scale)
-        return g.view(B, N, -1), None, None
+        g = _bwd(x[:, :, 0], x[:, :, 1], x[:, :, 2], out, lse, dout.view(out.shape), ctx.scale, drop)
+        return g.view(B, N, -1), None, None, None
 
 
-def attention_qkv(qkv, heads, scale=None):
+def attention_qkv(qkv, heads, scale=None, dropout=0.0):
     """Fused-projection attention: qkv (B, N, 3*heads*64) bf16 -> (B, N, heads*64)."""
     if scale is None:
         scale = 1.0 / math.sqrt(HEAD_DIM)
-    return _AttentionQKV.apply(qkv, heads, scale)
+    return _AttentionQKV.apply(qkv, heads, scale, float(dropout))
 
 
 def attention_bnhd(q, k, v, scale=None, dropout=0.0):

@@ -72,6 +72,54 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+class _QKVFn(torch.autograd.Function):
+    """y = x [Wq; Wk; Wv]^T + [bq; bk; bv]: a self-attention's three projections of the same
+    input as ONE GEMM each way. Forward: one N = 3E GEMM (columns identical to the three
+    autocast F.linear calls: bf16 operands, fp32 accumulation, bf16 out); backward: dX as one
+    K = 3E GEMM (autograd would sum three dX products with two extra bf16 adds), dW as one
+    split-K GEMM over [3E][K] and db as one column sum, split back per projection."""
+
+    @staticmethod
+    def forward(ctx, x, wq, bq, wk, bk, wv, bv):
+        xb = x.to(torch.bfloat16)
+        wb = torch.cat([wq, wk, wv]).to(torch.bfloat16)  # = cat of the per-weight casts, bit for bit
+        bb = None if bq is None else torch.cat([bq, bk, bv]).to(torch.bfloat16)
+        ctx.save_for_backward(xb, wb)
+        ctx.meta = (x.dtype, wq.dtype, None if bq is None else bq.dtype, (wq.shape[0], wk.shape[0], wv.shape[0]))
+        return F.linear(xb, wb, bb)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb = ctx.saved_tensors
+        x_dtype, w_dtype, b_dtype, sizes = ctx.meta
+        O, K = wb.shape
+        dy2 = dy.reshape(-1, O).to(torch.bfloat16).contiguous()
+        x2 = xb.reshape(-1, K)
+        if x2.stride(1) != 1 or x2.stride(0) != K:
+            x2 = x2.contiguous()
+        dx = torch.mm(dy2, wb).view(*xb.shape).to(x_dtype) if ctx.needs_input_grad[0] else None
+        dws = [None] * 3
+        if any(ctx.needs_input_grad[i] for i in (1, 3, 5)):
+            dws = [t.to(w_dtype) for t in weight_grad(dy2, x2).split(sizes)]
+        dbs = [None] * 3
+        if b_dtype is not None and any(ctx.needs_input_grad[i] for i in (2, 4, 6)):
+            from .ops import colsum
+            db = colsum(dy2, torch.bfloat16 if b_dtype == torch.bfloat16 else torch.float32).to(b_dtype)
+            dbs = list(db.split(sizes))
+        return dx, dws[0], dbs[0], dws[1], dbs[1], dws[2], dbs[2]
+
+
+def qkv_eligible(q: nn.Linear, k: nn.Linear, v: nn.Linear, x: torch.Tensor) -> bool:
+    """The fused projection applies where TriadLinear would to each of the three."""
+    return (all(_eligible(m, x) for m in (q, k, v)) and q.in_features == k.in_features == v.in_features
+            and (q.bias is None) == (k.bias is None) == (v.bias is None))
+
+
+def qkv_projection(q: nn.Linear, k: nn.Linear, v: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    """[q(x) | k(x) | v(x)] along the last dim (bf16, autocast numerics) via _QKVFn."""
+    return _QKVFn.apply(x, q.weight, q.bias, k.weight, k.bias, v.weight, v.bias)
+
+
 def _eligible(mod: nn.Linear, x: torch.Tensor) -> bool:
     if not (x.is_cuda and mod.weight.requires_grad and torch.is_autocast_enabled("cuda")
             and torch.get_autocast_dtype("cuda") == torch.bfloat16):

@@ -147,12 +147,29 @@ def dropout_keep(n, p, seed, device):
     return out
 
 
+def self_attention(attn, x):
+    """transformers HubertAttention.forward (self-attention, no mask) with q / k / v as ONE
+    projection GEMM (linear.qkv_projection) and the HIP attention kernels on strided views of
+    its output; anything the fused form does not cover runs the module itself."""
+    from . import attention as A
+    from .linear import qkv_eligible, qkv_projection
+    B, N, E = x.shape
+    H, d = attn.num_heads, attn.head_dim
+    if not (qkv_eligible(attn.q_proj, attn.k_proj, attn.v_proj, x) and attn.q_proj.out_features == E
+            and attn.k_proj.out_features == E and attn.v_proj.out_features == E and H * d == E
+            and A.supported(x, N, d) and not getattr(attn, "is_causal", False)):
+        return attn(x)[0]
+    p = float(attn.dropout) if attn.training else 0.0
+    o = A.attention_qkv(qkv_projection(attn.q_proj, attn.k_proj, attn.v_proj, x), H, attn.scaling, dropout=p)
+    return attn.out_proj(o)
+
+
 def fused_layer(layer, res, res_b, seeds):
     """One HubertEncoderLayer (post-LN) on (fp32 residual, its bf16 copy) -> the same pair."""
     p_h = layer.dropout.p if layer.training else 0.0
     ff = layer.feed_forward
     p_a = ff.intermediate_dropout.p if layer.training else 0.0
-    a = layer.attention(res_b)[0]
+    a = self_attention(layer.attention, res_b)
     h1, h1b = drop_add_ln(res, a, layer.layer_norm, p_h, seeds())
     v = gelu_drop(ff.intermediate_dense(h1b), p_a, seeds())
     f = ff.output_dense(v)
