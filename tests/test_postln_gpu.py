@@ -197,17 +197,22 @@ def test_gelu_table_every_bf16_pattern(p):
     torch.testing.assert_close(ud.grad, torch.ops.aten.gelu_backward(dg, u), rtol=0, atol=0, equal_nan=True)
 
 
-def test_fused_qkv_self_attention_matches_module():
+@pytest.mark.parametrize("family", ["hubert", "distilbert"])
+def test_fused_qkv_self_attention_matches_module(family):
     """postln.self_attention (q / k / v as one projection GEMM, linear._QKVFn, and the fused-qkv
-    HIP attention with dropout) against the HubertAttention module itself (three projections,
-    the same HIP attention kernels via the 'triad' interface) on the same dropout masks: values
-    and gradients of the input and of every projection parameter."""
+    HIP attention with dropout) against the HubertAttention / DistilBertSelfAttention module
+    itself (three projections, the same HIP attention kernels via the 'triad' interface) on the
+    same dropout masks: values and gradients of the input and of every projection parameter."""
     from triad_amd import model as Mdl, postln
     torch.manual_seed(0)
-    over = dict(hidden_size=768, num_hidden_layers=1, num_attention_heads=12, intermediate_size=3072,
-                attention_dropout=0.1, mask_time_prob=0.0)
-    hub = Mdl.hubert_execution_tweaks(Mdl._hf_model("HubertModel", "none/none", over)).to(dev)
-    attn = hub.encoder.layers[0].attention.train()
+    if family == "hubert":
+        over = dict(hidden_size=768, num_hidden_layers=1, num_attention_heads=12, intermediate_size=3072,
+                    attention_dropout=0.1, mask_time_prob=0.0)
+        hub = Mdl.hubert_execution_tweaks(Mdl._hf_model("HubertModel", "none/none", over)).to(dev)
+        attn = hub.encoder.layers[0].attention.train()
+    else:
+        enc = Mdl._hf_model("DistilBertModel", "none/none", dict(n_layers=1, attention_dropout=0.1)).to(dev)
+        attn = enc.transformer.layer[0].attention.train()
     x0 = (torch.randn(64, 128, 768, device=dev)).to(torch.bfloat16)
     gy = torch.randn(64, 128, 768, device=dev)
 
@@ -226,6 +231,6 @@ def test_fused_qkv_self_attention_matches_module():
     assert _rel(gx_f, gx_m) < 2e-2
     assert set(g_f) == set(g_m) and len(g_m) == 8
     for n in g_m:
-        if n == "k_proj.bias":  # softmax shift invariance: exactly 0 up to rounding noise
+        if n in ("k_proj.bias", "k_lin.bias"):  # softmax shift invariance: exactly 0 up to rounding noise
             continue
         assert _rel(g_f[n], g_m[n]) < 2e-2, (n, _rel(g_f[n], g_m[n]))

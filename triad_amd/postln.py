@@ -147,21 +147,29 @@ def dropout_keep(n, p, seed, device):
     return out
 
 
+def _attn_parts(attn):
+    """(q, k, v, out, heads, head_dim, scaling, dropout p) of a transformers HubertAttention or
+    DistilBertSelfAttention."""
+    if hasattr(attn, "q_proj"):
+        return (attn.q_proj, attn.k_proj, attn.v_proj, attn.out_proj, attn.num_heads, attn.head_dim, attn.scaling,
+                float(attn.dropout))
+    return (attn.q_lin, attn.k_lin, attn.v_lin, attn.out_lin, attn.n_heads, attn.attention_head_size, attn.scaling,
+            float(attn.dropout.p))
+
+
 def self_attention(attn, x):
-    """transformers HubertAttention.forward (self-attention, no mask) with q / k / v as ONE
-    projection GEMM (linear.qkv_projection) and the HIP attention kernels on strided views of
-    its output; anything the fused form does not cover runs the module itself."""
+    """transformers HubertAttention / DistilBertSelfAttention forward (self-attention, no mask)
+    with q / k / v as ONE projection GEMM (linear.qkv_projection) and the fused-qkv HIP
+    attention kernels on its output; anything the fused form does not cover runs the module."""
     from . import attention as A
     from .linear import qkv_eligible, qkv_projection
     B, N, E = x.shape
-    H, d = attn.num_heads, attn.head_dim
-    if not (qkv_eligible(attn.q_proj, attn.k_proj, attn.v_proj, x) and attn.q_proj.out_features == E
-            and attn.k_proj.out_features == E and attn.v_proj.out_features == E and H * d == E
+    q, k, v, o, H, d, scaling, p = _attn_parts(attn)
+    if not (qkv_eligible(q, k, v, x) and q.out_features == k.out_features == v.out_features == E == H * d
             and A.supported(x, N, d) and not getattr(attn, "is_causal", False)):
         return attn(x)[0]
-    p = float(attn.dropout) if attn.training else 0.0
-    o = A.attention_qkv(qkv_projection(attn.q_proj, attn.k_proj, attn.v_proj, x), H, attn.scaling, dropout=p)
-    return attn.out_proj(o)
+    p = p if attn.training else 0.0
+    return o(A.attention_qkv(qkv_projection(q, k, v, x), H, scaling, dropout=p))
 
 
 def fused_layer(layer, res, res_b, seeds):
@@ -228,7 +236,7 @@ def install_fused_encoder(hubert):
 def fused_distilbert_block(block, res, res_b, seeds):
     ffn = block.ffn
     p = ffn.dropout.p if block.training else 0.0
-    a = block.attention(res_b)[0]
+    a = self_attention(block.attention, res_b)
     h1, h1b = drop_add_ln(res, a, block.sa_layer_norm, 0.0, 0)
     v = gelu_drop(ffn.lin1(h1b), 0.0, 0)
     return drop_add_ln(h1, ffn.lin2(v), block.output_layer_norm, p, seeds())
