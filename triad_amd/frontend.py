@@ -435,7 +435,9 @@ class _PosConv(torch.autograd.Function):
                                device=dyb.device)
             call("triad_posconv_dw", ptr(xb), ptr(dyb), B, T, C, G, pad, splits, ptr(part), stream_ptr(dyb.device))
             cg = C // G
-            dw = part.view(splits, -1).sum(0).view(G, K, cg, cg).permute(0, 2, 3, 1).reshape(C, cg, K)
+            dsum = torch.empty(part.numel() // splits, dtype=torch.float32, device=dyb.device)
+            call("triad_sum_slabs", ptr(part), splits, dsum.numel(), None, 0, ptr(dsum), stream_ptr(dyb.device))
+            dw = dsum.view(G, K, cg, cg).permute(0, 2, 3, 1).reshape(C, cg, K)
             dw = dw.to(ctx.dtypes[1])
         elif ctx.needs_input_grad[1]:
             # the conv's full output has T_full = T + 2*pad - K + 1 steps; the dropped tail gets 0
@@ -448,7 +450,8 @@ class _PosConv(torch.autograd.Function):
                                                      False, [0, 0], G, [False, True, False])[1]
             dw = dw.squeeze(2).to(ctx.dtypes[1])
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = torch.sum(dyb.view(B * T, C), 0, dtype=torch.float32).to(ctx.dtypes[2])
+            from .ops import colsum
+            db = colsum(dyb.view(B * T, C), torch.float32).to(ctx.dtypes[2])
         return dx, dw, db, None, None
 
 
