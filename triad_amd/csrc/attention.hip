@@ -129,22 +129,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
   char* vl = lds + NKT * 32 * 128;
   const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, ql = lane & 31;
-  load_rows2<NKT>(kl, a.k + b * a.k_sB + hh * HD, a.k_sN, vl, a.v + b * a.v_sB + hh * HD, a.v_sN, a.N);
-  __syncthreads();
+  // this wave's query fragments are requested before the block's K / V staging, so their
+  // latency overlaps it (issued after the barrier they were a second exposed round trip)
   const int qt = blockIdx.x * 4 + wave;
-  if (qt * 32 >= a.N) return;
   const int q = qt * 32 + ql;
   const bool qok = q < a.N;
-
   bf16x8 qf[4];
   {
     const bf16* qp = a.q + b * a.q_sB + (long long)(qok ? q : 0) * a.q_sN + hh * HD + 8 * h;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      qf[s] = *(const bf16x8*)(qp + 16 * s);
-      if (!qok) qf[s] = (bf16x8){};
-    }
+    for (int s = 0; s < 4; ++s) qf[s] = qok ? *(const bf16x8*)(qp + 16 * s) : (bf16x8){};
   }
+  load_rows2<NKT>(kl, a.k + b * a.k_sB + hh * HD, a.k_sN, vl, a.v + b * a.v_sB + hh * HD, a.v_sN, a.N);
+  __syncthreads();
+  if (qt * 32 >= a.N) return;
   f32x16 acc[NKT];
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
@@ -212,14 +210,10 @@ __global__ __launch_bounds__(256, 2) void attn_dq_kernel(AttnArgs a) {
   char* vl = lds + NKT * 32 * 128;
   const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, ql = lane & 31;
-  load_rows2<NKT>(kl, a.k + b * a.k_sB + hh * HD, a.k_sN, vl, a.v + b * a.v_sB + hh * HD, a.v_sN, a.N);
-  __syncthreads();
   const int qt = blockIdx.x * 4 + wave;
-  if (qt * 32 >= a.N) return;
   const int q = qt * 32 + ql;
-  const bool qok = q < a.N;
-  bf16x8 qf[4], df[4];
-  float dl = 0.f;  // D = rowsum(dO * O) of this query: the lane's 32 dims + the other half's
+  const bool qok = q < a.N;  // (the wave's global loads below are issued before the barrier)
+  bf16x8 qf[4], df[4], ov[4];
   {
     const long long qq = qok ? q : 0;
     const bf16* qp = a.q + b * a.q_sB + qq * a.q_sN + hh * HD + 8 * h;
@@ -229,15 +223,21 @@ __global__ __launch_bounds__(256, 2) void attn_dq_kernel(AttnArgs a) {
     for (int s = 0; s < 4; ++s) {
       qf[s] = qok ? *(const bf16x8*)(qp + 16 * s) : (bf16x8){};
       df[s] = qok ? *(const bf16x8*)(dp + 16 * s) : (bf16x8){};
-      const bf16x8 ov = qok ? *(const bf16x8*)(op + 16 * s) : (bf16x8){};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) dl = fmaf((float)df[s][i], (float)ov[i], dl);
+      ov[s] = qok ? *(const bf16x8*)(op + 16 * s) : (bf16x8){};
     }
   }
+  const float lse2 = qok ? a.lse[(long long)bh * a.N + q] * LOG2E : 0.f;
+  load_rows2<NKT>(kl, a.k + b * a.k_sB + hh * HD, a.k_sN, vl, a.v + b * a.v_sB + hh * HD, a.v_sN, a.N);
+  __syncthreads();
+  if (qt * 32 >= a.N) return;
+  float dl = 0.f;  // D = rowsum(dO * O) of this query: the lane's 32 dims + the other half's
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dl = fmaf((float)df[s][i], (float)ov[s][i], dl);
   dl += __shfl_xor(dl, 32);
   if (qok && h == 0) a.delta[(long long)bh * a.N + q] = dl;  // for the dkv kernel (launched after)
   const float c2 = a.scale * LOG2E;
-  const float lse2 = qok ? a.lse[(long long)bh * a.N + q] * LOG2E : 0.f;
   f32x16 g0 = {}, g1 = {};
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
@@ -280,18 +280,10 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_kernel(AttnArgs a) {
   char* dl_ = lds + NQT * 32 * 128;
   const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, kl = lane & 31;
-  load_rows2<NQT>(ql_, a.q + b * a.q_sB + hh * HD, a.q_sN, dl_, a.dout + b * a.do_sB + hh * HD, a.do_sN, a.N);
-  for (int i = threadIdx.x; i < NQT * 32; i += blockDim.x) {
-    const bool ok = i < a.N;
-    stat[0][i] = ok ? a.lse[(long long)bh * a.N + i] * LOG2E : INFINITY;  // p = 0 past N
-    stat[1][i] = ok ? a.delta[(long long)bh * a.N + i] : 0.f;
-  }
-  __syncthreads();
   const int kt = blockIdx.x * 4 + wave;
-  if (kt * 32 >= a.N) return;
   const int key = kt * 32 + kl;
   const bool kok = key < a.N;
-  bf16x8 kf[4], vf[4];
+  bf16x8 kf[4], vf[4];  // requested before the block's Q / dO staging (latency overlapped)
   {
     const long long kk = kok ? key : 0;
     const bf16* kp = a.k + b * a.k_sB + kk * a.k_sN + hh * HD + 8 * h;
@@ -302,6 +294,14 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_kernel(AttnArgs a) {
       vf[s] = kok ? *(const bf16x8*)(vp + 16 * s) : (bf16x8){};
     }
   }
+  load_rows2<NQT>(ql_, a.q + b * a.q_sB + hh * HD, a.q_sN, dl_, a.dout + b * a.do_sB + hh * HD, a.do_sN, a.N);
+  for (int i = threadIdx.x; i < NQT * 32; i += blockDim.x) {
+    const bool ok = i < a.N;
+    stat[0][i] = ok ? a.lse[(long long)bh * a.N + i] * LOG2E : INFINITY;  // p = 0 past N
+    stat[1][i] = ok ? a.delta[(long long)bh * a.N + i] : 0.f;
+  }
+  __syncthreads();
+  if (kt * 32 >= a.N) return;
   const float c2 = a.scale * LOG2E;
   f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
 #pragma unroll 1
