@@ -74,6 +74,9 @@ class TriadTrainer:
                  av_weight_start=0.8, av_weight_end=0.5, global_negatives=False, bf16_weights=None):
         self.model = model
         self.device = torch.device(device)
+        if self.device.type == "cuda":  # committed library-GEMM solution choices (gemm_tuning.py)
+            from .gemm_tuning import load_gemm_tuning
+            load_gemm_tuning(self.device)
         self.grad_accum = gradient_accumulation_steps
         self.unfreeze = dict(audio=unfreeze_audio_step, text=unfreeze_text_step, vit=unfreeze_vit_step)
         self.av_weight_start, self.av_weight_end = av_weight_start, av_weight_end
