@@ -5,6 +5,11 @@ bench.py (TRIAD_PROFILE_MARK=1) launches one l2norm_rows_kernel right before its
 timed steps. Writes per-kernel ms/step, calls/step and the total, so MIOpen's one-time
 algorithm search in the warmup does not drown the profile.
 
+Also writes <out>_by_grid.csv: every launch of the whole trace for the §8 head kernels
+(pairsim / tile_gemm) grouped by (kernel, grid size) -- the AV and TV forward launches share a
+kernel name, so this is where the AV launch's own average duration is read (bench.py's
+roofline.avg_ms names the same launch).
+
 usage: python tools/trace_summary.py <kernel_trace.csv> <steps> <out.csv>
 """
 import csv
@@ -42,6 +47,17 @@ def main(path, steps, out):
         w.writerow(["TOTAL_KERNEL_TIME", "", round(total / steps, 3), "", 100])
         w.writerow(["WALL_FIRST_TO_LAST", "", round((t_last - t_first) / 1e6 / steps, 3), "", ""])
     print(f"kernel time {total / steps:.2f} ms/step over {steps} steps; wall {(t_last - t_first) / 1e6 / steps:.2f} ms/step")
+    grid_k = "Grid_Size" if "Grid_Size" in rows[0] else None
+    if grid_k:
+        by = defaultdict(list)
+        for r in rows:
+            if "pairsim" in r[name_k] or "tile_gemm" in r[name_k]:
+                by[(r[name_k][:120], r[grid_k])].append((int(r[e_k]) - int(r[s_k])) / 1e6)
+        with open(out.replace(".csv", "_by_grid.csv"), "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["kernel", "grid_size", "launches", "avg_ms", "min_ms", "max_ms"])
+            for (k, g), d in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+                w.writerow([k, g, len(d), round(sum(d) / len(d), 4), round(min(d), 4), round(max(d), 4)])
 
 
 if __name__ == "__main__":
