@@ -378,16 +378,18 @@ __global__ __launch_bounds__(256, 2) void attn_dkv_kernel(AttnArgs a) {
 
 // keep bits of the attention-probability dropout in both layouts (AttnArgs::wq / wk): bit of
 // (bh, q, key) = element e = (bh N + q) N + key of the (B H, N, N) probability tensor.
-// Block = one 32 x 32 (query tile, key tile) of one (sample, head): 32 threads hash their query
-// row's pairs into its wq word, the words meet in LDS and 32 threads transpose them into wk.
-__global__ __launch_bounds__(64) void attn_dropmask_kernel(int N, int nkt, unsigned seed, unsigned thr,
-                                                           unsigned* __restrict__ wq, unsigned* __restrict__ wk) {
-  __shared__ unsigned words[32];
-  const int kt = blockIdx.x, qt = blockIdx.y;
-  const long long bh = blockIdx.z;
-  const int t = threadIdx.x;
-  if (t < 32) {
-    const int q = qt * 32 + t;
+// Block = one 32-query row band (query tile qt) of one (sample, head), all key tiles: thread
+// (row r, key tile kt) hashes its 16 element pairs into the wq word, the band's words meet in
+// LDS and thread (key row j, key tile kt) gathers bit j of the 32 words of tile kt into the wk
+// word of key kt * 32 + j (query bits of tile qt). (One 64-thread block per 32 x 32 tile, 32
+// threads busy per phase, made this a 90 us launch at HuBERT's shape.)
+__global__ __launch_bounds__(256) void attn_dropmask_kernel(int N, int nkt, unsigned seed, unsigned thr,
+                                                            unsigned* __restrict__ wq, unsigned* __restrict__ wk) {
+  __shared__ unsigned words[MAX_KT][33];
+  const int qt = blockIdx.x;
+  const long long bh = blockIdx.y;
+  for (int t = threadIdx.x; t < 32 * nkt; t += 256) {
+    const int r = t & 31, kt = t >> 5, q = qt * 32 + r;
     unsigned bits = 0u;
     if (q < N) {
       const unsigned long long e0 = (unsigned long long)((bh * N + q) * N + kt * 32);
@@ -397,21 +399,23 @@ __global__ __launch_bounds__(64) void attn_dropmask_kernel(int N, int nkt, unsig
       const int off = (int)(e0 & 1);
       unsigned long long stream = 0ull;  // bit i = element e0 - off + i
       const int npairs = (ncol + off + 1) >> 1;
-      for (int i = 0; i < npairs; ++i) stream |= (unsigned long long)keep_pair(p0 + i, seed, thr) << (2 * i);
+#pragma unroll
+      for (int i = 0; i < 17; ++i)  // constant shifts (npairs <= 17)
+        if (i < npairs) stream |= (unsigned long long)keep_pair(p0 + i, seed, thr) << (2 * i);
       bits = (unsigned)(stream >> off);
       if (ncol < 32) bits &= (1u << ncol) - 1u;
       wq[(bh * N + q) * nkt + kt] = bits;
     }
-    words[t] = bits;
+    words[kt][r] = bits;
   }
   __syncthreads();
-  if (t >= 32) {
-    const int j = t - 32;  // key row kt * 32 + j: bit i = query qt * 32 + i
+  for (int t = threadIdx.x; t < 32 * nkt; t += 256) {
+    const int j = t & 31, kt = t >> 5;  // key row kt * 32 + j: bit i = query qt * 32 + i
     const int key = kt * 32 + j;
     if (key < N) {
       unsigned w = 0u;
 #pragma unroll
-      for (int i = 0; i < 32; ++i) w |= ((words[i] >> j) & 1u) << i;
+      for (int i = 0; i < 32; ++i) w |= ((words[kt][i] >> j) & 1u) << i;
       wk[(bh * N + key) * nkt + qt] = w;
     }
   }
@@ -427,7 +431,7 @@ int triad_attn_dropmask(int B, int H, int N, float p, unsigned seed, unsigned* w
   if (B <= 0 || H <= 0 || N <= 0 || N > MAX_KT * 32 || p < 0.f || p >= 1.f || (long long)B * H > 65535)
     return TRIAD_EINVAL;
   const int nkt = (N + 31) / 32;
-  hipLaunchKernelGGL(attn_dropmask_kernel, dim3(nkt, nkt, B * H), dim3(64), 0, stream, N, nkt, seed,
+  hipLaunchKernelGGL(attn_dropmask_kernel, dim3(nkt, B * H), dim3(256), 0, stream, N, nkt, seed,
                      triad_drop_thr(p), wq, wk);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
