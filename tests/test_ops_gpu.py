@@ -285,3 +285,41 @@ def test_colsum_matches_torch(rows, cols):
     assert float((got.double() - ref).abs().max()) <= 1e-5 * float(x.double().abs().sum(0).max()) + 1e-6
     gb = ops.colsum(x, torch.bfloat16)
     assert gb.dtype == torch.bfloat16 and torch.allclose(gb.float(), got, rtol=8e-3, atol=1e-2)
+
+
+def test_side_stream_weight_grads_bit_identical():
+    """Weight gradients of bf16 (mixed-precision shadow) Linear / fused-qkv weights computed on
+    the side stream (linear.on_side_stream, joined at the end of the backward pass) equal the
+    in-stream ones bit for bit, with a long dependent backward chain behind each dW."""
+    from triad_amd import linear as L
+    torch.manual_seed(3)
+    layers = torch.nn.ModuleList([torch.nn.Linear(768, 768) for _ in range(6)]).to(dev)
+    qkv = [torch.nn.Linear(768, 768).to(dev) for _ in range(3)]
+    for m in list(layers) + qkv:
+        m.weight.data = m.weight.data.to(torch.bfloat16)
+    L.install_fast_linear(layers)
+    x0 = torch.randn(64, 128, 768, device=dev)
+
+    def run(side):
+        L.SIDE_STREAM_DW = side
+        for m in list(layers) + qkv:
+            m.weight.grad = None
+            m.bias.grad = None
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            h = L.qkv_projection(*qkv, x)
+            h = h[..., :768] + h[..., 768:1536] * 0.5 + h[..., 1536:] * 0.25
+            for m in layers:
+                h = torch.nn.functional.gelu(m(h))
+        h.float().square().mean().backward()
+        return [m.weight.grad.clone() for m in list(layers) + qkv], x.grad.clone()
+
+    try:
+        g_main, gx_main = run(False)
+        g_side, gx_side = run(True)
+    finally:
+        L.SIDE_STREAM_DW = True
+    assert all(a.dtype == torch.bfloat16 for a in g_side)
+    for a, b in zip(g_side, g_main):
+        assert torch.equal(a, b)
+    assert torch.equal(gx_side, gx_main)

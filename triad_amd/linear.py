@@ -12,6 +12,8 @@ Numerics equal autocast's F.linear: bf16 operands, fp32 accumulation, bf16 dX / 
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -42,6 +44,57 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return dw
 
 
+# ---- weight gradients on a side stream ------------------------------------------------------
+# A layer's dW does not feed the rest of the backward, so it runs on a second stream beside the
+# next layers' dX GEMMs and (HBM-bound) elementwise passes. Only for bf16 (mixed-precision
+# shadow) weights whose .grad is still empty: autograd then just stores the tensor (no kernel on
+# the main stream reads it); the main stream waits for the side stream at the end of the
+# backward pass (autograd callback), before anything can read a gradient.
+_SIDE = {}
+_JOIN_QUEUED = set()
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def _join(dev):
+    def cb():
+        _JOIN_QUEUED.discard(dev.index)
+        torch.cuda.current_stream(dev).wait_stream(_side_stream(dev))
+    return cb
+
+
+def side_stream_ok(w: torch.Tensor) -> bool:
+    return (SIDE_STREAM_DW and w.is_cuda and w.dtype == torch.bfloat16 and w.grad is None
+            and torch._C._current_graph_task_id() != -1)
+
+
+def on_side_stream(fn, inputs):
+    """Run fn() on the device's side stream after the work queued so far; `inputs` (produced on
+    the main stream) are kept alive for it, the outputs are recorded for the main stream."""
+    dev = inputs[0].device
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        outs = fn()
+    for t in inputs:
+        t.record_stream(side)
+    for o in (outs if isinstance(outs, (list, tuple)) else (outs,)):
+        o.record_stream(main)
+    if dev.index not in _JOIN_QUEUED:
+        _JOIN_QUEUED.add(dev.index)
+        torch.autograd.Variable._execution_engine.queue_callback(_join(dev))
+    return outs
+
+
+SIDE_STREAM_DW = os.environ.get("TRIAD_SIDE_STREAM_DW", "1") != "0"
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
@@ -50,6 +103,7 @@ class _LinearFn(torch.autograd.Function):
         bb = None if b is None else b.to(torch.bfloat16)
         ctx.save_for_backward(xb, wb)
         ctx.meta = (x.dtype, w.dtype, None if b is None else b.dtype)
+        ctx.w_ref = w
         return F.linear(xb, wb, bb)
 
     @staticmethod
@@ -65,7 +119,10 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy2, wb).view(*xb.shape).to(x_dtype)
         if ctx.needs_input_grad[1]:
-            dw = weight_grad(dy2, x2).to(w_dtype)
+            if w_dtype == torch.bfloat16 and side_stream_ok(ctx.w_ref):
+                dw = on_side_stream(lambda: weight_grad(dy2, x2), (dy2, x2))
+            else:
+                dw = weight_grad(dy2, x2).to(w_dtype)
         if b_dtype is not None and ctx.needs_input_grad[2]:
             from .ops import colsum
             db = colsum(dy2, torch.bfloat16 if b_dtype == torch.bfloat16 else torch.float32).to(b_dtype)
@@ -86,6 +143,7 @@ class _QKVFn(torch.autograd.Function):
         bb = None if bq is None else torch.cat([bq, bk, bv]).to(torch.bfloat16)
         ctx.save_for_backward(xb, wb)
         ctx.meta = (x.dtype, wq.dtype, None if bq is None else bq.dtype, (wq.shape[0], wk.shape[0], wv.shape[0]))
+        ctx.w_refs = (wq, wk, wv)
         return F.linear(xb, wb, bb)
 
     @staticmethod
@@ -100,7 +158,11 @@ class _QKVFn(torch.autograd.Function):
         dx = torch.mm(dy2, wb).view(*xb.shape).to(x_dtype) if ctx.needs_input_grad[0] else None
         dws = [None] * 3
         if any(ctx.needs_input_grad[i] for i in (1, 3, 5)):
-            dws = [t.to(w_dtype) for t in weight_grad(dy2, x2).split(sizes)]
+            if w_dtype == torch.bfloat16 and all(side_stream_ok(w) for w in ctx.w_refs):
+                # separate tensors (not views of one): autograd stores each as .grad as is
+                dws = list(on_side_stream(lambda: [t.clone() for t in weight_grad(dy2, x2).split(sizes)], (dy2, x2)))
+            else:
+                dws = [t.to(w_dtype) for t in weight_grad(dy2, x2).split(sizes)]
         dbs = [None] * 3
         if b_dtype is not None and any(ctx.needs_input_grad[i] for i in (2, 4, 6)):
             from .ops import colsum
