@@ -183,3 +183,35 @@ def test_posconv_weight_grad_vs_fp32(B, T, splits):
     dy_full = torch.cat([dy.float(), torch.zeros(B, 1, C, device=dev)], 1).transpose(1, 2)
     ref = torch.nn.grad.conv1d_weight(x.float().transpose(1, 2), (C, 48, K), dy_full, padding=pad, groups=G)
     assert _rel(dw, ref) < 1e-5
+
+
+def test_feature_encoder_side_stream_weight_grads_bit_identical():
+    """Conv-stack weight gradients of bf16 (shadow) conv weights on the side stream
+    (frontend._FrameConvS2, queued before the input-gradient GEMMs) equal the in-stream ones
+    bit for bit."""
+    import transformers
+    from triad_amd import frontend, linear as L
+    torch.manual_seed(0)
+    m = transformers.HubertModel(transformers.HubertConfig()).to(dev).train()
+    frontend.install_hubert_frontend(m)
+    fe = m.feature_extractor
+    for layer in fe.conv_layers:
+        layer.conv.weight.data = layer.conv.weight.data.to(torch.bfloat16)
+    x = torch.randn(4, 16000, device=dev) * 0.5
+
+    def run(side):
+        L.SIDE_STREAM_DW = side
+        fe.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = fe(x)
+        (y.float() ** 2).mean().backward()
+        return [layer.conv.weight.grad.clone() for layer in fe.conv_layers]
+
+    try:
+        g_main = run(False)
+        g_side = run(True)
+    finally:
+        L.SIDE_STREAM_DW = True
+    for a, b in zip(g_side, g_main):
+        assert a.dtype == torch.bfloat16 and a.is_contiguous()
+        assert torch.equal(a, b)

@@ -291,6 +291,14 @@ class _FrameConvS2(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous()
         wb = w.to(torch.bfloat16)
         wj = [wb[:, :, j] for j in range(k)]  # [O][C] each
+
+        def weight_grad():  # [O][k*C] (column j*C + c) -> contiguous [O][C][k]
+            dwr = _weight_grad_rows(dy, M, x, 2 * Cin, k * Cin)
+            return dwr.view(O, k, Cin).permute(0, 2, 1).to(wdt).contiguous()
+
+        from .linear import on_side_stream, side_stream_ok
+        # bf16 shadow weight: dW on the side stream, queued before (and running beside) the dX GEMMs
+        dw = on_side_stream(weight_grad, (dy, x)) if wdt == torch.bfloat16 and side_stream_ok(w) else None
         dx = torch.empty(M + 1, 2 * Cin, dtype=torch.bfloat16, device=x.device)  # = B*Tp + 2 frames
         if k == 3:
             # even frames 2q: dY[q-1] W2 + dY[q] W0 -- rows q = 1..M over overlapping dY rows
@@ -303,8 +311,8 @@ class _FrameConvS2(torch.autograd.Function):
             bk = torch.cat([wj[0].t(), wj[1].t()], dim=0).contiguous()  # [2C][O]
             _gemm_rows(dy, 0, O, M, O, bk, dx, 0, 2 * Cin)
         dx[M].zero_()  # spare frames: constants
-        dwr = _weight_grad_rows(dy, M, x, 2 * Cin, k * Cin)  # [O][k*C], column j*C + c
-        dw = dwr.view(O, k, Cin).permute(0, 2, 1).to(wdt)
+        if dw is None:
+            dw = weight_grad()
         return dx.view(2 * M + 2, Cin), dw, None, None
 
 
