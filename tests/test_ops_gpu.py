@@ -323,3 +323,41 @@ def test_side_stream_weight_grads_bit_identical():
     for a, b in zip(g_side, g_main):
         assert torch.equal(a, b)
     assert torch.equal(gx_side, gx_main)
+
+
+def test_modality_streams_match_single_stream():
+    """forward_triad with the audio / text backbones on their own streams (and their backward
+    chains with them) against the single-stream order: the same losses and the same reduced
+    gradient buffer after one trainer step from identical models / seeds (library GEMMs may
+    differ in summation order between launches, so to 1e-4 relative, far below what a stream
+    race would produce)."""
+    import os
+    from triad_amd.model import MultiModalModel
+    from triad_amd.train import TriadTrainer
+    B = 128
+    g = torch.Generator().manual_seed(5)
+    frames = torch.randn(B, 3, 224, 224, generator=g).to(dev)
+    audio = (torch.randn(B, 16000, generator=g) * 0.1).to(dev)
+    text = [f"caption number {i} of a scene" for i in range(B)]
+
+    def run(streams):
+        os.environ["TRIAD_MODALITY_STREAMS"] = "1" if streams else "0"
+        torch.manual_seed(0)
+        m = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.8, patch_sparsity_weight=0.01,
+                            visual_dropout_prob=0.25, use_amp=True).to(dev)
+        m.train()
+        tr = TriadTrainer(m, total_updates=100, unfreeze_audio_step=0, unfreeze_text_step=0, unfreeze_vit_step=0,
+                          device=dev)
+        torch.manual_seed(1)
+        np.random.seed(1)  # SpecAugment masks (transformers' _compute_mask_indices draws from numpy)
+        out = tr.step(frames, audio, text)
+        torch.cuda.synchronize()
+        return float(out["loss"]), tr.space.flat_g.clone()
+
+    try:
+        l_single, g_single = run(False)
+        l_multi, g_multi = run(True)
+    finally:
+        os.environ.pop("TRIAD_MODALITY_STREAMS", None)
+    assert abs(l_multi - l_single) <= 1e-5 * abs(l_single)
+    assert float((g_multi - g_single).norm()) <= 1e-4 * float(g_single.norm())

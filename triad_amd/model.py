@@ -338,12 +338,34 @@ class MultiModalModel(nn.Module):
         model.py:326-327, so this equals two separate encodes given the masks).
         Returns (av_tuple, tv_tuple) as forward_audio_visual / forward_text_visual."""
         ve = self.visual_embedder
+        streams = _modality_streams(frames)
         with torch.autocast("cuda", enabled=self.use_amp, dtype=self.amp_dtype):
-            patches = ve.encode_patches(frames)
-            v_av = ve.patch_dropout(patches, ve.patch_dropout_rate, av_keep)
-            v_tv = ve.patch_dropout(patches, ve.patch_dropout_rate, tv_keep)
-            audio_feats = self.audio_embedder(audio)
-            text_feats, attention_mask = self.text_embedder(text_list)
+            if streams is None:
+                patches = ve.encode_patches(frames)
+                v_av = ve.patch_dropout(patches, ve.patch_dropout_rate, av_keep)
+                v_tv = ve.patch_dropout(patches, ve.patch_dropout_rate, tv_keep)
+                audio_feats = self.audio_embedder(audio)
+                text_feats, attention_mask = self.text_embedder(text_list)
+            else:
+                # the three backbones are independent until the heads: audio and text run on
+                # their own streams beside the ViT (and, since autograd runs each backward op on
+                # its forward op's stream, so do their backward chains)
+                # (the same host-side call order as above, so every RNG draw is unchanged)
+                main, s_audio, s_text = streams
+                s_audio.wait_stream(main)
+                s_text.wait_stream(main)
+                patches = ve.encode_patches(frames)
+                v_av = ve.patch_dropout(patches, ve.patch_dropout_rate, av_keep)
+                v_tv = ve.patch_dropout(patches, ve.patch_dropout_rate, tv_keep)
+                with torch.cuda.stream(s_audio):
+                    audio_feats = self.audio_embedder(audio)
+                with torch.cuda.stream(s_text):
+                    text_feats, attention_mask = self.text_embedder(text_list)
+                main.wait_stream(s_audio)
+                main.wait_stream(s_text)
+                for t in (audio_feats, text_feats, attention_mask):
+                    if isinstance(t, torch.Tensor) and t.is_cuda:
+                        t.record_stream(main)
         return self._av_head(audio_feats, v_av)[0], self._tv_head(text_feats, v_tv, attention_mask)[0]
 
     def forward(self, frames=None, audio=None, text_list=None):
@@ -367,6 +389,23 @@ class MultiModalModel(nn.Module):
         if audio is not None and text_list is not None:
             emb["text_audio_sim_matrix"] = self.compute_similarity_matrix(emb["text_feats"], emb["audio_feats"])
         return emb
+
+
+_STREAMS = {}
+
+
+def _modality_streams(frames):
+    """(current, audio, text) streams for forward_triad's concurrent backbones, or None (CPU
+    tensors, or TRIAD_MODALITY_STREAMS=0)."""
+    import os
+    if not (isinstance(frames, torch.Tensor) and frames.is_cuda) or os.environ.get("TRIAD_MODALITY_STREAMS",
+                                                                                   "1") == "0":
+        return None
+    dev = frames.device
+    pair = _STREAMS.get(dev.index)
+    if pair is None:
+        pair = _STREAMS[dev.index] = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+    return (torch.cuda.current_stream(dev),) + pair
 
 
 def _load_image(path, device):

@@ -172,7 +172,10 @@ class FlatParamSpace:
         table = host.to(self.device, non_blocking=True)
         call("triad_gather_grads", ptr(table), len(rows), ptr(self.flat_g), int(accumulate and True),
              stream_ptr(self.device))
+        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         for i in ids:
+            if cur is not None:  # grads made on other streams (side-stream dW, modality streams)
+                self.params[i].grad.record_stream(cur)
             self.params[i].grad = None
         self.touched[ids] = True
 

@@ -94,6 +94,7 @@ def gelu_table(device):
     if t is None:
         t = torch.empty(int(call("triad_gelu_table_bytes")), dtype=torch.uint8, device=device)
         call("triad_gelu_table", ptr(t), stream_ptr(device))
+        torch.cuda.current_stream(device).synchronize()  # once: other streams read it without a wait
         _GELU_TABLES[key] = t
     return t
 
