@@ -205,6 +205,9 @@ __device__ __forceinline__ unsigned bf16_bits(bf16 v) { return (unsigned)__built
 // 8 consecutive elements (4 pairs) per iteration; DROP = false: p = 0 (plain GELU, no hash).
 // TABLE = false: the direct formula (no table buffer given).
 constexpr int GL_NT = 512;
+#ifndef GL_BPC
+#define GL_BPC 2  // persistent blocks per CU
+#endif
 
 template <bool DROP, bool TABLE>
 __global__ __launch_bounds__(GL_NT) void geludrop_fwd_kernel(const bf16* __restrict__ u, long long n, unsigned seed,
@@ -273,7 +276,7 @@ int gl_blocks(long long n) {
     if (cus <= 0) cus = 256;
   }
   const long long need = (n / 8 + GL_NT - 1) / GL_NT;
-  return (int)(need < 2LL * cus ? need : 2LL * cus);
+  return (int)(need < (long long)GL_BPC * cus ? need : (long long)GL_BPC * cus);
 }
 
 __global__ __launch_bounds__(256) void dropout_keep_kernel(long long n, unsigned seed, unsigned thr,
