@@ -185,7 +185,7 @@ def main():
             "roofline": {"kernel": "triad_pairsim_fwd[AV]", "bound": "mfma", "achieved": achieved,
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
                          "traffic": pmc_traffic("pairsim_kernel<0>" if os.environ.get("TRIAD_FWD_V1")
-                                                else "pairsim_fwd2_kernel<true>", fwd["grid"]), "avg_ms": avg_ms,
+                                                else "pairsim_fwd2_kernel<true, false>", fwd["grid"]), "avg_ms": avg_ms,
                          "algorithmic_bytes": fwd["bytes"] / max(1, fwd["launches"]),
                          "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                                            "same kernel and grid; FETCH x2 gfx950 correction)"},

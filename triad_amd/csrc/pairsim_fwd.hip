@@ -261,7 +261,10 @@ struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in 
   }
 };
 
-template <bool TRAIN>
+// SHORTQ tags the launches over short query lists (text captions, Nq <= 32) with their own
+// symbol, so profiler summaries report the AV (long-query) launches' durations on their own; the
+// code is identical.
+template <bool TRAIN, bool SHORTQ>
 __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 kbuf[NBUF * KT_ELEMS + 16 * WAVES];
   double* red = (double*)(kbuf + NBUF * KT_ELEMS);
@@ -522,8 +525,12 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
   a.rowmax = rowmax; a.argmax = argmax; a.part = nn_part;
   a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part; a.klen = k_len;
   const int xw = xb * (256 / ROWS_PER_WG);  // xb counts 256-row blocks
-  if (dS) hipLaunchKernelGGL(pairsim_fwd2_kernel<true>, dim3(xw, ys), dim3(64 * WAVES), 0, stream, a);
-  else hipLaunchKernelGGL(pairsim_fwd2_kernel<false>, dim3(xw, ys), dim3(64 * WAVES), 0, stream, a);
+  const bool sq = Nq <= 32;
+  const dim3 grid(xw, ys), block(64 * WAVES);
+  if (dS && sq) hipLaunchKernelGGL((pairsim_fwd2_kernel<true, true>), grid, block, 0, stream, a);
+  else if (dS) hipLaunchKernelGGL((pairsim_fwd2_kernel<true, false>), grid, block, 0, stream, a);
+  else if (sq) hipLaunchKernelGGL((pairsim_fwd2_kernel<false, true>), grid, block, 0, stream, a);
+  else hipLaunchKernelGGL((pairsim_fwd2_kernel<false, false>), grid, block, 0, stream, a);
   TRIAD_CHECK_LAUNCH();
   if (diagS && diag) {
     hipLaunchKernelGGL(diag_sim_kernel, dim3((Nq + 31) / 32, Bq), dim3(256), 0, stream, (const bf16*)Q,
