@@ -41,6 +41,26 @@ __device__ __forceinline__ void stage_a_piece(const bf16* __restrict__ A, long l
   }
 }
 
+// Register-staged form of a piece (GEMM_REGSTAGE): the same source address as the LDS-DMA piece,
+// loaded into a VGPR quad now and written to the same lane-linear LDS slot later.
+template <bool A_KCONTIG>
+__device__ __forceinline__ bf16x8 load_a_piece(const bf16* __restrict__ A, long long lda, int m0, int k0, int wave,
+                                               int lane, int u) {
+  const int inst = wave * 4 + u;
+  if (A_KCONTIG) {
+    const int m = inst * 8 + (lane >> 3), cp = lane & 7;
+    const int c = cp ^ ((m >> 1) & 7);
+    return *(const bf16x8*)(A + (size_t)(m0 + m) * lda + k0 + c * 8);
+  }
+  const int k = inst * 4 + (lane >> 4), cp = lane & 15;
+  const int c = cp ^ ((k & 3) << 2);
+  return *(const bf16x8*)(A + (size_t)(k0 + k) * lda + m0 + c * 8);
+}
+
+__device__ __forceinline__ void put_piece(bf16* dst, int wave, int lane, int u, bf16x8 v) {
+  *(bf16x8*)(dst + (wave * 4 + u) * 512 + lane * 8) = v;
+}
+
 template <bool A_KCONTIG>
 __device__ __forceinline__ void stage_a(const bf16* __restrict__ A, long long lda, int m0, int k0, bf16* dst,
                                         int wave, int lane) {
@@ -48,6 +68,9 @@ __device__ __forceinline__ void stage_a(const bf16* __restrict__ A, long long ld
   for (int u = 0; u < 4; ++u) stage_a_piece<A_KCONTIG>(A, lda, m0, k0, dst, wave, lane, u);
 }
 
+#ifndef GEMM_REGSTAGE
+#define GEMM_REGSTAGE 0  // 1: 128 x 128 form stages through VGPRs + ds_write instead of LDS-DMA
+#endif
 #ifndef GEMM_SPREAD
 #define GEMM_SPREAD 0  // 1: next stage's 8 DMA pieces issued between the 16 MFMAs, not in a burst
 #endif
@@ -104,15 +127,31 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
   const int kbeg = blockIdx.y * k_per_split;
   const int nk = min(k_per_split, Kd - kbeg) / BK;
   C += (size_t)blockIdx.y * slab_stride;
+  bf16x8 ra[4], rb[4];  // GEMM_REGSTAGE: next stage's pieces in flight in registers
   if (nk > 0) {
-  stage_a<A_KCONTIG>(A, lda, m0, kbeg, lds, wave, lane);
-  stage_b<B_KCONTIG>(B, ldb, n0, kbeg, lds + A_ELEMS, wave, lane);
+    if (GEMM_REGSTAGE) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        put_piece(lds, wave, lane, u, load_a_piece<A_KCONTIG>(A, lda, m0, kbeg, wave, lane, u));
+        put_piece(lds + A_ELEMS, wave, lane, u, load_a_piece<B_KCONTIG>(B, ldb, n0, kbeg, wave, lane, u));
+      }
+    } else {
+      stage_a<A_KCONTIG>(A, lda, m0, kbeg, lds, wave, lane);
+      stage_b<B_KCONTIG>(B, ldb, n0, kbeg, lds + A_ELEMS, wave, lane);
+    }
   }
   for (int kt = 0; kt < nk; ++kt) {
     lds_dma_barrier();
     bf16* const nb = lds + ((kt + 1) & 1) * (A_ELEMS + B_ELEMS);
     const bool pf = kt + 1 < nk;
-    if (!GEMM_SPREAD && pf) {
+    if (GEMM_REGSTAGE && pf) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ra[u] = load_a_piece<A_KCONTIG>(A, lda, m0, kbeg + (kt + 1) * BK, wave, lane, u);
+        rb[u] = load_a_piece<B_KCONTIG>(B, ldb, n0, kbeg + (kt + 1) * BK, wave, lane, u);
+      }
+    }
+    if (!GEMM_REGSTAGE && !GEMM_SPREAD && pf) {
       stage_a<A_KCONTIG>(A, lda, m0, kbeg + (kt + 1) * BK, nb, wave, lane);
       stage_b<B_KCONTIG>(B, ldb, n0, kbeg + (kt + 1) * BK, nb + A_ELEMS, wave, lane);
     }
@@ -142,7 +181,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           acc[a][b] = mfma32(af[a], bfr[b], acc[a][b]);
-          if (GEMM_SPREAD && (a * 2 + b) % 2 == 1) {  // 2 pieces per k-step: A piece s, B piece s
+          if (!GEMM_REGSTAGE && GEMM_SPREAD && (a * 2 + b) % 2 == 1) {  // 2 pieces per k-step: A piece s, B piece s
             __builtin_amdgcn_sched_barrier(0);
             if (pf) {
               if (a == 0) stage_a_piece<A_KCONTIG>(A, lda, m0, kbeg + (kt + 1) * BK, nb, wave, lane, s);
@@ -151,6 +190,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
             __builtin_amdgcn_sched_barrier(0);
           }
         }
+    }
+    if (GEMM_REGSTAGE && pf) {  // the other buffer was last read before this stage's barrier
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        put_piece(nb, wave, lane, u, ra[u]);
+        put_piece(nb + A_ELEMS, wave, lane, u, rb[u]);
+      }
     }
   }
 
