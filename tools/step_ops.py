@@ -36,6 +36,11 @@ def main(rows=60):
         torch.cuda.synchronize()
     print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_device_time_total", row_limit=int(rows),
                                                              max_name_column_width=36, max_shapes_column_width=100))
+    print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=40, max_name_column_width=50))
+    # where the copy / cast kernels come from: copy_ by input shape, with the python stack
+    copies = [e for e in prof.key_averages(group_by_input_shape=True) if e.key in ("aten::copy_", "aten::add_")]
+    for e in sorted(copies, key=lambda e: -e.self_device_time_total)[:30]:
+        print(f"{e.key:12s} {e.count:5d} {e.self_device_time_total / 1e3:8.3f} ms  {str(e.input_shapes)[:150]}")
 
 
 if __name__ == "__main__":

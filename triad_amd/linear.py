@@ -159,8 +159,9 @@ class _QKVFn(torch.autograd.Function):
         dws = [None] * 3
         if any(ctx.needs_input_grad[i] for i in (1, 3, 5)):
             if w_dtype == torch.bfloat16 and all(side_stream_ok(w) for w in ctx.w_refs):
-                # separate tensors (not views of one): autograd stores each as .grad as is
-                dws = list(on_side_stream(lambda: [t.clone() for t in weight_grad(dy2, x2).split(sizes)], (dy2, x2)))
+                # three tensors over the one buffer's storage that are not autograd views, so
+                # autograd stores each as .grad as is (a view might be cloned on the main stream)
+                dws = list(on_side_stream(lambda: _split_rows(weight_grad(dy2, x2), sizes), (dy2, x2)))
             else:
                 dws = [t.to(w_dtype) for t in weight_grad(dy2, x2).split(sizes)]
         dbs = [None] * 3
@@ -169,6 +170,19 @@ class _QKVFn(torch.autograd.Function):
             db = colsum(dy2, torch.bfloat16 if b_dtype == torch.bfloat16 else torch.float32).to(b_dtype)
             dbs = list(db.split(sizes))
         return dx, dws[0], dbs[0], dws[1], dbs[1], dws[2], dbs[2]
+
+
+def _split_rows(buf: torch.Tensor, sizes):
+    """Row blocks of a contiguous [sum(sizes)][K] tensor as separate (non-view) tensors sharing
+    its storage."""
+    out, r = [], 0
+    K = buf.shape[1]
+    for n in sizes:
+        t = torch.empty((0,), dtype=buf.dtype, device=buf.device)
+        t.set_(buf.untyped_storage(), buf.storage_offset() + r * K, (n, K), (K, 1))
+        out.append(t)
+        r += n
+    return out
 
 
 def qkv_eligible(q: nn.Linear, k: nn.Linear, v: nn.Linear, x: torch.Tensor) -> bool:

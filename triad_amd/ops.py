@@ -354,7 +354,7 @@ class _ProjectionHead(torch.autograd.Function):
         dev = h.device
         st = stream_ptr(dev)
         Mp = _rup(max(M, 1), 128)
-        hb = _pad_rows(h.reshape(M, H).to(torch.bfloat16), Mp)
+        hb = _pad_rows(h.to(torch.bfloat16).reshape(M, H), Mp)  # cast first: one pass over a strided h
         w1b = w1.detach().to(torch.bfloat16).contiguous()
         w2b = w2.detach().to(torch.bfloat16).contiguous()
         # autocast runs F.linear with the bias cast to bf16 (model.py:483/603)
