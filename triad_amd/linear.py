@@ -51,7 +51,7 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
 # the main stream reads it); the main stream waits for the side stream at the end of the
 # backward pass (autograd callback), before anything can read a gradient.
 _SIDE = {}
-_JOIN_QUEUED = set()
+_JOIN_TASK = {}  # device index -> autograd graph task that already has a join callback queued
 
 
 def _side_stream(dev):
@@ -63,7 +63,6 @@ def _side_stream(dev):
 
 def _join(dev):
     def cb():
-        _JOIN_QUEUED.discard(dev.index)
         torch.cuda.current_stream(dev).wait_stream(_side_stream(dev))
     return cb
 
@@ -86,8 +85,9 @@ def on_side_stream(fn, inputs):
         t.record_stream(side)
     for o in (outs if isinstance(outs, (list, tuple)) else (outs,)):
         o.record_stream(main)
-    if dev.index not in _JOIN_QUEUED:
-        _JOIN_QUEUED.add(dev.index)
+    task = torch._C._current_graph_task_id()
+    if _JOIN_TASK.get(dev.index) != task:  # once per backward pass (robust to an aborted one)
+        _JOIN_TASK[dev.index] = task
         torch.autograd.Variable._execution_engine.queue_callback(_join(dev))
     return outs
 
