@@ -82,7 +82,7 @@ def time_steps(B=4, steps=2, warmup=1, threads=None, seed=1234):
         for o in opts:
             o.step()
             o.zero_grad()
-        return float(loss)
+        return float(loss.detach())
 
     for _ in range(warmup):
         step()
