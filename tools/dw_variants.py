@@ -62,7 +62,7 @@ def triad_splitk(M=50944):
                           "TFLOPs": round(2.0 * M * K * N / ms / 1e9, 1)}), flush=True)
         one = torch.ones(1, device="cuda")
         flops = 2.0 * M * K * N
-        for sp in (2, 4, 8, 16):
+        for sp in [int(v) for v in os.environ.get("TRIAD_DW_SPLITS", "2,4,8,16").split(",")]:
             slabs = torch.empty(sp * N * K, device="cuda")
             out = torch.empty(N, K, device="cuda")
             fn = lambda: call("triad_gemm_bf16_splitk", ptr(dy), N, 0, ptr(x), K, 0, N, K, M, sp, ptr(one),  # noqa: E731

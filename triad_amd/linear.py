@@ -24,10 +24,24 @@ from ._lib import call, ptr, stream_ptr
 MIN_TOKENS = 4096  # DistilBERT at B=256 (8,192 tokens) still gains 1.1-1.8x
 
 
+# Split-K factors measured per output-tile count on MI355X (tools/dw_variants.py with
+# TRIAD_DW_SPLITS, profiles/r01_dw_splits_{50944,8192}.log). The best factor is set by how
+# tiles x splits workgroups quantise onto the CUs' slots, not by a smooth rule: e.g. 144 tiles
+# run 7 splits (1,008 workgroups) 8-11 % faster than 8 (1,152) at 50,944 tokens, and 3 splits
+# (432) 15-26 % faster than 4 (576) at 8,192 tokens.
+_SPLITS_LONG = {36: 7, 108: 9, 144: 7}   # M >= 32,768 tokens (HuBERT at c3: 50,944)
+_SPLITS_SHORT = {36: 7, 108: 4, 144: 3}  # 4,096 <= M < 16,384 (DistilBERT at c3: 8,192)
+SPLIT_TABLE = os.environ.get("TRIAD_DW_SPLIT_TABLE", "1") != "0"
+
+
 def _splits(M, out_f, in_f):
-    """Token-range splits: 8 for the 36-144-tile outputs at 50 K tokens, ~2 K tokens per split
-    below that (measured, tools/dw_variants.py)."""
+    """Token-range splits for dW: the measured table for the c3 tile counts, else 8 for the
+    36-144-tile outputs at 50 K tokens and ~2 K tokens per split below that."""
     tiles = (out_f // 128) * (in_f // 128)
+    if SPLIT_TABLE:
+        table = _SPLITS_LONG if M >= 32768 else _SPLITS_SHORT if 4096 <= M < 16384 else {}
+        if tiles in table:
+            return table[tiles]
     return min(8 if tiles <= 160 else 4, max(2, M // 2048))
 
 
