@@ -1,0 +1,56 @@
+# One parameterised GPU-box runner (replaces the round-1 one-off tools/gpu_run*.sh scripts).
+#
+# usage (from this container):
+#   gpurun --timeout 1200 -- bash tools/gpu.sh <tag> <step> [<step> ...]
+# steps (run in order; the first failing / timed-out step ends the call, nothing later touches the GPU):
+#   tests            full `pytest -m gpu` suite                      -> gpurun_out/<tag>_tests.log
+#   tests:<expr>     `pytest -m gpu -k <expr>`                        -> gpurun_out/<tag>_tests.log
+#   smoke            __graft_entry__.smoke()                          -> gpurun_out/<tag>_smoke.log
+#   bench            default bench.py line (with the CPU baseline)    -> gpurun_out/<tag>_bench.json
+#   benchq           bench.py --no-cpu-baseline                       -> gpurun_out/<tag>_benchq.json
+#   prof             rocprofv3 --kernel-trace --stats of a 3-step bench -> gpurun_out/<tag>_prof/
+#   pmc:<name>:<counters>  one rocprofv3 --pmc pass (counters comma-separated) of a 3-step bench
+#   py:<script args>       python <script> (tools/ micro-benchmarks)    -> gpurun_out/<tag>_py<N>.log
+# environment: extra env for every step may be given as STEP_ENV="A=1 B=2" (exported first).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+tag=$1; shift
+[ -n "$STEP_ENV" ] && export $STEP_ENV
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  echo "[gpu.sh] $(date +%T) step $n: $step"
+  case "$step" in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        > "gpurun_out/${tag}_tests.log" 2>&1 ;;
+    tests:*)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        -k "${step#tests:}" > "gpurun_out/${tag}_tests.log" 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "gpurun_out/${tag}_smoke.log" 2>&1 ;;
+    bench)
+      timeout -k 10 900 python bench.py > "gpurun_out/${tag}_bench.json" 2> "gpurun_out/${tag}_bench.err" ;;
+    benchq)
+      timeout -k 10 600 python bench.py --no-cpu-baseline > "gpurun_out/${tag}_benchq.json" \
+        2> "gpurun_out/${tag}_benchq.err" ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${tag}_prof" -o bench \
+        -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline > "gpurun_out/${tag}_prof.log" 2>&1 ;;
+    pmc:*)
+      rest=${step#pmc:}; name=${rest%%:*}; ctr=${rest#*:}
+      timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "gpurun_out/${tag}_pmc_${name}" -o run \
+        -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "gpurun_out/${tag}_pmc_${name}.log" 2>&1 ;;
+    py:*)
+      timeout -k 10 600 python ${step#py:} > "gpurun_out/${tag}_py${n}.log" 2>&1 ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "[gpu.sh] step $n ($step) failed rc=$rc"; exit $rc
+  fi
+done
+echo "[gpu.sh] all done"

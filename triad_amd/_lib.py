@@ -11,10 +11,10 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtriad_hip.so")
+DEFAULT_LIB = os.path.join(_HERE, "libtriad_hip.so")
 # A/B experiments only: load a variant build of the same library (tools/build_variants.py);
-# the default is the in-tree build above
-LIB_PATH = os.environ.get("TRIAD_LIB_VARIANT", LIB_PATH)
+# the default is the in-tree build above, which must match the sources (see load())
+LIB_PATH = os.environ.get("TRIAD_LIB_VARIANT", DEFAULT_LIB)
 
 vp, i32, u32, i64, f32, f64 = C.c_void_p, C.c_int, C.c_uint, C.c_longlong, C.c_float, C.c_double
 
@@ -101,6 +101,8 @@ def load():
             if not os.path.exists(LIB_PATH):
                 raise TriadError(f"{LIB_PATH} not found: build it with `python -m triad_amd.build` "
                                  "(or __graft_entry__.build()); there is no CPU fallback")
+            if LIB_PATH == DEFAULT_LIB:
+                _check_fresh()
             lib = C.CDLL(LIB_PATH)
             for name, args in SIGNATURES.items():
                 fn = getattr(lib, name)
@@ -110,17 +112,26 @@ def load():
     return _lib
 
 
+def _check_fresh():
+    """Refuse a library built from other sources than the ones in the tree (a stale prebuilt
+    .so must not pass tests against edited kernels): build.py stamps the source hash."""
+    from . import build
+    stamp = DEFAULT_LIB + ".srchash"
+    have = open(stamp).read().strip() if os.path.exists(stamp) else None
+    if have != build.source_hash():
+        raise TriadError(f"{DEFAULT_LIB} is stale (built from different sources than triad_amd/csrc + "
+                         "include): rebuild with `python -m triad_amd.build`")
+
+
 # Optional live timing of launches: {entry point name: [(start_event, end_event, meta), ...]}.
 # Enabled by bench.py over its timed region; events are recorded on the current HIP stream,
 # which is the stream every entry point is launched on.
 TIMERS = None
-META = None  # set by callers (ops) just before a timed call: per-launch metadata (e.g. FLOPs)
 
 
-def call(name, *args):
-    """Invoke an entry point; non-zero status -> TriadError (RuntimeError)."""
-    global META
-    meta, META = META, None
+def call(name, *args, meta=None):
+    """Invoke an entry point; non-zero status -> TriadError (RuntimeError).
+    meta: per-launch metadata (e.g. algorithmic FLOPs) recorded with the timing when enabled."""
     if TIMERS is not None and name in TIMERS:
         import torch
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

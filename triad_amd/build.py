@@ -3,10 +3,17 @@
 The library is built in-tree (triad_amd/libtriad_hip.so) so it travels with the
 repository snapshot to the GPU box. No hipify, no CUDA shims: the sources are
 CDNA4 HIP compiled with --offload-arch=gfx950.
+
+Staleness is decided by CONTENT, not file times: every object records the hash of
+its source + all headers + flags, and the library records the hash of the whole
+source set (`libtriad_hip.so.srchash`). `_lib.load()` recomputes that hash and
+refuses a library built from different sources, so a stale prebuilt `.so` can never
+pass tests against edited kernels.
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -14,11 +21,12 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 ROOT = os.path.dirname(PKG)
+INCLUDE = os.path.join(ROOT, "include")
 LIB = os.environ.get("TRIAD_LIB_OUT", os.path.join(PKG, "libtriad_hip.so"))
 OBJ = os.environ.get("TRIAD_OBJ_DIR", os.path.join(PKG, "_build"))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-ARCH = os.environ.get("TRIAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", os.path.join(ROOT, "include"),
+ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE,
          "-Wno-unused-result"] + os.environ.get("TRIAD_EXTRA_FLAGS", "").split()
 # per-file extras: the pipelined forward wants scalar f32 VALU beside its MFMAs (SLP-packed
 # v_pk_mul_f32 + operand moves cost more issue slots than two v_mul_f32 there)
@@ -29,12 +37,33 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
 
 
+def headers():
+    hs = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    hs += [os.path.join(INCLUDE, h) for h in os.listdir(INCLUDE) if h.endswith(".h")]
+    return sorted(hs)
+
+
+def _digest(paths, extra=()):
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    for e in extra:
+        h.update(repr(e).encode())
+    return h.hexdigest()
+
+
+def source_hash():
+    """Hash of every source, header and flag the library is built from."""
+    return _digest(sources() + headers(), (FLAGS, sorted(EXTRA.items())))
+
+
 def _compile(src, save_temps=False):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
-    deps.append(os.path.join(ROOT, "include", "triad_hip.h"))
-    if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps if os.path.exists(d)) \
-            and not save_temps:
+    stamp = obj + ".hash"
+    want = _digest([src] + headers(), (FLAGS, EXTRA.get(os.path.basename(src), [])))
+    if not save_temps and os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == want:
         return obj
     cmd = [HIPCC, *FLAGS, *EXTRA.get(os.path.basename(src), []), "-c", src, "-o", obj]
     if save_temps:
@@ -42,6 +71,8 @@ def _compile(src, save_temps=False):
     r = subprocess.run(cmd, capture_output=True, text=True, cwd=OBJ)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    with open(stamp, "w") as f:
+        f.write(want)
     return obj
 
 
@@ -49,17 +80,21 @@ def build(verbose=False, save_temps=False, force=False):
     os.makedirs(OBJ, exist_ok=True)
     if force:
         for f in os.listdir(OBJ):
-            if f.endswith(".o"):
+            if f.endswith((".o", ".hash")):
                 os.remove(os.path.join(OBJ, f))
     srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, save_temps), srcs))
-    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(o) for o in objs):
+    want = source_hash()
+    stamp = LIB + ".srchash"
+    if os.path.exists(LIB) and os.path.exists(stamp) and open(stamp).read() == want and not force:
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
+    with open(stamp, "w") as f:
+        f.write(want)
     if verbose:
         print("built", LIB)
     return LIB

@@ -16,20 +16,14 @@
 // keys on the lane), no second copy of dS in HBM.
 //
 // Workgroup: 8 waves, 128 output rows x all 512 columns (A is streamed from HBM exactly
-// once); wave w owns columns [64w, 64w+64): 4 x 2 tiles of 32 x 32 accumulators. Stage =
-// two 32-deep k tiles (32 MFMAs per wave per barrier); A (8 tiles, 16 KB) and B (64 rows x
-// 512, 64 KB) double-buffered in LDS (the full 160 KB) via 16-byte LDS-DMA with source-side
-// swizzles (conflict-free reads).
+// once); wave w owns columns [64w, 64w+64): 4 x 2 tiles of 32 x 32 accumulators; A and B
+// through a 4-slot LDS ring by 16-byte LDS-DMA with source-side swizzles (conflict-free reads).
 // Optional split-K over grid.y with fp32 slabs.
 #include "common.h"
 
 namespace {
 
 constexpr int TBM = 128, TBN = 512, TBK = 32;
-constexpr int KPS = 2;                   // k tiles per stage
-constexpr int A_ST = KPS * 4 * 1024;     // 8 tiles
-constexpr int B_ST = KPS * TBK * TBN;    // 64 rows x 512
-constexpr int ST = A_ST + B_ST;
 
 // 16-byte chunk swizzles inside a 2 KB tile (involutions; glds writes lane-linear, the
 // source chunk is permuted instead).
@@ -37,31 +31,6 @@ __device__ __forceinline__ int swz_q(int c) { return c ^ ((c >> 4) & 1); }      
 __device__ __forceinline__ int swz_k(int c) { return c ^ (((c >> 6) & 1) << 3); }   // dK transposed reads
 // B image [32][512], 1 KB rows: chunk c of row k at c ^ ((k & 3) << 2)
 __device__ __forceinline__ int b_off(int k, int col) { return k * TBN + ((((col >> 3) ^ ((k & 3) << 2))) << 3) + (col & 7); }
-
-// Stage k tiles [kt, kt + nk) (nk = 1 or 2) into `dst`: A tile (kk, t) at kk*4096 + t*1024,
-// B rows kk*32 .. at A_ST + (kk*32 + k)*512.
-template <bool DK>
-__device__ __forceinline__ void stage(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ B, int mt0,
-                                      int kt, int nk, bf16* dst, int wave, int lane) {
-#pragma unroll
-  for (int kk = 0; kk < KPS; ++kk) {
-    if (kk < nk) {  // uniform
-      {  // A: 4 tiles = 8 x 1 KB pieces, one per wave
-        const int t = wave >> 1, half = wave & 1;
-        const int pos = half * 64 + lane;
-        const int c = DK ? swz_k(pos) : swz_q(pos);
-        const long long tile = DK ? ((long long)(kt + kk) * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + kt + kk);
-        glds16(Dt + tile * 1024 + c * 8, dst + kk * 4096 + t * 1024 + half * 512);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {  // B: 32 rows of 1 KB, four per wave
-        const int k = wave * 4 + u;
-        const int c = lane ^ ((k & 3) << 2);
-        glds16(B + ((long long)(kt + kk) * TBK + k) * TBN + c * 8, dst + A_ST + (kk * TBK + k) * TBN);
-      }
-    }
-  }
-}
 
 // B fragment (rows = k, columns = n0 + lane&31): two 4-row transposed reads at rows r0, r0 + dr.
 __device__ __forceinline__ bf16x8 bfrag(const bf16* img, int r0, int dr, int n0, int lane) {
@@ -72,91 +41,6 @@ __device__ __forceinline__ bf16x8 bfrag(const bf16* img, int r0, int dr, int n0,
   rp[0] = lds_tr16(img + b_off(r0, col));
   rp[1] = lds_tr16(img + b_off(r0 + dr, col));
   return r;
-}
-
-template <bool DK, bool SLAB>
-__global__ __launch_bounds__(512, 2) void tile_gemm_kernel(const bf16* __restrict__ Dt, long long CT,
-                                                           const bf16* __restrict__ B, int M, int nkt_total,
-                                                           int kt_per_split, const float* __restrict__ alpha_p,
-                                                           void* __restrict__ Cout) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * ST];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h = lane >> 5, l32 = lane & 31;
-  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
-  // XCD-aware: consecutive row panels on one XCD share the streamed B panel in that XCD's L2
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
-  const int m0 = swz * TBM, mt0 = m0 / 32;
-  const int kt0 = blockIdx.y * kt_per_split;
-  const int nkt = min(kt_per_split, nkt_total - kt0);
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) acc[t][n] = (f32x16){};
-
-  const int nst = (nkt + KPS - 1) / KPS;
-  if (nst > 0) stage<DK>(Dt, CT, B, mt0, kt0, min(KPS, nkt), lds, wave, lane);
-  for (int it = 0; it < nst; ++it) {
-    lds_dma_barrier();
-    if (it + 1 < nst)
-      stage<DK>(Dt, CT, B, mt0, kt0 + (it + 1) * KPS, min(KPS, nkt - (it + 1) * KPS), lds + ((it + 1) & 1) * ST,
-                wave, lane);
-    const int nk_here = min(KPS, nkt - it * KPS);
-#pragma unroll
-    for (int kk = 0; kk < KPS; ++kk) {
-    if (kk >= nk_here) break;  // uniform: odd tail
-    const bf16* As = lds + (it & 1) * ST + kk * 4096;
-    const bf16* Bs = lds + (it & 1) * ST + A_ST + kk * TBK * TBN;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[4], bf[2];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf16* tile = As + t * 1024;
-        if (!DK) {
-          af[t] = *(const bf16x8*)(tile + swz_q(2 * l32 + 64 * h + s) * 8);
-        } else {
-          // queries 16s + 8h + 4tt + q4 (k axis), keys 16(g&1) + 4p4 + (0..3) on the lanes
-          const int a = 2 * (g & 1) + (p4 >> 1), hh = p4 & 1;
-          s16x4* rp = (s16x4*)&af[t];
-#pragma unroll
-          for (int tt = 0; tt < 2; ++tt) {
-            const int qry = 16 * s + 8 * h + 4 * tt + q4;
-            const int c = (qry + 32 * hh) * 2 + (a >> 1);
-            rp[tt] = lds_tr16(tile + swz_k(c) * 8 + 4 * (a & 1));
-          }
-        }
-      }
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int n0 = wave * 64 + n * 32;
-        bf[n] = DK ? bfrag(Bs, 16 * s + 8 * h + q4, 4, n0, lane) : bfrag(Bs, 16 * s + 4 * h + q4, 8, n0, lane);
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[t][n] = mfma32(af[t], bf[n], acc[t][n]);
-    }
-    }
-  }
-
-  const float alpha = SLAB ? 1.f : *alpha_p;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int col = wave * 64 + n * 32 + l32;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = m0 + t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        const float val = alpha * acc[t][n][v];
-        if (SLAB) ((float*)Cout)[((size_t)blockIdx.y * M + m) * TBN + col] = val;
-        else ((bf16*)Cout)[(size_t)m * TBN + col] = (bf16)val;
-      }
-    }
 }
 
 // Ring form of the same GEMM: stage = ONE 32-deep k tile (A 4 tiles = 8 KB, B 32 rows x 512 =
@@ -193,11 +77,6 @@ __device__ __forceinline__ void stage_ring(const bf16* __restrict__ Dt, long lon
   for (int u = 0; u < RING_PIECES; ++u) ring_piece<DK>(Dt, CT, B, mt0, kt, dst, wave, lane, u);
 }
 
-#ifndef TG_SPREAD
-#define TG_SPREAD 1  // 1: the next tile's DMA pieces issued between the MFMAs (one per 3) instead of in a burst
-                     // after the barrier (A/B: dQ/dK 3-4 % faster)
-#endif
-
 template <bool DK, bool SLAB>
 __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __restrict__ Dt, long long CT,
                                                                 const bf16* __restrict__ B, int M, int nkt_total,
@@ -231,7 +110,6 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __re
     __syncthreads();
     const bool pf = it + RING_NB - 1 < nkt;
     bf16* const pdst = lds + ((it + RING_NB - 1) % RING_NB) * RING_ST;
-    if (!TG_SPREAD && pf) stage_ring<DK>(Dt, CT, B, mt0, kt0 + it + RING_NB - 1, pdst, wave, lane);
     const bf16* As = lds + (it % RING_NB) * RING_ST;
     const bf16* Bs = As + 4096;
 #pragma unroll
@@ -264,7 +142,9 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __re
         for (int n = 0; n < 2; ++n) {
           acc[t][n] = mfma32(af[t], bf[n], acc[t][n]);
           const int m = s * 8 + t * 2 + n;
-          if (TG_SPREAD && m % 3 == 0 && m / 3 < RING_PIECES) {
+          // the next-but-two tile's DMA pieces between the MFMAs, one per 3 (measured 3-4 %
+          // faster than a burst after the barrier)
+          if (m % 3 == 0 && m / 3 < RING_PIECES) {
             __builtin_amdgcn_sched_barrier(0);
             if (pf) ring_piece<DK>(Dt, CT, B, mt0, kt0 + it + RING_NB - 1, pdst, wave, lane, m / 3);
             __builtin_amdgcn_sched_barrier(0);
@@ -291,17 +171,6 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __re
 
 }  // namespace
 
-#ifndef TG_RING
-#define TG_RING 1  // 1: tile_gemm_ring_kernel (one k tile per stage, 4-slot ring); 0: 2-stage form
-#endif
-#if TG_RING
-#define TG_KERNEL tile_gemm_ring_kernel
-#define TG_KPS 1
-#else
-#define TG_KERNEL tile_gemm_kernel
-#define TG_KPS KPS
-#endif
-
 extern "C" {
 
 // dQ (dk = 0): M = query rows (R_pad), nkt = key tiles (C_pad / 32), B = K [C_pad][512].
@@ -310,19 +179,18 @@ extern "C" {
 int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
                     int splits, float* slabs, void* C, hipStream_t stream) {
   if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
-  int kps = (nkt + splits - 1) / splits;
-  kps = (kps + TG_KPS - 1) / TG_KPS * TG_KPS;  // whole stages per split
+  const int kps = (nkt + splits - 1) / splits;
   dim3 grid(M / TBM, splits);
   const bf16* d = (const bf16*)Dt;
   const bf16* b = (const bf16*)B;
   if (splits == 1) {
-    if (dk) hipLaunchKernelGGL((TG_KERNEL<true, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
-    else hipLaunchKernelGGL((TG_KERNEL<false, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
+    if (dk) hipLaunchKernelGGL((tile_gemm_ring_kernel<true, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
+    else hipLaunchKernelGGL((tile_gemm_ring_kernel<false, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
-  if (dk) hipLaunchKernelGGL((TG_KERNEL<true, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
-  else hipLaunchKernelGGL((TG_KERNEL<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
+  if (dk) hipLaunchKernelGGL((tile_gemm_ring_kernel<true, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
+  else hipLaunchKernelGGL((tile_gemm_ring_kernel<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
   TRIAD_CHECK_LAUNCH();
   return triad_sum_slabs(slabs, splits, (long long)M * TBN, alpha, 1, C, stream);
 }

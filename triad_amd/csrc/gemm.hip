@@ -41,26 +41,6 @@ __device__ __forceinline__ void stage_a_piece(const bf16* __restrict__ A, long l
   }
 }
 
-// Register-staged form of a piece (GEMM_REGSTAGE): the same source address as the LDS-DMA piece,
-// loaded into a VGPR quad now and written to the same lane-linear LDS slot later.
-template <bool A_KCONTIG>
-__device__ __forceinline__ bf16x8 load_a_piece(const bf16* __restrict__ A, long long lda, int m0, int k0, int wave,
-                                               int lane, int u) {
-  const int inst = wave * 4 + u;
-  if (A_KCONTIG) {
-    const int m = inst * 8 + (lane >> 3), cp = lane & 7;
-    const int c = cp ^ ((m >> 1) & 7);
-    return *(const bf16x8*)(A + (size_t)(m0 + m) * lda + k0 + c * 8);
-  }
-  const int k = inst * 4 + (lane >> 4), cp = lane & 15;
-  const int c = cp ^ ((k & 3) << 2);
-  return *(const bf16x8*)(A + (size_t)(k0 + k) * lda + m0 + c * 8);
-}
-
-__device__ __forceinline__ void put_piece(bf16* dst, int wave, int lane, int u, bf16x8 v) {
-  *(bf16x8*)(dst + (wave * 4 + u) * 512 + lane * 8) = v;
-}
-
 template <bool A_KCONTIG>
 __device__ __forceinline__ void stage_a(const bf16* __restrict__ A, long long lda, int m0, int k0, bf16* dst,
                                         int wave, int lane) {
@@ -68,12 +48,8 @@ __device__ __forceinline__ void stage_a(const bf16* __restrict__ A, long long ld
   for (int u = 0; u < 4; ++u) stage_a_piece<A_KCONTIG>(A, lda, m0, k0, dst, wave, lane, u);
 }
 
-#ifndef GEMM_REGSTAGE
-#define GEMM_REGSTAGE 0  // 1: 128 x 128 form stages through VGPRs + ds_write instead of LDS-DMA
-#endif
-#ifndef GEMM_SPREAD
-#define GEMM_SPREAD 0  // 1: next stage's 8 DMA pieces issued between the 16 MFMAs, not in a burst
-#endif
+// (Measured and not kept: staging through VGPRs + ds_write instead of LDS-DMA, and the next
+// stage's DMA pieces spread between the MFMAs -- DESIGN.md §4b.)
 
 // B is [k][n] (B_KCONTIG=0, n-contiguous) or [n][k] (B_KCONTIG=1) -- the same two
 // images as A with the roles of m and n swapped.
@@ -127,31 +103,15 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
   const int kbeg = blockIdx.y * k_per_split;
   const int nk = min(k_per_split, Kd - kbeg) / BK;
   C += (size_t)blockIdx.y * slab_stride;
-  bf16x8 ra[4], rb[4];  // GEMM_REGSTAGE: next stage's pieces in flight in registers
   if (nk > 0) {
-    if (GEMM_REGSTAGE) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        put_piece(lds, wave, lane, u, load_a_piece<A_KCONTIG>(A, lda, m0, kbeg, wave, lane, u));
-        put_piece(lds + A_ELEMS, wave, lane, u, load_a_piece<B_KCONTIG>(B, ldb, n0, kbeg, wave, lane, u));
-      }
-    } else {
-      stage_a<A_KCONTIG>(A, lda, m0, kbeg, lds, wave, lane);
-      stage_b<B_KCONTIG>(B, ldb, n0, kbeg, lds + A_ELEMS, wave, lane);
-    }
+    stage_a<A_KCONTIG>(A, lda, m0, kbeg, lds, wave, lane);
+    stage_b<B_KCONTIG>(B, ldb, n0, kbeg, lds + A_ELEMS, wave, lane);
   }
   for (int kt = 0; kt < nk; ++kt) {
     lds_dma_barrier();
     bf16* const nb = lds + ((kt + 1) & 1) * (A_ELEMS + B_ELEMS);
     const bool pf = kt + 1 < nk;
-    if (GEMM_REGSTAGE && pf) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        ra[u] = load_a_piece<A_KCONTIG>(A, lda, m0, kbeg + (kt + 1) * BK, wave, lane, u);
-        rb[u] = load_a_piece<B_KCONTIG>(B, ldb, n0, kbeg + (kt + 1) * BK, wave, lane, u);
-      }
-    }
-    if (!GEMM_REGSTAGE && !GEMM_SPREAD && pf) {
+    if (pf) {
       stage_a<A_KCONTIG>(A, lda, m0, kbeg + (kt + 1) * BK, nb, wave, lane);
       stage_b<B_KCONTIG>(B, ldb, n0, kbeg + (kt + 1) * BK, nb + A_ELEMS, wave, lane);
     }
@@ -181,22 +141,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           acc[a][b] = mfma32(af[a], bfr[b], acc[a][b]);
-          if (!GEMM_REGSTAGE && GEMM_SPREAD && (a * 2 + b) % 2 == 1) {  // 2 pieces per k-step: A piece s, B piece s
-            __builtin_amdgcn_sched_barrier(0);
-            if (pf) {
-              if (a == 0) stage_a_piece<A_KCONTIG>(A, lda, m0, kbeg + (kt + 1) * BK, nb, wave, lane, s);
-              else stage_a_piece<B_KCONTIG>(B, ldb, n0, kbeg + (kt + 1) * BK, nb + A_ELEMS, wave, lane, s);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-          }
         }
-    }
-    if (GEMM_REGSTAGE && pf) {  // the other buffer was last read before this stage's barrier
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        put_piece(nb, wave, lane, u, ra[u]);
-        put_piece(nb + A_ELEMS, wave, lane, u, rb[u]);
-      }
     }
   }
 
@@ -224,9 +169,7 @@ constexpr int GB_M = 256, GB_NB = 3;
 constexpr int GB_A = GB_M * BK, GB_ST = GB_A + B_ELEMS;  // elements per stage (48 KB)
 constexpr int GB_PIECES = 6;
 
-#ifndef GBIG_SPREAD
-#define GBIG_SPREAD 1  // 1: the 6 pieces between the 16 MFMAs of a stage (one per 2); 0: burst
-#endif
+// the 6 DMA pieces of a stage issued between its 16 MFMAs (one per 2), not in a burst (measured)
 
 template <bool A_KCONTIG, bool B_KCONTIG>
 __device__ __forceinline__ void gb_piece(const bf16* __restrict__ A, long long lda, const bf16* __restrict__ B,
@@ -297,9 +240,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
     const bool pf = kt + GB_NB - 1 < nk;
     bf16* const nb = lds + ((kt + GB_NB - 1) % GB_NB) * GB_ST;
     const int kn = kbeg + (kt + GB_NB - 1) * BK;
-    if (!GBIG_SPREAD && pf)
-#pragma unroll
-      for (int u = 0; u < GB_PIECES; ++u) gb_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, u);
     const bf16* ai = lds + (kt % GB_NB) * GB_ST;
     const bf16* bi = ai + GB_A;
 #pragma unroll
@@ -320,7 +260,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
         for (int b = 0; b < 2; ++b) {
           acc[a][b] = mfma32(af[a], bfr[b], acc[a][b]);
           const int mi = s * 4 + a * 2 + b;
-          if (GBIG_SPREAD && (mi & 1) && mi / 2 < GB_PIECES) {
+          if ((mi & 1) && mi / 2 < GB_PIECES) {
             __builtin_amdgcn_sched_barrier(0);
             if (pf) gb_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, mi / 2);
             __builtin_amdgcn_sched_barrier(0);
@@ -474,9 +414,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
 // launch(), 1 = 128 x 128, 2 = 256 x 128 ring, 3 = 256 x 256 four-wave (when the shape allows).
 int g_gemm_form = 0;
 
-#ifndef GEMM_BIG
-#define GEMM_BIG 1  // 1: gemm_big_kernel where it measured faster (see launch)
-#endif
 
 template <bool AK, bool BK_, typename OutT>
 int launch(const void* A, long long lda, const void* B, long long ldb, int M, int N, int Kd, const float* alpha,
@@ -498,7 +435,7 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
     return TRIAD_OK;
   }
   if (g_gemm_form != 1 && M % GB_M == 0 &&
-      (g_gemm_form == 2 || (GEMM_BIG && (M >= 8192 || Kd / splits >= 32768)))) {
+      (g_gemm_form == 2 || M >= 8192 || Kd / splits >= 32768)) {
     const int nwg = (M / GB_M) * (N / BN);
     hipLaunchKernelGGL((gemm_big_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
                        (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride);

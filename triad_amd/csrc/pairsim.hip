@@ -23,8 +23,6 @@
 // the row max/argmax is lane-local plus one half-wave exchange.
 #include "common.h"
 
-#include <stdlib.h>
-
 int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
                               int Nk_eff, const float* temp, float clamp_lo, int diag, int diag_off, float* rowmax,
                               int* argmax, double* nn_part, float* diagS, void* dS, long long CT, double* st_part,
@@ -86,8 +84,9 @@ __device__ __forceinline__ void stage_key_tile(const PairArgs& a, bf16* dst, int
   }
 }
 
-template <int EPI>
-__global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
+// Recompute form of dL/dS (any mix of upstream gradients): S per tile, then the full dS
+// (clamp + max + diagonal terms) into the tiled layout and the per-workgroup dL/dtemp partial.
+__global__ __launch_bounds__(512, 2) void pairsim_dS_kernel(PairArgs a) {
   // All LDS in ONE array (a second __shared__ object can make hipcc drain the
   // in-flight LDS-DMA before every ds_read).
   __shared__ __attribute__((aligned(16))) bf16 kbuf[2 * KT_ELEMS + 8 * WAVES];
@@ -111,7 +110,6 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
   if (nblocks <= 0) {  // uniform across the workgroup
     if (threadIdx.x == 0) {
       a.part[blockIdx.y * gridDim.x + blockIdx.x] = 0.0;
-      if (EPI == 0 && a.part2) a.part2[blockIdx.y * gridDim.x + blockIdx.x] = 0.0;
     }
     return;
   }
@@ -128,16 +126,12 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
   const float temp = *a.temp;
   const float lo = a.clamp_lo;
 
-  float c_ce = 0.f, c_nn = 0.f, c_dg = 0.f;
-  if (EPI == 1) { c_ce = a.coef[0]; c_nn = a.coef[1]; c_dg = a.coef[2]; }
-  const float wrow = (EPI == 1 && row_ok) ? a.qw[row] : 0.f;
+  const float c_ce = a.coef[0], c_nn = a.coef[1], c_dg = a.coef[2];
+  const float wrow = row_ok ? a.qw[row] : 0.f;
 
-  float m = -INFINITY;
-  int am = 0;
   float gmax = 0.f;
   int amax = -1;
-  int nk = a.Nk_eff;  // valid keys of the current key sample
-  double accd = 0.0, accd2 = 0.0;
+  double accd = 0.0;
   const int rt = blockIdx.x * WAVES + wave;  // this wave's row tile of dS
 
   for (int b = 0; b < nblocks; ++b) {
@@ -160,86 +154,38 @@ __global__ __launch_bounds__(512, 2) void pairsim_kernel(PairArgs a) {
 
     const bool diag_pair = a.diag && row_ok && (j == qi + a.diag_off);
     const int key0 = kb * 32 + 4 * h;
-    if (kb == 0 && a.klen) nk = min(a.klen[j], a.Nk_eff);
 
-    if (EPI == 0) {
-      float nn = 0.f, st = 0.f;
-      bf16 dn[16];
-      // nvalid: keys of this tile that take part (0 for padded query rows); most tiles are full
-      const int nvalid = row_ok ? min(32, nk - kb * 32) : 0;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const bool ok = 4 * h + (v & 3) + 8 * (v >> 2) < nvalid;
-        const float s = acc[v] * temp;
-        if (ok && s > m) { m = s; am = key0 + (v & 3) + 8 * (v >> 2); }  // keys ascend with v: first index kept
-        const float c = ok ? fminf(fmaxf(s, lo), 0.f) : 0.f;
-        nn += c * c;
-        // unit gradient of the l_nonneg term, (d/dS clamp(S,lo,0)^2)/2 = S on [lo, 0] (inclusive)
-        const float d = (ok && c == s) ? s : 0.f;
-        st += d * acc[v];
-        dn[v] = (bf16)d;
-      }
-      accd += (double)nn;
-      if (a.dS) {
-        accd2 += (double)st;
-        store_tile(a.dS, a.CT, rt, (long long)j * nkb + kb, lane, dn);
-      }
-      if (a.diagS && __any(diag_pair)) {  // only the key sample paired with this wave's rows
-        if (diag_pair) {
-          float* drow = a.diagS + ((size_t)qi * a.Nq + qq) * a.Nk_pad;
-#pragma unroll
-          for (int v = 0; v < 16; ++v) {
-            const int key = key0 + (v & 3) + 8 * (v >> 2);
-            if (key < nk) drow[key] = acc[v] * temp;
-          }
-        }
-      }
-      if (kb == nkb - 1) {
-        const float m2 = __shfl_xor(m, 32);
-        const int am2 = __shfl_xor(am, 32);
-        if (m2 > m || (m2 == m && am2 < am)) { m = m2; am = am2; }
-        if (h == 0) {
-          a.rowmax[(size_t)j * a.R_pad + row] = m;
-          a.argmax[(size_t)j * a.R_pad + row] = am;
-        }
-        m = -INFINITY;
-        am = 0;
-      }
-    } else {
-      if (kb == 0) {
-        gmax = row_ok ? c_ce * a.dclip[(size_t)qi * a.Bk + j] * wrow : 0.f;
-        amax = row_ok ? a.argmax[(size_t)j * a.R_pad + row] : -1;
-      }
-      const float* dg = (diag_pair && a.dSdiag) ? a.dSdiag + ((size_t)qi * a.Nq + qq) * a.Nk_pad : nullptr;
-      float dt = 0.f;
-      bf16 out[16];
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int key = key0 + (v & 3) + 8 * (v >> 2);
-        const float sraw = acc[v];
-        const float s = sraw * temp;
-        float g = (s >= lo && s <= 0.f) ? c_nn * s : 0.f;  // clamp grad, inclusive bounds
-        if (key == amax) g += gmax;
-        if (dg && key < a.Nk_eff) g += c_dg * dg[key];
-        g = (row_ok && key < a.Nk_eff) ? g : 0.f;
-        dt += g * sraw;
-        out[v] = (bf16)g;
-      }
-      accd += (double)dt;
-      store_tile(a.dS, a.CT, rt, (long long)j * nkb + kb, lane, out);
+    if (kb == 0) {
+      gmax = row_ok ? c_ce * a.dclip[(size_t)qi * a.Bk + j] * wrow : 0.f;
+      amax = row_ok ? a.argmax[(size_t)j * a.R_pad + row] : -1;
     }
+    const float* dg = (diag_pair && a.dSdiag) ? a.dSdiag + ((size_t)qi * a.Nq + qq) * a.Nk_pad : nullptr;
+    float dt = 0.f;
+    bf16 out[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int key = key0 + (v & 3) + 8 * (v >> 2);
+      const float sraw = acc[v];
+      const float s = sraw * temp;
+      float g = (s >= lo && s <= 0.f) ? c_nn * s : 0.f;  // clamp grad, inclusive bounds
+      if (key == amax) g += gmax;
+      if (dg && key < a.Nk_eff) g += c_dg * dg[key];
+      g = (row_ok && key < a.Nk_eff) ? g : 0.f;
+      dt += g * sraw;
+      out[v] = (bf16)g;
+    }
+    accd += (double)dt;
+    store_tile(a.dS, a.CT, rt, (long long)j * nkb + kb, lane, out);
   }
 
-  // Workgroup partials of l_nonneg (fwd) or dL/dtemp (bwd), and sum(S*S_raw) (fwd + dS), in double.
-  double v = wave_sum_d(accd);
-  double v2 = wave_sum_d(accd2);
-  if (lane == 0) { red[wave] = v; red[WAVES + wave] = v2; }
+  // Workgroup partial of dL/dtemp, in double.
+  const double v = wave_sum_d(accd);
+  if (lane == 0) red[wave] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
-    double t = 0.0, t2 = 0.0;
-    for (int w = 0; w < WAVES; ++w) { t += red[w]; t2 += red[WAVES + w]; }
+    double t = 0.0;
+    for (int w = 0; w < WAVES; ++w) t += red[w];
     a.part[blockIdx.y * gridDim.x + blockIdx.x] = t;
-    if (EPI == 0 && a.part2) a.part2[blockIdx.y * gridDim.x + blockIdx.x] = t2;
   }
 }
 
@@ -577,16 +523,9 @@ int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, in
   a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part; a.klen = k_len;
   int ys;
   const int xb = grid_for(R_pad, Bk, &a.j_per_wg, &ys);
-  // pipelined forward (pairsim_fwd.hip) unless TRIAD_FWD_V1 is set or K exceeds its 32-bit
-  // buffer offsets; pairsim_kernel<0> below is the serialised-epilogue original
-  static const bool v1 = getenv("TRIAD_FWD_V1") != nullptr;
-  if (!v1 && (unsigned long long)Bk * Nk_pad * 512 * 2 < (1ull << 31))
-    return triad_pairsim_fwd2_launch(Q, K, R, R_pad, Nq, Bq, Bk, Nk_pad, Nk_eff, temp, clamp_lo, diag, diag_off,
-                                     rowmax, argmax, nn_part, diagS, dS, CT, st_part, k_len, xb, ys, a.j_per_wg,
-                                     stream);
-  hipLaunchKernelGGL(pairsim_kernel<0>, dim3(xb, ys), dim3(512), 0, stream, a);
-  TRIAD_CHECK_LAUNCH();
-  return TRIAD_OK;
+  return triad_pairsim_fwd2_launch(Q, K, R, R_pad, Nq, Bq, Bk, Nk_pad, Nk_eff, temp, clamp_lo, diag, diag_off,
+                                   rowmax, argmax, nn_part, diagS, dS, CT, st_part, k_len, xb, ys, a.j_per_wg,
+                                   stream);
 }
 
 int triad_clip_reduce(const float* rowmax, int R_pad, int Nq, int Bq, int Bk, const float* qmask,
@@ -641,7 +580,7 @@ int triad_pairsim_dS(const void* Q, const void* K, int R, int R_pad, int Nq, int
   a.dS = (bf16*)dS; a.CT = CT; a.part = dt_part;
   int ys;
   const int xb = grid_for(R_pad, Bk, &a.j_per_wg, &ys);
-  hipLaunchKernelGGL(pairsim_kernel<1>, dim3(xb, ys), dim3(512), 0, stream, a);
+  hipLaunchKernelGGL(pairsim_dS_kernel, dim3(xb, ys), dim3(512), 0, stream, a);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

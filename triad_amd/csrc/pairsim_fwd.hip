@@ -1,7 +1,6 @@
 // Forward of the fused similarity head with the epilogue software-pipelined into the MFMA chain.
 //
-// Same contract as pairsim_kernel<0> (pairsim.hip; SajayR/TRIAD model.py:370-392 / 490-514 /
-// 417-418 / 524-525): rowmax / argmax per (key sample, query row), l_nonneg partial sums,
+// SajayR/TRIAD model.py:370-392 / 490-514 / 417-418 / 524-525: rowmax / argmax per (key sample, query row), l_nonneg partial sums,
 // diagonal S (diag_sim_kernel below), and (training) the unit l_nonneg gradient written in the
 // tiled dS layout.
 //
@@ -12,7 +11,7 @@
 //    tile (the next tile's DMA stays in flight across it);
 //  * the epilogue of tile b-1 (scale, max/argmax, clamp^2, unit dS, bf16 pack) is carried by
 //    tile b's 32-step MFMA chain, one element per two k-steps, so its VALU issues in the MFMA
-//    shadows (pairsim_kernel<0> runs it after the chain, serialised with it).
+//    shadows.
 #include "common.h"
 
 #include <type_traits>
@@ -21,42 +20,16 @@ namespace {
 
 constexpr int D = 512;
 constexpr int NS = D / 16;  // 32 k-steps
-#ifndef FWD_WAVES
-#define FWD_WAVES 8  // waves per workgroup (8: one workgroup per CU; 4: two, NBUF must be 2)
-#endif
-#ifndef FWD_NBUF
-#define FWD_NBUF 3   // key-tile LDS ring slots (prefetch distance NBUF - 1)
-#endif
-#ifndef FWD_LDSPF
-#define FWD_LDSPF 2  // key fragments read from LDS ahead of their MFMA
-#endif
-#ifndef FWD_NT
-#define FWD_NT 0     // 1: dS stores non-temporal
-#endif
-constexpr int WAVES = FWD_WAVES;
-constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 at 8 waves, as pairsim_kernel (same grid / partial arrays)
+// Measured choices (DESIGN.md §4 tuning record): 8 waves (two per SIMD, one workgroup per CU),
+// a 3-slot key ring (prefetch distance 2), key fragments read 2 k-steps ahead of their MFMA,
+// scheduling regions of 2 k-steps, plain (temporal) dS stores, scalar f32 epilogue VALU.
+constexpr int WAVES = 8;
+constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 query rows per workgroup
 constexpr int KT_ELEMS = 32 * D;
-constexpr int NBUF = FWD_NBUF;
-static_assert(NBUF == 2 || NBUF == 3, "ring of 2 or 3 key tiles");
+constexpr int NBUF = 3;                  // key-tile LDS ring slots
+constexpr int LDSPF = 2;                 // key fragments read from LDS ahead of their MFMA
+constexpr int REGION = 2;                // k-steps per scheduling region (sched_barrier spacing)
 constexpr int GLDS_PER_TILE = 32 / WAVES;  // 1-KB LDS-DMA pieces per wave per key tile (4)
-
-// tuning knobs (A/B builds, tools/build_variants.py)
-#ifndef FWD_SETPRIO
-#define FWD_SETPRIO 0  // 1: waves 4-7 at s_setprio 1 (MI355X_MICROARCH.md "two waves per SIMD" item 4)
-#endif
-#ifndef FWD_EXPERIMENT
-#define FWD_EXPERIMENT 0  // A/B timing only (results wrong): 1 = no key DMA after the prologue,
-                          // 2 = no epilogue elements, 4 = no dS stores
-#endif
-#ifndef FWD_SPREAD
-#define FWD_SPREAD 0  // 1: the key-tile DMA pieces issued between the chain's MFMAs
-#endif
-#ifndef FWD_PK
-#define FWD_PK 0  // 1: packed v_pk_fma_f32 / v_pk_mul_f32 in the epilogue; 0: scalar pairs
-#endif
-#ifndef FWD_REGION
-#define FWD_REGION 2  // k-steps per scheduling region (sched_barrier spacing; 2 measured best)
-#endif
 
 struct FwdArgs {
   const bf16* Q;
@@ -117,11 +90,7 @@ __device__ __forceinline__ void stage_tile(i32x4 kr, const FwdArgs& a, bf16* dst
 // s_nop 1 covers the store-data read (cdna_hip_programming.md §5.7). Counted in sync_tile.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void store16(void* p, u32x4 v) {
-#if FWD_NT
-  asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-#else
   asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-#endif
 }
 
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {  // one v_cvt_pk_bf16_f32
@@ -170,12 +139,8 @@ __device__ __forceinline__ float maxf(float a, float b) {
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
-__device__ __forceinline__ f32x2 pk_fma_sq(f32x2 c, f32x2 acc) {  // acc + c * c
-  asm("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(acc) : "v"(c));
-  return acc;
-}
-// scalar forms (FWD_PK 0): beside MFMAs a packed f32 op costs ~22 issue cycles more than two
-// scalar ones (MI355X_MICROARCH.md, 'price of one filler beside MFMAs')
+// scalar forms: beside MFMAs a packed f32 op costs ~22 issue cycles more than two scalar ones
+// (MI355X_MICROARCH.md, 'price of one filler beside MFMAs')
 __device__ __forceinline__ float fma_sq(float c, float acc) {  // acc + c * c
   asm("v_fmac_f32 %0, %1, %1" : "+v"(acc) : "v"(c));
   return acc;
@@ -183,11 +148,6 @@ __device__ __forceinline__ float fma_sq(float c, float acc) {  // acc + c * c
 __device__ __forceinline__ float mulf(float a, float b) {
   float r;
   asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) {
-  f32x2 r;
-  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
 
@@ -211,20 +171,12 @@ __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 s
   const float c = __builtin_amdgcn_fmed3f(u, lo, 0.f);
   if (v & 1) {
     const f32x2 cc = {e.prev, c};
-#if FWD_PK
-    e.nn2 = pk_fma_sq(cc, e.nn2);
-#else
     e.nn2.x = fma_sq(cc.x, e.nn2.x);
     e.nn2.y = fma_sq(cc.y, e.nn2.y);
-#endif
     PIN(e.nn2);
     if constexpr (TRAIN) {
       e.mn = min3f(e.mn, p[v - 1], u);
-#if FWD_PK
-      const f32x2 d = pk_mul(cc, su2);
-#else
       const f32x2 d = {mulf(cc.x, su2.x), mulf(cc.y, su2.y)};
-#endif
       e.pk[v >> 1] = pack_bf16x2(d.x, d.y);
       PIN(e.mn);
       PIN(e.pk[v >> 1]);
@@ -275,7 +227,6 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) 
   const int row = blockIdx.x * ROWS_PER_WG + wave * 32 + ql;
   const bool rok = row < a.R;
   const int rt = (blockIdx.x * ROWS_PER_WG + wave * 32) / 32;
-  if (FWD_SETPRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   const int j0 = blockIdx.y * a.j_per_wg;
   const int j1 = min(a.Bk, j0 + a.j_per_wg);
@@ -289,33 +240,25 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) 
     return;
   }
 
-  // K through a buffer descriptor (32-bit offsets; the host guarantees < 2 GB)
-  // buffer descriptor words: base, stride 0, num_records, gfx950 raw-buffer flags
-  const unsigned long long kaddr = (unsigned long long)a.K;
+  // K through a buffer descriptor based at this workgroup's first key sample j0: 32-bit
+  // offsets cover its j_per_wg samples (the host checks j_per_wg * Nk_pad * 1 KB < 2 GB), so the
+  // whole key set may exceed 4 GB (global negatives). Descriptor words: base, stride 0,
+  // num_records, gfx950 raw-buffer flags.
+  const unsigned long long kaddr = (unsigned long long)(a.K + (size_t)j0 * a.Nk_pad * D);
   const i32x4 kr = {__builtin_amdgcn_readfirstlane((int)(unsigned)kaddr),
                     __builtin_amdgcn_readfirstlane((int)((unsigned)(kaddr >> 32) & 0xffffu)),
-                    __builtin_amdgcn_readfirstlane((int)((unsigned)a.Bk * a.Nk_pad * (D * 2))), 0x00020000};
+                    __builtin_amdgcn_readfirstlane((int)((unsigned)(j1 - j0) * a.Nk_pad * (D * 2))), 0x00020000};
   // walk cursors: prefetch (tile b+2), chain (tile b), epilogue (tile b-1); ring slots
   Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
   int fslot = 0, cslot = 0;
   auto prefetch = [&](int b2) {
-    if (b2 < nblocks && (!(FWD_EXPERIMENT & 1) || b2 < 2))
-      stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j, fc.kb, wave, lane);
-    fc.next(nkb);
-    fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
-  };
-  // FWD_SPREAD: piece u of tile b2 issued inside the chain; the cursor advances after the last
-  auto prefetch_piece = [&](int b2, int u) {
-    if (b2 < nblocks && (!(FWD_EXPERIMENT & 1) || b2 < 2))
-      stage_piece(kr, a, kbuf + fslot * KT_ELEMS, fc.j, fc.kb, wave, lane, u);
-  };
-  auto prefetch_done = [&]() {
+    if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j - j0, fc.kb, wave, lane);
     fc.next(nkb);
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
   };
   // prologue: NBUF - 1 tiles in flight
   prefetch(0);
-  if (NBUF == 3) prefetch(1);
+  prefetch(1);
 
   bf16x8 qf[NS];
   {
@@ -358,8 +301,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) 
     // VMEM ops younger than tile b's DMA, at least: tile b+1's 4 pieces (if any) and, in
     // training, one epilogue's 2 dS stores (b >= 2); vmcnt counts both, in issue order
     // (3-slot ring; a 2-slot ring has no younger tile in flight)
-    const bool more = NBUF == 3 && b + 1 < nblocks;
-    const bool st = TRAIN && !(FWD_EXPERIMENT & 4) && b >= 2;
+    const bool more = b + 1 < nblocks;
+    const bool st = TRAIN && b >= 2;
     if (more && st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_TILE + 2) : "memory");
     else if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_TILE) : "memory");
     else if (st) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -377,10 +320,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) 
       const float st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup(e, p, su, lo) : nn;
       accd2 += (double)st;
       bf16* d = dS_w + ((long long)ec.j * nkb + ec.kb) * 1024 + lane * 16;
-      if (!(FWD_EXPERIMENT & 4)) {
-        store16(d, (u32x4){e.pk[0], e.pk[1], e.pk[2], e.pk[3]});
-        store16(d + 8, (u32x4){e.pk[4], e.pk[5], e.pk[6], e.pk[7]});
-      }
+      store16(d, (u32x4){e.pk[0], e.pk[1], e.pk[2], e.pk[3]});
+      store16(d + 8, (u32x4){e.pk[4], e.pk[5], e.pk[6], e.pk[7]});
     }
     if (ec.kb == nkb - 1) {  // end of a key sample: combine the half-waves' max / argmax
       float m = e.m;
@@ -404,10 +345,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) 
     constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value, full = decltype(FULLT)::value;
     if constexpr (ch) {
       sync_tile(b);
-      if (!FWD_SPREAD) prefetch(b + NBUF - 1);
+      prefetch(b + NBUF - 1);
       const char* kt = (const char*)kbuf + cslot * (KT_ELEMS * 2);
       cslot = __builtin_amdgcn_readfirstlane(cslot == NBUF - 1 ? 0 : cslot + 1);
-      constexpr int P = FWD_LDSPF;
+      constexpr int P = LDSPF;
       bf16x8 af[P + 1];
 #pragma unroll
       for (int s = 0; s < P; ++s) af[s] = *(const bf16x8*)(kt + xo[s & 7] + (s >> 3) * 256);
@@ -416,21 +357,13 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) 
       for (int s = 0; s < NS; ++s) {
         if (s + P < NS) af[(s + P) % (P + 1)] = *(const bf16x8*)(kt + xo[(s + P) & 7] + ((s + P) >> 3) * 256);
         c = mfma32(af[s % (P + 1)], qf[s], c);
-        if constexpr (ep && !(FWD_EXPERIMENT & 2)) {
+        if constexpr (ep) {
           if (s & 1) epi_elem<TRAIN, full>(e, p, s >> 1, su2, lo);
         }
         // scheduling regions of 4 k-steps: two epilogue elements interleave and fill each
         // other's VALU->SGPR-mask wait states
-        if (s % FWD_REGION == FWD_REGION - 1) __builtin_amdgcn_sched_barrier(0);
-        // next-but-one tile's DMA pieces between the MFMAs, one per 8 k-steps (not a burst
-        // right after the barrier, where every wave of the SIMD would issue them at once)
-        if (FWD_SPREAD && s % (NS / GLDS_PER_TILE) == 3) {
-          __builtin_amdgcn_sched_barrier(0);
-          prefetch_piece(b + NBUF - 1, s / (NS / GLDS_PER_TILE));
-          __builtin_amdgcn_sched_barrier(0);
-        }
+        if (s % REGION == REGION - 1) __builtin_amdgcn_sched_barrier(0);
       }
-      if (FWD_SPREAD) prefetch_done();
     } else if constexpr (ep) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full>(e, p, v, su2, lo);
@@ -511,13 +444,13 @@ __global__ __launch_bounds__(256) void diag_sim_kernel(const bf16* __restrict__ 
 
 }  // namespace
 
-// Same grid decomposition as pairsim_kernel (triad_pairsim_nparts), so partial arrays match.
+// Grid: triad_pairsim_nparts' decomposition (pairsim.hip grid_for), so partial arrays match.
 // The diagonal S (diagS != null) comes from diag_sim_kernel, launched after on the same stream.
 int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
                               int Nk_eff, const float* temp, float clamp_lo, int diag, int diag_off, float* rowmax,
                               int* argmax, double* nn_part, float* diagS, void* dS, long long CT, double* st_part,
                               const int* k_len, int xb, int ys, int jpw, hipStream_t stream) {
-  if ((unsigned long long)Bk * Nk_pad * D * 2 >= (1ull << 31)) return TRIAD_EINVAL;  // 32-bit buffer offsets
+  if ((unsigned long long)jpw * Nk_pad * D * 2 >= (1ull << 31)) return TRIAD_EINVAL;  // 32-bit buffer offsets
   FwdArgs a = {};
   a.Q = (const bf16*)Q; a.K = (const bf16*)K;
   a.R = R; a.R_pad = R_pad; a.Nq = Nq; a.Bq = Bq; a.Bk = Bk; a.Nk_pad = Nk_pad; a.Nk_eff = Nk_eff;

@@ -205,9 +205,7 @@ __device__ __forceinline__ unsigned bf16_bits(bf16 v) { return (unsigned)__built
 // 8 consecutive elements (4 pairs) per iteration; DROP = false: p = 0 (plain GELU, no hash).
 // TABLE = false: the direct formula (no table buffer given).
 constexpr int GL_NT = 512;
-#ifndef GL_BPC
-#define GL_BPC 2  // persistent blocks per CU
-#endif
+constexpr int GL_BPC = 2;  // persistent blocks per CU
 
 template <bool DROP, bool TABLE>
 __global__ __launch_bounds__(GL_NT) void geludrop_fwd_kernel(const bf16* __restrict__ u, long long n, unsigned seed,

@@ -162,9 +162,8 @@ def _gemm_rows(a, a_row, lda, M, K, b, out, out_row, ldc):
     a.flat[(a_row + m) * lda + k] (rows may overlap), b [N][K] contiguous bf16."""
     N = b.shape[0]
     if M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and lda % 8 == 0 and ldc % 8 == 0:
-        _lib.META = dict(backbone=True)
         call("triad_gemm_bf16", _addr(a, a_row, lda), lda, 1, ptr(b), K, 1, M, N, K, None, _addr(out, out_row, ldc), ldc,
-             1, stream_ptr(a.device))
+             1, stream_ptr(a.device), meta=dict(backbone=True))
     else:  # same product through torch (it copies the overlapping operand)
         A = a.as_strided((M, K), (lda, 1), a.storage_offset() + a_row * lda)
         out.as_strided((M, N), (ldc, 1), out.storage_offset() + out_row * ldc).copy_(torch.mm(A, b.t()))
@@ -177,9 +176,8 @@ def _weight_grad_rows(dy, M, x, ldx, N):
         sp = 8
         slabs = torch.empty(sp * O * N, dtype=torch.float32, device=dy.device)
         out = torch.empty(O, N, dtype=torch.float32, device=dy.device)
-        _lib.META = dict(backbone=True)
         call("triad_gemm_bf16_splitk", ptr(dy), O, 0, ptr(x), ldx, 0, O, N, M, sp, None, ptr(slabs), ptr(out), 0,
-             stream_ptr(dy.device))
+             stream_ptr(dy.device), meta=dict(backbone=True))
         return out
     X = x.as_strided((M, N), (ldx, 1), x.storage_offset())
     return torch.mm(dy[:M].t(), X, out_dtype=torch.float32)

@@ -31,17 +31,15 @@ MIN_TOKENS = 4096  # DistilBERT at B=256 (8,192 tokens) still gains 1.1-1.8x
 # (432) 15-26 % faster than 4 (576) at 8,192 tokens.
 _SPLITS_LONG = {36: 7, 108: 9, 144: 7}   # M >= 32,768 tokens (HuBERT at c3: 50,944)
 _SPLITS_SHORT = {36: 7, 108: 4, 144: 3}  # 4,096 <= M < 16,384 (DistilBERT at c3: 8,192)
-SPLIT_TABLE = os.environ.get("TRIAD_DW_SPLIT_TABLE", "1") != "0"
 
 
 def _splits(M, out_f, in_f):
     """Token-range splits for dW: the measured table for the c3 tile counts, else 8 for the
     36-144-tile outputs at 50 K tokens and ~2 K tokens per split below that."""
     tiles = (out_f // 128) * (in_f // 128)
-    if SPLIT_TABLE:
-        table = _SPLITS_LONG if M >= 32768 else _SPLITS_SHORT if 4096 <= M < 16384 else {}
-        if tiles in table:
-            return table[tiles]
+    table = _SPLITS_LONG if M >= 32768 else _SPLITS_SHORT if 4096 <= M < 16384 else {}
+    if tiles in table:
+        return table[tiles]
     return min(8 if tiles <= 160 else 4, max(2, M // 2048))
 
 
@@ -52,9 +50,8 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     sp = _splits(M, O, K)
     slabs = torch.empty(sp * O * K, dtype=torch.float32, device=dy2.device)
     dw = torch.empty(O, K, dtype=torch.bfloat16, device=dy2.device)
-    _lib.META = dict(backbone=True)
     call("triad_gemm_bf16_splitk", ptr(dy2), dy2.stride(0), 0, ptr(x2), x2.stride(0), 0, O, K, M, sp, None,
-         ptr(slabs), ptr(dw), 1, stream_ptr(dy2.device))
+         ptr(slabs), ptr(dw), 1, stream_ptr(dy2.device), meta=dict(backbone=True))
     return dw
 
 

@@ -95,14 +95,14 @@ def colsum(x, out_dtype=torch.float32):
     return out
 
 
-def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream):
+def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream, meta=None):
     """dQ = alpha dS K (dk=0) / dK = alpha dS^T Q (dk=1) over the tiled dS (triad_tile_gemm),
     split-K over the CUs when the row panels alone leave them idle. (A stream-K form -- one run
     of (row panel, k tile) units per CU, no slab round trip -- measured slower: runs start at
     different k offsets, so CUs of one XCD no longer share the streamed B panel in L2.)"""
     sp = _gemm_splits(M // 128, nkt)
     slabs = torch.empty(sp * M * D, dtype=torch.float32, device=out.device) if sp > 1 else None
-    call("triad_tile_gemm", ptr(dS), CT, dk, ptr(B), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream)
+    call("triad_tile_gemm", ptr(dS), CT, dk, ptr(B), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream, meta=meta)
 
 
 def _gemm_splits(wgs, nkt, cus=256, max_splits=8):
@@ -168,12 +168,11 @@ class _ContrastiveHead(torch.autograd.Function):
         CT = _rup(g.C_pad // 32, 4)
         dS = torch.empty((g.R_pad // 32) * CT * 1024, dtype=torch.bfloat16, device=dev) if need_grad else None
         st_part = torch.empty(nparts, dtype=torch.float64, device=dev) if need_grad else None
-        _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, grid=nparts * 512,
-                         bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R
-                         + (2.0 * g.R_pad * g.C_pad if need_grad else 0.0))
         call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
              ptr(temp), CLAMP_LO[kind], 1, rank * Bq, ptr(rowmax), ptr(argmax), ptr(nn_part), ptr(diagS),
-             ptr(dS), CT, ptr(st_part), None, st)
+             ptr(dS), CT, ptr(st_part), None, st, meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, grid=nparts * 512,
+                         bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R
+                         + (2.0 * g.R_pad * g.C_pad if need_grad else 0.0)))
         clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
         qw = torch.empty(g.R, dtype=torch.float32, device=dev)
         qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
@@ -252,24 +251,23 @@ class _ContrastiveHead(torch.autograd.Function):
         else:
             coef = torch.stack([c_ce, c_nn, c_diag, c_cal]).contiguous()
             dt_part = torch.empty(ctx.nparts, dtype=torch.float64, device=dev)
-            _lib.META = dict(kind=kind, flops=0.0, recompute_flops=2.0 * g.R * g.Bk * g.Nk_eff * D)
             call("triad_pairsim_dS", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
                  ptr(temp), CLAMP_LO[kind], 1, rank * g.Bq, ptr(argmax), ptr(dclip), ptr(qw), ptr(gdiag), ptr(coef),
-                 ptr(dS), CT, ptr(dt_part), st)
+                 ptr(dS), CT, ptr(dt_part), st, meta=dict(kind=kind, flops=0.0, recompute_flops=2.0 * g.R * g.Bk * g.Nk_eff * D))
             alpha = temp
             w = torch.stack([torch.ones_like(c_ce), zero, zero, c_cal]).contiguous()
             parts = (dt_part, ctx.nparts, None, 0, None, 0)
         gq = gk = gt = None
         if ctx.needs_input_grad[0]:
             dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
-            _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dQ")
-            tile_gemm(dS, CT, 0, Kb, g.R_pad, g.C_pad // 32, alpha, dQ, st)
+            tile_gemm(dS, CT, 0, Kb, g.R_pad, g.C_pad // 32, alpha, dQ, st,
+                      meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dQ"))
             gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(ctx.q_dtype)
         if ctx.needs_input_grad[1]:
             Mk = CT * 32
             dK = torch.empty(Mk, D, dtype=torch.bfloat16, device=dev)
-            _lib.META = dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dK")
-            tile_gemm(dS, CT, 1, Qb, Mk, g.R_pad // 32, alpha, dK, st)
+            tile_gemm(dS, CT, 1, Qb, Mk, g.R_pad // 32, alpha, dK, st,
+                      meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dK"))
             Nk_pad = g.Nk_pad
             if W > 1:
                 from . import dist as tdist
