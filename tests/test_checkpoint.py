@@ -110,3 +110,82 @@ def test_checkpoint_save_load_roundtrip(trainer_pair, tmp_path):
     p0 = b.space.params[0]
     assert p0.data_ptr() == b.space.flat_p[b.space.offsets[0]:].data_ptr()
     assert np.all(b.space.steps >= 3)
+
+
+def _reference_shaped_state_dict(model, seed):
+    """A `model_state_dict` as the reference's train.py:413 would write it, built WITHOUT the
+    mirror's key mapping: HuBERT / DistilBERT keys from the stock `transformers` classes (no
+    execution tweaks installed), the ViT under peft's wrapper names, all fp32, with the
+    `_orig_mod.` prefix of a torch.compile'd model (train.py:412)."""
+    import transformers
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    hub = transformers.HubertModel(transformers.HubertConfig()).state_dict()
+    dbert = transformers.DistilBertModel(transformers.DistilBertConfig()).state_dict()
+    for prefix, part in (("audio_embedder.hubert.", hub), ("text_embedder.encoder.", dbert)):
+        for k, v in part.items():
+            sd[prefix + k] = v
+    ours = model.state_dict()
+    for k, v in ours.items():
+        if k.startswith(ck.VIT):
+            rest = k[len(ck.VIT):]
+            if rest.endswith(".base.weight") or rest.endswith(".base.bias"):
+                rest = rest.replace(".base.", ".base_layer.")
+            elif rest.endswith(".lora_A") or rest.endswith(".lora_B"):
+                rest += ".default.weight"
+            sd[ck.PEFT + rest] = v
+        elif not (k.startswith("audio_embedder.hubert.") or k.startswith("text_embedder.encoder.")):
+            sd[k] = v  # projection heads, temperature
+    out = {}
+    for k, v in sd.items():
+        if v.is_floating_point():
+            v = torch.randn(v.shape, generator=g, dtype=torch.float32) * 0.02
+        out["_orig_mod." + k] = v.clone()
+    return out
+
+
+def test_reference_shaped_checkpoint_loads_and_saves_bit_exact(trainer_pair):
+    """A reference-layout fp32 state dict loads strictly (every stock transformers / peft key is
+    matched, none left over) and saves back bit-exact -- including the frozen ViT base, which
+    executes from bf16 copies (vit.store_frozen_base_bf16) but is kept and saved in fp32."""
+    _, b = trainer_pair
+    sd = _reference_shaped_state_dict(b.model, 5)
+    missing, unexpected = ck.load_reference_state_dict(b.model, sd, strict=True, space=b.space)
+    assert not missing and not unexpected
+    back = ck.reference_state_dict(b.model, b.space)
+    assert set(back) == {k[len("_orig_mod."):] for k in sd}
+    frozen_bf16 = 0
+    for k, v in back.items():
+        want = sd["_orig_mod." + k]
+        assert v.dtype == want.dtype, k
+        assert torch.equal(v, want), k
+    for n, p in b.model.named_parameters():
+        frozen_bf16 += int(p.dtype == torch.bfloat16 and not p.requires_grad)
+    assert frozen_bf16 > 0  # the bf16 execution copies exist and did not leak into the save
+
+
+def test_state_load_refreshes_positional_embedding_cache():
+    """The ViT caches its interpolated positional embedding for frozen weights; a state load
+    after a forward must invalidate it (the cache is keyed on the tensor version, and the
+    loader copies in place under no_grad, which bumps it; refresh_frozen_copies clears it)."""
+    from triad_amd.vit import DinoVisionTransformer, apply_lora
+    torch.manual_seed(0)
+    vit = apply_lora(DinoVisionTransformer("dinov2_vits14_reg"))
+    x = torch.randn(1, 3, 56, 70)   # 4 x 5 patches: the 16 x 16 table is interpolated
+    with torch.no_grad():
+        y0 = vit.get_intermediate_layers(x, n=1)[0].clone()
+        sd = {ck.VIT + k: v.clone() for k, v in vit.state_dict().items()}
+        sd[ck.VIT + "pos_embed"] = torch.randn_like(sd[ck.VIT + "pos_embed"])
+
+        class Holder(torch.nn.Module):
+            pass
+        h = Holder()
+        h.visual_embedder = torch.nn.Module()
+        h.visual_embedder.model = vit
+        ck.load_reference_state_dict(h, sd)
+        y1 = vit.get_intermediate_layers(x, n=1)[0]
+        fresh = apply_lora(DinoVisionTransformer("dinov2_vits14_reg"))
+        fresh.load_state_dict({k[len(ck.VIT):]: v for k, v in sd.items()})
+        y2 = fresh.get_intermediate_layers(x, n=1)[0]
+    assert not torch.equal(y0, y1)
+    assert torch.equal(y1, y2)

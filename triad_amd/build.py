@@ -54,15 +54,21 @@ def _digest(paths, extra=()):
     return h.hexdigest()
 
 
+def _portable(flags):
+    """Flags with this checkout's absolute path taken out: the GPU box unpacks the tree under
+    another root, and the hash must describe the sources, not where they lie."""
+    return [f.replace(ROOT, "<root>") for f in flags]
+
+
 def source_hash():
     """Hash of every source, header and flag the library is built from."""
-    return _digest(sources() + headers(), (FLAGS, sorted(EXTRA.items())))
+    return _digest(sources() + headers(), (_portable(FLAGS), sorted(EXTRA.items())))
 
 
 def _compile(src, save_temps=False):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
     stamp = obj + ".hash"
-    want = _digest([src] + headers(), (FLAGS, EXTRA.get(os.path.basename(src), [])))
+    want = _digest([src] + headers(), (_portable(FLAGS), EXTRA.get(os.path.basename(src), [])))
     if not save_temps and os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == want:
         return obj
     cmd = [HIPCC, *FLAGS, *EXTRA.get(os.path.basename(src), []), "-c", src, "-o", obj]

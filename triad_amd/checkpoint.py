@@ -56,12 +56,19 @@ def from_reference_key(k: str) -> str:
 
 
 def _masters(model, space):
-    """{state_dict key: fp32 master} for parameters held as bf16 model weights by `space`."""
+    """{state_dict key: fp32 master} for parameters held as bf16 model weights: trainable ones
+    by the optimizer's flat `space`, frozen ones (the ViT base, vit.store_frozen_base_bf16) by
+    the module's `frozen_fp32` dict."""
+    out = {}
+    for mname, mod in model.named_modules():
+        for k, v in getattr(mod, "frozen_fp32", {}).items():
+            out[f"{mname}.{k}" if mname else k] = v
     if space is None or not getattr(space, "shadowed", np.zeros(0, bool)).any():
-        return {}
+        return out
     by_id = {id(p): k for k, p in model.named_parameters()}
-    return {by_id[id(space.params[i])]: space.master(i) for i in np.nonzero(space.shadowed)[0]
-            if id(space.params[i]) in by_id}
+    out.update({by_id[id(space.params[i])]: space.master(i) for i in np.nonzero(space.shadowed)[0]
+                if id(space.params[i]) in by_id})
+    return out
 
 
 def reference_state_dict(model: torch.nn.Module, space=None) -> "OrderedDict[str, torch.Tensor]":
@@ -96,9 +103,12 @@ def load_reference_state_dict(model: torch.nn.Module, sd: Dict[str, torch.Tensor
             src = mapped[k]
             if tuple(src.shape) != tuple(t.shape):
                 raise ValueError(f"{k}: shape {tuple(src.shape)} vs {tuple(t.shape)}")
-            t.data.copy_(src.to(device=t.device, dtype=t.dtype))
-    if hasattr(model, "refresh_frozen_copies"):
-        model.refresh_frozen_copies()
+            # an in-place copy under no_grad bumps the tensor version (caches keyed on it see the
+            # new values) and keeps flat optimizer buffers that alias the parameter valid
+            t.copy_(src.to(device=t.device, dtype=t.dtype))
+    for mod in model.modules():
+        if hasattr(mod, "refresh_frozen_copies"):
+            mod.refresh_frozen_copies()
     return missing, unexpected
 
 
@@ -112,6 +122,11 @@ def trainer_checkpoint(trainer, epoch: int, step: int, best_loss: float = float(
     rng_state = {"torch": torch.get_rng_state(),
                  "cuda": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else [],
                  "numpy": np.random.get_state(), "python": random.getstate()}
+    ve = getattr(trainer.model, "visual_embedder", None)
+    if ve is not None and hasattr(ve, "_mask_gen"):
+        # extra key (the reference ignores it): the host generator of the patch-dropout masks,
+        # so a resumed run draws the masks an uninterrupted one would
+        rng_state["triad_patch_mask"] = ve._mask_gen.get_state()
     ck = {"epoch": epoch, "step": step, "current_batch_idx": current_batch_idx, "current_segment": current_segment,
           "rng_state": rng_state, "model_state_dict": reference_state_dict(trainer.model, trainer.space)}
     for n in _OPTS:
@@ -170,5 +185,8 @@ def load_checkpoint(trainer, path_or_dict, restore_rng: bool = True) -> dict:
                 torch.cuda.set_rng_state(torch.as_tensor(s, dtype=torch.uint8).cpu(), device=i)
         np.random.set_state(rs["numpy"])
         random.setstate(rs["python"])
+        ve = getattr(trainer.model, "visual_embedder", None)
+        if rs.get("triad_patch_mask") is not None and ve is not None and hasattr(ve, "_mask_gen"):
+            ve._mask_gen.set_state(torch.as_tensor(rs["triad_patch_mask"], dtype=torch.uint8).cpu())
     trainer._update_frozen_params(trainer.global_step)
     return ck

@@ -74,13 +74,34 @@ class LazyStats(Mapping):
         return repr(dict(self._materialise()))
 
 
+RANDOM_INIT = {}  # backbone / tokenizer name -> reason it is NOT the pretrained one (reported by bench)
+
+
+def _hub_online():
+    """from_pretrained may reach the network only when asked to (TRIAD_HF_ONLINE=1): this build
+    runs on machines without egress, where a download attempt would stall, not fail."""
+    import os
+    return os.environ.get("TRIAD_HF_ONLINE", "0") == "1"
+
+
+def _fallback(name, what, err):
+    """Record and announce LOUDLY that `name` runs without its pretrained weights / vocabulary."""
+    RANDOM_INIT[name] = f"{what}: {type(err).__name__}: {str(err).splitlines()[0][:160] if str(err) else ''}"
+    warnings.warn(f"triad_amd: '{name}' is not available locally ({type(err).__name__}); using {what}. "
+                  "Results are NOT those of the pretrained model (set TRIAD_HF_ONLINE=1 to allow a "
+                  "download, or populate the HF cache).", RuntimeWarning, stacklevel=3)
+
+
 def _hf_model(kind, name, config_overrides=None):
-    """Load `name` from a local HF cache if present, else random-init its architecture."""
+    """Load `name` from the HF cache (or the hub with TRIAD_HF_ONLINE=1); when it is not there
+    (OSError -- the only failure that means "no such local checkpoint"), random-init its
+    architecture, warn and record it in RANDOM_INIT. Any other error propagates."""
     import transformers
     try:
-        return install_fast_linear(getattr(transformers, kind).from_pretrained(name, local_files_only=True))
-    except Exception:
-        pass
+        return install_fast_linear(getattr(transformers, kind).from_pretrained(
+            name, local_files_only=not _hub_online()))
+    except OSError as e:
+        _fallback(name, "random-init " + kind, e)
     cfg_cls = {"HubertModel": transformers.HubertConfig, "DistilBertModel": transformers.DistilBertConfig}[kind]
     cfg = cfg_cls(**(config_overrides or {}))
     try:
@@ -184,8 +205,9 @@ class TextEmbedder(nn.Module):
         super().__init__()
         try:
             from transformers import AutoTokenizer
-            self.tokenizer = AutoTokenizer.from_pretrained(model_name, local_files_only=True)
-        except Exception:
+            self.tokenizer = AutoTokenizer.from_pretrained(model_name, local_files_only=not _hub_online())
+        except OSError as e:
+            _fallback(model_name + " (tokenizer)", "HashTokenizer (hashed word ids)", e)
             self.tokenizer = HashTokenizer()
         self.encoder = install_fused_distilbert(_hf_model("DistilBertModel", model_name))
         self.projection1 = nn.Linear(self.encoder.config.hidden_size, 512)
@@ -214,19 +236,44 @@ class TextEmbedder(nn.Module):
         return _project(self, h), inputs["attention_mask"]
 
 
+def _dist_rank():
+    import torch.distributed as dist
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def _load_dinov2_base(vit, arch):
+    """The reference fetches pretrained DINOv2 through torch.hub (model.py:218). Offline, a hub
+    state dict saved to a file can be named by TRIAD_DINOV2_WEIGHTS (loaded weights_only); the
+    hub parameter names match this restatement. Without it the base is random-init (warned,
+    recorded in RANDOM_INIT)."""
+    import os
+    path = os.environ.get("TRIAD_DINOV2_WEIGHTS")
+    if path:
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        vit.load_state_dict(sd, strict=True)
+        return
+    _fallback(f"facebookresearch/dinov2:{arch}", "random-init DINOv2 restatement (triad_amd.vit)",
+              OSError("torch.hub is not reachable offline and TRIAD_DINOV2_WEIGHTS is not set"))
+
+
 class ViTLoRAEmbedder(nn.Module):
     """DINOv2(-reg) + LoRA + projection head + patch dropout (model.py:207-329)."""
 
     def __init__(self, model_name="facebookresearch/dinov2", arch="dinov2_vitb14", embedding_dim=512,
                  dropout_prob=0.1, lora_rank=8, lora_alpha=16):
         super().__init__()
-        self.model = apply_lora(DinoVisionTransformer(arch), lora_rank, lora_alpha)
+        self.model = DinoVisionTransformer(arch)
+        _load_dinov2_base(self.model, arch)
+        self.model = apply_lora(self.model, lora_rank, lora_alpha)
         self.projection1 = nn.Linear(self.model.embed_dim, 512)
         self.layer_norm = nn.LayerNorm(512)
         self.projection2 = nn.Linear(512, embedding_dim)
         self.patch_dropout_rate = dropout_prob
+        # host generator of the patch-dropout masks; its state is saved in trainer checkpoints
+        # (checkpoint.trainer_checkpoint) and, in Mode R, the rank is mixed into its seed so
+        # replicas seeded alike still draw different masks
         self._mask_gen = torch.Generator()
-        self._mask_gen.manual_seed(torch.initial_seed() % (2 ** 63))
+        self._mask_gen.manual_seed((torch.initial_seed() + 0x9E3779B1 * _dist_rank()) % (2 ** 63))
         self.mask_world = (1, 0)  # (W, rank): draw the global (W*B, N) mask, keep this rank's rows
 
     def set_global_mask(self, world, rank, seed=1234):

@@ -84,8 +84,20 @@ class FlatParamSpace:
                     self._hooks.append(p.register_post_accumulate_grad_hook(self._mark(i)))
         self.shadow_base = (torch.from_numpy(shadow_base.view(np.int64)).to(self.device)
                             if self.shadowed.any() else None)
+        # where each shadowed bf16 model weight lived when shadow_base was taken: the AdamW
+        # kernel writes there, so check_shadows() refuses to launch if one has moved
+        self._shadow_ptrs = {int(i): self.params[i].data_ptr() for i in np.nonzero(self.shadowed)[0]}
         self._chunk_cache: Dict[tuple, tuple] = {}
         self._index_cache: Dict[tuple, torch.Tensor] = {}
+
+    def check_shadows(self, ids: Sequence[int]):
+        """Raise if a shadowed parameter's bf16 storage was reallocated (model.to(), p.data = ...)
+        since the flat space was built: the step would otherwise write into freed memory."""
+        for i in ids:
+            want = self._shadow_ptrs.get(int(i))
+            if want is not None and self.params[i].data_ptr() != want:
+                raise TriadError(f"parameter {i} ({tuple(self.params[i].shape)}) was reallocated after the "
+                                 "optimizer was built; rebuild the trainer (FlatParamSpace) after moving the model")
 
     def _mark(self, i):
         def hook(_p):
@@ -231,6 +243,7 @@ class FusedAdamW(torch.optim.Optimizer):
             pp[3 * i + 1] = 1.0 / math.sqrt(bc2)
             pp[3 * i + 2] = 1.0 - lr * wd
         pp_dev = host.to(sp.device, non_blocking=True)
+        sp.check_shadows(ids)
         table, n, _ = sp.chunks(ids)
         call("triad_adamw_step", ptr(sp.flat_p), ptr(sp.flat_g), ptr(sp.exp_avg), ptr(sp.exp_avg_sq), ptr(table), n,
              ptr(pp_dev), ptr(sp.scale), float(b1), float(b2), float(eps), ptr(sp.shadow_base),

@@ -259,6 +259,10 @@ class DinoVisionTransformer(nn.Module):
             if m.bias is not None:
                 nn.init.zeros_(m.bias)
 
+    def refresh_frozen_copies(self):
+        """Called after a state_dict load: drop the cached interpolated positional embedding."""
+        self._pos_cache = {}
+
     def interpolate_pos_encoding(self, n_patches_h, n_patches_w, dtype):
         key = (n_patches_h, n_patches_w, dtype, self.pos_embed._version)
         if not self.pos_embed.requires_grad and key in self._pos_cache:
@@ -352,10 +356,18 @@ def store_frozen_base_bf16(vit: nn.Module):
     they never change (frozen, model.py:223-224,261-262), so storing the cast once gives
     bit-identical matmul operands and removes ~86 M x 6 B of cast traffic and ~170 cast
     launches per step. LayerNorm / LayerScale / token parameters stay fp32 (autocast keeps
-    their ops in fp32)."""
-    for mod in vit.modules():
+    their ops in fp32).
+
+    The fp32 values are kept (host memory, `vit.frozen_fp32`, keyed by parameter name): they
+    are what a checkpoint saves (the reference keeps the frozen base in fp32, train.py:413), so
+    a reference checkpoint loaded here and saved again comes back bit-exact."""
+    masters = {}
+    for mname, mod in vit.named_modules():
         if isinstance(mod, (nn.Linear, nn.Conv2d)):
-            for p in mod.parameters(recurse=False):
-                if not p.requires_grad:
+            for pname, p in mod.named_parameters(recurse=False):
+                if not p.requires_grad and p.dtype != torch.bfloat16:
+                    masters[f"{mname}.{pname}" if mname else pname] = p.data.detach().to("cpu", torch.float32,
+                                                                                            copy=True)
                     p.data = p.data.to(torch.bfloat16)
+    vit.frozen_fp32 = {**getattr(vit, "frozen_fp32", {}), **masters}
     return vit
