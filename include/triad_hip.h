@@ -127,12 +127,24 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
 int triad_gemm_set_form(int form);
 
 /* Fused projection head forward (model.py:32-34,68 / 81-83,116 / 253-255,326 under bf16
- * autocast): y = bf16(LN(bf16(h W1^T + b1)) W2^T + b2) for M rows of H features; also
- * saves y1 = bf16(h W1^T + b1), ln = bf16(LN(y1)), mean/rstd per row for the backward.
- * W1 [512][H], W2 [512][512] bf16 (nn.Linear layout); b1, b2, gamma, beta fp32. */
+ * autocast): y = bf16(LN(bf16(h W1^T + b1)) W2^T + b2) for M rows of H features (H % 32 == 0);
+ * also saves y1 = bf16(h W1^T + b1), ln = bf16(LN(y1)) ([M][512] bf16) and mean / rstd per row
+ * for the backward. W1 [512][H], W2 [512][512] bf16 (nn.Linear layout); b1, b2 (bf16-valued),
+ * gamma, beta fp32. Persistent row-panel kernel: each wave owns 32 rows x 512 features. */
 int triad_projhead_fwd(const void* h, int M, int H, const void* W1, const float* b1, const float* gamma,
                        const float* beta, float eps, const void* W2, const float* b2, void* y, long long ldy,
                        void* y1, void* ln, float* mean, float* rstd, hipStream_t stream);
+
+/* Fused projection head backward, row part (autograd of the head under autocast, H % 256 == 0):
+ * dln = bf16(dy W2), dy1 = bf16(LN'(dln)) (fp32 LayerNorm backward at y1 / mean / rstd / gamma),
+ * dh = bf16(dy1 W1) into dh (row stride ldh); dy1 [M][512] written for the weight gradients.
+ * W2t = W2^T [512][512], W1t = W1^T [H][512] bf16. colpart: triad_projhead_bwd_slabs(M) slabs of
+ * [3][512] fp32 partial column sums (dgamma, dbeta, db1), reduced by triad_sum_slabs.
+ * dW2 = dy^T ln, dW1 = dy1^T h and db2 = colsum(dy) are the caller's (split-K GEMM, triad_colsum). */
+int triad_projhead_bwd_slabs(int M);
+int triad_projhead_bwd(const void* dy, int M, int H, const void* W2t, const void* W1t, const void* y1,
+                       const float* mean, const float* rstd, const float* gamma, void* dy1, void* dh, long long ldh,
+                       float* colpart, hipStream_t stream);
 
 /* LayerNorm(512) backward: dy1 (bf16) from dln (fp32), y1, mean, rstd, gamma; per-block
  * column partials of dgamma / dbeta in dgb_part [nblocks][2][512]. */
@@ -305,6 +317,28 @@ int triad_geludrop_fwd(const void* u, long long n, float p, unsigned seed, const
 int triad_geludrop_bwd(const void* u, const void* dv, long long n, float p, unsigned seed, const void* table, void* du,
                        hipStream_t stream);
 int triad_dropout_keep(long long n, float p, unsigned seed, void* out, hipStream_t stream);
+
+/* Materialising debug path (csrc/dense.hip; SURVEY §8b keeps the reference's small-B methods):
+ * S = token similarities fp32 (Bq, Bk, Nq, Nk) as model.py:384-387 / 502-505 return them.
+ * triad_dense_nparts(n): number of per-block partials the reductions below write for n elements.
+ * triad_dense_rowmax: rowmax[j][i*Nq+q] = max_k S, argmax = first max index (model.py:389 / 507);
+ *                     feeds triad_clip_reduce for clip (model.py:391 / 509-512).
+ * triad_nonneg_fwd:   part[b] = sum clamp(S, lo, 0)^2 (model.py:417-418 / 524-525).
+ * triad_nonneg_bwd:   dS = coef[0] * scale * 2 clamp(S, lo, 0) [lo <= S <= 0] (coef may be NULL = 1).
+ * triad_sims_bwd_pack: G = dtok (may be NULL) + [k == argmax] dclip[i][j] qw[r] (dclip may be NULL) as the
+ *                     bf16 GEMM operand A[i*Nq+q][j*Nk+k] (row stride lda, caller zeroes the padding) and
+ *                     part[b] = sum G * S / temp; dQ / dK are then two triad_gemm_bf16 calls.
+ * triad_sum_parts:    out[0] = scale * sum part (float). */
+int triad_dense_nparts(long long n);
+int triad_dense_rowmax(const float* S, int Bq, int Bk, int Nq, int Nk, int R_pad, float* rowmax, int* argmax,
+                       hipStream_t stream);
+int triad_nonneg_fwd(const float* S, long long n, float lo, double* part, hipStream_t stream);
+int triad_nonneg_bwd(const float* S, long long n, float lo, float scale, const float* coef, float* dS,
+                     hipStream_t stream);
+int triad_sims_bwd_pack(const float* S, const float* dtok, const float* dclip, const float* qw, const int* argmax,
+                        int Bq, int Bk, int Nq, int Nk, int R_pad, const float* temp, void* A, long long lda,
+                        double* part, hipStream_t stream);
+int triad_sum_parts(const double* part, int n, double scale, float* out, hipStream_t stream);
 
 #ifdef __cplusplus
 }

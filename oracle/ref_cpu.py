@@ -219,3 +219,103 @@ def recall_at_k(sim):
         ranks.append(int(np.where(order == i)[0][0]))
     ranks = np.array(ranks)
     return {f"r{k}": float(np.mean(ranks < k)) for k in (1, 5, 10, 20)}
+
+
+# ---- chunked form for BASELINE-size parity checks -----------------------------------------
+def head_loss_chunked(kind, q, k, temperature, q_mask=None, threshold=0.8, weight=0.01, chunk=8,
+                      dtype=torch.float64, grads=True):
+    """The same values as av_loss (kind "av", model.py:370-472) / tv_loss (kind "tv",
+    model.py:490-593), evaluated in chunks of query samples so the (B, B, Nq, Nk) tensor is never
+    held whole (c3: 13 GB in fp32). Runs on whatever device the inputs are on (plain torch;
+    test infrastructure only).
+
+    Pass 1 builds clip, the l_nonneg sum and the diagonal regulariser sums chunk by chunk; the CE
+    and the statistics are evaluated on the full (B, B) clip exactly as _symmetric_ce / _stats.
+    Pass 2 (grads=True) re-evaluates each chunk under autograd with the surrogate
+        sum(dCE/dclip * clip_chunk) + 0.15 * sum clamp(S)^2 / N_el + w_diag * diag_chunk / cnt,
+    whose gradient equals the loss gradient (every term is additive over query samples, and the
+    CE enters only through clip). Returns a dict of floats / tensors (fp64)."""
+    av = kind == "av"
+    B, Nq, _ = q.shape
+    Nk = k.shape[1]
+    lo = -60.0 if av else -20.0
+    Qd, Kd = q.detach().to(dtype), k.detach().to(dtype)
+    t = torch.as_tensor(temperature, dtype=dtype, device=q.device).detach()
+    m = None if av else q_mask.to(device=q.device, dtype=dtype)
+
+    def chunk_terms(Qc, Kall, tt, i0):
+        s = torch.einsum("iqd,jkd->ijqk", Qc, Kall) * tt
+        mx = s.max(dim=3).values
+        if av:
+            clip_c = mx.mean(dim=2)
+        else:
+            mc = m[i0:i0 + Qc.shape[0]][:, None, :]
+            clip_c = (mx * mc).sum(dim=2) / mc.sum(dim=2).clamp(min=1e-7)
+        nn_c = s.clamp(min=lo, max=0).pow(2).sum()
+        c = Qc.shape[0]
+        ar = torch.arange(c, device=q.device)
+        diag = s[ar, i0 + ar]   # (c, Nq, Nk)
+        if av:
+            d = diag[:, 1:] - diag[:, :-1]
+            dg_c = (d * d).sum()
+        else:
+            frac = torch.softmax(diag, dim=-1).sum(dim=1) / Nq
+            dg_c = F.relu(frac - threshold).pow(2).sum()
+        return clip_c, nn_c, dg_c
+
+    clip = torch.zeros(B, B, dtype=dtype, device=q.device)
+    nn_sum = torch.zeros((), dtype=dtype, device=q.device)
+    dg_sum = torch.zeros((), dtype=dtype, device=q.device)
+    with torch.no_grad():
+        for i0 in range(0, B, chunk):
+            c_, n_, d_ = chunk_terms(Qd[i0:i0 + chunk], Kd, t, i0)
+            clip[i0:i0 + chunk] = c_
+            nn_sum += n_
+            dg_sum += d_
+    n_el = float(B) * B * Nq * Nk
+    cnt = float(B * (Nq - 1) * Nk) if av else float(B * Nk)
+    l_nonneg = nn_sum / n_el
+    l_dg = dg_sum / cnt if cnt > 0 else torch.full((), float("nan"), dtype=dtype, device=q.device)
+    l_cal = (-torch.log(t)).clamp(min=0).pow(2)
+    if av:
+        reg = 20 * l_cal + 0.15 * l_nonneg + 0.01 * l_dg
+        aux = 0.01 * l_dg
+        w_dg = 0.01
+    else:
+        reg = 0.15 * l_nonneg + weight * l_dg
+        aux = l_dg
+        w_dg = weight
+    cl = clip.clone().requires_grad_(True)
+    ce = _symmetric_ce_dev(cl)
+    ce.backward()
+    ce = ce.detach()
+    dclip = cl.grad.detach()
+    keys = AV_STAT_KEYS if av else TV_STAT_KEYS
+    stats = _stats(clip.cpu(), keys)
+    out = dict(total=float(ce + reg), ce=float(ce), reg=float(reg), aux=float(aux), l_nonneg=float(l_nonneg),
+               l_cal=float(l_cal), diag=float(l_dg), stats=stats, clip=clip)
+    if not grads:
+        return out
+    Qg = Qd.clone().requires_grad_(True)
+    Kg = Kd.clone().requires_grad_(True)
+    tg = t.clone().requires_grad_(True)
+    for i0 in range(0, B, chunk):
+        c_, n_, d_ = chunk_terms(Qg[i0:i0 + chunk], Kg, tg, i0)
+        sur = (dclip[i0:i0 + chunk] * c_).sum() + 0.15 * n_ / n_el + (w_dg * d_ / cnt if cnt > 0 else 0.0)
+        sur.backward()
+    dtemp = tg.grad.detach().clone()
+    if av:
+        tc = t.clone().requires_grad_(True)
+        (20 * (-torch.log(tc)).clamp(min=0).pow(2)).backward()
+        dtemp += tc.grad
+    out.update(dq=Qg.grad.detach(), dk=Kg.grad.detach(), dtemp=float(dtemp))
+    return out
+
+
+def _symmetric_ce_dev(clip):
+    """_symmetric_ce on any device."""
+    n = clip.shape[0]
+    idx = torch.arange(n, device=clip.device)
+    row = -F.log_softmax(clip, dim=1)[idx, idx]
+    col = -F.log_softmax(clip.t(), dim=1)[idx, idx]
+    return (row + col).mean() / 2

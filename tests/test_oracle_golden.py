@@ -74,3 +74,30 @@ def test_patch_dropout_matches_reference(name):
     f = G.load(name)
     out = ref_cpu.patch_dropout(G.bf16(f["x"]), torch.from_numpy(f["keep"]))
     np.testing.assert_array_equal(out.numpy(), G.bf16(f["out"]).numpy())
+
+
+@pytest.mark.parametrize("kind", ["av", "tv"])
+def test_chunked_oracle_equals_materialising_oracle(kind):
+    """ref_cpu.head_loss_chunked (used for the BASELINE-size GPU parity tests) reproduces the
+    materialising restatement -- losses, statistics and all gradients -- with zero-padded keys,
+    a ragged text mask, and chunks that do not divide B."""
+    g = torch.Generator().manual_seed(0)
+    B, Nq, Nk = 7, 9, 13
+    q = torch.randn(B, Nq, 512, generator=g, dtype=torch.float64) * 0.58
+    k = torch.randn(B, Nk, 512, generator=g, dtype=torch.float64) * 0.58
+    k[2, 9:] = 0
+    mask = (torch.arange(Nq)[None] < torch.randint(1, Nq + 1, (B, 1), generator=g)).long()
+    t = torch.tensor(0.9, dtype=torch.float64, requires_grad=True)
+    qr, kr = q.clone().requires_grad_(True), k.clone().requires_grad_(True)
+    if kind == "av":
+        tot, ce, reg, sm, st = ref_cpu.av_loss(qr, kr, t)
+    else:
+        tot, st = ref_cpu.tv_loss(qr, kr, mask, t, 0.1, 0.3)
+    tot.backward()
+    o = ref_cpu.head_loss_chunked(kind, q, k, 0.9, q_mask=mask, threshold=0.1, weight=0.3, chunk=3)
+    assert abs(o["total"] - float(tot)) < 1e-12 * abs(float(tot))
+    for key in st:
+        assert abs(o["stats"][key] - st[key]) < 1e-12 * max(1.0, abs(st[key]))
+    assert torch.allclose(o["dq"], qr.grad, rtol=0, atol=1e-14)
+    assert torch.allclose(o["dk"], kr.grad, rtol=0, atol=1e-14)
+    assert abs(o["dtemp"] - float(t.grad)) < 1e-12 * abs(float(t.grad))

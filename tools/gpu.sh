@@ -11,6 +11,8 @@
 #   prof             rocprofv3 --kernel-trace --stats of a 3-step bench -> gpurun_out/<tag>_prof/
 #   pmc:<name>:<counters>  one rocprofv3 --pmc pass (counters comma-separated) of a 3-step bench
 #   py:<script args>       python <script> (tools/ micro-benchmarks)    -> gpurun_out/<tag>_py<N>.log
+#   profpy:<script args>   the same under rocprofv3 --kernel-trace --stats -> gpurun_out/<tag>_profpy<N>/
+#   pmcpy:<name>:<counters>:<script args>  one rocprofv3 --pmc pass over a python script
 # environment: extra env for every step may be given as STEP_ENV="A=1 B=2" (exported first).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -18,6 +20,11 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 tag=$1; shift
 [ -n "$STEP_ENV" ] && export $STEP_ENV
+# heartbeat: long single steps (model builds, large parity tests) print nothing for minutes;
+# every step still runs under its own `timeout`
+( while sleep 50; do echo "[gpu.sh] $(date +%T) running"; done ) &
+hb=$!
+trap 'kill $hb 2>/dev/null' EXIT
 n=0
 for step in "$@"; do
   n=$((n + 1))
@@ -27,7 +34,7 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
         > "gpurun_out/${tag}_tests.log" 2>&1 ;;
     tests:*)
-      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread \
         -k "${step#tests:}" > "gpurun_out/${tag}_tests.log" 2>&1 ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "gpurun_out/${tag}_smoke.log" 2>&1 ;;
@@ -43,6 +50,13 @@ for step in "$@"; do
       rest=${step#pmc:}; name=${rest%%:*}; ctr=${rest#*:}
       timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "gpurun_out/${tag}_pmc_${name}" -o run \
         -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "gpurun_out/${tag}_pmc_${name}.log" 2>&1 ;;
+    profpy:*)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${tag}_profpy${n}" -o run \
+        -- python3 ${step#profpy:} > "gpurun_out/${tag}_profpy${n}.log" 2>&1 ;;
+    pmcpy:*)
+      rest=${step#pmcpy:}; name=${rest%%:*}; rest=${rest#*:}; ctr=${rest%%:*}; script=${rest#*:}
+      timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "gpurun_out/${tag}_pmcpy_${name}" -o run \
+        -- python3 $script > "gpurun_out/${tag}_pmcpy_${name}.log" 2>&1 ;;
     py:*)
       timeout -k 10 600 python ${step#py:} > "gpurun_out/${tag}_py${n}.log" 2>&1 ;;
     *)

@@ -35,6 +35,8 @@ SIGNATURES = {
     "triad_gemm_bf16": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, i32, vp],
     "triad_gemm_bf16_splitk": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp],
     "triad_projhead_fwd": [vp, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, i64, vp, vp, vp, vp, vp],
+    "triad_projhead_bwd_slabs": [i32],
+    "triad_projhead_bwd": [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp],
     "triad_ln_bwd": [vp, vp, vp, vp, vp, i32, vp, vp, i32, vp],
     "triad_sum_slabs": [vp, i32, i64, vp, i32, vp, vp],
     "triad_colsum_splits": [i64, i32],
@@ -77,13 +79,20 @@ SIGNATURES = {
     "triad_attn_fwd": [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, f32, vp, i64, i64, vp, vp],
     "triad_attn_bwd": [vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, i32, i32, i32,
                        i32, f32, vp, i64, i64, vp, i64, i64, vp, i64, i64, vp, vp],
+    "triad_dense_nparts": [i64],
+    "triad_dense_rowmax": [vp, i32, i32, i32, i32, i32, vp, vp, vp],
+    "triad_nonneg_fwd": [vp, i64, f32, vp, vp],
+    "triad_nonneg_bwd": [vp, i64, f32, f32, vp, vp, vp],
+    "triad_sims_bwd_pack": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, vp, i64, vp, vp],
+    "triad_sum_parts": [vp, i32, f64, vp, vp],
 }
 # entry points returning a value rather than a status
 RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_longlong,
             "triad_conv0_dw_workspace_bytes": C.c_longlong, "triad_gelu_table_bytes": C.c_longlong,
             "triad_posconv_dw_part_bytes": C.c_longlong,
             "triad_lora_tn_blocks": C.c_int, "triad_dropaddln_bwd_blocks": C.c_int,
-            "triad_colsum_splits": C.c_int}
+            "triad_colsum_splits": C.c_int, "triad_dense_nparts": C.c_int,
+            "triad_projhead_bwd_slabs": C.c_int}
 
 _lock = threading.Lock()
 _lib = None

@@ -1,208 +1,11 @@
-// Fused per-token projection head proj2(LN(proj1(h))) (SajayR/TRIAD src/model.py:32-34,68 /
-// 81-83,116 / 253-255,326) under bf16 autocast semantics (model.py:483,603):
-//   y1  = bf16(h . W1^T + b1)                  Linear(H -> 512), bf16 out
-//   ln  = LayerNorm(y1) in fp32 (eps 1e-5), affine, then bf16 for the next Linear
-//   y   = bf16(ln . W2^T + b2)                 Linear(512 -> 512), bf16 out
-// One workgroup owns 64 token rows x all 512 features, so the LayerNorm row
-// statistics never leave the chip and `ln` feeds the second GEMM from LDS.
-// Also: LayerNorm backward, column sums (bias / affine grads) and the split-K
-// reduce used by the head's backward GEMMs.
+// Projection-head helpers (the head itself is csrc/projhead_rows.hip): the standalone LayerNorm
+// backward (heads whose width does not tile the fused backward), column sums (bias gradients,
+// also of the backbones) and the split-K slab reduce.
 #include "common.h"
 
 namespace {
 
-constexpr int PM = 64;        // rows per workgroup
 constexpr int PN = 512;       // projection width
-constexpr int PK = 32;        // k per stage
-constexpr int PWAVES = 8;     // wave w owns columns [64w, 64w+64)
-constexpr int A_STAGE = PM * PK;           // 2048 elems (4 KB)
-constexpr int B_STAGE = PN * PK;           // 16384 elems (32 KB)
-constexpr int STAGE = A_STAGE + B_STAGE;
-constexpr int LN_ELEMS = PM * PN;          // 64 KB bf16 LN output (GEMM2 A operand)
-
-// [rows][32 k] images with 64-B rows: 16-B chunk c (0..3) of row m at c ^ ((m >> 2) & 3)
-__device__ __forceinline__ int k32_off(int m, int c) { return m * PK + ((c ^ ((m >> 2) & 3)) << 3); }
-// [64 rows][512 k] LN image, 1 KB rows: chunk c (0..63) at c ^ (m & 15)
-__device__ __forceinline__ int ln_off(int m, int c) { return m * PN + ((c ^ (m & 15)) << 3); }
-
-// Stage rows [r0, r0+nrows) x k [k0, k0+32) of a k-contiguous bf16 matrix into a k32 image.
-// One wave-instruction covers 16 rows x 64 B. Rows >= limit read row limit-1 (masked later).
-__device__ __forceinline__ void stage_k32(const bf16* __restrict__ X, long long ld, int r0, int nrows, int limit,
-                                          int k0, bf16* dst, int wave, int lane) {
-  const int ninst = nrows / 16;
-  for (int inst = wave; inst < ninst; inst += PWAVES) {
-    const int m = inst * 16 + (lane >> 2), cp = lane & 3;
-    const int c = cp ^ ((m >> 2) & 3);
-    int r = r0 + m;
-    r = r < limit ? r : limit - 1;
-    glds16(X + (size_t)r * ld + k0 + c * 8, dst + inst * 512);
-  }
-}
-
-__global__ __launch_bounds__(512, 1) void projhead_fwd_kernel(
-    const bf16* __restrict__ h, int M, int H, const bf16* __restrict__ W1, const float* __restrict__ b1,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, const bf16* __restrict__ W2,
-    const float* __restrict__ b2, bf16* __restrict__ y, long long ldy, bf16* __restrict__ y1_out,
-    bf16* __restrict__ ln_out, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * STAGE + LN_ELEMS + 2 * PWAVES * PM * 2];
-  bf16* lnimg = lds + 2 * STAGE;
-  float* red = (float*)(lnimg + LN_ELEMS);  // [PWAVES][PM]
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h2 = lane >> 5,
-            l32 = lane & 31;
-  const int r0 = blockIdx.x * PM;
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){};
-
-  // ---------------- GEMM1: y1 = h . W1^T ----------------
-  const int nk1 = H / PK;
-  stage_k32(h, H, r0, PM, M, 0, lds, wave, lane);
-  stage_k32(W1, H, 0, PN, PN, 0, lds + A_STAGE, wave, lane);
-  for (int kt = 0; kt < nk1; ++kt) {
-    lds_dma_barrier();
-    if (kt + 1 < nk1) {
-      bf16* nb = lds + ((kt + 1) & 1) * STAGE;
-      stage_k32(h, H, r0, PM, M, (kt + 1) * PK, nb, wave, lane);
-      stage_k32(W1, H, 0, PN, PN, (kt + 1) * PK, nb + A_STAGE, wave, lane);
-    }
-    const bf16* ai = lds + (kt & 1) * STAGE;
-    const bf16* bi = ai + A_STAGE;
-#pragma unroll
-    for (int s = 0; s < PK / 16; ++s) {
-      bf16x8 af[2], bfr[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        af[t] = *(const bf16x8*)(ai + k32_off(t * 32 + l32, 2 * s + h2));
-        bfr[t] = *(const bf16x8*)(bi + k32_off(wave * 64 + t * 32 + l32, 2 * s + h2));
-      }
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[a], bfr[b], acc[a][b]);
-    }
-  }
-
-  // ---------------- bias, bf16 rounding, LayerNorm ----------------
-  // lane holds column n = wave*64 + b*32 + l32 for rows m = a*32 + (v&3) + 8(v>>2) + 4*h2.
-  float colb1[2], colg[2], colbt[2];
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const int n = wave * 64 + b * 32 + l32;
-    colb1[b] = b1[n];
-    colg[b] = gamma[n];
-    colbt[b] = beta[n];
-  }
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[a][b][v] = (float)(bf16)(acc[a][b][v] + colb1[b]);
-  // row sums: over the 2 column tiles, the 32 lanes of a half, then the 8 waves (LDS)
-  float mean[2][16], rstd[2][16];
-  for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        float s;
-        if (pass == 0) s = acc[a][0][v] + acc[a][1][v];
-        else {
-          const float d0 = acc[a][0][v] - mean[a][v], d1 = acc[a][1][v] - mean[a][v];
-          s = d0 * d0 + d1 * d1;
-        }
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o);  // within the 32-lane half
-        const int m = a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h2;
-        if (l32 == 0) red[wave * PM + m] = s;
-      }
-    __syncthreads();
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h2;
-        float t = 0.f;
-#pragma unroll
-        for (int w = 0; w < PWAVES; ++w) t += red[w * PM + m];
-        if (pass == 0) mean[a][v] = t * (1.f / PN);
-        else rstd[a][v] = rsqrtf(t * (1.f / PN) + eps);
-      }
-    __syncthreads();
-  }
-  // normalise, affine, round to bf16; save y1 / ln / stats; LN image in LDS for GEMM2
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int n = wave * 64 + b * 32 + l32;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h2;
-        const float x = acc[a][b][v];
-        const bf16 lnv = (bf16)((x - mean[a][v]) * rstd[a][v] * colg[b] + colbt[b]);
-        lnimg[ln_off(m, n >> 3) + (n & 7)] = lnv;
-        if (r0 + m < M) {
-          y1_out[(size_t)(r0 + m) * PN + n] = (bf16)x;
-          ln_out[(size_t)(r0 + m) * PN + n] = lnv;
-        }
-      }
-    }
-  if (wave == 0) {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h2;
-        if (l32 == 0 && r0 + m < M) {
-          mean_out[r0 + m] = mean[a][v];
-          rstd_out[r0 + m] = rstd[a][v];
-        }
-      }
-  }
-
-  // ---------------- GEMM2: y = ln . W2^T + b2 ----------------
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){};
-  const int nk2 = PN / PK;
-  __syncthreads();  // LN image complete; staging buffers free
-  stage_k32(W2, PN, 0, PN, PN, 0, lds + A_STAGE, wave, lane);
-  for (int kt = 0; kt < nk2; ++kt) {
-    lds_dma_barrier();
-    if (kt + 1 < nk2) stage_k32(W2, PN, 0, PN, PN, (kt + 1) * PK, lds + ((kt + 1) & 1) * STAGE + A_STAGE, wave, lane);
-    const bf16* bi = lds + (kt & 1) * STAGE + A_STAGE;
-#pragma unroll
-    for (int s = 0; s < PK / 16; ++s) {
-      bf16x8 af[2], bfr[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        af[t] = *(const bf16x8*)(lnimg + ln_off(t * 32 + l32, kt * 4 + 2 * s + h2));
-        bfr[t] = *(const bf16x8*)(bi + k32_off(wave * 64 + t * 32 + l32, 2 * s + h2));
-      }
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = mfma32(af[a], bfr[b], acc[a][b]);
-    }
-  }
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const int n = wave * 64 + b * 32 + l32;
-    const float bias = b2[n];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h2;
-        if (r0 + m < M) y[(size_t)(r0 + m) * ldy + n] = (bf16)(acc[a][b][v] + bias);
-      }
-  }
-}
 
 // LayerNorm backward, one wave per row (512 features, 8 per lane):
 //   xh = (y1 - mean) * rstd;  g = dln * gamma
@@ -333,17 +136,6 @@ __global__ __launch_bounds__(256) void sum_slabs_kernel(const float* __restrict_
 }  // namespace
 
 extern "C" {
-
-int triad_projhead_fwd(const void* h, int M, int H, const void* W1, const float* b1, const float* gamma,
-                       const float* beta, float eps, const void* W2, const float* b2, void* y, long long ldy,
-                       void* y1, void* ln, float* mean, float* rstd, hipStream_t stream) {
-  if (M <= 0 || H % PK || H < PK) return TRIAD_EINVAL;
-  const int grid = (M + PM - 1) / PM;
-  hipLaunchKernelGGL(projhead_fwd_kernel, dim3(grid), dim3(512), 0, stream, (const bf16*)h, M, H, (const bf16*)W1,
-                     b1, gamma, beta, eps, (const bf16*)W2, b2, (bf16*)y, ldy, (bf16*)y1, (bf16*)ln, mean, rstd);
-  TRIAD_CHECK_LAUNCH();
-  return TRIAD_OK;
-}
 
 int triad_ln_bwd(const float* dln, const void* y1, const float* mean, const float* rstd, const float* gamma, int M,
                  void* dy1, float* dgb_part, int nblocks, hipStream_t stream) {

@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import _lib, attention, frontend, ops
+from . import _lib, attention, dense, frontend, ops
 from .linear import install_fast_linear
 from .postln import install_fused_distilbert, install_fused_encoder
 from .vit import DinoVisionTransformer, apply_lora, store_frozen_base_bf16
@@ -356,14 +356,46 @@ class MultiModalModel(nn.Module):
                                                    group=self.negatives_group)
         return (losses[0], LazyStats(_TV_KEYS, stats)), clip
 
+    # ---- materialising debug path (small B), reference model.py:370-593 -------
+    # Same names, arguments, composition and return tuples as the reference; every piece is a
+    # differentiable HIP op of triad_amd.dense, so autograd through these matches the reference's.
     def compute_all_similarities_av(self, audio_feats, visual_feats):
-        """Materialising debug path (small B only): (clip (B,B), token_sims (B,B,Na,Nv))."""
-        clip = ops.clip_similarities(ops.AV, audio_feats, visual_feats, self.temperature)
-        return clip, ops.token_similarities(audio_feats, visual_feats, self.temperature)
+        """-> (clip_sims (B,B), token_sims (B,B,Na,Nv) fp32) (model.py:370-392)."""
+        return dense.all_similarities(audio_feats, visual_feats, self.temperature)
+
+    def compute_temporal_smoothness_loss(self, token_sims):
+        """mean of squared steps along Na over the diagonal pairs (model.py:394-408)."""
+        return dense.diag_smoothness(token_sims)
+
+    def compute_regularization_losses_av(self, token_sims):
+        """-> (20 l_cal + 0.15 l_nonneg + 0.01 l_smooth, 0.01 l_smooth) (model.py:410-428)."""
+        l_nonneg = dense.nonneg(token_sims, ops.CLAMP_LO[ops.AV])
+        l_cal = torch.clamp(-torch.log(self.temperature), min=0) ** 2   # log(1) - log(temp); temp_high unused
+        l_smooth = self.compute_temporal_smoothness_loss(token_sims)
+        reg_loss = 20 * l_cal + 0.15 * l_nonneg + 0.01 * l_smooth
+        return reg_loss, 0.01 * l_smooth
+
+    def compute_contrastive_loss_av(self, clip_sims, token_sims):
+        """-> (contrastive + reg, contrastive, reg, 0.01 l_smooth, stats) (model.py:430-472)."""
+        contrastive_loss, st = dense.clip_ce(clip_sims)
+        reg_loss, l_smooth = self.compute_regularization_losses_av(token_sims)
+        return contrastive_loss + reg_loss, contrastive_loss, reg_loss, l_smooth, LazyStats(_AV_KEYS, st)
 
     def compute_all_similarities_tv(self, text_feats, visual_feats, attention_mask):
-        clip = ops.clip_similarities(ops.TV, text_feats, visual_feats, self.temperature, q_mask=attention_mask)
-        return clip, ops.token_similarities(text_feats, visual_feats, self.temperature)
+        """-> (clip_sims (B,B) masked mean over Nt, token_sims (B,B,Nt,Nv) fp32) (model.py:490-514)."""
+        return dense.all_similarities(text_feats, visual_feats, self.temperature, q_mask=attention_mask)
+
+    def compute_regularization_losses_tv(self, token_sims):
+        """-> 0.15 l_nonneg + w * sparsity (model.py:516-542)."""
+        l_nonneg = dense.nonneg(token_sims, ops.CLAMP_LO[ops.TV])
+        loss_sparsity = dense.diag_sparsity(token_sims, self.patch_sparsity_threshold)
+        return 0.15 * l_nonneg + self.patch_sparsity_weight * loss_sparsity
+
+    def compute_contrastive_loss_tv(self, clip_sims, token_sims):
+        """-> (contrastive + reg, stats) (model.py:544-593)."""
+        contrastive_loss, st = dense.clip_ce(clip_sims)
+        reg_loss = self.compute_regularization_losses_tv(token_sims)
+        return contrastive_loss + reg_loss, LazyStats(_TV_KEYS, st)
 
     def forward_audio_visual(self, frames, audio):
         """-> (total, contrastive, reg, 0.01*l_smooth, stats) (model.py:474-488)."""

@@ -382,6 +382,8 @@ class _ProjectionHead(torch.autograd.Function):
         st = stream_ptr(dev)
         f32 = torch.float32
         dyp = _pad_rows(dy.reshape(M, D).to(torch.bfloat16), Mp)
+        if H % 256 == 0:
+            return _projhead_bwd_fused(ctx, dyp, hb, w1b, w2b, g32, y1, ln, mean, rstd)
         # d ln = dy . W2          [Mp][512] fp32
         dln = torch.empty(Mp, D, dtype=f32, device=dev)
         call("triad_gemm_bf16", ptr(dyp), D, 1, ptr(w2b), D, 0, Mp, D, D, None, ptr(dln), D, 0, st)
@@ -413,6 +415,39 @@ class _ProjectionHead(torch.autograd.Function):
         hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
         return (dh[:M].view(*lead, H).to(hd), dw1.to(w1d), db1.to(b1d), dgb[0].to(gd), dgb[1].to(bd), dw2.to(w2d),
                 db2.to(b2d), None)
+
+
+def _projhead_bwd_fused(ctx, dyp, hb, w1b, w2b, g32, y1, ln, mean, rstd):
+    """Backward of the projection head on the fused row-panel kernel (triad_projhead_bwd: dln,
+    LayerNorm backward, dh and the dgamma / dbeta / db1 column sums in one pass over the rows) plus
+    the two weight-gradient GEMMs over the tokens (split-K) and db2."""
+    lead, H, M, Mp = ctx.shape
+    dev = dyp.device
+    st = stream_ptr(dev)
+    f32 = torch.float32
+    w2t = w2b.t().contiguous()
+    w1t = w1b.t().contiguous()
+    dy1 = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
+    if Mp > M:
+        dy1[M:].zero_()
+    dh = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    ns = call("triad_projhead_bwd_slabs", M)
+    colpart = torch.empty(ns * 3 * D, dtype=f32, device=dev)
+    call("triad_projhead_bwd", ptr(dyp), M, H, ptr(w2t), ptr(w1t), ptr(y1), ptr(mean), ptr(rstd), ptr(g32), ptr(dy1),
+         ptr(dh), H, ptr(colpart), st)
+    cols = torch.empty(3, D, dtype=f32, device=dev)
+    call("triad_sum_slabs", ptr(colpart), ns, 3 * D, None, 0, ptr(cols), st)
+    db2 = colsum(dyp, f32)
+    sp2 = _splitk(Mp, (D // 128) * (D // 128))
+    sp1 = _splitk(Mp, (D // 128) * (H // 128))
+    slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
+    dw2 = torch.empty(D, D, dtype=f32, device=dev)
+    call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2), 0, st)
+    dw1 = torch.empty(D, H, dtype=f32, device=dev)
+    call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), 0, st)
+    hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
+    return (dh.view(*lead, H).to(hd), dw1.to(w1d), cols[2].to(b1d), cols[0].to(gd), cols[1].to(bd), dw2.to(w2d),
+            db2.to(b2d), None)
 
 
 def projection_head(h, proj1: torch.nn.Linear, layer_norm: torch.nn.LayerNorm, proj2: torch.nn.Linear):
@@ -508,35 +543,3 @@ def similarity_maps(f1: torch.Tensor, f2: torch.Tensor, temperature: torch.Tenso
         f2 = f2.unsqueeze(0)
     t = temperature.detach().reshape(1).to(torch.float32).contiguous()
     return _bmm_nt(l2_normalize(f1), l2_normalize(f2), t)
-
-
-def token_similarities(q: torch.Tensor, k: torch.Tensor, temperature: torch.Tensor) -> torch.Tensor:
-    """Materialised (Bq, Bk, Nq, Nk) token similarities (debug path for small B only)."""
-    _check_device(q, k)
-    Bq, Nq, _ = q.shape
-    Bk, Nk, _ = k.shape
-    qq = q.to(torch.bfloat16).reshape(1, Bq * Nq, D)
-    kk = k.to(torch.bfloat16).reshape(1, Bk * Nk, D)
-    t = temperature.detach().reshape(1).to(torch.float32).contiguous()
-    s = _bmm_nt(qq, kk, t)[0]
-    return s.view(Bq, Nq, Bk, Nk).permute(0, 2, 1, 3).contiguous()
-
-
-def clip_similarities(kind, q, k, temperature, q_mask=None):
-    """clip (B, B) from the fused kernel (no token tensor)."""
-    _check_device(q, k)
-    g = Geometry(q.shape[0], q.shape[1], k.shape[0], k.shape[1])
-    dev = q.device
-    st = stream_ptr(dev)
-    Qb, Kb = pack_queries(q, g), pack_keys(k, g)
-    temp = temperature.detach().reshape(1).to(torch.float32).contiguous()
-    nparts = call("triad_pairsim_nparts", g.R_pad, g.Bk)
-    rowmax = torch.empty(g.Bk, g.R_pad, dtype=torch.float32, device=dev)
-    argmax = torch.empty(g.Bk, g.R_pad, dtype=torch.int32, device=dev)
-    nn_part = torch.empty(nparts, dtype=torch.float64, device=dev)
-    call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D, ptr(temp),
-         CLAMP_LO[kind], 0, 0, ptr(rowmax), ptr(argmax), ptr(nn_part), None, None, 0, None, None, st)
-    clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
-    qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
-    call("triad_clip_reduce", ptr(rowmax), g.R_pad, g.Nq, g.Bq, g.Bk, ptr(qm), ptr(clip), None, st)
-    return clip
