@@ -28,7 +28,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "tri-modal triples/sec (whole node) + loss parity, B=256 at 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
-TRACKED = ("triad_pairsim_fwd", "triad_pairsim_dS", "triad_gemm_bf16", "triad_projhead_fwd",
+TRACKED = ("triad_pairsim_fwd", "triad_pairsim_dS", "triad_gemm_bf16", "triad_projhead_fwd", "triad_projhead_bwd",
            "triad_gemm_bf16_splitk", "triad_tile_gemm", "triad_dS_patch", "triad_clip_reduce", "triad_losshead",
            "triad_diag_smooth", "triad_diag_sparsity", "triad_dtemp_finalize", "triad_ln_bwd",
            "triad_colsum", "triad_sum_slabs", "triad_gather_rows", "triad_global_znorm",
@@ -42,7 +42,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=256, help="triples per GPU")
     ap.add_argument("--cpu-batch", type=int, default=4)
-    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-head-batch", type=int, default=16, help="batch of the CPU hot-path timing (extrapolated)")
+    ap.add_argument("--separate-steps", type=int, default=3,
+                    help="timed steps of the --separate-frames variant reported beside the headline (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate-frames", action="store_true",
                     help="encode the AV and TV frame batches separately (2x ViT work)")
@@ -98,7 +101,9 @@ def kernel_report(timers):
         for e0, e1, meta in evs:
             key = name
             if meta is not None and meta.get("backbone"):
-                key += "[backbone]"  # the same GEMM entry points serve backbone layers (linear.py, frontend.py)
+                key += "[backbone]"  # the same entry points serve backbone layers (linear.py, frontend.py, postln.py)
+            elif meta is not None and "tag" in meta:
+                key += "[" + meta["tag"] + "]"   # projection heads: per (width x rows)
             elif meta is not None:
                 key += "[" + ("AV" if meta.get("kind") == 0 else "TV") + ("/" + meta["what"] if "what" in meta else "") + "]"
             ms = e0.elapsed_time(e1)
@@ -107,6 +112,7 @@ def kernel_report(timers):
             r["ms"] += ms
             r["flops"] += (meta or {}).get("flops", 0.0)
             r["bytes"] += (meta or {}).get("bytes", 0.0)
+            r["ds_bytes"] = r.get("ds_bytes", 0.0) + (meta or {}).get("ds_bytes", 0.0)
             r["grid"] = (meta or {}).get("grid")
     return rep
 
@@ -167,6 +173,29 @@ def main():
         dt = float(t)
     loss = float(out["loss"])
     rep = kernel_report(timers)
+    sep = None
+    if a.separate_steps > 0 and not a.separate_frames:
+        # the --separate-frames figure beside the headline: AV and TV frames encoded separately
+        frames_sep = frames.roll(1, 0).contiguous()
+
+        def step_sep():
+            return trainer.step(frames, audio, text, phase="full_joint", shared_frames=False, frames_tv=frames_sep)
+        step_sep()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(a.separate_steps):
+            step_sep()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dts = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([dts], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dts = float(t)
+        sep = world * a.batch * a.separate_steps / dts
 
     if rank == 0:
         value = world * a.batch * a.steps / dt
@@ -175,10 +204,21 @@ def main():
         fwd = rep.get("triad_pairsim_fwd[AV]", {"launches": 0, "ms": 1.0, "flops": 0.0, "bytes": 0.0, "grid": None})
         avg_ms = fwd["ms"] / max(1, fwd["launches"])
         achieved = (fwd["flops"] / max(1, fwd["launches"])) / (avg_ms * 1e-3) / 1e12
-        # every hand-written kernel of the hot path (heads fwd+bwd, optimizer); backbone GEMMs apart
+        # every hand-written kernel of the hot path (heads fwd+bwd, projection heads, trainer
+        # optimizer); launches tagged as backbone work (the same GEMM / column-sum entry points serve the
+        # backbones) are kept apart
         head_keys = [k for k in rep if not k.endswith("[backbone]")]
         head_ms = sum(rep[k]["ms"] for k in head_keys) / a.steps
         head_flops = sum(rep[k]["flops"] for k in head_keys) / a.steps
+
+        def kstats(k):
+            v = rep[k]
+            avg = v["ms"] / max(1, v["launches"])
+            out = {"avg_ms": avg, "launches": v["launches"]}
+            if v["flops"]:
+                tf = v["flops"] / max(1, v["launches"]) / (avg * 1e-3) / 1e12
+                out.update(achieved_TFLOPs=tf, frac=tf / PEAK_BF16_TFLOPS)
+            return out
         res = {
             "metric": METRIC, "value": value, "unit": "triples/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
@@ -192,25 +232,47 @@ def main():
             "loss": loss,
             "roofline": {"kernel": "triad_pairsim_fwd[AV]", "bound": "mfma", "achieved": achieved,
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
-                         "traffic": pmc_traffic("pairsim_kernel<0>" if os.environ.get("TRIAD_FWD_V1")
-                                                else "pairsim_fwd2_kernel<true, false>", fwd["grid"]), "avg_ms": avg_ms,
+                         "traffic": pmc_traffic("pairsim_fwd2_kernel<true, false>", fwd["grid"]), "avg_ms": avg_ms,
                          "algorithmic_bytes": fwd["bytes"] / max(1, fwd["launches"]),
+                         "ds_stream_bytes": fwd.get("ds_bytes", 0.0) / max(1, fwd["launches"]),
                          "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
-                                           "same kernel and grid; FETCH x2 gfx950 correction)"},
+                                           "same kernel and grid; FETCH x2 gfx950 correction); algorithmic bytes = "
+                                           "Q + K features + rowmax/argmax (SURVEY 8d); the training forward also "
+                                           "streams the tiled unit-dS gradient (ds_stream_bytes), which is traffic"},
             "head": {"ms_per_step": head_ms, "algo_TFLOPs_per_step": head_flops / 1e12,
                      "achieved_TFLOPs": head_flops / max(head_ms, 1e-9) / 1e9,
-                     "kernels": {k: {"avg_ms": v["ms"] / max(1, v["launches"]), "launches": v["launches"]}
-                                 for k, v in sorted(rep.items()) if k in head_keys}},
+                     "kernels": {k: kstats(k) for k in sorted(rep) if k in head_keys}},
             "backbone_hip_gemm_ms_per_step": sum(v["ms"] for k, v in rep.items() if k not in head_keys) / a.steps,
         }
+        if sep is not None:
+            res["separate_frames"] = {"value": sep, "unit": "triples/s", "steps": a.separate_steps,
+                                      "note": "AV and TV frame batches encoded separately, as the reference's "
+                                              "two data loaders do (2x ViT work)"}
         if world == 1 and not a.no_cpu_baseline:
             from oracle import cpu_step
-            threads = min(16, os.cpu_count() or 1)
+            threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+            model = "unknown"
+            try:
+                for line in open("/proc/cpuinfo"):
+                    if line.startswith("model name"):
+                        model = line.split(":", 1)[1].strip()
+                        break
+            except OSError:
+                pass
             sec = cpu_step.time_steps(B=a.cpu_batch, steps=a.cpu_steps, warmup=1, threads=threads)
+            hb = a.cpu_head_batch
+            hsec = cpu_step.time_head(B=hb, steps=a.cpu_steps, warmup=1, threads=threads)
             res["cpu_baseline"] = {"value": a.cpu_batch / sec, "unit": "triples/s", "cores": threads, "kind": "port",
+                                   "cpu_model": model,
                                    "sample": f"oracle/cpu_step.py full_joint step (fp32 CPU backbones + materialising "
-                                             f"reference loss), B={a.cpu_batch}, {a.cpu_steps} timed step(s) "
-                                             f"after 1 warmup: {sec:.2f} s/step"}
+                                             f"reference loss), B={a.cpu_batch}, {a.cpu_steps} timed steps after 1 "
+                                             f"warmup: {sec:.2f} s/step on {threads} threads",
+                                   "hot_path": {"measured_B": hb, "s_per_step": hsec,
+                                                "extrapolated_B": a.batch,
+                                                "extrapolated_s_per_step": hsec * (a.batch / hb) ** 2,
+                                                "note": "AV+TV losses fwd+bwd of the reference on random features "
+                                                        "(Na=199, Nv=205, Nt=32); B^2-extrapolated to the bench batch "
+                                                        "(EXTRAPOLATED, not measured at that size)"}}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

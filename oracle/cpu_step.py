@@ -90,3 +90,29 @@ def time_steps(B=4, steps=2, warmup=1, threads=None, seed=1234):
     for _ in range(steps):
         step()
     return (time.perf_counter() - t0) / steps
+
+
+def time_head(B=8, Na=199, Nv=205, Nt=32, steps=3, warmup=1, threads=None, seed=1234):
+    """Seconds per hot-path step of the CPU port at batch B: the AV + TV losses of the reference
+    (materialising (B,B,Nq,Nv) fp32 tensors, model.py:370-593) forward + backward on random
+    head-output features. Its pairwise part grows as B^2 (bench.py extrapolates to B = 256)."""
+    if threads:
+        torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(seed)
+    a = (torch.randn(B, Na, 512, generator=g) * 0.58).requires_grad_(True)
+    t = (torch.randn(B, Nt, 512, generator=g) * 0.58).requires_grad_(True)
+    v = (torch.randn(B, Nv, 512, generator=g) * 0.58).requires_grad_(True)
+    mask = torch.ones(B, Nt, dtype=torch.long)
+    temp = torch.tensor(1.5, requires_grad=True)
+
+    def step():
+        av = ref_cpu.av_loss(a, v, temp, dtype=torch.float32)[0]
+        tv = ref_cpu.tv_loss(t, v, mask, temp, 0.80, 0.01, dtype=torch.float32)[0]
+        (av + tv).backward()
+
+    for _ in range(warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    return (time.perf_counter() - t0) / steps

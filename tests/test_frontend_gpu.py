@@ -69,8 +69,9 @@ def test_hubert_feature_encoder_gemm_matches_transformers(B, L):
 
 @pytest.mark.parametrize("C,G,T", [(768, 16, 199), (768, 16, 37), (1024, 16, 499), (768, 16, 1)])
 def test_hubert_pos_conv_matches_transformers(C, G, T):
-    """Implicit-GEMM positional conv (forward + input grad) + MIOpen weight grad vs the
-    transformers module (conv -> SamePad -> GELU) under bf16 autocast."""
+    """Implicit-GEMM positional conv (forward + input grad) + HIP weight grad (triad_posconv_dw at
+    48 channels per group, the overlapping-row GEMM at 64) vs the transformers module
+    (conv -> SamePad -> GELU) under bf16 autocast."""
     import transformers
     from transformers.models.hubert.modeling_hubert import HubertPositionalConvEmbedding
     from triad_amd import frontend
@@ -182,6 +183,23 @@ def test_posconv_weight_grad_vs_fp32(B, T, splits):
     # full conv output has T + 1 steps; the dropped last one gets zero gradient
     dy_full = torch.cat([dy.float(), torch.zeros(B, 1, C, device=dev)], 1).transpose(1, 2)
     ref = torch.nn.grad.conv1d_weight(x.float().transpose(1, 2), (C, 48, K), dy_full, padding=pad, groups=G)
+    assert _rel(dw, ref) < 1e-5
+
+
+@pytest.mark.parametrize("B,T,C,G", [(3, 499, 1024, 16), (2, 37, 256, 4), (2, 60, 512, 4)])
+def test_posconv_weight_grad_gemm_vs_fp32(B, T, C, G):
+    """frontend._posconv_dw_gemm (channels per group dividing 128: HuBERT-large's 64; one split-K
+    GEMM per 128-channel block with overlapping B rows) against the fp32 grouped-conv weight
+    gradient of the same bf16 operands."""
+    from triad_amd import frontend
+    K, pad = 128, 64
+    g = torch.Generator(device=dev).manual_seed(T + C)
+    x = torch.randn(B, T, C, device=dev, generator=g).to(torch.bfloat16)
+    dy = torch.randn(B, T, C, device=dev, generator=g).to(torch.bfloat16)
+    dw = frontend._posconv_dw_gemm(x, dy, G, pad, K)
+    dy_full = torch.cat([dy.float(), torch.zeros(B, 1, C, device=dev)], 1).transpose(1, 2)
+    ref = torch.nn.grad.conv1d_weight(x.float().transpose(1, 2), (C, C // G, K), dy_full, padding=pad, groups=G)
+    assert dw.shape == ref.shape
     assert _rel(dw, ref) < 1e-5
 
 

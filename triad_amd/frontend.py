@@ -401,8 +401,8 @@ def _hubert_feature_encoder_forward(self, input_values):
 class _PosConv(torch.autograd.Function):
     """Grouped conv1d(C, C, K=128, padding=pad, groups) over channels-last x (B, T, C), first T
     outputs (HubertSamePadLayer drops the last): forward and input gradient by the implicit-GEMM
-    HIP kernel (triad_posconv), weight gradient by triad_posconv_dw (48 channels per group;
-    aten.convolution_backward otherwise)."""
+    HIP kernel (triad_posconv), weight gradient by triad_posconv_dw (48 channels per group) or the
+    overlapping-row GEMM of _posconv_dw_gemm (channels per group dividing 128)."""
 
     @staticmethod
     def forward(ctx, x, w, bias, groups, pad):
@@ -442,9 +442,12 @@ class _PosConv(torch.autograd.Function):
             call("triad_posconv_dw", ptr(xb), ptr(dyb), B, T, C, G, pad, splits, ptr(part), stream_ptr(dyb.device))
             cg = C // G
             dsum = torch.empty(part.numel() // splits, dtype=torch.float32, device=dyb.device)
-            call("triad_sum_slabs", ptr(part), splits, dsum.numel(), None, 0, ptr(dsum), stream_ptr(dyb.device))
+            call("triad_sum_slabs", ptr(part), splits, dsum.numel(), None, 0, ptr(dsum), stream_ptr(dyb.device),
+                 meta=dict(backbone=True))
             dw = dsum.view(G, K, cg, cg).permute(0, 2, 3, 1).reshape(C, cg, K)
             dw = dw.to(ctx.dtypes[1])
+        elif ctx.needs_input_grad[1] and 128 % (C // G) == 0:
+            dw = _posconv_dw_gemm(xb, dyb, G, pad, K).to(ctx.dtypes[1])
         elif ctx.needs_input_grad[1]:
             # the conv's full output has T_full = T + 2*pad - K + 1 steps; the dropped tail gets 0
             t_full = T + 2 * pad - K + 1
@@ -457,8 +460,48 @@ class _PosConv(torch.autograd.Function):
             dw = dw.squeeze(2).to(ctx.dtypes[1])
         if ctx.has_bias and ctx.needs_input_grad[2]:
             from .ops import colsum
-            db = colsum(dyb.view(B * T, C), torch.float32).to(ctx.dtypes[2])
+            db = colsum(dyb.view(B * T, C), torch.float32, backbone=True).to(ctx.dtypes[2])
         return dx, dw, db, None, None
+
+
+def _posconv_dw_gemm(xb, dyb, G, pad, K):
+    """Weight gradient of the grouped positional conv for CG = C / G dividing 128 (HuBERT-large:
+    CG = 64) on the HIP split-K GEMM, no im2col and no MIOpen (whose grouped backward-weight solver
+    choice depends on the free device memory it sees -- a multi-minute naive fallback was observed).
+
+    For a block of P = 128 / CG consecutive groups (128 channels), with the padded channels-last
+    copies xp[b][tp][c] = x[b][tp - pad][c] (zero outside [0, T), Tp = T + K - 1 rows per sample)
+    and dyp[b][t][n] = dy (zero for t >= T):
+        dWblk[n][j * 128 + c] = sum_{r = b Tp + t} dyp[r][n] * xp_flat[r * 128 + j * 128 + c]
+    i.e. ONE GEMM whose B operand rows OVERLAP (row r = xp_flat[128 r .. 128 r + 128 K), ldb = 128);
+    rows t >= T carry dy = 0. dW of group p of the block = dWblk[p CG:(p+1) CG][j, p CG:(p+1) CG]
+    (the cross-group blocks are computed and dropped: P-fold work, acceptable for this config)."""
+    from ._lib import call, ptr, stream_ptr
+    B, T, C = xb.shape
+    CG = C // G
+    P = 128 // CG
+    Tp = T + K - 1
+    rows = B * Tp
+    Kd = (rows + 63) // 64 * 64
+    dev = xb.device
+    out = torch.empty(C, CG, K, dtype=torch.float32, device=dev)
+    splits = 4
+    slabs = torch.empty(splits * 128 * 128 * K, dtype=torch.float32, device=dev)
+    blk = torch.empty(128, K * 128, dtype=torch.float32, device=dev)
+    st = stream_ptr(dev)
+    for c0 in range(0, C, 128):
+        xp = torch.zeros(Kd + K, 128, dtype=torch.bfloat16, device=dev)   # + K rows: the last windows
+        xp[:rows].view(B, Tp, 128)[:, pad:pad + T] = xb[:, :, c0:c0 + 128]
+        dyp = torch.zeros(Kd, 128, dtype=torch.bfloat16, device=dev)
+        dyp[:rows].view(B, Tp, 128)[:, :T] = dyb[:, :, c0:c0 + 128]
+        call("triad_gemm_bf16_splitk", ptr(dyp), 128, 0, ptr(xp), 128, 0, 128, K * 128, Kd, splits, None,
+             ptr(slabs), ptr(blk), 0, st, meta=dict(backbone=True))
+        v = blk.view(128, K, 128)
+        for q in range(P):
+            g0 = c0 + q * CG
+            # dW[g0 + n][c][j] = blk[q CG + n][j][q CG + c]
+            out[g0:g0 + CG] = v[q * CG:(q + 1) * CG, :, q * CG:(q + 1) * CG].permute(0, 2, 1)
+    return out
 
 
 def _hubert_pos_conv_forward(self, hidden_states):

@@ -85,13 +85,14 @@ def pack_keys(k: torch.Tensor, g: Geometry) -> torch.Tensor:
     return out
 
 
-def colsum(x, out_dtype=torch.float32):
-    """Column sums of a bf16 [rows][cols] matrix (bias gradients) at HBM rate (triad_colsum)."""
+def colsum(x, out_dtype=torch.float32, backbone=False):
+    """Column sums of a bf16 [rows][cols] matrix (bias gradients) at HBM rate (triad_colsum).
+    backbone: tag the launch as backbone work (bench.py keeps it out of the hot-path head figures)."""
     rows, cols = x.shape
     part = torch.empty(call("triad_colsum_splits", rows, cols) * cols, dtype=torch.float32, device=x.device)
     out = torch.empty(cols, dtype=out_dtype, device=x.device)
     call("triad_colsum", ptr(x), rows, cols, x.stride(0), ptr(part), 1.0, int(out_dtype == torch.bfloat16), ptr(out),
-         stream_ptr(x.device))
+         stream_ptr(x.device), meta=dict(backbone=True) if backbone else dict(tag="proj-bias", flops=0.0))
     return out
 
 
@@ -170,9 +171,13 @@ class _ContrastiveHead(torch.autograd.Function):
         st_part = torch.empty(nparts, dtype=torch.float64, device=dev) if need_grad else None
         call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
              ptr(temp), CLAMP_LO[kind], 1, rank * Bq, ptr(rowmax), ptr(argmax), ptr(nn_part), ptr(diagS),
-             ptr(dS), CT, ptr(st_part), None, st, meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, grid=nparts * 512,
-                         bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R
-                         + (2.0 * g.R_pad * g.C_pad if need_grad else 0.0)))
+             ptr(dS), CT, ptr(st_part), None, st,
+             meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, grid=nparts * 512,
+                       # algorithmic bytes: the feature operands + rowmax / argmax; the
+                       # tiled unit-dS stream the training forward also writes is NOT algorithmic
+                       # (bench.py reports it, from PMC, as traffic)
+                       bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R,
+                       ds_bytes=(2.0 * g.R_pad * g.C_pad if need_grad else 0.0)))
         clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
         qw = torch.empty(g.R, dtype=torch.float32, device=dev)
         qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
@@ -368,7 +373,8 @@ class _ProjectionHead(torch.autograd.Function):
         mean = torch.empty(M, dtype=torch.float32, device=dev)
         rstd = torch.empty(M, dtype=torch.float32, device=dev)
         call("triad_projhead_fwd", ptr(hb), M, H, ptr(w1b), ptr(b1r), ptr(g32), ptr(be32), float(eps), ptr(w2b),
-             ptr(b2r), ptr(y), D, ptr(y1), ptr(ln), ptr(mean), ptr(rstd), st)
+             ptr(b2r), ptr(y), D, ptr(y1), ptr(ln), ptr(mean), ptr(rstd), st,
+             meta=dict(tag=f"proj{H}x{M}", flops=2.0 * M * (H * D + D * D)))
         ctx.save_for_backward(hb, w1b, w2b, g32, y1, ln, mean, rstd)
         ctx.shape = (lead, H, M, Mp)
         ctx.dtypes = (h.dtype, w1.dtype, b1.dtype, gamma.dtype, beta.dtype, w2.dtype, b2.dtype)
@@ -434,17 +440,19 @@ def _projhead_bwd_fused(ctx, dyp, hb, w1b, w2b, g32, y1, ln, mean, rstd):
     ns = call("triad_projhead_bwd_slabs", M)
     colpart = torch.empty(ns * 3 * D, dtype=f32, device=dev)
     call("triad_projhead_bwd", ptr(dyp), M, H, ptr(w2t), ptr(w1t), ptr(y1), ptr(mean), ptr(rstd), ptr(g32), ptr(dy1),
-         ptr(dh), H, ptr(colpart), st)
+         ptr(dh), H, ptr(colpart), st, meta=dict(tag=f"proj{H}x{M}", flops=2.0 * M * (H * D + D * D)))
     cols = torch.empty(3, D, dtype=f32, device=dev)
-    call("triad_sum_slabs", ptr(colpart), ns, 3 * D, None, 0, ptr(cols), st)
+    call("triad_sum_slabs", ptr(colpart), ns, 3 * D, None, 0, ptr(cols), st, meta=dict(tag="proj-cols", flops=0.0))
     db2 = colsum(dyp, f32)
     sp2 = _splitk(Mp, (D // 128) * (D // 128))
     sp1 = _splitk(Mp, (D // 128) * (H // 128))
     slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
     dw2 = torch.empty(D, D, dtype=f32, device=dev)
-    call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2), 0, st)
+    call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2), 0, st,
+         meta=dict(tag=f"proj-dW2x{M}", flops=2.0 * M * D * D))
     dw1 = torch.empty(D, H, dtype=f32, device=dev)
-    call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), 0, st)
+    call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), 0, st,
+         meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
     hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
     return (dh.view(*lead, H).to(hd), dw1.to(w1d), cols[2].to(b1d), cols[0].to(gd), cols[1].to(bd), dw2.to(w2d),
             db2.to(b2d), None)

@@ -80,7 +80,7 @@ class _DropAddLN(torch.autograd.Function):
         call("triad_dropaddln_bwd", ptr(dh), ptr(dhb), ptr(res), ptr(y), ptr(mean), ptr(rstd), ptr(w), M, D, p, seed,
              ptr(dres), ptr(dy), ptr(part), st)
         gwb = torch.empty(2 * D, dtype=torch.float32, device=dev)
-        call("triad_sum_slabs", ptr(part), nb, 2 * D, None, 0, ptr(gwb), st)
+        call("triad_sum_slabs", ptr(part), nb, 2 * D, None, 0, ptr(gwb), st, meta=dict(backbone=True))
         return dres, dy, gwb[:D], gwb[D:], None, None, None
 
 
