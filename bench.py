@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="triples per GPU")
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--cpu-steps", type=int, default=3)
-    ap.add_argument("--cpu-head-batch", type=int, default=16, help="batch of the CPU hot-path timing (extrapolated)")
+    ap.add_argument("--cpu-head-batch", type=int, default=48, help="batch of the CPU hot-path timing (extrapolated)")
     ap.add_argument("--separate-steps", type=int, default=3,
                     help="timed steps of the --separate-frames variant reported beside the headline (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -167,6 +167,8 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     timers, _lib.TIMERS = _lib.TIMERS, None
+    if rank == 0:
+        print(f"[bench] {a.steps} timed steps: {dt:.2f} s", file=sys.stderr, flush=True)
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -196,6 +198,8 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dts = float(t)
         sep = world * a.batch * a.separate_steps / dts
+        if rank == 0:
+            print(f"[bench] {a.separate_steps} separate-frames steps: {dts:.2f} s", file=sys.stderr, flush=True)
 
     if rank == 0:
         value = world * a.batch * a.steps / dt
@@ -250,7 +254,13 @@ def main():
                                               "two data loaders do (2x ViT work)"}
         if world == 1 and not a.no_cpu_baseline:
             from oracle import cpu_step
-            threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+            # the threads this process may use: torch's intra-op pool honours OMP_NUM_THREADS (the GPU box
+            # sets it to the job's CPU share; its affinity mask shows the whole machine, and oversubscribing
+            # that stalls the run)
+            threads = torch.get_num_threads()
+            if hasattr(os, "sched_getaffinity"):
+                threads = min(threads, len(os.sched_getaffinity(0)))
+            print(f"[bench] cpu baseline on {threads} threads", file=sys.stderr, flush=True)
             model = "unknown"
             try:
                 for line in open("/proc/cpuinfo"):
@@ -260,8 +270,10 @@ def main():
             except OSError:
                 pass
             sec = cpu_step.time_steps(B=a.cpu_batch, steps=a.cpu_steps, warmup=1, threads=threads)
+            print(f"[bench] cpu full step: {sec:.2f} s", file=sys.stderr, flush=True)
             hb = a.cpu_head_batch
             hsec = cpu_step.time_head(B=hb, steps=a.cpu_steps, warmup=1, threads=threads)
+            print(f"[bench] cpu hot path B={hb}: {hsec:.2f} s", file=sys.stderr, flush=True)
             res["cpu_baseline"] = {"value": a.cpu_batch / sec, "unit": "triples/s", "cores": threads, "kind": "port",
                                    "cpu_model": model,
                                    "sample": f"oracle/cpu_step.py full_joint step (fp32 CPU backbones + materialising "
