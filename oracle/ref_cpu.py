@@ -183,6 +183,16 @@ def loss_mix(phase, av, tv, progress=0.0, av_start=0.8, av_end=0.5):
     return av + tv
 
 
+# ---- audio front-end ----------------------------------------------------------------------
+def audio_znorm(x, eps=1e-7):
+    """AudioEmbedder.forward's processor call (model.py:56-62): the hubert-large-ls960-ft
+    Wav2Vec2FeatureExtractor receives the (B, T) tensor as ONE utterance (a tensor is not taken as
+    a batch), so one mean and one population variance over all B*T samples:
+    (x - mean) / sqrt(var + 1e-7). Pinned by tests/golden/znorm_*.npz."""
+    xd = torch.as_tensor(x).double()
+    return (xd - xd.mean()) / torch.sqrt(xd.var(unbiased=False) + eps)
+
+
 # ---- 1000-way retrieval (src/retrieval.py) ---------------------------------------------
 def aggregator_a2v(a_feats, v_feats, temperature):
     """retrieval.py:106-109 (and 190-193 for text): mean over query tokens of the max over keys,
@@ -210,14 +220,19 @@ def retrieval_matrices(q_list, k_list, temperature):
     return q2k, k2q
 
 
-def recall_at_k(sim):
-    """retrieval.py:117-144 with a stable sort (ties resolved by index)."""
+def recall_ranks(sim):
+    """retrieval.py:124-131: rank of the matching item i in np.argsort(-row) with numpy's DEFAULT
+    (unstable) sort, so exact ties are ordered as the reference orders them (pinned by
+    tests/golden/retrieval_*_ties.npz, which the reference itself produced)."""
     import numpy as np
-    ranks = []
-    for i in range(sim.shape[0]):
-        order = np.argsort(-sim[i], kind="stable")
-        ranks.append(int(np.where(order == i)[0][0]))
-    ranks = np.array(ranks)
+    sim = np.asarray(sim, np.float32)   # the reference's np.zeros((N, N), float32) matrices
+    return np.array([int(np.where(np.argsort(-sim[i]) == i)[0][0]) for i in range(sim.shape[0])])
+
+
+def recall_at_k(sim):
+    """retrieval.py:117-144."""
+    import numpy as np
+    ranks = recall_ranks(sim)
     return {f"r{k}": float(np.mean(ranks < k)) for k in (1, 5, 10, 20)}
 
 

@@ -24,6 +24,10 @@ Methods exercised (file:line in /root/reference/src/model.py):
   compute_all_similarities_tv          490-514
   compute_contrastive_loss_tv          544-593 (-> 516-542)
   ViTLoRAEmbedder.patch_dropout        268-308
+and from /root/reference/src/retrieval.py: aggregator_av_a2v / _v2a (106-114),
+compute_recall_at_k (117-144), aggregator_tv_t2v / _v2t (236-244); plus the
+audio z-norm of AudioEmbedder.forward (model.py:56-62) through transformers'
+Wav2Vec2FeatureExtractor.
 
 Inputs are bf16-representable fp32 values (SURVEY §7 "hard parts": the parity
 target is the fp32 computation on bf16-rounded inputs). Gradients are taken
@@ -173,6 +177,79 @@ def gen_dropout(ref_model, name, B, N, drop, seed):
     print(name, tuple(out.shape), keep.sum(1).tolist())
 
 
+def _import_retrieval():
+    sys.path.insert(0, REF_SRC)
+    import retrieval as ref_retrieval  # the reference module (json/numpy/torch/tqdm only)
+    return ref_retrieval
+
+
+def _token_lists(g, n, lo, hi, normalize):
+    out = []
+    for _ in range(n):
+        L = int(torch.randint(lo, hi + 1, (1,), generator=g))
+        x = torch.randn(L, D, generator=g)
+        if normalize:  # embed_av_subset L2-normalises (retrieval.py:93-94)
+            x = torch.nn.functional.normalize(x, dim=-1)
+        out.append(_bf16(x))
+    return out
+
+
+def gen_retrieval(ref_retrieval, name, kind, N, q_lens, k_lens, temp, seed, dup_items=(), zero_queries=()):
+    """The reference's per-pair aggregators (retrieval.py:106-114 / 236-244) in its own double
+    loop (retrieval.py:161-174, 255-264) and compute_recall_at_k (retrieval.py:117-144) on both
+    N x N matrices. `dup_items` makes those item token lists identical (exact ties in every row);
+    `zero_queries` zeroes those queries (a whole row of exact ties): both exercise the reference's
+    unstable np.argsort tie order."""
+    g = torch.Generator().manual_seed(seed)
+    q = _token_lists(g, N, q_lens[0], q_lens[1], kind == "av")
+    k = _token_lists(g, N, k_lens[0], k_lens[1], kind == "av")
+    for i in range(N):  # matching pairs share content so recall is informative
+        n = min(len(q[i]), len(k[i]))
+        k[i][:n] = _bf16(k[i][:n] + 0.5 * q[i][:n])
+    for j in dup_items[1:]:
+        k[j] = k[dup_items[0]].clone()
+    for i in zero_queries:
+        q[i] = torch.zeros_like(q[i])
+    f_qk = ref_retrieval.aggregator_av_a2v if kind == "av" else ref_retrieval.aggregator_tv_t2v
+    f_kq = ref_retrieval.aggregator_av_v2a if kind == "av" else ref_retrieval.aggregator_tv_v2t
+    s_qk = np.zeros((N, N), dtype=np.float32)
+    s_kq = np.zeros((N, N), dtype=np.float32)
+    for i in range(N):
+        for j in range(N):
+            s_qk[i, j] = f_qk(q[i], k[j], temp)      # query i (audio/text) vs item j (video)
+            s_kq[i, j] = f_kq(q[j], k[i], temp)      # video i vs audio/text j (retrieval.py:171-174)
+    r_qk = ref_retrieval.compute_recall_at_k(s_qk)
+    r_kq = ref_retrieval.compute_recall_at_k(s_kq)
+    ranks = lambda s: np.array([int(np.where(np.argsort(-s[i]) == i)[0][0]) for i in range(N)], np.int32)
+    np.savez_compressed(
+        os.path.join(OUT, name + ".npz"), kind="retrieval_" + kind, temp=np.float32(temp),
+        q=_u16(torch.cat(q)), q_len=np.array([len(x) for x in q], np.int32),
+        k=_u16(torch.cat(k)), k_len=np.array([len(x) for x in k], np.int32),
+        sim_qk=s_qk, sim_kq=s_kq, ranks_qk=ranks(s_qk), ranks_kq=ranks(s_kq),
+        recall_qk=np.array([r_qk[x] for x in ("r1", "r5", "r10", "r20")], np.float64),
+        recall_kq=np.array([r_kq[x] for x in ("r1", "r5", "r10", "r20")], np.float64))
+    print(name, r_qk, r_kq)
+
+
+def gen_znorm(name, B, T, seed, offset=0.0, scale=0.1):
+    """The reference's audio z-norm: AutoProcessor("facebook/hubert-large-ls960-ft") called on the
+    (B, T) waveform tensor (model.py:56-62). That checkpoint's processor is a
+    Wav2Vec2FeatureExtractor(feature_size=1, sampling_rate=16000, padding_value=0.0,
+    do_normalize=True, return_attention_mask=True) (its preprocessor_config.json); built here from
+    those values because the hub is unreachable. A torch tensor is not recognised as a batch, so
+    the whole (B, T) array is one utterance: ONE mean / variance over all B*T samples."""
+    from transformers import Wav2Vec2FeatureExtractor
+    fe = Wav2Vec2FeatureExtractor(feature_size=1, sampling_rate=16000, padding_value=0.0, do_normalize=True,
+                                  return_attention_mask=True)
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, T, generator=g) * scale + offset
+    y = fe(x, return_tensors="pt", sampling_rate=16000, padding=True,
+           return_attention_mask=True).input_values.squeeze(0)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), kind="znorm", x=x.numpy().astype(np.float32),
+                        y=y.numpy().astype(np.float32))
+    print(name, tuple(y.shape), float(y.mean()), float(y.std()))
+
+
 def main():
     torch.set_num_threads(8)
     ref = _import_reference()
@@ -191,6 +268,14 @@ def main():
     gen_simmat(ref, "simmat_b2_n7_n16", 2, 7, 16, 1.5, 21)
     gen_dropout(ref, "dropout_b4_n64", 4, 64, 0.25, 31)
     gen_dropout(ref, "dropout_b3_n256", 3, 256, 0.25, 32)
+    rr = _import_retrieval()
+    gen_retrieval(rr, "retrieval_av_n40", "av", 40, (6, 24), (10, 30), 1.5, 41)
+    gen_retrieval(rr, "retrieval_av_n24_ties", "av", 24, (4, 12), (5, 16), 0.9, 42, dup_items=(3, 7, 12, 20))
+    gen_retrieval(rr, "retrieval_tv_n32_ties", "tv", 32, (1, 12), (8, 20), 1.5, 43, dup_items=(5, 9),
+                  zero_queries=(2, 17))
+    gen_znorm("znorm_b3_t8000", 3, 8000, 51)
+    gen_znorm("znorm_b2_t4000_offset", 2, 4000, 52, offset=0.3, scale=0.02)
+    gen_znorm("znorm_b1_t16000", 1, 16000, 53, scale=0.5)
 
 
 if __name__ == "__main__":

@@ -62,6 +62,17 @@ def test_global_znorm_matches_processor_semantics():
     np.testing.assert_allclose(y.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("name", G.names("znorm"))
+def test_global_znorm_matches_feature_extractor_fixture(name):
+    """triad_global_znorm against the reference processor's own output (Wav2Vec2FeatureExtractor
+    of hubert-large-ls960-ft on the (B, T) tensor, model.py:56-62; tests/golden/gen_golden.py)."""
+    from triad_amd import ops
+    f = G.load(name)
+    y = ops.global_znorm(torch.from_numpy(f["x"]).to(dev), 1e-7)
+    assert y.shape == f["y"].shape
+    np.testing.assert_allclose(y.cpu().numpy(), f["y"], rtol=1e-5, atol=2e-5)
+
+
 @pytest.mark.parametrize("name", G.names("dropout"))
 def test_patch_dropout_matches_reference(name):
     from triad_amd import ops

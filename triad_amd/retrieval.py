@@ -60,14 +60,31 @@ def aggregated_similarity(queries: Sequence[torch.Tensor], items: Sequence[torch
     return sim
 
 
-def recall_at_k(sim: torch.Tensor, ks=(1, 5, 10, 20)) -> Dict[str, float]:
-    """retrieval.py:117-144: rank of the matching item j = i per query row (stable tie order)."""
-    n = sim.shape[0]
-    diag = sim.diagonal()[:, None]
-    idx = torch.arange(n, device=sim.device)
-    ahead = (sim > diag) | ((sim == diag) & (idx[None, :] < idx[:, None]))
-    ranks = ahead.sum(1)
-    return {f"r{k}": float((ranks < k).float().mean()) for k in ks}
+def ranks(sim: torch.Tensor, ties: str = "reference") -> torch.Tensor:
+    """Rank of the matching item j = i in each query row (retrieval.py:124-131).
+
+    ties="reference" orders exact ties as the reference does: its ranking is numpy's default
+    (unstable) argsort of -row on the host, whose tie order is not an index rule, so the (N x N)
+    fp32 matrix -- 4 MB at N = 1000 -- is ranked by that same host call (one batched argsort,
+    not N). ties="stable" ranks on the device, ties resolved by item index."""
+    if ties == "stable":
+        n = sim.shape[0]
+        diag = sim.diagonal()[:, None]
+        idx = torch.arange(n, device=sim.device)
+        ahead = (sim > diag) | ((sim == diag) & (idx[None, :] < idx[:, None]))
+        return ahead.sum(1)
+    if ties != "reference":
+        raise ValueError(f"ties must be 'reference' or 'stable', not {ties!r}")
+    import numpy as np
+    s = sim.detach().to(torch.float32).cpu().numpy()
+    order = np.argsort(-s, axis=1)   # row-wise identical to the reference's per-row np.argsort(-row)
+    return torch.from_numpy((order == np.arange(s.shape[0])[:, None]).argmax(1))
+
+
+def recall_at_k(sim: torch.Tensor, ks=(1, 5, 10, 20), ties: str = "reference") -> Dict[str, float]:
+    """compute_recall_at_k (retrieval.py:117-144): fraction of queries whose match ranks < k."""
+    r = ranks(sim, ties)
+    return {f"r{k}": float((r < k).double().mean()) for k in ks}
 
 
 def av_retrieval_metrics(audio_feats: List[torch.Tensor], video_feats: List[torch.Tensor], temperature: float,
