@@ -86,3 +86,127 @@ def test_global_negatives_two_ranks_match_single_process(kind):
         np.testing.assert_allclose(gk, ref_k, rtol=0, atol=2e-2 * np.abs(ref_k).max())
         dt += gt
     assert abs(dt - float(t.grad)) <= 1e-3 * abs(float(t.grad)) + 1e-6
+
+
+# ---- Mode R: TriadTrainer itself at world size 2 ---------------------------------------
+def _mode_r_model():
+    """ViT-S/14-reg + HuBERT-base + DistilBERT (c1-sized backbones), every dropout / LayerDrop /
+    SpecAugment mask off so two processes and one process draw nothing random
+    (tools/grad_determinism.py: with them on, two identical single-process steps differ)."""
+    from triad_amd.model import MultiModalModel
+    torch.manual_seed(1234)
+    m = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.80, patch_sparsity_weight=0.01,
+                        visual_dropout_prob=0.25, use_amp=True, vit_arch="dinov2_vits14_reg").cuda()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+        if isinstance(getattr(mod, "dropout", None), float):
+            mod.dropout = 0.0
+        cfg = getattr(mod, "config", None)
+        if cfg is not None and hasattr(cfg, "layerdrop"):
+            cfg.layerdrop = 0.0
+        if cfg is not None and hasattr(cfg, "apply_spec_augment"):
+            cfg.apply_spec_augment = False   # HuBERT's training-mode time masks come from numpy's RNG
+    m.train()
+    return m
+
+
+def _mode_r_batch(step, rank, B=2):
+    g = torch.Generator().manual_seed(1000 * step + rank)
+    frames = torch.randn(B, 3, 224, 224, generator=g).cuda()
+    audio = (torch.randn(B, 32000, generator=g) * 0.1).cuda()
+    words = "a dog runs across the wet grass while two children laugh near an old red barn".split()
+    text = [" ".join(words[(3 * i + step + rank) % 5:][:10]) for i in range(B)]
+    av_keep = torch.rand(B, 256, generator=g) < 0.75
+    tv_keep = torch.rand(B, 256, generator=g) < 0.75
+    return frames, audio, text, av_keep, tv_keep
+
+
+def _trainer(model, accum, group=None, wire="fp32"):
+    """TriadTrainer whose reduced gradient buffer is snapshotted at each optimizer step (after the
+    all-reduce, before clipping) in `tr.reduced`."""
+    from triad_amd.train import TriadTrainer
+    tr = TriadTrainer(model, learning_rate=1e-4, total_updates=50, gradient_accumulation_steps=accum,
+                      unfreeze_audio_step=0, unfreeze_text_step=0, process_group=group, bucket_mb=16.0,
+                      grad_wire=wire)
+    tr.reduced = []
+    inner = tr._allreduce_grads
+
+    def snap():
+        inner()
+        tr.reduced.append(tr.space.flat_g.clone())
+    tr._allreduce_grads = snap
+    return tr
+
+
+def _group_rel(tr, a, b):
+    out = {}
+    sp = tr.space
+    for name, ps in tr.groups.items():
+        ids = sp.param_ids(ps)
+        if not ids:
+            continue
+        x = np.concatenate([a[sp.offsets[i]:sp.offsets[i] + sp.params[i].numel()] for i in ids])
+        y = np.concatenate([b[sp.offsets[i]:sp.offsets[i] + sp.params[i].numel()] for i in ids])
+        out[name] = float(np.linalg.norm(x - y) / max(np.linalg.norm(y), 1e-30))
+    return out
+
+
+def _mode_r_worker(rank, world, port, wire, q_out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        m = _mode_r_model()
+        tr = _trainer(m, 1, dist.group.WORLD, wire)
+        launched = []
+        for step in range(2):
+            f, a, t, ak, tk = _mode_r_batch(step, rank)
+            tr.step(f, a, t, phase="full_joint", av_keep=ak, tv_keep=tk)
+            launched.append(tr.reducer.launched_in_backward)
+        torch.cuda.synchronize()
+        q_out.put((rank, tr.reduced[0].cpu().numpy(), tr.space.flat_p.cpu().numpy(), launched,
+                   len(tr.reducer.buckets)))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q_out.put((rank, "error", traceback.format_exc(), None, None))
+
+
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_mode_r_trainer_two_ranks_match_accumulated_single_process(wire):
+    """TriadTrainer at world size 2 (Mode R, gradients all-reduced by the overlapped bucket
+    reducer; gloo over device tensors -- RCCL refuses two ranks on one GPU). The reduced gradient
+    of the first step equals ONE process accumulating the same two micro-batches
+    (gradient_accumulation_steps=2, i.e. the average of the ranks' gradients), per parameter
+    group; both ranks hold identical parameters after two optimizer steps; from the second step
+    on, buckets leave during backward. (Updates are not compared with the single process: AdamW's
+    first steps are ~lr * sign(g), so run-to-run noise in near-zero gradients -- which two
+    single-process runs show too -- flips whole elements.)"""
+    world = 2
+    ctx = mp.get_context("spawn")
+    qo = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_mode_r_worker, args=(r, world, port, wire, qo)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([qo.get(timeout=600) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert not isinstance(r[1], str), r[2]
+    (_, g0, p0, l0, nb), (_, g1, p1, l1, _) = res
+    assert nb >= 4
+    np.testing.assert_array_equal(g0, g1)          # one all-reduced gradient on both ranks
+    np.testing.assert_array_equal(p0, p1)          # -> identical updates
+    assert l0[0] == 0 and l0[1] >= 1 and l1[1] >= 1
+    m = _mode_r_model()
+    tr = _trainer(m, 2)
+    for rank in range(world):
+        f, a, t, ak, tk = _mode_r_batch(0, rank)
+        tr.step(f, a, t, phase="full_joint", av_keep=ak, tv_keep=tk)
+    rel = _group_rel(tr, g0, tr.reduced[0].cpu().numpy())
+    print(f"mode R {wire}: reduced-gradient rel error per group {rel}")
+    bar = 1e-2 if wire == "fp32" else 2e-2
+    for name, r in rel.items():
+        assert r < bar, (name, r)

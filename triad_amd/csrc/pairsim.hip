@@ -481,9 +481,27 @@ __global__ void dtemp_finalize_kernel(const double* __restrict__ p0, int n0, con
   }
 }
 
+#ifndef TRIAD_FWD_GRID_TARGET
+#define TRIAD_FWD_GRID_TARGET 2048
+#endif
 int grid_for(int R_pad, int Bk, int* jpw, int* ysplit) {
   const int xb = R_pad / ROWS_PER_WG;
-  int ys = (2048 + xb - 1) / xb;
+#ifdef TRIAD_FWD_GRID_BAL
+  {  // A/B: key-split count minimising (dispatch rounds over 256 CUs) x (samples + query-load cost)
+    double best = 1e30;
+    int bys = 1;
+    for (int y = 1; y <= Bk; ++y) {
+      const int j = (Bk + y - 1) / y, ya = (Bk + j - 1) / j;
+      const double rounds = (double)((xb * ya + 255) / 256);
+      const double c = rounds * (j + TRIAD_FWD_GRID_BAL * 0.1);
+      if (c < best - 1e-9) { best = c; bys = ya; }
+    }
+    *jpw = (Bk + bys - 1) / bys;
+    *ysplit = (Bk + *jpw - 1) / *jpw;
+    return xb;
+  }
+#endif
+  int ys = (TRIAD_FWD_GRID_TARGET + xb - 1) / xb;
   if (ys > Bk) ys = Bk;
   if (ys < 1) ys = 1;
   *jpw = (Bk + ys - 1) / ys;

@@ -86,3 +86,185 @@ def allreduce_grads(flat: torch.Tensor, bucket_elems: int, average: bool, group=
         dist.all_reduce(b, op=dist.ReduceOp.SUM, group=group)
         if average:
             b.mul_(1.0 / W)
+
+
+class GradBucketReducer:
+    """Mode R / Mode G gradient reduction overlapped with backward.
+
+    The flat fp32 gradient buffer of a FlatParamSpace is cut into contiguous buckets of about
+    `bucket_mb` (parameter-aligned ranges of the buffer). A post-accumulate-grad hook on every
+    parameter counts arrivals; when a bucket's last expected gradient has been accumulated, the
+    bucket is handed to a dedicated communication stream (which first waits on every stream its
+    gradients were produced on) and all-reduced asynchronously while autograd continues with the
+    earlier layers. `finish()` flushes buckets whose gradients never came (unused in this phase),
+    makes the caller's stream wait on every reduction, and scatters bf16 wire buffers back.
+
+    Launch order is a property of the job, not of one rank's timing: a bucket is launched only
+    after every bucket before it in `order` -- collectives must be issued in the same sequence on
+    every rank. The first reducing step reduces after backward in buffer order while recording
+    when each parameter's gradient arrived; `order` is then rank 0's arrival order of the buckets,
+    broadcast to all ranks, and from the next step on the reductions overlap backward.
+
+    Wire format: "fp32" all-reduces the buffer in place (prescaled by 1/W when averaging);
+    "bf16" prescales, casts each bucket to bf16 and all-reduces that (half the xGMI bytes; the
+    sum of W bf16 terms carries bf16 rounding, ~2^-9 relative per element). Bucket size: ring
+    all-reduce over point-to-point xGMI is per-link bound, so buckets are sized for a few
+    ms of link time each (64 MB default) rather than for latency.
+
+    Shadowed (bf16 model-weight) parameters: their bf16 autograd gradient is folded into the
+    flat fp32 buffer inside the hook (so it can join a bucket) instead of by the single
+    after-backward `gather_shadow_grads` launch.
+    """
+
+    def __init__(self, space, bucket_mb: float = 64.0, wire: str = "fp32", average: bool = True, group=None):
+        if wire not in ("fp32", "bf16"):
+            raise ValueError(f"wire must be 'fp32' or 'bf16', not {wire!r}")
+        self.space, self.wire, self.average, self.group = space, wire, average, group
+        self.world, _ = world_rank(group)
+        self.cuda = space.device.type == "cuda"
+        n = len(space.params)
+        bounds, acc, start = [], 0, 0
+        limit = max(1, int(bucket_mb * (1 << 20) / 4))
+        for i in range(n):
+            acc += space.params[i].numel()
+            if acc >= limit or i == n - 1:
+                bounds.append((start, i + 1))
+                start, acc = i + 1, 0
+        self.buckets = bounds                                   # parameter-index ranges
+        self.bucket_of = [0] * n
+        for b, (s, e) in enumerate(bounds):
+            for i in range(s, e):
+                self.bucket_of[i] = b
+        self.order = None                                       # launch order (bucket ids)
+        self.active = False
+        self.comm = torch.cuda.Stream(space.device) if self.cuda else None
+        self.launched_in_backward = 0                           # overlap evidence (tests, logs)
+        self._hooks = {}   # registered lazily: a frozen parameter (requires_grad False) takes no hook
+
+    def _arm_hooks(self):
+        for i, p in enumerate(self.space.params):
+            if p.requires_grad and i not in self._hooks:
+                self._hooks[i] = p.register_post_accumulate_grad_hook(self._hook(i))
+
+    # -- per step ------------------------------------------------------------------------
+    def begin(self, accumulate: bool):
+        """Arm the hooks for the backward that completes an accumulation window."""
+        sp = self.space
+        self._arm_hooks()
+        self.accumulate = accumulate
+        self.expected = [0] * len(self.buckets)
+        for i, p in enumerate(sp.params):
+            if p.requires_grad:
+                self.expected[self.bucket_of[i]] += 1
+        self.arrived = [0] * len(self.buckets)
+        self.streams = [set() for _ in self.buckets]
+        self.ready = [False] * len(self.buckets)
+        self.works = {}
+        self.next = 0                                           # position in self.order
+        self.arrival = [] if self.order is None else None
+        self.launched_in_backward = 0
+        self.active = True
+
+    def _hook(self, i):
+        def hook(p):
+            if not self.active:
+                return
+            sp = self.space
+            cur = torch.cuda.current_stream(sp.device) if self.cuda else None
+            if sp.shadowed[i] and p.grad is not None:
+                view = sp.flat_g[sp.offsets[i]:sp.offsets[i] + p.numel()].view(p.shape)
+                if cur is not None:
+                    # a bf16 weight gradient may still be in flight on the side stream
+                    # (linear.on_side_stream: autograd stored it without a main-stream wait), so
+                    # fold it on that stream, after the work this stream has queued so far
+                    from .linear import _side_stream
+                    side = _side_stream(sp.device)
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        view.add_(p.grad) if self.accumulate else view.copy_(p.grad)
+                    p.grad.record_stream(side)
+                    cur = side
+                elif self.accumulate:
+                    view.add_(p.grad)
+                else:
+                    view.copy_(p.grad)
+                p.grad = None
+                sp.touched[i] = True
+            b = self.bucket_of[i]
+            self.arrived[b] += 1
+            if cur is not None:
+                self.streams[b].add(cur)
+            if self.arrival is not None:
+                self.arrival.append(b)
+            if self.arrived[b] == self.expected[b]:
+                self.ready[b] = True
+                if self.order is not None:
+                    self._drain(in_backward=True)
+        return hook
+
+    def _drain(self, in_backward=False, flush=False):
+        while self.next < len(self.order):
+            b = self.order[self.next]
+            if not (self.ready[b] or flush):
+                return
+            self._launch(b)
+            self.next += 1
+            if in_backward:
+                self.launched_in_backward += 1
+
+    def _range(self, b):
+        s, e = self.buckets[b]
+        sp = self.space
+        hi = sp.offsets[e] if e < len(sp.params) else sp.numel
+        return sp.flat_g[sp.offsets[s]:hi]
+
+    def _launch(self, b):
+        if self.expected[b] == 0:       # every parameter frozen (identically on all ranks): nothing to reduce
+            self.works[b] = None
+            return
+        g = self._range(b)
+        scale = 1.0 / self.world if self.average else 1.0
+        if not self.cuda:
+            if scale != 1.0:
+                g.mul_(scale)
+            buf = g.to(torch.bfloat16) if self.wire == "bf16" else g
+            self.works[b] = (dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True), buf)
+            return
+        for s in self.streams[b] or {torch.cuda.current_stream(self.space.device)}:
+            self.comm.wait_stream(s)
+        with torch.cuda.stream(self.comm):
+            if scale != 1.0:
+                g.mul_(scale)
+            buf = g.to(torch.bfloat16) if self.wire == "bf16" else g
+            work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self.works[b] = (work, buf)
+
+    def finish(self):
+        """After backward: flush, then order the caller's stream after every reduction."""
+        if not self.active:
+            return
+        self.active = False
+        if self.order is None:
+            # first reducing step: fix the launch order from rank 0's arrival order
+            first = {}
+            for k, b in enumerate(self.arrival):
+                first[b] = k                                    # last arrival = bucket ready time
+            rank_order = sorted(range(len(self.buckets)), key=lambda b: (first.get(b, 1 << 60), b))
+            t = torch.tensor(rank_order, dtype=torch.int64,
+                             device=self.space.device if _is_nccl(self.group) else "cpu")
+            dist.broadcast(t, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0,
+                           group=self.group)
+            self.order = [int(x) for x in t.cpu()]
+            self.arrival = None
+        self._drain(flush=True)
+        cur = torch.cuda.current_stream(self.space.device) if self.cuda else None
+        for b in self.order:
+            item = self.works.pop(b)
+            if item is None:
+                continue
+            work, buf = item
+            work.wait()                                         # cur stream (GPU) / host (gloo) waits
+            if self.wire == "bf16":
+                if cur is not None:
+                    buf.record_stream(cur)
+                self._range(b).copy_(buf)

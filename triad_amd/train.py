@@ -15,9 +15,10 @@ fused HIP AdamW (`optimizer="fused"`, default; `"torch"` keeps torch.optim.AdamW
 parity tests); stats/grad norms stay on the device (no per-step `.item()`), and
 `torch.cuda.empty_cache()` is not called every step.
 
-Data parallel (one process per GPU, RCCL over xGMI): after backward the flat
-gradient buffer is averaged with bucketed all-reduces -- the reference has no
-distributed code; this is SURVEY §8e Mode R. `global_negatives=True` is Mode G
+Data parallel (one process per GPU, RCCL over xGMI): the flat gradient buffer is
+averaged with bucketed all-reduces launched from gradient hooks while backward is still
+running (triad_amd.dist.GradBucketReducer; fp32 or bf16 on the wire) -- the reference
+has no distributed code; this is SURVEY §8e Mode R. `global_negatives=True` is Mode G
 (triad_amd.dist).
 """
 from __future__ import annotations
@@ -70,8 +71,9 @@ def _one_cycle(opt, max_lr, total):
 class TriadTrainer:
     def __init__(self, model, learning_rate=1e-4, total_updates=10000, gradient_accumulation_steps=1,
                  unfreeze_audio_step=5000, unfreeze_text_step=5000, unfreeze_vit_step=5000,
-                 optimizer="fused", device="cuda", process_group=None, bucket_mb=256.0,
-                 av_weight_start=0.8, av_weight_end=0.5, global_negatives=False, bf16_weights=None):
+                 optimizer="fused", device="cuda", process_group=None, bucket_mb=64.0,
+                 av_weight_start=0.8, av_weight_end=0.5, global_negatives=False, bf16_weights=None,
+                 overlap_grad_reduce=True, grad_wire="fp32"):
         self.model = model
         self.device = torch.device(device)
         if self.device.type == "cuda":  # committed library-GEMM solution choices (gemm_tuning.py)
@@ -111,6 +113,11 @@ class TriadTrainer:
             p.requires_grad = False
         for p in self.groups["vit_lora"]:
             p.requires_grad = True
+        # data parallel: bucketed gradient all-reduce overlapped with backward (fused optimizer)
+        self.reducer = None
+        if self.world > 1 and self.space is not None and overlap_grad_reduce:
+            self.reducer = tdist.GradBucketReducer(self.space, bucket_mb, grad_wire,
+                                                   average=not self.global_negatives, group=process_group)
         self.total_updates = total_updates
         self.sched_others = _one_cycle(self.opt_others, learning_rate, total_updates)
         self.sched_audio = _one_cycle(self.opt_audio, learning_rate * 0.25, total_updates - unfreeze_audio_step)
@@ -146,6 +153,9 @@ class TriadTrainer:
         the set of parameters with gradients is identical across ranks by construction."""
         if self.world <= 1:
             return
+        if self.reducer is not None:   # launched during backward; wait for the reductions
+            self.reducer.finish()
+            return
         avg = not self.global_negatives
         if self.space is None:
             for p in self.model.parameters():
@@ -172,6 +182,8 @@ class TriadTrainer:
         av_loss = av[0] if av is not None else None
         tv_loss = tv[0] if tv is not None else None
         loss_total = self._loss_mix(phase, av_loss, tv_loss, progress)
+        if self.reducer is not None and (self.accumulation_counter + 1) % self.grad_accum == 0:
+            self.reducer.begin(accumulate=self.accumulation_counter % self.grad_accum != 0)
         (loss_total / self.grad_accum).backward()
         if self.space is not None:  # bf16 weight grads -> flat fp32 grads (accumulating micro-steps)
             self.space.gather_shadow_grads(accumulate=self.accumulation_counter % self.grad_accum != 0)
