@@ -107,6 +107,12 @@ int triad_dtemp_finalize(const double* p0, int n0, const double* p1, int n1, con
 int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
                     int splits, float* slabs, void* C, hipStream_t stream);
 
+/* The same GEMM into unscaled fp32 slabs [splits][M][512] only (no reduction): partial sums the
+ * caller reduces with triad_sum_slabs, e.g. dQ over the key-sample chunks of the memory-bounded
+ * (recompute) backward. */
+int triad_tile_gemm_slabs(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, int splits,
+                          float* slabs, hipStream_t stream);
+
 /* C = alpha * op(A) . op(B): A [M][Kd] (a_kcontig=1) or [Kd][M] (0); B [N][Kd] (b_kcontig=1)
  * or [Kd][N] (0); C fp32 or bf16 (out_bf16). M, N multiples of 128, Kd of 64.
  * dQ = temp * dS . K and dK = temp * dS^T . Q of S = temp * Q K^T (model.py:387/505),

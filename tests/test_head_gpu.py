@@ -148,6 +148,51 @@ def test_tv_head_vs_oracle_random(B, Nt, Nv, mix):
     assert _scalar_close(float(tg.grad), float(tr.grad), 2e-3, 1e-5)
 
 
+@pytest.mark.parametrize("kind,B,Nq,Nv", [(0, 10, 61, 90), (1, 9, 24, 70), (0, 4, 33, 40)])
+def test_memory_bounded_recompute_backward(kind, B, Nq, Nv):
+    """ds_budget below the tiled dS size: the forward writes no dS and the backward recomputes S in
+    chunks of 4 key samples (last chunk ragged; one chunk when B = 4), dQ summed over the chunks'
+    fp32 partials. Same losses as the materialising head, gradients and d/dtemp against the fp64
+    oracle at the bf16 bar, and against the materialising head."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(300 + B)
+    Q = _rand_feats(g, (B, Nq, 512))
+    V = _rand_feats(g, (B, Nv, 512))
+    lens = torch.randint(Nv // 2, Nv + 1, (B,), generator=g)
+    lens[0] = Nv
+    for j in range(B):
+        V[j, lens[j]:] = 0
+    mask = (torch.arange(Nq)[None, :] < torch.randint(1, Nq + 1, (B, 1), generator=g)).long()
+    temp, thr, w = 1.3, 0.005, 0.3
+    Qr, Vr = Q.double().requires_grad_(True), V.double().requires_grad_(True)
+    tr = torch.tensor(temp, dtype=torch.float64, requires_grad=True)
+    if kind == 0:
+        total = ref_cpu.av_loss(Qr, Vr, tr)[0]
+    else:
+        total = ref_cpu.tv_loss(Qr, Vr, mask, tr, thr, w)[0]
+    total.backward()
+    geo = ops.Geometry(B, Nq, B, ((Nv + 31) // 32) * 32)
+    per_sample = (geo.R_pad // 32) * (geo.Nk_pad // 32) * 2048
+    res = []
+    for budget in (None, 4 * per_sample):
+        Qg = Q.to(dev, torch.bfloat16).requires_grad_(True)
+        Vg = V.to(dev, torch.bfloat16).requires_grad_(True)
+        tg = torch.tensor(temp, device=dev, requires_grad=True)
+        kw = dict(q_mask=mask.to(dev), threshold=thr, sparsity_weight=w) if kind == 1 else {}
+        losses, st, clip = ops.contrastive_head(kind, Qg, Vg, tg, ds_budget=budget, **kw)
+        losses[0].backward()
+        assert _scalar_close(float(losses[0]), float(total))
+        _check_grad(Qg.grad, Qr.grad.numpy())
+        _check_grad(Vg.grad, Vr.grad.numpy())
+        assert _scalar_close(float(tg.grad), float(tr.grad), 2e-3, 1e-5)
+        res.append((Qg.grad.float().cpu(), Vg.grad.float().cpu(), float(tg.grad)))
+    assert ops.ds_chunk_samples(geo, 4 * per_sample) == (4 if B > 4 else B)
+    (q0, v0, t0), (q1, v1, t1) = res
+    assert float((q0 - q1).norm() / q0.norm()) < 1e-2
+    assert float((v0 - v1).norm() / v0.norm()) < 1e-2
+    assert _scalar_close(t1, t0, 1e-3, 1e-6)
+
+
 @pytest.mark.parametrize("form", [0, 1, 2, 3])
 @pytest.mark.parametrize("kcontig,bk", [(1, 0), (0, 0), (1, 1), (0, 1)])
 def test_gemm_layouts_vs_torch(kcontig, bk, form):

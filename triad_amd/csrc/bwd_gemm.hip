@@ -195,4 +195,20 @@ int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, 
   return triad_sum_slabs(slabs, splits, (long long)M * TBN, alpha, 1, C, stream);
 }
 
+// Unscaled fp32 slabs only: slabs[s][M][512] = partial (split s of nkt) of dS K (dk = 0) or
+// dS^T Q (dk = 1); the caller reduces (triad_sum_slabs), possibly over several launches' slabs
+// (the memory-bounded backward sums the dQ partials of its key-sample chunks this way).
+int triad_tile_gemm_slabs(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, int splits,
+                          float* slabs, hipStream_t stream) {
+  if (M % TBM || nkt <= 0 || splits < 1 || !slabs) return TRIAD_EINVAL;
+  const int kps = (nkt + splits - 1) / splits;
+  dim3 grid(M / TBM, splits);
+  const bf16* d = (const bf16*)Dt;
+  const bf16* b = (const bf16*)B;
+  if (dk) hipLaunchKernelGGL((tile_gemm_ring_kernel<true, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  else hipLaunchKernelGGL((tile_gemm_ring_kernel<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
 }  // extern "C"

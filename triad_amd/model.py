@@ -331,6 +331,7 @@ class MultiModalModel(nn.Module):
         self.use_amp = use_amp
         self.amp_dtype = torch.bfloat16
         self.negatives_group = None  # process group for global negatives (SURVEY §8e Mode G)
+        self.ds_budget = None        # bytes of tiled dS a head may materialise (None: ops.DS_BUDGET_BYTES)
 
     def enable_global_negatives(self, group=None):
         """Contrast every local query against the keys of all data-parallel ranks."""
@@ -346,14 +347,16 @@ class MultiModalModel(nn.Module):
     # ---- fused training heads -------------------------------------------------------
     def _av_head(self, audio_feats, visual_feats):
         losses, stats, clip = ops.contrastive_head(ops.AV, audio_feats, visual_feats, self.temperature,
-                                                   group=self.negatives_group)
+                                                   group=self.negatives_group,
+                                                   ds_budget=getattr(self, "ds_budget", None))
         return (losses[0], losses[1], losses[2], losses[3], LazyStats(_AV_KEYS, stats)), clip
 
     def _tv_head(self, text_feats, visual_feats, attention_mask):
         losses, stats, clip = ops.contrastive_head(ops.TV, text_feats, visual_feats, self.temperature,
                                                    q_mask=attention_mask, threshold=self.patch_sparsity_threshold,
                                                    sparsity_weight=self.patch_sparsity_weight,
-                                                   group=self.negatives_group)
+                                                   group=self.negatives_group,
+                                                   ds_budget=getattr(self, "ds_budget", None))
         return (losses[0], LazyStats(_TV_KEYS, stats)), clip
 
     # ---- materialising debug path (small B), reference model.py:370-593 -------

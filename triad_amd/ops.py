@@ -119,6 +119,92 @@ def _gemm_splits(wgs, nkt, cus=256, max_splits=8):
     return best
 
 
+# Largest tiled dS a head materialises (bytes); above it the backward recomputes S in chunks.
+# Measured (tools/recompute_ab.py, profiles/r02_recompute_ab.log): materialising is faster at every
+# shape -- c3 AV 9.70 vs 13.02 ms fwd+bwd, c4 per-rank (256 x 2048 samples, 47 GB dS) 74.7 vs
+# 101-110 ms -- so the budget is memory, not speed: a quarter of the device's HBM, at most 64 GiB
+# (the c4 per-rank dS fits on a 288 GB MI355X beside the step's activations).
+DS_BUDGET_BYTES = None
+
+
+def _default_budget(dev) -> int:
+    if DS_BUDGET_BYTES is not None:
+        return int(DS_BUDGET_BYTES)
+    total = torch.cuda.get_device_properties(dev).total_memory
+    return min(64 << 30, total // 4)
+
+
+def ds_bytes(g: Geometry) -> int:
+    """Bytes of the tiled bf16 dS of a head geometry ([R_pad/32][CT][1024])."""
+    return (g.R_pad // 32) * _rup(g.C_pad // 32, 4) * 2048
+
+
+def ds_chunk_samples(g: Geometry, budget: int) -> int:
+    """Key samples per chunk of the memory-bounded backward: all of them when the whole dS fits
+    the budget, else the largest multiple of 4 whose dS chunk does (at least 4)."""
+    if ds_bytes(g) <= budget:
+        return g.Bk
+    per = (g.R_pad // 32) * (g.Nk_pad // 32) * 2048
+    return max(4, (budget // per) // 4 * 4)
+
+
+def recompute_backward(g: Geometry, Qb, Kb, temp, kind, diag_off, argmax, dclip, qw, gdiag, coef, need_q, need_k,
+                       chunk, stream, ds_buf=None):
+    """dQ / dK / dL-dtemp partials WITHOUT a forward-written dS: per chunk of `chunk` key samples,
+    triad_pairsim_dS recomputes S for those keys and writes that chunk's full dS (clamp + max +
+    diagonal terms, weighted by coef), dK rows of those keys come from one tile GEMM (complete:
+    a key's gradient only involves its own dS columns), and dQ accumulates the chunks' fp32 partial
+    sums (triad_tile_gemm_slabs), reduced once at the end. Peak dS memory = one chunk.
+    Returns (dQ [R_pad][512] bf16 | None, dK [CT*32][512] bf16 | None, dt_part fp64)."""
+    dev = Qb.device
+    nkb = g.Nk_pad // 32
+    CT = _rup(g.C_pad // 32, 4)
+    nchunks = -(-g.Bk // chunk)
+    CT_c = _rup(chunk * nkb, 4)
+    n_ds = (g.R_pad // 32) * CT_c * 1024
+    dS = ds_buf if ds_buf is not None and ds_buf.numel() >= n_ds else \
+        torch.empty(n_ds, dtype=torch.bfloat16, device=dev)
+    dQ = dK = slabs = None
+    splits = 1
+    if need_q:
+        if nchunks == 1:
+            dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
+        else:
+            splits = _gemm_splits(g.R_pad // 128, chunk * nkb)
+            slabs = torch.empty(nchunks * splits, g.R_pad, D, dtype=torch.float32, device=dev)
+    if need_k:
+        dK = torch.empty(CT * 32, D, dtype=torch.bfloat16, device=dev)
+    parts = []
+    for c in range(nchunks):
+        j0 = c * chunk
+        nc = min(chunk, g.Bk - j0)
+        gc = Geometry(g.Bq, g.Nq, nc, g.Nk_eff)
+        ctc = _rup(nc * nkb, 4)
+        Kc = Kb[j0 * g.Nk_pad:]
+        dclip_c = dclip[:, j0:j0 + nc].contiguous() if nchunks > 1 else dclip
+        dt_c = torch.empty(call("triad_pairsim_nparts", g.R_pad, nc), dtype=torch.float64, device=dev)
+        call("triad_pairsim_dS", ptr(Qb), ptr(Kc), g.R, g.R_pad, g.Nq, g.Bq, nc, g.Nk_pad, g.Nk_eff, D,
+             ptr(temp), CLAMP_LO[kind], 1, diag_off - j0, ptr(argmax[j0:]), ptr(dclip_c), ptr(qw), ptr(gdiag),
+             ptr(coef), ptr(dS), ctc, ptr(dt_c), stream,
+             meta=dict(kind=kind, flops=0.0, recompute_flops=2.0 * g.R * nc * g.Nk_eff * D))
+        parts.append(dt_c)
+        fl = 2.0 * g.R * nc * g.Nk_eff * D
+        if need_q:
+            if nchunks == 1:
+                tile_gemm(dS, ctc, 0, Kc, g.R_pad, nc * nkb, temp, dQ, stream,
+                          meta=dict(kind=kind, flops=fl, what="dQ"))
+            else:
+                call("triad_tile_gemm_slabs", ptr(dS), ctc, 0, ptr(Kc), g.R_pad, nc * nkb, splits,
+                     ptr(slabs[c * splits]), stream, meta=dict(kind=kind, flops=fl, what="dQ"))
+        if need_k:
+            tile_gemm(dS, ctc, 1, Qb, ctc * 32, g.R_pad // 32, temp, dK[j0 * g.Nk_pad:], stream,
+                      meta=dict(kind=kind, flops=fl, what="dK"))
+    if need_q and nchunks > 1:
+        dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
+        call("triad_sum_slabs", ptr(slabs), nchunks * splits, g.R_pad * D, ptr(temp), 1, ptr(dQ), stream)
+    return dQ, dK, torch.cat(parts) if len(parts) > 1 else parts[0]
+
+
 class _ContrastiveHead(torch.autograd.Function):
     """Outputs: total, contrastive, reg, aux (0.01*l_smooth for AV, sparsity for TV), stats[9], clip.
 
@@ -134,7 +220,7 @@ class _ContrastiveHead(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, q, k, temperature, kind, q_mask, thr, w_sparse, group):
+    def forward(ctx, q, k, temperature, kind, q_mask, thr, w_sparse, group, ds_budget):
         _check_device(q, k, temperature, q_mask)
         Bq, Nq, dq = q.shape
         Bl, Nk, dk = k.shape
@@ -167,8 +253,13 @@ class _ContrastiveHead(torch.autograd.Function):
         diagS = torch.empty(g.Bq, g.Nq, g.Nk_pad, dtype=torch.float32, device=dev)
         need_grad = any(ctx.needs_input_grad[:3])  # (forward itself runs under no_grad)
         CT = _rup(g.C_pad // 32, 4)
-        dS = torch.empty((g.R_pad // 32) * CT * 1024, dtype=torch.bfloat16, device=dev) if need_grad else None
-        st_part = torch.empty(nparts, dtype=torch.float64, device=dev) if need_grad else None
+        budget = _default_budget(dev) if ds_budget is None else int(ds_budget)
+        chunk = ds_chunk_samples(g, budget)
+        # materialise the unit dS in the forward only when it fits the budget; otherwise the
+        # backward recomputes it chunk by chunk (recompute_backward)
+        write_ds = need_grad and chunk == g.Bk
+        dS = torch.empty((g.R_pad // 32) * CT * 1024, dtype=torch.bfloat16, device=dev) if write_ds else None
+        st_part = torch.empty(nparts, dtype=torch.float64, device=dev) if write_ds else None
         call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
              ptr(temp), CLAMP_LO[kind], 1, rank * Bq, ptr(rowmax), ptr(argmax), ptr(nn_part), ptr(diagS),
              ptr(dS), CT, ptr(st_part), None, st,
@@ -177,7 +268,7 @@ class _ContrastiveHead(torch.autograd.Function):
                        # tiled unit-dS stream the training forward also writes is NOT algorithmic
                        # (bench.py reports it, from PMC, as traffic)
                        bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R,
-                       ds_bytes=(2.0 * g.R_pad * g.C_pad if need_grad else 0.0)))
+                       ds_bytes=(2.0 * g.R_pad * g.C_pad if write_ds else 0.0)))
         clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
         qw = torch.empty(g.R, dtype=torch.float32, device=dev)
         qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
@@ -210,6 +301,7 @@ class _ContrastiveHead(torch.autograd.Function):
         if need_grad:
             ctx.save_for_backward(Qb, Kb, argmax, rowmax, dclip_rows, qw, gdiag, temp, dS, st_part, dgt_part)
         ctx.geom, ctx.kind, ctx.n_el, ctx.w_sparse, ctx.nparts, ctx.CT = g, kind, n_el, float(w_sparse), nparts, CT
+        ctx.chunk = chunk
         ctx.group, ctx.W, ctx.rank, ctx.Nk = group, W, rank, Nk
         ctx.q_dtype, ctx.k_dtype, ctx.t_dtype = q.dtype, k.dtype, temperature.dtype
         losses, stats = out[:4].clone(), out[4:].clone()
@@ -219,9 +311,9 @@ class _ContrastiveHead(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_total, g_ce, g_reg, g_aux, g_stats, g_clip):
-        none8 = (None,) * 8
+        none9 = (None,) * 9
         if g_total is None and g_ce is None and g_reg is None and g_aux is None:
-            return none8
+            return none9
         Qb, Kb, argmax, rowmax, dclip, qw, gdiag, temp, dS, st_part, dgt_part = ctx.saved_tensors
         g, kind, W, rank, CT = ctx.geom, ctx.kind, ctx.W, ctx.rank, ctx.CT
         dev = Qb.device
@@ -239,7 +331,8 @@ class _ContrastiveHead(torch.autograd.Function):
             c_diag = ctx.w_sparse * c_reg + ga_  # reg = ... + w*sparsity; aux = sparsity
             c_cal = torch.zeros_like(c_reg)
         has_cal = 1 if (kind == AV and rank == 0) else 0   # the l_cal term is counted once
-        fast = g_total is not None and g_ce is None and g_reg is None and g_aux is None
+        fast = g_total is not None and g_ce is None and g_reg is None and g_aux is None and dS is not None
+        gq = gk = gt = None
         if fast:
             # dS = c_nn * (unit l_nonneg grad [written by the forward] + ratio_max * max term
             #               + ratio_diag * diagonal term); the ratios are host constants here
@@ -254,25 +347,26 @@ class _ContrastiveHead(torch.autograd.Function):
             w = torch.stack([c_nn, c_ce / temp[0], c_diag / temp[0], c_cal]).contiguous()
             parts = (st_part, ctx.nparts, max_part, nmp, dgt_part, g.Bq)
         else:
+            # recompute form: any mix of upstream gradients, or a dS over the memory budget
             coef = torch.stack([c_ce, c_nn, c_diag, c_cal]).contiguous()
-            dt_part = torch.empty(ctx.nparts, dtype=torch.float64, device=dev)
-            call("triad_pairsim_dS", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
-                 ptr(temp), CLAMP_LO[kind], 1, rank * g.Bq, ptr(argmax), ptr(dclip), ptr(qw), ptr(gdiag), ptr(coef),
-                 ptr(dS), CT, ptr(dt_part), st, meta=dict(kind=kind, flops=0.0, recompute_flops=2.0 * g.R * g.Bk * g.Nk_eff * D))
-            alpha = temp
+            dQ, dK, dt_part = recompute_backward(g, Qb, Kb, temp, kind, rank * g.Bq, argmax, dclip, qw, gdiag, coef,
+                                                 ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.chunk, st,
+                                                 ds_buf=dS)
             w = torch.stack([torch.ones_like(c_ce), zero, zero, c_cal]).contiguous()
-            parts = (dt_part, ctx.nparts, None, 0, None, 0)
-        gq = gk = gt = None
-        if ctx.needs_input_grad[0]:
+            parts = (dt_part, dt_part.numel(), None, 0, None, 0)
+            if dQ is not None:
+                gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(ctx.q_dtype)
+        if fast and ctx.needs_input_grad[0]:
             dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
             tile_gemm(dS, CT, 0, Kb, g.R_pad, g.C_pad // 32, alpha, dQ, st,
                       meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dQ"))
             gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(ctx.q_dtype)
         if ctx.needs_input_grad[1]:
-            Mk = CT * 32
-            dK = torch.empty(Mk, D, dtype=torch.bfloat16, device=dev)
-            tile_gemm(dS, CT, 1, Qb, Mk, g.R_pad // 32, alpha, dK, st,
-                      meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dK"))
+            if fast:
+                Mk = CT * 32
+                dK = torch.empty(Mk, D, dtype=torch.bfloat16, device=dev)
+                tile_gemm(dS, CT, 1, Qb, Mk, g.R_pad // 32, alpha, dK, st,
+                          meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dK"))
             Nk_pad = g.Nk_pad
             if W > 1:
                 from . import dist as tdist
@@ -284,10 +378,11 @@ class _ContrastiveHead(torch.autograd.Function):
             call("triad_dtemp_finalize", ptr(p0), n0, ptr(p1), n1, ptr(p2), n2, ptr(temp), ptr(w), has_cal,
                  ptr(dt), st)
             gt = dt.reshape(()).to(ctx.t_dtype)
-        return gq, gk, gt, None, None, None, None, None
+        return gq, gk, gt, None, None, None, None, None, None
 
 
-def contrastive_head(kind, q, k, temperature, q_mask=None, threshold=0.0, sparsity_weight=0.0, group=None):
+def contrastive_head(kind, q, k, temperature, q_mask=None, threshold=0.0, sparsity_weight=0.0, group=None,
+                     ds_budget=None):
     """Fused similarity + aggregation + InfoNCE + regularisers.
 
     kind AV: q = audio feats (B,Na,512), k = visual feats (B,Nv,512) (model.py:470-472)
@@ -296,9 +391,12 @@ def contrastive_head(kind, q, k, temperature, q_mask=None, threshold=0.0, sparsi
     Returns (losses, stats[9], clip[B_g,B_g]); losses = (total, contrastive, reg, aux) 0-dim tensors.
     In global mode the gradients w.r.t. q, k, temperature are this rank's share of the
     full-loss gradient: sum them over ranks (the trainer's Mode-G all-reduce does).
+    ds_budget: bytes of tiled dS the training forward may materialise (default: a quarter of the
+    device's HBM, at most 64 GiB); above it the backward recomputes S in key-sample chunks of at
+    most that size (recompute_backward). The c4 per-rank shape (256 x 2048 samples) needs 47 GB.
     """
     total, ce, reg, aux, stats, clip = _ContrastiveHead.apply(q, k, temperature, kind, q_mask, threshold,
-                                                              sparsity_weight, group)
+                                                              sparsity_weight, group, ds_budget)
     return (total, ce, reg, aux), stats, clip
 
 
