@@ -152,6 +152,17 @@ int triad_projhead_bwd(const void* dy, int M, int H, const void* W2t, const void
                        const float* mean, const float* rstd, const float* gamma, void* dy1, void* dh, long long ldh,
                        float* colpart, hipStream_t stream);
 
+/* LayerNorm(512) forward of the library-GEMM projection head (model.py:68/116/326 under
+ * autocast): ln = bf16((y1 - mean) rstd gamma + beta) over bf16 y1 [M][512], fp32 statistics
+ * (biased variance, eps) kept in mean / rstd [M]. */
+int triad_ln_fwd(const void* y1, int M, const float* gamma, const float* beta, float eps, void* ln, float* mean,
+                 float* rstd, hipStream_t stream);
+
+/* Its backward from a bf16 dln: dy1 (bf16) and per-block column partials [nblocks][3][512] of
+ * dgamma, dbeta, db1 (= column sums of dy1), reduced by triad_sum_slabs. */
+int triad_ln_bwd3(const void* dln, const void* y1, const float* mean, const float* rstd, const float* gamma, int M,
+                  void* dy1, float* part, int nblocks, hipStream_t stream);
+
 /* LayerNorm(512) backward: dy1 (bf16) from dln (fp32), y1, mean, rstd, gamma; per-block
  * column partials of dgamma / dbeta in dgb_part [nblocks][2][512]. */
 int triad_ln_bwd(const float* dln, const void* y1, const float* mean, const float* rstd, const float* gamma, int M,

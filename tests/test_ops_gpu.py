@@ -20,8 +20,9 @@ def _rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
+@pytest.mark.parametrize("form", ["fused", "lib"])
 @pytest.mark.parametrize("rows,H", [(130, 768), (256, 384), (64 * 5 + 3, 1024)])
-def test_projection_head_fwd_bwd(rows, H):
+def test_projection_head_fwd_bwd(rows, H, form):
     from triad_amd import ops
     torch.manual_seed(rows + H)
     p1, ln, p2 = nn.Linear(H, 512), nn.LayerNorm(512), nn.Linear(512, 512)
@@ -42,7 +43,7 @@ def test_projection_head_fwd_bwd(rows, H):
     for a, b in zip((d1, dln, d2), (p1, ln, p2)):
         a.load_state_dict(b.state_dict())
     hd = h.to(dev).requires_grad_(True)
-    y = ops.projection_head(hd, d1, dln, d2)
+    y = ops.projection_head(hd, d1, dln, d2, form=form)
     assert y.dtype == torch.bfloat16 and y.shape == (2, rows, 512)
     # forward: bf16-rounded outputs of the same bf16 arithmetic (1-ulp bf16 tolerance)
     y_ref = y_ref.detach()

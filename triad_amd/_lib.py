@@ -39,6 +39,8 @@ SIGNATURES = {
     "triad_projhead_bwd_slabs": [i32],
     "triad_projhead_bwd": [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp],
     "triad_ln_bwd": [vp, vp, vp, vp, vp, i32, vp, vp, i32, vp],
+    "triad_ln_fwd": [vp, i32, vp, vp, f32, vp, vp, vp, vp],
+    "triad_ln_bwd3": [vp, vp, vp, vp, vp, i32, vp, vp, i32, vp],
     "triad_sum_slabs": [vp, i32, i64, vp, i32, vp, vp],
     "triad_colsum_splits": [i64, i32],
     "triad_colsum": [vp, i64, i32, i64, vp, f32, i32, vp, vp],
@@ -155,6 +157,20 @@ def call(name, *args, meta=None):
         what = "invalid argument/shape" if rc == 1001 else f"hipError_t {rc}"
         raise TriadError(f"{name} failed: {what}")
     return rc
+
+
+def timed(name, fn, meta=None):
+    """Run fn() (library work on the current stream, e.g. a hipBLASLt GEMM) and, when TIMERS
+    tracks `name`, record its HIP-event interval like an entry point's."""
+    if TIMERS is not None and name in TIMERS:
+        import torch
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn()
+        e1.record()
+        TIMERS[name].append((e0, e1, meta))
+        return out
+    return fn()
 
 
 def ptr(t):

@@ -481,29 +481,22 @@ __global__ void dtemp_finalize_kernel(const double* __restrict__ p0, int n0, con
   }
 }
 
-#ifndef TRIAD_FWD_GRID_TARGET
-#define TRIAD_FWD_GRID_TARGET 2048
-#endif
+// Key-sample split of the (256-row block, key samples) grid: the count minimising
+// (dispatch rounds of one workgroup per CU over 256 CUs) x (key samples per workgroup + the
+// query-fragment load, ~0.3 sample). Whole rounds keep the last wave of workgroups from leaving
+// CUs idle; fewer, longer workgroups amortise the query load (TV: 32 row blocks -> 8 splits of
+// 32 samples, one round; AV: 200 row blocks -> 32 splits of 8). Measured against the former fixed
+// 2048-workgroup target: AV train forward 3.00 -> 2.96 ms, TV 0.567 -> 0.532 ms
+// (profiles/r02_fwd_grid_ab.log).
 int grid_for(int R_pad, int Bk, int* jpw, int* ysplit) {
   const int xb = R_pad / ROWS_PER_WG;
-#ifdef TRIAD_FWD_GRID_BAL
-  {  // A/B: key-split count minimising (dispatch rounds over 256 CUs) x (samples + query-load cost)
-    double best = 1e30;
-    int bys = 1;
-    for (int y = 1; y <= Bk; ++y) {
-      const int j = (Bk + y - 1) / y, ya = (Bk + j - 1) / j;
-      const double rounds = (double)((xb * ya + 255) / 256);
-      const double c = rounds * (j + TRIAD_FWD_GRID_BAL * 0.1);
-      if (c < best - 1e-9) { best = c; bys = ya; }
-    }
-    *jpw = (Bk + bys - 1) / bys;
-    *ysplit = (Bk + *jpw - 1) / *jpw;
-    return xb;
+  double best = 1e30;
+  int ys = 1;
+  for (int y = 1; y <= Bk; ++y) {
+    const int j = (Bk + y - 1) / y, ya = (Bk + j - 1) / j;
+    const double c = (double)((xb * ya + 255) / 256) * (j + 0.3);
+    if (c < best - 1e-9) { best = c; ys = ya; }
   }
-#endif
-  int ys = (TRIAD_FWD_GRID_TARGET + xb - 1) / xb;
-  if (ys > Bk) ys = Bk;
-  if (ys < 1) ys = 1;
   *jpw = (Bk + ys - 1) / ys;
   *ysplit = (Bk + *jpw - 1) / *jpw;
   return xb;

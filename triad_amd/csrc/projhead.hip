@@ -51,6 +51,86 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
   }
 }
 
+// LayerNorm(512) forward of the library-GEMM projection head, one wave per row (8 features per
+// lane): mean / biased variance in fp32 over the bf16 y1 row (F.layer_norm under autocast runs in
+// fp32, model.py:68/116/326), ln = bf16((y1 - mean) * rstd * gamma + beta) -- the operand autocast
+// feeds projection2 -- and mean / rstd kept for the backward.
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16* __restrict__ y1, int M, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps, bf16* __restrict__ ln,
+                                                     float* __restrict__ mean, float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float gm[8], bt[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { gm[k] = gamma[lane * 8 + k]; bt[k] = beta[lane * 8 + k]; }
+  for (int r = blockIdx.x * 4 + wave; r < M; r += gridDim.x * 4) {
+    const bf16x8 yv = *(const bf16x8*)(y1 + (size_t)r * PN + lane * 8);
+    float x[8], s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { x[k] = (float)yv[k]; s += x[k]; }
+    const float mu = wave_sum(s) * (1.f / PN);
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { const float d = x[k] - mu; q += d * d; }
+    const float rs = rsqrtf(wave_sum(q) * (1.f / PN) + eps);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (bf16)((x[k] - mu) * rs * gm[k] + bt[k]);
+    *(bf16x8*)(ln + (size_t)r * PN + lane * 8) = o;
+    if (lane == 0) { mean[r] = mu; rstd[r] = rs; }
+  }
+}
+
+// LayerNorm backward of the library-GEMM head: dln bf16 (autocast's projection2 input gradient),
+// dy1 = bf16(rstd (g - mean(g) - xh mean(g xh))), g = dln gamma, and per-workgroup column
+// partials [grid][3][512] of dgamma = sum dln xh, dbeta = sum dln, db1 = sum dy1 (the layout of
+// triad_projhead_bwd's colpart, reduced by triad_sum_slabs).
+__global__ __launch_bounds__(256) void ln_bwd3_kernel(const bf16* __restrict__ dln, const bf16* __restrict__ y1,
+                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                      const float* __restrict__ gamma, int M, bf16* __restrict__ dy1,
+                                                      float* __restrict__ part) {
+  __shared__ float sp[3][4][PN];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float pg[8], pb[8], p1[8], gm[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { pg[k] = 0.f; pb[k] = 0.f; p1[k] = 0.f; gm[k] = gamma[lane * 8 + k]; }
+  for (int r = blockIdx.x * 4 + wave; r < M; r += gridDim.x * 4) {
+    const float mu = mean[r], rs = rstd[r];
+    const bf16x8 dv8 = *(const bf16x8*)(dln + (size_t)r * PN + lane * 8);
+    const bf16x8 yv = *(const bf16x8*)(y1 + (size_t)r * PN + lane * 8);
+    float xh[8], g[8], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      xh[k] = ((float)yv[k] - mu) * rs;
+      const float dv = (float)dv8[k];
+      g[k] = dv * gm[k];
+      s1 += g[k];
+      s2 += g[k] * xh[k];
+      pg[k] += dv * xh[k];
+      pb[k] += dv;
+    }
+    s1 = wave_sum(s1) * (1.f / PN);
+    s2 = wave_sum(s2) * (1.f / PN);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o[k] = (bf16)(rs * (g[k] - s1 - xh[k] * s2));
+      p1[k] += (float)o[k];
+    }
+    *(bf16x8*)(dy1 + (size_t)r * PN + lane * 8) = o;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sp[0][wave][lane * 8 + k] = pg[k];
+    sp[1][wave][lane * 8 + k] = pb[k];
+    sp[2][wave][lane * 8 + k] = p1[k];
+  }
+  __syncthreads();
+  for (int n = threadIdx.x; n < 3 * PN; n += blockDim.x) {
+    const int c = n / PN, f = n - c * PN;
+    part[(size_t)blockIdx.x * 3 * PN + n] = sp[c][0][f] + sp[c][1][f] + sp[c][2][f] + sp[c][3][f];
+  }
+}
+
 // Column sums, HBM-rate form (bias gradients over 8-65 K token rows): thread = 8 consecutive
 // columns (one 16-byte load per row) x a strided set of rows of the block's row slice; the row
 // lanes meet in LDS; part[slice][cols] fp32. Then colsum_reduce_kernel: 64 columns x 16 slice
@@ -142,6 +222,25 @@ int triad_ln_bwd(const float* dln, const void* y1, const float* mean, const floa
   if (M <= 0 || nblocks <= 0) return TRIAD_EINVAL;
   hipLaunchKernelGGL(ln_bwd_kernel, dim3(nblocks), dim3(256), 0, stream, dln, (const bf16*)y1, mean, rstd, gamma, M,
                      (bf16*)dy1, dgb_part);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_ln_fwd(const void* y1, int M, const float* gamma, const float* beta, float eps, void* ln, float* mean,
+                 float* rstd, hipStream_t stream) {
+  if (M <= 0) return TRIAD_EINVAL;
+  const int nb = (M + 3) / 4 < 4096 ? (M + 3) / 4 : 4096;
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3(nb), dim3(256), 0, stream, (const bf16*)y1, M, gamma, beta, eps, (bf16*)ln,
+                     mean, rstd);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_ln_bwd3(const void* dln, const void* y1, const float* mean, const float* rstd, const float* gamma, int M,
+                  void* dy1, float* part, int nblocks, hipStream_t stream) {
+  if (M <= 0 || nblocks <= 0) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(ln_bwd3_kernel, dim3(nblocks), dim3(256), 0, stream, (const bf16*)dln, (const bf16*)y1, mean,
+                     rstd, gamma, M, (bf16*)dy1, part);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

@@ -15,7 +15,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import TriadError, call, ptr, stream_ptr
+from ._lib import TriadError, call, ptr, stream_ptr, timed
 
 D = 512
 ROWS_PER_WG = 256
@@ -556,10 +556,88 @@ def _projhead_bwd_fused(ctx, dyp, hb, w1b, w2b, g32, y1, ln, mean, rstd):
             db2.to(b2d), None)
 
 
-def projection_head(h, proj1: torch.nn.Linear, layer_norm: torch.nn.LayerNorm, proj2: torch.nn.Linear):
-    """Fused HIP projection head; returns bf16 (B, N, 512) like the autocast reference."""
-    return _ProjectionHead.apply(h, proj1.weight, proj1.bias, layer_norm.weight, layer_norm.bias, proj2.weight,
-                                 proj2.bias, layer_norm.eps)
+class _ProjectionHeadLib(torch.autograd.Function):
+    """The projection head as autocast runs it (model.py:68/116/326): library GEMMs (hipBLASLt via
+    torch.addmm / mm, bias in the GEMM epilogue, one bf16 rounding -- F.linear under autocast) for
+    projection1 / projection2 and their input gradients, the LayerNorm and its backward as single
+    HIP row passes (triad_ln_fwd / triad_ln_bwd3, dgamma / dbeta / db1 column partials in the same
+    pass), the weight gradients on the split-K HIP GEMM (2-4x the library on these
+    contraction-over-tokens shapes, tools/projhead_lib_probe.py)."""
+
+    @staticmethod
+    def forward(ctx, h, w1, b1, gamma, beta, w2, b2, eps):
+        _check_device(h, w1)
+        lead, H = h.shape[:-1], h.shape[-1]
+        M = h.numel() // H
+        if w1.shape != (D, H) or w2.shape != (D, D):
+            raise TriadError("projection head expects Linear(H->512), Linear(512->512)")
+        dev = h.device
+        st = stream_ptr(dev)
+        Mp = _rup(max(M, 1), 128)
+        bf = torch.bfloat16
+        hb = _pad_rows(h.to(bf).reshape(M, H), Mp)
+        w1b = w1.detach().to(bf).contiguous()
+        w2b = w2.detach().to(bf).contiguous()
+        b1b, b2b = b1.detach().to(bf), b2.detach().to(bf)
+        g32 = gamma.detach().to(torch.float32).contiguous()
+        be32 = beta.detach().to(torch.float32).contiguous()
+        fl1, fl2 = 2.0 * M * H * D, 2.0 * M * D * D
+        y1 = timed("hipblaslt", lambda: torch.addmm(b1b, hb, w1b.t()), dict(tag=f"proj-fwd1x{M}", flops=fl1))
+        ln = torch.empty(Mp, D, dtype=bf, device=dev)
+        mean = torch.empty(Mp, dtype=torch.float32, device=dev)
+        rstd = torch.empty(Mp, dtype=torch.float32, device=dev)
+        call("triad_ln_fwd", ptr(y1), Mp, ptr(g32), ptr(be32), float(eps), ptr(ln), ptr(mean), ptr(rstd), st,
+             meta=dict(tag=f"proj-ln{M}", flops=0.0))
+        y = timed("hipblaslt", lambda: torch.addmm(b2b, ln[:M], w2b.t()), dict(tag=f"proj-fwd2x{M}", flops=fl2))
+        ctx.save_for_backward(hb, w1b, w2b, g32, y1, ln, mean, rstd)
+        ctx.shape = (lead, H, M, Mp)
+        ctx.dtypes = (h.dtype, w1.dtype, b1.dtype, gamma.dtype, beta.dtype, w2.dtype, b2.dtype)
+        return y.view(*lead, D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        hb, w1b, w2b, g32, y1, ln, mean, rstd = ctx.saved_tensors
+        lead, H, M, Mp = ctx.shape
+        dev = dy.device
+        st = stream_ptr(dev)
+        f32 = torch.float32
+        dyp = _pad_rows(dy.reshape(M, D).to(torch.bfloat16), Mp)
+        dln = timed("hipblaslt", lambda: torch.mm(dyp, w2b), dict(tag=f"proj-dX2x{M}", flops=2.0 * M * D * D))
+        dy1 = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
+        if Mp > M:
+            dy1[M:].zero_()
+        nb = max(1, min(1024, (M + 3) // 4))
+        part = torch.empty(nb, 3, D, dtype=f32, device=dev)
+        call("triad_ln_bwd3", ptr(dln), ptr(y1), ptr(mean), ptr(rstd), ptr(g32), M, ptr(dy1), ptr(part), nb, st,
+             meta=dict(tag=f"proj-lnbwd{M}", flops=0.0))
+        cols = torch.empty(3, D, dtype=f32, device=dev)
+        call("triad_sum_slabs", ptr(part), nb, 3 * D, None, 0, ptr(cols), st, meta=dict(tag="proj-cols", flops=0.0))
+        dh = timed("hipblaslt", lambda: torch.mm(dy1[:M], w1b), dict(tag=f"proj-dX1x{M}", flops=2.0 * M * D * H))
+        db2 = colsum(dyp, f32)
+        sp2 = _splitk(Mp, (D // 128) * (D // 128))
+        sp1 = _splitk(Mp, (D // 128) * (H // 128))
+        slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
+        dw2 = torch.empty(D, D, dtype=f32, device=dev)
+        call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2), 0, st,
+             meta=dict(tag=f"proj-dW2x{M}", flops=2.0 * M * D * D))
+        dw1 = torch.empty(D, H, dtype=f32, device=dev)
+        call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), 0, st,
+             meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
+        hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
+        return (dh.view(*lead, H).to(hd), dw1.to(w1d), cols[2].to(b1d), cols[0].to(gd), cols[1].to(bd), dw2.to(w2d),
+                db2.to(b2d), None)
+
+
+PROJHEAD_FORM = "fused"
+
+
+def projection_head(h, proj1: torch.nn.Linear, layer_norm: torch.nn.LayerNorm, proj2: torch.nn.Linear, form=None):
+    """HIP projection head; returns bf16 (B, N, 512) like the autocast reference.
+    form "fused": the persistent row-panel kernels (projhead_rows.hip); "lib": library GEMMs +
+    HIP LayerNorm passes (_ProjectionHeadLib)."""
+    fn = _ProjectionHeadLib if (form or PROJHEAD_FORM) == "lib" else _ProjectionHead
+    return fn.apply(h, proj1.weight, proj1.bias, layer_norm.weight, layer_norm.bias, proj2.weight,
+                    proj2.bias, layer_norm.eps)
 
 
 # ----------------------------------------------------------------------------------------
