@@ -435,9 +435,13 @@ def _pad_rows(x: torch.Tensor, rows: int) -> torch.Tensor:
 
 
 def _splitk(Kd, mn_tiles):
-    """Split count so that tiles * splits ~ 2 x CUs, >= 1 k-block (64) per split."""
-    want = max(1, (512 + mn_tiles - 1) // mn_tiles)
-    return max(1, min(want, Kd // 256))
+    """Split-K factor of the projection-head weight gradients (128 x 128 tiles): one round of
+    workgroups over the 256 CUs, >= 640 token rows per split. Measured (tools/dw_proj_forms.py,
+    profiles/r02_dw_proj_forms.log): fewer, longer splits beat two rounds once the slab
+    reduction is counted -- dW2 at 65,536 rows 66 us (16 splits) vs 78 us (32), dW1 86 vs 96 us;
+    the 256 x 256 four-wave form is no faster at its best split."""
+    want = max(1, 256 // mn_tiles)
+    return max(1, min(want, Kd // 640))
 
 
 def _bf16_round(t):
@@ -628,7 +632,9 @@ class _ProjectionHeadLib(torch.autograd.Function):
                 db2.to(b2d), None)
 
 
-PROJHEAD_FORM = "fused"
+# Measured per call, kernel time only (tools/projhead_kernels.py, profiles/r02_projhead_kernels.log):
+# "lib" fwd 142 / bwd 474 us vs "fused" 174 / 600 us at 65,536 rows; lower at every c3 / c5 row count.
+PROJHEAD_FORM = "lib"
 
 
 def projection_head(h, proj1: torch.nn.Linear, layer_norm: torch.nn.LayerNorm, proj2: torch.nn.Linear, form=None):
