@@ -101,3 +101,20 @@ def test_cpu_port_step_runs():
     from oracle import cpu_step
     sec = cpu_step.time_steps(B=2, steps=1, warmup=0, threads=8)
     assert sec > 0
+
+
+def test_reference_compile_line_leaves_the_step_methods_eager():
+    """The reference wraps the model in torch.compile(mode="max-autotune") (train.py:378) but its
+    step calls model.forward_audio_visual / forward_text_visual (train.py:954, 969), which the
+    compiled wrapper delegates to the original module: the HIP head (ctypes entry points inside
+    autograd Functions) runs exactly as without the compile line -- no graph breaks, no tracing.
+    (Why the head is not a torch.library op: DESIGN.md §1b.)"""
+    import torch.nn as nn
+    from triad_amd.model import MultiModalModel
+    m = MultiModalModel.__new__(MultiModalModel)
+    nn.Module.__init__(m)
+    cm = torch.compile(m, mode="max-autotune")
+    assert cm._orig_mod is m
+    for name in ("forward_audio_visual", "forward_text_visual", "forward_triad", "compute_contrastive_loss_av"):
+        bound = getattr(cm, name)
+        assert bound.__self__ is m and bound.__func__ is getattr(MultiModalModel, name)
