@@ -32,7 +32,7 @@ TRACKED = ("triad_pairsim_fwd", "triad_pairsim_dS", "triad_gemm_bf16", "triad_pr
            "triad_gemm_bf16_splitk", "triad_tile_gemm", "triad_dS_patch", "triad_clip_reduce", "triad_losshead",
            "triad_diag_smooth", "triad_diag_sparsity", "triad_dtemp_finalize", "triad_ln_bwd",
            "triad_colsum", "triad_sum_slabs", "triad_gather_rows", "triad_global_znorm",
-           "triad_grad_sumsq", "triad_adamw_step", "triad_ln_fwd", "triad_ln_bwd3", "hipblaslt")
+           "triad_grad_sumsq", "triad_adamw_step", "triad_ln_fwd", "triad_ln_bwd3", "triad_gemm_bf16_bias")
 
 
 def parse():

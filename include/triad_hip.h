@@ -121,6 +121,12 @@ int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, 
                     int M, int N, int Kd, const float* alpha, void* C, long long ldc, int out_bf16,
                     hipStream_t stream);
 
+/* C = op(A) . op(B) (+ bias[n], fp32, added before the single bf16 rounding), bf16 out, tile form
+ * chosen from the shape: the backbone projections (F.linear / its input gradient under autocast)
+ * without a vendor BLAS. M, N multiples of 128, Kd of 64; bias may be NULL. */
+int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                         int M, int N, int Kd, const float* bias, void* C, long long ldc, hipStream_t stream);
+
 /* Split-K GEMM (weight gradients of the projection heads, train.py:987 backward):
  * `splits` fp32 partial slabs [splits][M][N] in caller-owned `slabs`, then C = alpha * sum. */
 int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,

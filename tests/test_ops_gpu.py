@@ -20,7 +20,7 @@ def _rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
-@pytest.mark.parametrize("form", ["fused", "lib"])
+@pytest.mark.parametrize("form", ["fused", "passes"])
 @pytest.mark.parametrize("rows,H", [(130, 768), (256, 384), (64 * 5 + 3, 1024)])
 def test_projection_head_fwd_bwd(rows, H, form):
     from triad_amd import ops
@@ -257,8 +257,9 @@ def test_trainer_bf16_model_weights_track_fp32_masters():
 @pytest.mark.parametrize("M,K,O,bias", [(50944 // 4, 768, 2304, True), (16384, 3072, 768, False),
                                         (20480, 512, 768, True)])
 def test_triad_linear_matches_autocast_linear(M, K, O, bias):
-    """TriadLinear (dW on the HIP split-K GEMM) against nn.Linear under bf16 autocast: same output,
-    dX, dW, db to bf16 tolerance (different fp32 summation order only)."""
+    """TriadLinear (forward and dX on the tiled HIP GEMM with the bias epilogue, dW on the split-K
+    HIP GEMM) against nn.Linear under bf16 autocast (the vendor BLAS): output, dX, dW, db to the
+    bf16 tolerance -- the same bf16 operands and one rounding, a different fp32 summation order."""
     from triad_amd.linear import TriadLinear
     torch.manual_seed(M + K)
     ref = torch.nn.Linear(K, O, bias=bias).to(dev).to(torch.bfloat16)
@@ -273,17 +274,43 @@ def test_triad_linear_matches_autocast_linear(M, K, O, bias):
         yr = ref(xr)
         yf = fast(xf)
     assert yf.dtype == yr.dtype == torch.bfloat16
-    assert torch.equal(yf, yr)
+    d = (yf.float() - yr.float()).abs()
+    assert float((d / (yr.float().abs() + 1e-2)).max()) < 1.6e-2   # <= about one bf16 ulp
+    assert float(d.norm() / yr.float().norm()) < 2e-3
     (yr.float() * gy).sum().backward()
     (yf.float() * gy).sum().backward()
 
     def rel(a, b):
         return float((a.float() - b.float()).norm() / b.float().norm())
-    assert rel(xf.grad, xr.grad) < 1e-6
+    assert rel(xf.grad, xr.grad) < 4e-3
     assert fast.weight.grad.dtype == torch.bfloat16
     assert rel(fast.weight.grad, ref.weight.grad) < 1e-2
     if bias:
         assert rel(fast.bias.grad, ref.bias.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K,bias,dx", [(50944, 2304, 768, True, False), (8192, 768, 3072, False, True),
+                                            (66816, 3072, 768, True, False), (66816, 768, 3072, False, True),
+                                            (256, 768, 768, True, False), (130, 768, 768, True, False)])
+def test_backbone_gemm_vs_fp32(M, N, K, bias, dx):
+    """gemm.linear / gemm.mm (triad_gemm_bf16_bias, tile form by shape; 130 rows -> vendor BLAS
+    fallback) against an fp32 matmul of the same bf16 operands, bias added before the rounding."""
+    from triad_amd import gemm
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    if dx:
+        a = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+        w = torch.randn(K, N, device=dev, generator=g).to(torch.bfloat16)
+        y = gemm.mm(a, w)
+        ref = a.float() @ w.float()
+    else:
+        a = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+        w = torch.randn(N, K, device=dev, generator=g).to(torch.bfloat16)
+        b = torch.randn(N, device=dev, generator=g).to(torch.bfloat16) if bias else None
+        y = gemm.linear(a, w, b)
+        ref = a.float() @ w.float().t() + (b.float() if bias else 0.0)
+    assert y.dtype == torch.bfloat16 and y.shape == (M, N)
+    assert torch.allclose(y.float(), ref.to(torch.bfloat16).float(), rtol=1.6e-2, atol=1e-2 * float(ref.abs().max()))
+    assert float((y.float() - ref).norm() / ref.norm()) < 3e-3
 
 
 @pytest.mark.parametrize("rows,cols", [(50944, 768), (8192, 3072), (100, 8), (65536, 512), (7, 2304)])
@@ -340,9 +367,9 @@ def test_side_stream_weight_grads_bit_identical():
 def test_modality_streams_match_single_stream():
     """forward_triad with the audio / text backbones on their own streams (and their backward
     chains with them) against the single-stream order: the same losses and the same reduced
-    gradient buffer after one trainer step from identical models / seeds (library GEMMs may
-    differ in summation order between launches, so to 1e-4 relative, far below what a stream
-    race would produce)."""
+    gradient buffer after one trainer step from identical models / seeds (the vendor convolution /
+    fallback GEMMs may pick a different algorithm on their first call, so to 1e-4 relative, far
+    below what a stream race would produce)."""
     import os
     from triad_amd.model import MultiModalModel
     from triad_amd.train import TriadTrainer
@@ -371,7 +398,7 @@ def test_modality_streams_match_single_stream():
         l_multi, g_multi = run(True)
     finally:
         os.environ.pop("TRIAD_MODALITY_STREAMS", None)
-    assert abs(l_multi - l_single) <= 1e-5 * abs(l_single)
+    assert abs(l_multi - l_single) <= 1e-4 * abs(l_single)
     assert float((g_multi - g_single).norm()) <= 1e-4 * float(g_single.norm())
 
 

@@ -11,7 +11,7 @@ import os
 import sys
 
 CASES = (("visual", 65536, 768), ("audio", 50944, 768), ("text", 8192, 768), ("c5-visual", 43808, 1024))
-FORMS = ("fused", "lib")
+FORMS = ("fused", "passes")
 
 
 def run(iters):

@@ -31,7 +31,7 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--forms", default="fused,lib")
+    ap.add_argument("--forms", default="fused,passes")
     a = ap.parse_args()
     from oracle import ref_cpu
     from triad_amd import _lib, ops

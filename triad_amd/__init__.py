@@ -6,3 +6,8 @@ aggregation / InfoNCE + regularisers and their backward) runs as hand-written
 HIP kernels from libtriad_hip.so.
 """
 __version__ = "0.1.0"
+
+# Library GEMMs go to rocBLAS, not hipBLASLt's stream-K kernels (triad_amd/blas.py).
+from . import blas as _blas  # noqa: E402
+
+_blas.configure()

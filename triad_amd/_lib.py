@@ -34,6 +34,7 @@ SIGNATURES = {
     "triad_tile_gemm": [vp, i64, i32, vp, i32, i32, vp, i32, vp, vp, vp],
     "triad_tile_gemm_slabs": [vp, i64, i32, vp, i32, i32, i32, vp, vp],
     "triad_gemm_bf16": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, i32, vp],
+    "triad_gemm_bf16_bias": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, vp],
     "triad_gemm_bf16_splitk": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp],
     "triad_projhead_fwd": [vp, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, i64, vp, vp, vp, vp, vp],
     "triad_projhead_bwd_slabs": [i32],
@@ -157,20 +158,6 @@ def call(name, *args, meta=None):
         what = "invalid argument/shape" if rc == 1001 else f"hipError_t {rc}"
         raise TriadError(f"{name} failed: {what}")
     return rc
-
-
-def timed(name, fn, meta=None):
-    """Run fn() (library work on the current stream, e.g. a hipBLASLt GEMM) and, when TIMERS
-    tracks `name`, record its HIP-event interval like an entry point's."""
-    if TIMERS is not None and name in TIMERS:
-        import torch
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        out = fn()
-        e1.record()
-        TIMERS[name].append((e0, e1, meta))
-        return out
-    return fn()
 
 
 def ptr(t):

@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
                                                       const bf16* __restrict__ B, long long ldb,
                                                       int M, int N, int Kd, const float* __restrict__ alpha_p,
                                                       OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                      long long slab_stride) {
+                                                      long long slab_stride, const float* __restrict__ bias) {
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * (A_ELEMS + B_ELEMS)];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -151,10 +151,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int n = n0 + wn * 64 + b * 32 + (lane & 31);
+      const float bn = bias ? bias[n] : 0.f;   // F.linear's bias, added before the one rounding
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int m = m0 + wm * 64 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v]);
+        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v] + bn);
       }
     }
 }
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
                                                           const bf16* __restrict__ B, long long ldb, int M, int N,
                                                           int Kd, const float* __restrict__ alpha_p,
                                                           OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                          long long slab_stride) {
+                                                          long long slab_stride, const float* __restrict__ bias) {
   __shared__ __attribute__((aligned(16))) bf16 lds[GB_NB * GB_ST];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -275,10 +276,11 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int n = n0 + wn * 64 + b * 32 + (lane & 31);
+      const float bn = bias ? bias[n] : 0.f;   // F.linear's bias, added before the one rounding
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int m = m0 + wm * 64 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v]);
+        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v] + bn);
       }
     }
 }
@@ -331,7 +333,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
                                                          const bf16* __restrict__ B, long long ldb, int M, int N,
                                                          int Kd, const float* __restrict__ alpha_p,
                                                          OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                         long long slab_stride) {
+                                                         long long slab_stride, const float* __restrict__ bias) {
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * GW_ST];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -402,10 +404,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int n = n0 + wn * 128 + b * 32 + (lane & 31);
+      const float bn = bias ? bias[n] : 0.f;
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int m = m0 + wm * 128 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v]);
+        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v] + bn);
       }
     }
 }
@@ -417,7 +420,9 @@ int g_gemm_form = 0;
 
 template <bool AK, bool BK_, typename OutT>
 int launch(const void* A, long long lda, const void* B, long long ldb, int M, int N, int Kd, const float* alpha,
-           void* C, long long ldc, hipStream_t st, int splits = 1, long long slab_stride = 0) {
+           void* C, long long ldc, hipStream_t st, int splits = 1, long long slab_stride = 0,
+           const float* bias = nullptr, int form = -1) {
+  if (form < 0) form = g_gemm_form;
   if (M % BM || N % BN || Kd % BK || lda % 8 || ldb % 8 || splits < 1) return TRIAD_EINVAL;
   const int kps = ((Kd / BK + splits - 1) / splits) * BK;
   // the 256-row ring pays off on long k loops or many row tiles (conv / projection GEMMs);
@@ -427,24 +432,24 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
   // 2.94 -> 2.67 ms at M = 1.6 M, N = 512, K = 1536); the split-K weight gradients and the
   // shorter forward shapes keep the smaller tiles
   const bool w4_auto = AK && BK_ && splits == 1 && M >= 65536 && Kd >= 1024;
-  if (w4_ok && (g_gemm_form == 3 || (g_gemm_form == 0 && w4_auto))) {
+  if (w4_ok && (form == 3 || (form == 0 && w4_auto))) {
     const int nwg = (M / GW_M) * (N / GW_N);
     hipLaunchKernelGGL((gemm_w4_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(256), 0, st, (const bf16*)A, lda,
-                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride);
+                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
-  if (g_gemm_form != 1 && M % GB_M == 0 &&
-      (g_gemm_form == 2 || M >= 8192 || Kd / splits >= 32768)) {
+  if (form != 1 && M % GB_M == 0 &&
+      (form == 2 || M >= 8192 || Kd / splits >= 32768)) {
     const int nwg = (M / GB_M) * (N / BN);
     hipLaunchKernelGGL((gemm_big_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
-                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride);
+                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
   const int nwg = (M / BM) * (N / BN);
   hipLaunchKernelGGL((gemm_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(256), 0, st, (const bf16*)A, lda,
-                     (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride);
+                     (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
@@ -467,6 +472,29 @@ int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, 
   TRIAD_GEMM_CASE(false, true)
   TRIAD_GEMM_CASE(false, false)
 #undef TRIAD_GEMM_CASE
+  return TRIAD_EINVAL;
+}
+
+// The backbone projections (torch's F.linear / matmul under autocast, routed here by
+// triad_amd/gemm.py): C = op(A) op(B) (+ bias[n] before the one bf16 rounding), bf16 out. Tile
+// form by shape, measured on the c3 shapes (tools/gemm_backend_probe.py,
+// profiles/r02_gemm_backend_probe.log): the 256 x 256 four-wave form when the output is tall and
+// the contraction or width large (M >= 32768 and N * Kd >= 768 * 2304), the 256 x 128 ring for
+// other tall outputs, 128 x 128 below 8192 rows. 740-990 TFLOP/s; rocBLAS's own kernels run the
+// same shapes at 300-790.
+int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                         int M, int N, int Kd, const float* bias, void* C, long long ldc, hipStream_t stream) {
+  int form = 1;
+  if (M >= 32768 && M % GW_M == 0 && N % GW_N == 0 && (long long)N * Kd >= 768LL * 2304) form = 3;
+  else if (M >= 8192 && M % GB_M == 0) form = 2;
+#define TRIAD_GEMM_B(AK, BKC)                                                                     \
+  if (!!a_kcontig == AK && !!b_kcontig == BKC)                                                    \
+    return launch<AK, BKC, bf16>(A, lda, B, ldb, M, N, Kd, nullptr, C, ldc, stream, 1, 0, bias, form);
+  TRIAD_GEMM_B(true, true)
+  TRIAD_GEMM_B(true, false)
+  TRIAD_GEMM_B(false, true)
+  TRIAD_GEMM_B(false, false)
+#undef TRIAD_GEMM_B
   return TRIAD_EINVAL;
 }
 

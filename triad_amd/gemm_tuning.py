@@ -32,6 +32,12 @@ def load_gemm_tuning(device=None) -> bool:
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     if dev.type != "cuda" or "gfx950" not in getattr(torch.cuda.get_device_properties(dev), "gcnArchName", ""):
         return False
+    from . import blas
+    if blas.configure() == "rocblas":
+        # the committed choices are hipBLASLt solution indices (also the "Rocblas" ones: rocBLAS
+        # forwarded them to hipBLASLt), i.e. the stream-K kernels triad_amd/blas.py avoids
+        return False
+    path = TUNING_FILE
     tun = torch.cuda.tunable
     # torch writes its results file at exit: point that at a per-process scratch path so the
     # committed file is never rewritten (and ranks never write one file together)
@@ -39,7 +45,7 @@ def load_gemm_tuning(device=None) -> bool:
     tun.enable(True)
     tun.tuning_enable(False)
     tun.record_untuned_enable(False)
-    ok = bool(tun.read_file(TUNING_FILE))
+    ok = bool(tun.read_file(path))
     if not ok:
         tun.enable(False)
         return False

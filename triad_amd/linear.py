@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from . import gemm as hipgemm
 from ._lib import call, ptr, stream_ptr
 
 MIN_TOKENS = 4096  # DistilBERT at B=256 (8,192 tokens) still gains 1.1-1.8x
@@ -115,7 +116,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(xb, wb)
         ctx.meta = (x.dtype, w.dtype, None if b is None else b.dtype)
         ctx.w_ref = w
-        return F.linear(xb, wb, bb)
+        return hipgemm.linear(xb, wb, bb)
 
     @staticmethod
     def backward(ctx, dy):
@@ -128,7 +129,7 @@ class _LinearFn(torch.autograd.Function):
             x2 = x2.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, wb).view(*xb.shape).to(x_dtype)
+            dx = hipgemm.mm(dy2, wb).view(*xb.shape).to(x_dtype)
         if ctx.needs_input_grad[1]:
             if w_dtype == torch.bfloat16 and side_stream_ok(ctx.w_ref):
                 dw = on_side_stream(lambda: weight_grad(dy2, x2), (dy2, x2))
@@ -155,7 +156,7 @@ class _QKVFn(torch.autograd.Function):
         ctx.save_for_backward(xb, wb)
         ctx.meta = (x.dtype, wq.dtype, None if bq is None else bq.dtype, (wq.shape[0], wk.shape[0], wv.shape[0]))
         ctx.w_refs = (wq, wk, wv)
-        return F.linear(xb, wb, bb)
+        return hipgemm.linear(xb, wb, bb)
 
     @staticmethod
     def backward(ctx, dy):
@@ -166,7 +167,7 @@ class _QKVFn(torch.autograd.Function):
         x2 = xb.reshape(-1, K)
         if x2.stride(1) != 1 or x2.stride(0) != K:
             x2 = x2.contiguous()
-        dx = torch.mm(dy2, wb).view(*xb.shape).to(x_dtype) if ctx.needs_input_grad[0] else None
+        dx = hipgemm.mm(dy2, wb).view(*xb.shape).to(x_dtype) if ctx.needs_input_grad[0] else None
         dws = [None] * 3
         if any(ctx.needs_input_grad[i] for i in (1, 3, 5)):
             if w_dtype == torch.bfloat16 and all(side_stream_ok(w) for w in ctx.w_refs):
@@ -208,16 +209,18 @@ def qkv_projection(q: nn.Linear, k: nn.Linear, v: nn.Linear, x: torch.Tensor) ->
 
 
 def _eligible(mod: nn.Linear, x: torch.Tensor) -> bool:
-    if not (x.is_cuda and mod.weight.requires_grad and torch.is_autocast_enabled("cuda")
-            and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+    # frozen weights too (the DINOv2 base, backbones before their unfreeze step): forward and dX
+    # still run on the HIP GEMM, the weight gradient is simply not requested
+    if not (x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
         return False
     M = x.numel() // max(1, x.shape[-1])
     return M >= MIN_TOKENS and M % 64 == 0 and mod.in_features % 128 == 0 and mod.out_features % 128 == 0
 
 
 class TriadLinear(nn.Linear):
-    """nn.Linear whose training-mode weight gradient runs on the HIP split-K GEMM (same
-    parameters and state-dict keys; any other case is nn.Linear.forward)."""
+    """nn.Linear under bf16 autocast on HIP GEMMs: forward and dX on the tiled GEMM with the bias
+    epilogue (gemm.py), the weight gradient on the split-K GEMM (same parameters and state-dict
+    keys; any other case is nn.Linear.forward)."""
 
     def forward(self, x):
         if _eligible(self, x):

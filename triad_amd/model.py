@@ -264,7 +264,7 @@ class ViTLoRAEmbedder(nn.Module):
         super().__init__()
         self.model = DinoVisionTransformer(arch)
         _load_dinov2_base(self.model, arch)
-        self.model = apply_lora(self.model, lora_rank, lora_alpha)
+        self.model = install_fast_linear(apply_lora(self.model, lora_rank, lora_alpha))  # MLP fc1 / fc2
         self.projection1 = nn.Linear(self.model.embed_dim, 512)
         self.layer_norm = nn.LayerNorm(512)
         self.projection2 = nn.Linear(512, embedding_dim)

@@ -15,7 +15,8 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import TriadError, call, ptr, stream_ptr, timed
+from . import gemm as hipgemm
+from ._lib import TriadError, call, ptr, stream_ptr
 
 D = 512
 ROWS_PER_WG = 256
@@ -101,29 +102,29 @@ def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream, meta=None):
     split-K over the CUs when the row panels alone leave them idle. (A stream-K form -- one run
     of (row panel, k tile) units per CU, no slab round trip -- measured slower: runs start at
     different k offsets, so CUs of one XCD no longer share the streamed B panel in L2.)"""
-    sp = _gemm_splits(M // 128, nkt)
+    sp = _gemm_splits(M // 128, nkt, M)
     slabs = torch.empty(sp * M * D, dtype=torch.float32, device=out.device) if sp > 1 else None
     call("triad_tile_gemm", ptr(dS), CT, dk, ptr(B), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream, meta=meta)
 
 
-def _gemm_splits(wgs, nkt, cus=256, max_splits=8):
-    """Split-K factor that best fills `cus` one-workgroup-per-CU slots (ties -> fewer splits)."""
-    best, best_eff = 1, 0.0
+def _gemm_splits(wgs, nkt, M, cus=256, max_splits=8, t_tile=1.0e-6, hbm=5.0e12):
+    """Split-K factor of the tile GEMM minimising (dispatch rounds of one workgroup per CU) x
+    (k tiles per workgroup) x t_tile + the fp32 slab round trip (write + reduce read of
+    splits x M x 512 x 4 B). The slab term matters when the k loop is short: TV dK (448 row
+    panels, 256 k tiles) ran 0.76 ms with 4 splits, of which ~0.38 ms was the 0.94 GB slab round
+    trip (profiles/r02_bench.json); with the slab term it takes 1 split (0.48 ms), AV dQ 3 instead
+    of 5 (2.98-3.01 vs 3.20 ms), AV dK stays at 4 (profiles/r02_tile_splits_ab.log)."""
+    best, best_c = 1, None
     for sp in range(1, max_splits + 1):
         if sp > nkt:
             break
-        n = wgs * sp
-        eff = n / (cus * -(-n // cus))
-        if eff > best_eff + 0.02:
-            best, best_eff = sp, eff
+        rounds = -(-(wgs * sp) // cus)
+        c = rounds * -(-nkt // sp) * t_tile + (sp * M * D * 8 / hbm if sp > 1 else 0.0)
+        if best_c is None or c < best_c * 0.98:
+            best, best_c = sp, c
     return best
 
 
-# Largest tiled dS a head materialises (bytes); above it the backward recomputes S in chunks.
-# Measured (tools/recompute_ab.py, profiles/r02_recompute_ab.log): materialising is faster at every
-# shape -- c3 AV 9.70 vs 13.02 ms fwd+bwd, c4 per-rank (256 x 2048 samples, 47 GB dS) 74.7 vs
-# 101-110 ms -- so the budget is memory, not speed: a quarter of the device's HBM, at most 64 GiB
-# (the c4 per-rank dS fits on a 288 GB MI355X beside the step's activations).
 DS_BUDGET_BYTES = None
 
 
@@ -170,7 +171,7 @@ def recompute_backward(g: Geometry, Qb, Kb, temp, kind, diag_off, argmax, dclip,
         if nchunks == 1:
             dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
         else:
-            splits = _gemm_splits(g.R_pad // 128, chunk * nkb)
+            splits = _gemm_splits(g.R_pad // 128, chunk * nkb, g.R_pad)
             slabs = torch.empty(nchunks * splits, g.R_pad, D, dtype=torch.float32, device=dev)
     if need_k:
         dK = torch.empty(CT * 32, D, dtype=torch.bfloat16, device=dev)
@@ -560,13 +561,14 @@ def _projhead_bwd_fused(ctx, dyp, hb, w1b, w2b, g32, y1, ln, mean, rstd):
             db2.to(b2d), None)
 
 
-class _ProjectionHeadLib(torch.autograd.Function):
-    """The projection head as autocast runs it (model.py:68/116/326): library GEMMs (hipBLASLt via
-    torch.addmm / mm, bias in the GEMM epilogue, one bf16 rounding -- F.linear under autocast) for
-    projection1 / projection2 and their input gradients, the LayerNorm and its backward as single
-    HIP row passes (triad_ln_fwd / triad_ln_bwd3, dgamma / dbeta / db1 column partials in the same
-    pass), the weight gradients on the split-K HIP GEMM (2-4x the library on these
-    contraction-over-tokens shapes, tools/projhead_lib_probe.py)."""
+class _ProjectionHeadPasses(torch.autograd.Function):
+    """The projection head as autocast runs it (model.py:68/116/326), as separate passes:
+    projection1 / projection2 and their input gradients on the tiled HIP GEMM (gemm.py:
+    256 x 256 / 256 x 128 forms, bias in the epilogue before the one bf16 rounding -- F.linear
+    under autocast), the LayerNorm and its backward as single HIP row passes (triad_ln_fwd /
+    triad_ln_bwd3, dgamma / dbeta / db1 column partials in the same pass), the weight gradients on
+    the split-K HIP GEMM (2-4x hipBLASLt on these contraction-over-tokens shapes,
+    tools/projhead_lib_probe.py)."""
 
     @staticmethod
     def forward(ctx, h, w1, b1, gamma, beta, w2, b2, eps):
@@ -586,13 +588,13 @@ class _ProjectionHeadLib(torch.autograd.Function):
         g32 = gamma.detach().to(torch.float32).contiguous()
         be32 = beta.detach().to(torch.float32).contiguous()
         fl1, fl2 = 2.0 * M * H * D, 2.0 * M * D * D
-        y1 = timed("hipblaslt", lambda: torch.addmm(b1b, hb, w1b.t()), dict(tag=f"proj-fwd1x{M}", flops=fl1))
+        y1 = hipgemm.linear(hb, w1b, b1b, meta=dict(tag=f"proj-fwd1x{M}", flops=fl1))
         ln = torch.empty(Mp, D, dtype=bf, device=dev)
         mean = torch.empty(Mp, dtype=torch.float32, device=dev)
         rstd = torch.empty(Mp, dtype=torch.float32, device=dev)
         call("triad_ln_fwd", ptr(y1), Mp, ptr(g32), ptr(be32), float(eps), ptr(ln), ptr(mean), ptr(rstd), st,
              meta=dict(tag=f"proj-ln{M}", flops=0.0))
-        y = timed("hipblaslt", lambda: torch.addmm(b2b, ln[:M], w2b.t()), dict(tag=f"proj-fwd2x{M}", flops=fl2))
+        y = hipgemm.linear(ln, w2b, b2b, meta=dict(tag=f"proj-fwd2x{M}", flops=fl2))[:M]
         ctx.save_for_backward(hb, w1b, w2b, g32, y1, ln, mean, rstd)
         ctx.shape = (lead, H, M, Mp)
         ctx.dtypes = (h.dtype, w1.dtype, b1.dtype, gamma.dtype, beta.dtype, w2.dtype, b2.dtype)
@@ -606,7 +608,7 @@ class _ProjectionHeadLib(torch.autograd.Function):
         st = stream_ptr(dev)
         f32 = torch.float32
         dyp = _pad_rows(dy.reshape(M, D).to(torch.bfloat16), Mp)
-        dln = timed("hipblaslt", lambda: torch.mm(dyp, w2b), dict(tag=f"proj-dX2x{M}", flops=2.0 * M * D * D))
+        dln = hipgemm.mm(dyp, w2b, meta=dict(tag=f"proj-dX2x{M}", flops=2.0 * M * D * D))
         dy1 = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
         if Mp > M:
             dy1[M:].zero_()
@@ -616,7 +618,7 @@ class _ProjectionHeadLib(torch.autograd.Function):
              meta=dict(tag=f"proj-lnbwd{M}", flops=0.0))
         cols = torch.empty(3, D, dtype=f32, device=dev)
         call("triad_sum_slabs", ptr(part), nb, 3 * D, None, 0, ptr(cols), st, meta=dict(tag="proj-cols", flops=0.0))
-        dh = timed("hipblaslt", lambda: torch.mm(dy1[:M], w1b), dict(tag=f"proj-dX1x{M}", flops=2.0 * M * D * H))
+        dh = hipgemm.mm(dy1, w1b, meta=dict(tag=f"proj-dX1x{M}", flops=2.0 * M * D * H))[:M]
         db2 = colsum(dyp, f32)
         sp2 = _splitk(Mp, (D // 128) * (D // 128))
         sp1 = _splitk(Mp, (D // 128) * (H // 128))
@@ -634,14 +636,14 @@ class _ProjectionHeadLib(torch.autograd.Function):
 
 # Measured per call, kernel time only (tools/projhead_kernels.py, profiles/r02_projhead_kernels.log):
 # "lib" fwd 142 / bwd 474 us vs "fused" 174 / 600 us at 65,536 rows; lower at every c3 / c5 row count.
-PROJHEAD_FORM = "lib"
+PROJHEAD_FORM = "passes"
 
 
 def projection_head(h, proj1: torch.nn.Linear, layer_norm: torch.nn.LayerNorm, proj2: torch.nn.Linear, form=None):
     """HIP projection head; returns bf16 (B, N, 512) like the autocast reference.
-    form "fused": the persistent row-panel kernels (projhead_rows.hip); "lib": library GEMMs +
-    HIP LayerNorm passes (_ProjectionHeadLib)."""
-    fn = _ProjectionHeadLib if (form or PROJHEAD_FORM) == "lib" else _ProjectionHead
+    form "fused": the persistent row-panel kernels (projhead_rows.hip); "passes": tiled HIP GEMMs +
+    HIP LayerNorm row passes (_ProjectionHeadPasses)."""
+    fn = _ProjectionHeadPasses if (form or PROJHEAD_FORM) == "passes" else _ProjectionHead
     return fn.apply(h, proj1.weight, proj1.bias, layer_norm.weight, layer_norm.bias, proj2.weight,
                     proj2.bias, layer_norm.eps)
 

@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import attention
+from . import gemm as hipgemm
 from ._lib import call, ptr, stream_ptr
 from .frontend import patch_embed
 from .postln import gelu
@@ -53,7 +54,7 @@ class _LoRALinear(torch.autograd.Function):
         st = stream_ptr(dev)
         Ab = A.detach().to(torch.bfloat16).contiguous()
         sB = (B.detach() * scaling).to(torch.bfloat16).contiguous()
-        y = F.linear(xb, w.to(torch.bfloat16), None if b is None else b.to(torch.bfloat16))
+        y = hipgemm.linear(xb, w.to(torch.bfloat16), None if b is None else b.to(torch.bfloat16)).contiguous()
         t = torch.empty(M, r, dtype=torch.bfloat16, device=dev)
         call("triad_rows_nt", ptr(xb), K, M, K, ptr(Ab), r, ptr(t), st)
         call("triad_lora_update", ptr(y), O, M, O, ptr(t), ptr(sB), st)
@@ -80,7 +81,7 @@ class _LoRALinear(torch.autograd.Function):
         call("triad_lora_tn", ptr(dy2), O, M, O, ptr(t), ptr(wt), ptr(dt), scaling, ptr(slabs), ptr(dB), st)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, w.to(torch.bfloat16))
+            dx = hipgemm.mm(dy2, w.to(torch.bfloat16))
             call("triad_lora_update", ptr(dx), K, M, K, ptr(dt), ptr(Ab.t().contiguous()), st)
             dx = dx.view(*lead, K).to(x_dtype)
         dAt = torch.empty(K, r, dtype=torch.float32, device=dev)
