@@ -151,9 +151,10 @@ class _Net(torch.nn.Module):
         self.w2 = torch.nn.Parameter(torch.randn(200, 300) * 0.05)
         self.l3 = torch.nn.Linear(200, 4)
 
-    def forward(self, x):
+    def forward(self, x, skip_w2=False):
         h = torch.relu(self.l1(x))
-        h = torch.relu(h @ self.w2.float().t())
+        # skip_w2: like a LayerDrop'd layer on one rank only -- w2 gets no gradient there
+        h = h[:, :200] if skip_w2 else torch.relu(h @ self.w2.float().t())
         return self.l3(h)
 
 
@@ -162,7 +163,7 @@ def _net_inputs(rank, step):
     return torch.randn(8, 16, generator=g), torch.randn(8, 4, generator=g)
 
 
-def _reducer_worker(rank, world, port, wire, q):
+def _reducer_worker(rank, world, port, wire, q, skip=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -178,7 +179,7 @@ def _reducer_worker(rank, world, port, wire, q):
             space.zero_grad(list(range(len(params))))
             x, y = _net_inputs(rank, step)
             red.begin(accumulate=False)
-            ((net(x) - y) ** 2).mean().backward()
+            ((net(x, skip_w2=skip and rank == 1 and step == 1) - y) ** 2).mean().backward()
             launched = red.launched_in_backward
             red.finish()
             out.append((space.flat_g.numpy().copy(), launched, list(red.order)))
@@ -191,18 +192,21 @@ def _reducer_worker(rank, world, port, wire, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("wire", ["fp32", "bf16"])
-def test_overlapped_bucket_reducer_averages_gradients(wire):
+@pytest.mark.parametrize("wire,skip", [("fp32", False), ("bf16", False), ("fp32", True)])
+def test_overlapped_bucket_reducer_averages_gradients(wire, skip):
     """GradBucketReducer (Mode R) on two gloo ranks: after each step the flat gradient buffer is
     the average of the ranks' gradients (bf16 master weight folded in by the hook); the launch
     order is fixed after the first step and identical on both ranks; from the second step on,
-    buckets are launched from the gradient hooks while backward is still running."""
+    buckets are launched from the gradient hooks while backward is still running. skip: in step
+    1 rank 1 produces no gradient for one parameter (a layer LayerDrop skipped on that rank
+    only): its bucket is flushed after backward, in the same order on both ranks, and the
+    average counts the missing gradient as zero."""
     from triad_amd import optim as fo
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_reducer_worker, args=(r, world, port, wire, q)) for r in range(world)]
+    procs = [ctx.Process(target=_reducer_worker, args=(r, world, port, wire, q, skip)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
@@ -222,9 +226,10 @@ def test_overlapped_bucket_reducer_averages_gradients(wire):
         for rank in range(world):
             space.zero_grad(list(range(len(space.params))))
             x, y = _net_inputs(rank, step)
-            ((net(x) - y) ** 2).mean().backward()
+            ((net(x, skip_w2=skip and rank == 1 and step == 1) - y) ** 2).mean().backward()
             i = space.index[id(net.w2)]   # fold the bf16 shadow gradient by hand (the HIP gather needs a GPU)
-            space.flat_g[space.offsets[i]:space.offsets[i] + net.w2.numel()].copy_(net.w2.grad.float().view(-1))
+            if net.w2.grad is not None:
+                space.flat_g[space.offsets[i]:space.offsets[i] + net.w2.numel()].copy_(net.w2.grad.float().view(-1))
             net.w2.grad = None
             acc += space.flat_g / world
         for rank in range(world):
@@ -235,5 +240,7 @@ def test_overlapped_bucket_reducer_averages_gradients(wire):
             assert order == res[0][1][step][2]
             if step == 0:
                 assert launched == 0
-            else:
+            elif not (skip and rank == 1 and step == 1):
                 assert launched >= 1   # overlap: at least one bucket went out during backward
+            # (skip, rank 1, step 1: the bucket of the missing gradient heads the launch order, so
+            # that rank issues everything at the flush -- in the same order as rank 0)
