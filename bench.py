@@ -28,7 +28,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "tri-modal triples/sec (whole node) + loss parity, B=256 at 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
-TRACKED = ("triad_pairsim_fwd", "triad_pairsim_dS", "triad_gemm_bf16", "triad_projhead_fwd", "triad_projhead_bwd",
+TRACKED = ("triad_pairsim_fwd", "triad_pairsim_fwd_multi", "triad_pairsim_dS", "triad_gemm_bf16", "triad_projhead_fwd", "triad_projhead_bwd",
            "triad_gemm_bf16_splitk", "triad_tile_gemm", "triad_dS_patch", "triad_clip_reduce", "triad_losshead",
            "triad_diag_smooth", "triad_diag_sparsity", "triad_dtemp_finalize", "triad_ln_bwd",
            "triad_colsum", "triad_sum_slabs", "triad_gather_rows", "triad_global_znorm",
@@ -105,7 +105,11 @@ def kernel_report(timers):
             elif meta is not None and "tag" in meta:
                 key += "[" + meta["tag"] + "]"   # projection heads: per (width x rows)
             elif meta is not None:
-                key += "[" + ("AV" if meta.get("kind") == 0 else "TV") + ("/" + meta["what"] if "what" in meta else "") + "]"
+                kind = meta.get("kind")
+                if kind in (0, 1):
+                    key += "[" + ("AV" if kind == 0 else "TV") + ("/" + meta["what"] if "what" in meta else "") + "]"
+                else:  # one launch over several heads (triad_pairsim_fwd_multi): "AV+TV"
+                    key += "[" + meta.get("what", "?") + "]"
             ms = e0.elapsed_time(e1)
             r = rep.setdefault(key, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "grid": None})
             r["launches"] += 1
@@ -203,9 +207,13 @@ def main():
 
     if rank == 0:
         value = world * a.batch * a.steps / dt
-        # dominant hot-path kernel: the fused AV pair-similarity forward (S = temp*A V^T, max/argmax,
-        # l_nonneg; never materialised). Algorithmic FLOPs = 2*B^2*Na*Nv_eff*512 per launch.
-        fwd = rep.get("triad_pairsim_fwd[AV]", {"launches": 0, "ms": 1.0, "flops": 0.0, "bytes": 0.0, "grid": None})
+        # dominant hot-path kernel: the similarity forward of both heads in one launch (S = temp*Q K^T,
+        # max/argmax, l_nonneg; S never leaves registers). Algorithmic FLOPs = 2*B^2*Nq*Nk_eff*512 per
+        # head (AV: Nq = Na, TV: Nq = Nt). With TRIAD_PAIR_FWD=0 (two launches): the AV launch.
+        roof_key, roof_sym = "triad_pairsim_fwd_multi[AV+TV]", "pairsim_fwd_multi_kernel<true>"
+        if roof_key not in rep:
+            roof_key, roof_sym = "triad_pairsim_fwd[AV]", "pairsim_fwd2_kernel<true, false>"
+        fwd = rep.get(roof_key, {"launches": 0, "ms": 1.0, "flops": 0.0, "bytes": 0.0, "grid": None})
         avg_ms = fwd["ms"] / max(1, fwd["launches"])
         achieved = (fwd["flops"] / max(1, fwd["launches"])) / (avg_ms * 1e-3) / 1e12
         # every hand-written kernel of the hot path (heads fwd+bwd, projection heads, trainer
@@ -234,9 +242,9 @@ def main():
                                       ", one frame batch per triple (dropout masks drawn per head)"),
                        "global_batch": a.batch * world, "per_gpu_batch": a.batch, "parallelism": f"dp{world}"},
             "loss": loss,
-            "roofline": {"kernel": "triad_pairsim_fwd[AV]", "bound": "mfma", "achieved": achieved,
+            "roofline": {"kernel": roof_key, "symbol": roof_sym, "bound": "mfma", "achieved": achieved,
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
-                         "traffic": pmc_traffic("pairsim_fwd2_kernel<true, false>", fwd["grid"]), "avg_ms": avg_ms,
+                         "traffic": pmc_traffic(roof_sym, fwd["grid"]), "avg_ms": avg_ms,
                          "algorithmic_bytes": fwd["bytes"] / max(1, fwd["launches"]),
                          "ds_stream_bytes": fwd.get("ds_bytes", 0.0) / max(1, fwd["launches"]),
                          "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "

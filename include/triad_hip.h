@@ -54,6 +54,31 @@ int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, in
                       float* rowmax, int* argmax, double* nn_part, float* diagS, void* dS, long long CT,
                       double* st_part, const int* k_len, hipStream_t stream);
 
+/* One head's forward for triad_pairsim_fwd_multi: the arguments of triad_pairsim_fwd (D = 512,
+ * no k_len) as a plain C struct. */
+typedef struct triad_pairsim_problem {
+  const void* Q;
+  const void* K;
+  int R, R_pad, Nq, Bq, Bk, Nk_pad, Nk_eff;
+  const float* temp;
+  float clamp_lo;
+  int diag, diag_off;
+  float* rowmax;
+  int* argmax;
+  double* nn_part;
+  float* diagS;
+  void* dS;
+  long long CT;
+  double* st_part;
+} triad_pairsim_problem;
+
+/* The forwards of n (1 or 2) heads as ONE kernel launch over their union of workgroups, each
+ * problem with exactly triad_pairsim_fwd's outputs (partial arrays of triad_pairsim_nparts
+ * entries each); either every problem writes dS (training) or none does. The tri-modal step's
+ * AV and TV heads (model.py:470-472 and 593, one launch for both pair losses: the reference has
+ * no audio-text loss, model.py:635-636 is inference only). */
+int triad_pairsim_fwd_multi(const triad_pairsim_problem* problems, int n, hipStream_t stream);
+
 /* clip[i][j] = sum_q m_iq rowmax[j][i*Nq+q] / norm_i (AV: qmask NULL, norm = Nq;
  * TV: norm = max(sum_q m_iq, 1e-7)); qw[r] = d clip / d rowmax (may be NULL).
  * Replaces model.py:389-391 (mean over Na) / 509-512 (masked mean over Nt). */
@@ -135,7 +160,7 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
 
 /* Select the form the two GEMM entry points above use from now on (process-wide tuning / test
  * knob): 0 = size policy (default), 1 = 128 x 128 tiles, 2 = 256 x 128 LDS ring, 3 = 256 x 256
- * four-wave tiles (M, N multiples of 256). */
+ * four-wave tiles, 4 = 256 x 256 eight-wave tiles (3 / 4: M, N multiples of 256). */
 int triad_gemm_set_form(int form);
 
 /* Fused projection head forward (model.py:32-34,68 / 81-83,116 / 253-255,326 under bf16

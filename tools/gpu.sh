@@ -5,9 +5,11 @@
 # steps (run in order; the first failing / timed-out step ends the call, nothing later touches the GPU):
 #   tests            full `pytest -m gpu` suite                      -> gpurun_out/<tag>_tests.log
 #   tests:<expr>     `pytest -m gpu -k <expr>`                        -> gpurun_out/<tag>_tests.log
+#   testsnx[:<expr>] the same without -x; test failures do not end the call
 #   smoke            __graft_entry__.smoke()                          -> gpurun_out/<tag>_smoke.log
 #   bench            default bench.py line (with the CPU baseline)    -> gpurun_out/<tag>_bench.json
 #   benchq           bench.py --no-cpu-baseline                       -> gpurun_out/<tag>_benchq.json
+#   benchenv:A=1,B=2 benchq with extra env for this step             -> gpurun_out/<tag>_benchenv<N>.json
 #   prof             rocprofv3 --kernel-trace --stats of a 3-step bench -> gpurun_out/<tag>_prof/
 #   pmc:<name>:<counters>  one rocprofv3 --pmc pass (counters comma-separated) of a 3-step bench
 #   py:<script args>       python <script> (tools/ micro-benchmarks)    -> gpurun_out/<tag>_py<N>.log
@@ -36,6 +38,14 @@ for step in "$@"; do
     tests:*)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread \
         -k "${step#tests:}" > "gpurun_out/${tag}_tests.log" 2>&1 ;;
+    testsnx|testsnx:*)
+      # every test runs (no -x); ordinary test failures (pytest rc 1) do not end the call
+      expr=${step#testsnx}; expr=${expr#:}
+      timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread \
+        ${expr:+-k "$expr"} > "gpurun_out/${tag}_tests.log" 2>&1
+      rc=$?; [ $rc -eq 1 ] && { echo "[gpu.sh] test failures (see log); continuing"; rc=0; }
+      [ $rc -ne 0 ] && { echo "[gpu.sh] step $n ($step) failed rc=$rc"; exit $rc; }
+      continue ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "gpurun_out/${tag}_smoke.log" 2>&1 ;;
     bench)
@@ -43,6 +53,11 @@ for step in "$@"; do
     benchq)
       timeout -k 10 600 python bench.py --no-cpu-baseline > "gpurun_out/${tag}_benchq.json" \
         2> "gpurun_out/${tag}_benchq.err" ;;
+    benchenv:*)
+      # benchq with extra environment for this step only: benchenv:A=1,B=2
+      ev=${step#benchenv:}
+      ( export ${ev//,/ }; timeout -k 10 600 python bench.py --no-cpu-baseline ) > "gpurun_out/${tag}_benchenv${n}.json" \
+        2> "gpurun_out/${tag}_benchenv${n}.err" ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${tag}_prof" -o bench \
         -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline > "gpurun_out/${tag}_prof.log" 2>&1 ;;

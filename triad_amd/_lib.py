@@ -23,6 +23,7 @@ SIGNATURES = {
     "triad_pairsim_nparts": [i32, i32],
     "triad_pairsim_fwd": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, f32, i32, i32, vp, vp, vp, vp, vp,
                           i64, vp, vp, vp],
+    "triad_pairsim_fwd_multi": [vp, i32, vp],
     "triad_clip_reduce": [vp, i32, i32, i32, i32, vp, vp, vp, vp],
     "triad_diag_smooth": [vp, i32, i32, i32, i32, f64, vp, vp, vp, vp],
     "triad_diag_sparsity": [vp, i32, i32, i32, i32, f32, f64, vp, vp, vp, vp],
@@ -97,6 +98,16 @@ RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_l
             "triad_lora_tn_blocks": C.c_int, "triad_dropaddln_bwd_blocks": C.c_int,
             "triad_colsum_splits": C.c_int, "triad_dense_nparts": C.c_int,
             "triad_projhead_bwd_slabs": C.c_int}
+
+
+
+class PairsimProblem(C.Structure):
+    """struct triad_pairsim_problem (include/triad_hip.h)."""
+    _fields_ = [("Q", vp), ("K", vp), ("R", i32), ("R_pad", i32), ("Nq", i32), ("Bq", i32), ("Bk", i32),
+                ("Nk_pad", i32), ("Nk_eff", i32), ("temp", vp), ("clamp_lo", f32), ("diag", i32), ("diag_off", i32),
+                ("rowmax", vp), ("argmax", vp), ("nn_part", vp), ("diagS", vp), ("dS", vp), ("CT", i64),
+                ("st_part", vp)]
+
 
 _lock = threading.Lock()
 _lib = None

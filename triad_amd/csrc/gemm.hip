@@ -413,8 +413,105 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
     }
 }
 
+// ---- 256 x 256 eight-wave form -----------------------------------------------------------------
+// The four-wave form's tile, LDS images and staging with 8 waves (two per SIMD: one wave's DMA
+// issue and barrier waits overlap the other's MFMAs): wave (wm, wn) of 2 x 4 owns 128 x 64 (4 x 2
+// tiles of 32 x 32, 128 accumulators per lane), reads 6 fragments per 8 MFMAs per 16-deep step, and
+// issues 8 of the next stage's 64 DMA pieces (one after every 2nd of its first 16 MFMAs).
+constexpr int GE_PIECES = 8;
+
+template <bool A_KCONTIG, bool B_KCONTIG>
+__device__ __forceinline__ void ge_piece(const bf16* __restrict__ A, long long lda, const bf16* __restrict__ B,
+                                         long long ldb, int m0, int n0, int k0, bf16* dst, int wave, int lane,
+                                         int u) {
+  if (u < 4) gw_piece_one<A_KCONTIG>(A, lda, m0, k0, dst, wave * 4 + u, lane);
+  else gw_piece_one<B_KCONTIG>(B, ldb, n0, k0, dst + GW_A, wave * 4 + (u - 4), lane);
+}
+
+template <bool A_KCONTIG, bool B_KCONTIG, typename OutT>
+__global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict__ A, long long lda,
+                                                         const bf16* __restrict__ B, long long ldb, int M, int N,
+                                                         int Kd, const float* __restrict__ alpha_p,
+                                                         OutT* __restrict__ C, long long ldc, int k_per_split,
+                                                         long long slab_stride, const float* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * GW_ST];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int h = lane >> 5;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  const int ntn = N / GW_N;
+  const int m0 = (swz / ntn) * GW_M, n0 = (swz % ntn) * GW_N;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){};
+
+  const int kbeg = blockIdx.y * k_per_split;
+  const int nk = __builtin_amdgcn_readfirstlane(max(0, min(k_per_split, Kd - kbeg)) / BK);
+  C += (size_t)blockIdx.y * slab_stride;
+  if (nk > 0)
+#pragma unroll
+    for (int u = 0; u < GE_PIECES; ++u)
+      ge_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kbeg, lds, wave, lane, u);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool pf = kt + 1 < nk;
+    bf16* const nb = lds + ((kt + 1) & 1) * GW_ST;
+    const int kn = kbeg + (kt + 1) * BK;
+    const bf16* ai = lds + (kt & 1) * GW_ST;
+    const bf16* bi = ai + GW_A;
+    bf16x8 af[2][4], bfr[2][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) af[0][t] = gw_frag<A_KCONTIG>(ai, wm * 128 + t * 32, 0, lane);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) bfr[0][t] = gw_frag<B_KCONTIG>(bi, wn * 64 + t * 32, 0, lane);
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const int cur = s & 1;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          acc[a][b] = mfma32(af[cur][a], bfr[cur][b], acc[a][b]);
+          const int j = a * 2 + b, mi = s * 8 + j;
+          if (s + 1 < BK / 16 && j < 6) {  // step s + 1's 6 fragments between step s's MFMAs
+            __builtin_amdgcn_sched_barrier(0);
+            if (j < 4) af[cur ^ 1][j] = gw_frag<A_KCONTIG>(ai, wm * 128 + j * 32, s + 1, lane);
+            else bfr[cur ^ 1][j - 4] = gw_frag<B_KCONTIG>(bi, wn * 64 + (j - 4) * 32, s + 1, lane);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (mi % 2 == 1 && mi / 2 < GE_PIECES) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (pf) ge_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, mi / 2);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+    }
+  }
+
+  const float alpha = alpha_p ? *alpha_p : 1.f;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int n = n0 + wn * 64 + b * 32 + (lane & 31);
+      const float bn = bias ? bias[n] : 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int m = m0 + wm * 128 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v] + bn);
+      }
+    }
+}
+
 // Form override for measurement and tests (triad_gemm_set_form): 0 = the size policy in
-// launch(), 1 = 128 x 128, 2 = 256 x 128 ring, 3 = 256 x 256 four-wave (when the shape allows).
+// launch(), 1 = 128 x 128, 2 = 256 x 128 ring, 3 = 256 x 256 four-wave, 4 = 256 x 256 eight-wave
+// (when the shape allows).
 int g_gemm_form = 0;
 
 
@@ -432,6 +529,13 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
   // 2.94 -> 2.67 ms at M = 1.6 M, N = 512, K = 1536); the split-K weight gradients and the
   // shorter forward shapes keep the smaller tiles
   const bool w4_auto = AK && BK_ && splits == 1 && M >= 65536 && Kd >= 1024;
+  if (w4_ok && form == 4) {
+    const int nwg = (M / GW_M) * (N / GW_N);
+    hipLaunchKernelGGL((gemm_w8_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
+                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias);
+    TRIAD_CHECK_LAUNCH();
+    return TRIAD_OK;
+  }
   if (w4_ok && (form == 3 || (form == 0 && w4_auto))) {
     const int nwg = (M / GW_M) * (N / GW_N);
     hipLaunchKernelGGL((gemm_w4_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(256), 0, st, (const bf16*)A, lda,
@@ -519,9 +623,9 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
 }
 
 // Select the GEMM form for later calls (0 = size policy, 1 = 128 x 128, 2 = 256 x 128 ring,
-// 3 = 256 x 256 four-wave). Process-wide tuning / test knob.
+// 3 = 256 x 256 four-wave, 4 = 256 x 256 eight-wave). Process-wide tuning / test knob.
 int triad_gemm_set_form(int form) {
-  if (form < 0 || form > 3) return TRIAD_EINVAL;
+  if (form < 0 || form > 4) return TRIAD_EINVAL;
   g_gemm_form = form;
   return TRIAD_OK;
 }

@@ -27,6 +27,8 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
                               int Nk_eff, const float* temp, float clamp_lo, int diag, int diag_off, float* rowmax,
                               int* argmax, double* nn_part, float* diagS, void* dS, long long CT, double* st_part,
                               const int* k_len, int xb, int ys, int jpw, hipStream_t stream);
+int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* xb, const int* ys, const int* jpw,
+                                   int n, hipStream_t stream);
 
 namespace {
 
@@ -537,6 +539,19 @@ int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, in
   return triad_pairsim_fwd2_launch(Q, K, R, R_pad, Nq, Bq, Bk, Nk_pad, Nk_eff, temp, clamp_lo, diag, diag_off,
                                    rowmax, argmax, nn_part, diagS, dS, CT, st_part, k_len, xb, ys, a.j_per_wg,
                                    stream);
+}
+
+int triad_pairsim_fwd_multi(const triad_pairsim_problem* problems, int n, hipStream_t stream) {
+  if (!problems || n < 1 || n > 2) return TRIAD_EINVAL;
+  int xb[2], ys[2], jpw[2];
+  for (int i = 0; i < n; ++i) {
+    const triad_pairsim_problem& p = problems[i];
+    if (int e = check_shape(p.R, p.R_pad, p.Nq, p.Bk, p.Nk_pad, p.Nk_eff, D)) return e;
+    if (p.dS && (p.CT < (long long)p.Bk * (p.Nk_pad / 32) || !p.st_part)) return TRIAD_EINVAL;
+    if (!p.Q || !p.K || !p.temp || !p.rowmax || !p.argmax || !p.nn_part) return TRIAD_EINVAL;
+    xb[i] = grid_for(p.R_pad, p.Bk, &jpw[i], &ys[i]);  // same decomposition as triad_pairsim_nparts
+  }
+  return triad_pairsim_fwd_multi_launch(problems, xb, ys, jpw, n, stream);
 }
 
 int triad_clip_reduce(const float* rowmax, int R_pad, int Nq, int Bq, int Bk, const float* qmask,

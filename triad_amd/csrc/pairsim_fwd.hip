@@ -216,26 +216,29 @@ struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in 
 // SHORTQ tags the launches over short query lists (text captions, Nq <= 32) with their own
 // symbol, so profiler summaries report the AV (long-query) launches' durations on their own; the
 // code is identical.
-template <bool TRAIN, bool SHORTQ>
-__global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 kbuf[NBUF * KT_ELEMS + 16 * WAVES];
+constexpr int KBUF_ELEMS = NBUF * KT_ELEMS + 16 * WAVES;
+
+// One workgroup of the forward: 256-row block bx, key-sample split by (of gx row blocks) of
+// problem a. kbuf = the workgroup's LDS (key ring + reduction scratch).
+template <bool TRAIN>
+__device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int bx, const int by, const int gx) {
   double* red = (double*)(kbuf + NBUF * KT_ELEMS);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
-  const int row = blockIdx.x * ROWS_PER_WG + wave * 32 + ql;
+  const int row = bx * ROWS_PER_WG + wave * 32 + ql;
   const bool rok = row < a.R;
-  const int rt = (blockIdx.x * ROWS_PER_WG + wave * 32) / 32;
+  const int rt = (bx * ROWS_PER_WG + wave * 32) / 32;
 
-  const int j0 = blockIdx.y * a.j_per_wg;
+  const int j0 = by * a.j_per_wg;
   const int j1 = min(a.Bk, j0 + a.j_per_wg);
   const int nkb = a.Nk_pad / 32;
   const int nblocks = (j1 - j0) * nkb;
   if (nblocks <= 0) {
     if (threadIdx.x == 0) {
-      a.part[blockIdx.y * gridDim.x + blockIdx.x] = 0.0;
-      if (a.part2) a.part2[blockIdx.y * gridDim.x + blockIdx.x] = 0.0;
+      a.part[by * gx + bx] = 0.0;
+      if (a.part2) a.part2[by * gx + bx] = 0.0;
     }
     return;
   }
@@ -403,9 +406,38 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) 
     double t = 0.0, t2 = 0.0;
     for (int w = 0; w < WAVES; ++w) { t += red[w]; t2 += red[WAVES + w]; }
     // sum clamp(S, lo, 0)^2 = su^2 sum c^2; sum S^2/temp over [lo, 0] = temp sum u^2 there
-    a.part[blockIdx.y * gridDim.x + blockIdx.x] = t * (double)su * (double)su;
-    if (a.part2) a.part2[blockIdx.y * gridDim.x + blockIdx.x] = t2 * (double)temp;
+    a.part[by * gx + bx] = t * (double)su * (double)su;
+    if (a.part2) a.part2[by * gx + bx] = t2 * (double)temp;
   }
+}
+
+template <bool TRAIN, bool SHORTQ>
+__global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 kbuf[KBUF_ELEMS];
+  fwd_body<TRAIN>(a, kbuf, blockIdx.x, blockIdx.y, gridDim.x);
+}
+
+// Several heads' forwards in ONE launch (the tri-modal step's AV and TV heads, model.py:470-472 /
+// 593, over their own key sets): a 1-D grid, problem p owning workgroups [first[p], first[p+1]),
+// each problem keeping its own (row block, key split) decomposition and partial arrays. The host
+// orders the problems by workgroup length, longest first, so the dispatcher back-fills the CUs
+// with the shorter workgroups and the launch ends in one tail instead of one per head.
+constexpr int MAX_PROBLEMS = 2;
+struct MultiArgs {
+  FwdArgs p[MAX_PROBLEMS];
+  int first[MAX_PROBLEMS + 1];
+  int gx[MAX_PROBLEMS];
+  int n;
+};
+
+template <bool TRAIN>
+__global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd_multi_kernel(MultiArgs m) {
+  __shared__ __attribute__((aligned(16))) bf16 kbuf[KBUF_ELEMS];
+  const int b = blockIdx.x;
+  const int q = (m.n > 1 && b >= m.first[1]) ? 1 : 0;  // uniform
+  const int local = b - m.first[q];
+  const int gx = m.gx[q];
+  fwd_body<TRAIN>(m.p[q], kbuf, local % gx, local / gx, gx);
 }
 
 // Diagonal blocks of S for the regularisers (model.py:417-418 / 524-525):
@@ -469,6 +501,45 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
     hipLaunchKernelGGL(diag_sim_kernel, dim3((Nq + 31) / 32, Bq), dim3(256), 0, stream, (const bf16*)Q,
                        (const bf16*)K, Nq, Nk_pad, Nk_eff, diag_off, temp, diagS);
     TRIAD_CHECK_LAUNCH();
+  }
+  return TRIAD_OK;
+}
+
+// triad_pairsim_fwd_multi's launch: per problem (validated and with its grid decomposition by the
+// caller) xb row blocks x ys key splits of jpw samples; problems with longer workgroups first.
+int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* xb, const int* ys, const int* jpw,
+                                   int n, hipStream_t stream) {
+  if (n < 1 || n > MAX_PROBLEMS) return TRIAD_EINVAL;
+  const bool train = pr[0].dS != nullptr;
+  int order[MAX_PROBLEMS] = {0, 1};
+  if (n == 2 && (long long)jpw[1] * pr[1].Nk_pad > (long long)jpw[0] * pr[0].Nk_pad) { order[0] = 1; order[1] = 0; }
+  MultiArgs m = {};
+  m.n = n;
+  m.first[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    const triad_pairsim_problem& p = pr[order[i]];
+    if ((p.dS != nullptr) != train) return TRIAD_EINVAL;
+    if ((unsigned long long)jpw[order[i]] * p.Nk_pad * D * 2 >= (1ull << 31)) return TRIAD_EINVAL;
+    FwdArgs& a = m.p[i];
+    a.Q = (const bf16*)p.Q; a.K = (const bf16*)p.K;
+    a.R = p.R; a.R_pad = p.R_pad; a.Nq = p.Nq; a.Bq = p.Bq; a.Bk = p.Bk; a.Nk_pad = p.Nk_pad;
+    a.Nk_eff = p.Nk_eff; a.j_per_wg = jpw[order[i]]; a.temp = p.temp; a.clamp_lo = p.clamp_lo;
+    a.rowmax = p.rowmax; a.argmax = p.argmax; a.part = p.nn_part;
+    a.dS = (bf16*)p.dS; a.CT = p.CT; a.part2 = p.st_part; a.klen = nullptr;
+    m.gx[i] = xb[order[i]] * (256 / ROWS_PER_WG);
+    m.first[i + 1] = m.first[i] + m.gx[i] * ys[order[i]];
+  }
+  const dim3 grid(m.first[n]), block(64 * WAVES);
+  if (train) hipLaunchKernelGGL((pairsim_fwd_multi_kernel<true>), grid, block, 0, stream, m);
+  else hipLaunchKernelGGL((pairsim_fwd_multi_kernel<false>), grid, block, 0, stream, m);
+  TRIAD_CHECK_LAUNCH();
+  for (int i = 0; i < n; ++i) {
+    const triad_pairsim_problem& p = pr[i];
+    if (p.diagS && p.diag) {
+      hipLaunchKernelGGL(diag_sim_kernel, dim3((p.Nq + 31) / 32, p.Bq), dim3(256), 0, stream, (const bf16*)p.Q,
+                         (const bf16*)p.K, p.Nq, p.Nk_pad, p.Nk_eff, p.diag_off, p.temp, p.diagS);
+      TRIAD_CHECK_LAUNCH();
+    }
   }
   return TRIAD_OK;
 }

@@ -448,7 +448,19 @@ class MultiModalModel(nn.Module):
                 for t in (audio_feats, text_feats, attention_mask):
                     if isinstance(t, torch.Tensor) and t.is_cuda:
                         t.record_stream(main)
-        return self._av_head(audio_feats, v_av)[0], self._tv_head(text_feats, v_tv, attention_mask)[0]
+        return self._triad_heads(audio_feats, v_av, text_feats, v_tv, attention_mask)
+
+    def _triad_heads(self, audio_feats, v_av, text_feats, v_tv, attention_mask):
+        """Both heads with ONE similarity-forward launch (ops.contrastive_heads_av_tv); the same
+        tuples as forward_audio_visual / forward_text_visual. TRIAD_PAIR_FWD=0: two launches."""
+        import os
+        if os.environ.get("TRIAD_PAIR_FWD", "1") == "0":
+            return self._av_head(audio_feats, v_av)[0], self._tv_head(text_feats, v_tv, attention_mask)[0]
+        (la, sa, _), (lt, st, _) = ops.contrastive_heads_av_tv(
+            audio_feats, v_av, text_feats, v_tv, self.temperature, attention_mask,
+            threshold=self.patch_sparsity_threshold, sparsity_weight=self.patch_sparsity_weight,
+            group=self.negatives_group, ds_budget=getattr(self, "ds_budget", None))
+        return (la[0], la[1], la[2], la[3], LazyStats(_AV_KEYS, sa)), (lt[0], LazyStats(_TV_KEYS, st))
 
     def forward(self, frames=None, audio=None, text_list=None):
         """Embeddings + L2-normalised similarity maps (model.py:610-637). `frames` is an

@@ -206,6 +206,216 @@ def recompute_backward(g: Geometry, Qb, Kb, temp, kind, diag_off, argmax, dclip,
     return dQ, dK, torch.cat(parts) if len(parts) > 1 else parts[0]
 
 
+class _Head:
+    """Per-head state of one forward (geometry, packed operands, outputs of the similarity
+    forward) shared by the single-head and the fused AV+TV autograd functions."""
+    pass
+
+
+def _head_begin(q, k, temperature, kind, q_mask, group, ds_budget, need_grad):
+    """Checks, operand packing (keys all-gathered in global mode) and the buffers of the
+    similarity forward of one head."""
+    _check_device(q, k, temperature, q_mask)
+    Bq, Nq, dq = q.shape
+    Bl, Nk, dk = k.shape
+    if dq != D or dk != D:
+        raise TriadError(f"feature dim must be {D}")
+    if Bq != Bl:
+        raise TriadError("query and key batches must match")
+    W, rank = (1, 0)
+    if group is not None:
+        from . import dist as tdist
+        W, rank = tdist.world_rank(group)
+    Bg = Bq * W
+    if Bg < 2:
+        # the reference takes max() of the empty off-diagonal set and raises (model.py:447/565)
+        raise TriadError("batch size must be >= 2 (no negatives for B == 1)")
+    h = _Head()
+    h.kind, h.group, h.W, h.rank, h.Nk, h.Bg = kind, group, W, rank, Nk, Bg
+    h.g = g = Geometry(Bq, Nq, Bg, Nk)
+    dev = q.device
+    h.Qb = pack_queries(q, g)
+    if W == 1:
+        h.Kb = pack_keys(k, g)
+    else:
+        gl = Geometry(Bq, Nq, Bq, Nk)
+        h.Kb = tdist.gather_keys(pack_keys(k, gl)[:gl.C_pad], g.C_alloc, group)
+    h.temp = temperature.detach().reshape(1).to(torch.float32).contiguous()
+    h.nparts = call("triad_pairsim_nparts", g.R_pad, g.Bk)
+    h.rowmax = torch.empty(g.Bk, g.R_pad, dtype=torch.float32, device=dev)
+    h.argmax = torch.empty(g.Bk, g.R_pad, dtype=torch.int32, device=dev)
+    h.nn_part = torch.empty(h.nparts, dtype=torch.float64, device=dev)
+    h.diagS = torch.empty(g.Bq, g.Nq, g.Nk_pad, dtype=torch.float32, device=dev)
+    h.CT = _rup(g.C_pad // 32, 4)
+    budget = _default_budget(dev) if ds_budget is None else int(ds_budget)
+    h.chunk = ds_chunk_samples(g, budget)
+    # materialise the unit dS in the forward only when it fits the budget; otherwise the
+    # backward recomputes it chunk by chunk (recompute_backward)
+    write_ds = need_grad and h.chunk == g.Bk
+    h.dS = torch.empty((g.R_pad // 32) * h.CT * 1024, dtype=torch.bfloat16, device=dev) if write_ds else None
+    h.st_part = torch.empty(h.nparts, dtype=torch.float64, device=dev) if write_ds else None
+    h.q_dtype, h.k_dtype, h.t_dtype = q.dtype, k.dtype, temperature.dtype
+    return h
+
+
+def _fwd_meta(h):
+    g = h.g
+    return dict(kind=h.kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, grid=h.nparts * 512,
+                # algorithmic bytes (SURVEY 8d): the feature operands + rowmax / argmax; the
+                # tiled unit-dS stream the training forward also writes is NOT algorithmic
+                # (bench.py reports it, from PMC, as traffic)
+                bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R,
+                ds_bytes=(2.0 * g.R_pad * g.C_pad if h.dS is not None else 0.0))
+
+
+def _head_launch(h, st):
+    g = h.g
+    call("triad_pairsim_fwd", ptr(h.Qb), ptr(h.Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
+         ptr(h.temp), CLAMP_LO[h.kind], 1, h.rank * g.Bq, ptr(h.rowmax), ptr(h.argmax), ptr(h.nn_part),
+         ptr(h.diagS), ptr(h.dS), h.CT, ptr(h.st_part), None, st, meta=_fwd_meta(h))
+
+
+def _problem(h):
+    g = h.g
+    return _lib.PairsimProblem(ptr(h.Qb), ptr(h.Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, ptr(h.temp),
+                               CLAMP_LO[h.kind], 1, h.rank * g.Bq, ptr(h.rowmax), ptr(h.argmax), ptr(h.nn_part),
+                               ptr(h.diagS), ptr(h.dS), h.CT, ptr(h.st_part))
+
+
+def _heads_launch(hs, st):
+    """Every head's similarity forward in ONE launch (triad_pairsim_fwd_multi)."""
+    arr = (_lib.PairsimProblem * len(hs))(*[_problem(h) for h in hs])
+    ms = [_fwd_meta(h) for h in hs]
+    meta = dict(kind=-1, what="+".join("AV" if h.kind == AV else "TV" for h in hs),
+                flops=sum(m["flops"] for m in ms), bytes=sum(m["bytes"] for m in ms),
+                ds_bytes=sum(m["ds_bytes"] for m in ms), grid=sum(h.nparts for h in hs) * 512)
+    call("triad_pairsim_fwd_multi", arr, len(hs), st, meta=meta)
+
+
+def _head_end(h, q_mask, thr, w_sparse, st):
+    """Clip reduction, diagonal regularisers and the loss head after the similarity forward.
+    Returns (losses[4], stats, clip_full); keeps what the backward needs on h."""
+    g, kind, W, rank, Bg = h.g, h.kind, h.W, h.rank, h.Bg
+    dev = h.Qb.device
+    clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
+    h.qw = torch.empty(g.R, dtype=torch.float32, device=dev)
+    qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
+    call("triad_clip_reduce", ptr(h.rowmax), g.R_pad, g.Nq, g.Bq, g.Bk, ptr(qm), ptr(clip), ptr(h.qw), st)
+    dg_part = torch.empty(g.Bq, dtype=torch.float64, device=dev)
+    h.dgt_part = torch.empty(g.Bq, dtype=torch.float64, device=dev)
+    h.gdiag = torch.empty_like(h.diagS)
+    if kind == AV:
+        cnt = float(Bg * (g.Nq - 1) * g.Nk_eff)
+        call("triad_diag_smooth", ptr(h.diagS), g.Bq, g.Nq, g.Nk_pad, g.Nk_eff, cnt, ptr(dg_part), ptr(h.gdiag),
+             ptr(h.dgt_part), st)
+    else:
+        cnt = float(Bg * g.Nk_eff)
+        call("triad_diag_sparsity", ptr(h.diagS), g.Bq, g.Nq, g.Nk_pad, g.Nk_eff, float(thr), cnt,
+             ptr(dg_part), ptr(h.gdiag), ptr(h.dgt_part), st)
+    h.n_el = float(Bg) * Bg * g.Nq * g.Nk_eff
+    h.w_sparse = float(w_sparse)
+    if W == 1:
+        clip_full, nn_in, n_nn, dg_in, n_dg = clip, h.nn_part, h.nparts, dg_part, g.Bq
+    else:
+        from . import dist as tdist
+        clip_full = tdist.gather_rows(clip, h.group)
+        sums = tdist.allreduce_sum(torch.stack([h.nn_part.sum(), dg_part.sum()]), h.group)
+        nn_in, n_nn, dg_in, n_dg = sums[0:1], 1, sums[1:2], 1
+    out = torch.empty(13, dtype=torch.float32, device=dev)
+    dclip = torch.empty(Bg, Bg, dtype=torch.float32, device=dev)
+    lse = torch.empty(2 * Bg, dtype=torch.float32, device=dev)
+    call("triad_losshead", ptr(clip_full), Bg, kind, ptr(h.temp), ptr(nn_in), n_nn, h.n_el, ptr(dg_in), n_dg,
+         cnt, float(w_sparse), ptr(out), ptr(dclip), ptr(lse), st)
+    h.dclip = dclip[rank * g.Bq:(rank + 1) * g.Bq].contiguous() if W > 1 else dclip
+    return out[:4].clone(), out[4:].clone(), clip_full
+
+
+_SAVED = ("Qb", "Kb", "argmax", "rowmax", "dclip", "qw", "gdiag", "temp", "dS", "st_part", "dgt_part")
+
+
+def _head_saved(h):
+    return [getattr(h, n) for n in _SAVED]
+
+
+def _head_light(h):
+    """h without its tensors (those travel through ctx.save_for_backward)."""
+    c = _Head()
+    for n in ("g", "kind", "W", "rank", "Nk", "n_el", "w_sparse", "nparts", "CT", "chunk", "group", "q_dtype",
+              "k_dtype", "t_dtype"):
+        setattr(c, n, getattr(h, n))
+    return c
+
+
+def _head_backward(h, saved, needs, g_total, g_ce, g_reg, g_aux):
+    """(gq, gk, gt) of one head; needs = (q, k, temperature) input-gradient flags."""
+    if g_total is None and g_ce is None and g_reg is None and g_aux is None:
+        return None, None, None
+    Qb, Kb, argmax, rowmax, dclip, qw, gdiag, temp, dS, st_part, dgt_part = saved
+    g, kind, W, rank, CT = h.g, h.kind, h.W, h.rank, h.CT
+    dev = Qb.device
+    st = stream_ptr(dev)
+    f32 = torch.float32
+    zero = torch.zeros((), dtype=f32, device=dev)
+    gt_, gc_, gr_, ga_ = [zero if x is None else x.to(f32) for x in (g_total, g_ce, g_reg, g_aux)]
+    c_ce = gt_ + gc_
+    c_reg = gt_ + gr_
+    c_nn = c_reg * (0.15 * 2.0 / h.n_el)
+    if kind == AV:
+        c_diag = 0.01 * (c_reg + ga_)   # reg = ... + 0.01*l_smooth; aux = 0.01*l_smooth
+        c_cal = 20.0 * c_reg
+    else:
+        c_diag = h.w_sparse * c_reg + ga_  # reg = ... + w*sparsity; aux = sparsity
+        c_cal = torch.zeros_like(c_reg)
+    has_cal = 1 if (kind == AV and rank == 0) else 0   # the l_cal term is counted once
+    fast = g_total is not None and g_ce is None and g_reg is None and g_aux is None and dS is not None
+    gq = gk = gt = None
+    if fast:
+        # dS = c_nn * (unit l_nonneg grad [written by the forward] + ratio_max * max term
+        #               + ratio_diag * diagonal term); the ratios are host constants here
+        ratio_max = h.n_el / 0.3
+        ratio_diag = (0.01 if kind == AV else h.w_sparse) * h.n_el / 0.3
+        nmp = 1024
+        max_part = torch.empty(nmp, dtype=torch.float64, device=dev)
+        call("triad_dS_patch", ptr(dS), CT, g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, rank * g.Bq,
+             ptr(argmax), ptr(rowmax), ptr(dclip), ptr(qw), float(ratio_max), ptr(gdiag), float(ratio_diag),
+             ptr(max_part), nmp, st)
+        alpha = (temp * c_nn).reshape(1).contiguous()
+        w = torch.stack([c_nn, c_ce / temp[0], c_diag / temp[0], c_cal]).contiguous()
+        parts = (st_part, h.nparts, max_part, nmp, dgt_part, g.Bq)
+    else:
+        # recompute form: any mix of upstream gradients, or a dS over the memory budget
+        coef = torch.stack([c_ce, c_nn, c_diag, c_cal]).contiguous()
+        dQ, dK, dt_part = recompute_backward(g, Qb, Kb, temp, kind, rank * g.Bq, argmax, dclip, qw, gdiag, coef,
+                                             needs[0], needs[1], h.chunk, st, ds_buf=dS)
+        w = torch.stack([torch.ones_like(c_ce), zero, zero, c_cal]).contiguous()
+        parts = (dt_part, dt_part.numel(), None, 0, None, 0)
+        if dQ is not None:
+            gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(h.q_dtype)
+    if fast and needs[0]:
+        dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
+        tile_gemm(dS, CT, 0, Kb, g.R_pad, g.C_pad // 32, alpha, dQ, st,
+                  meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dQ"))
+        gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(h.q_dtype)
+    if needs[1]:
+        if fast:
+            Mk = CT * 32
+            dK = torch.empty(Mk, D, dtype=torch.bfloat16, device=dev)
+            tile_gemm(dS, CT, 1, Qb, Mk, g.R_pad // 32, alpha, dK, st,
+                      meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dK"))
+        Nk_pad = g.Nk_pad
+        if W > 1:
+            from . import dist as tdist
+            dK = tdist.reduce_scatter_rows(dK, g.Bq * Nk_pad, h.group)  # this rank's keys, all queries
+        gk = dK[:g.Bq * Nk_pad].view(g.Bq, Nk_pad, D)[:, :h.Nk].to(h.k_dtype)
+    if needs[2]:
+        dt = torch.empty(1, dtype=f32, device=dev)
+        p0, n0, p1, n1, p2, n2 = parts
+        call("triad_dtemp_finalize", ptr(p0), n0, ptr(p1), n1, ptr(p2), n2, ptr(temp), ptr(w), has_cal,
+             ptr(dt), st)
+        gt = dt.reshape(()).to(h.t_dtype)
+    return gq, gk, gt
+
+
 class _ContrastiveHead(torch.autograd.Function):
     """Outputs: total, contrastive, reg, aux (0.01*l_smooth for AV, sparsity for TV), stats[9], clip.
 
@@ -222,164 +432,65 @@ class _ContrastiveHead(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, q, k, temperature, kind, q_mask, thr, w_sparse, group, ds_budget):
-        _check_device(q, k, temperature, q_mask)
-        Bq, Nq, dq = q.shape
-        Bl, Nk, dk = k.shape
-        if dq != D or dk != D:
-            raise TriadError(f"feature dim must be {D}")
-        if Bq != Bl:
-            raise TriadError("query and key batches must match")
-        W, rank = (1, 0)
-        if group is not None:
-            from . import dist as tdist
-            W, rank = tdist.world_rank(group)
-        Bg = Bq * W
-        if Bg < 2:
-            # the reference takes max() of the empty off-diagonal set and raises (model.py:447/565)
-            raise TriadError("batch size must be >= 2 (no negatives for B == 1)")
-        g = Geometry(Bq, Nq, Bg, Nk)
-        dev = q.device
-        st = stream_ptr(dev)
-        Qb = pack_queries(q, g)
-        if W == 1:
-            Kb = pack_keys(k, g)
-        else:
-            gl = Geometry(Bq, Nq, Bq, Nk)
-            Kb = tdist.gather_keys(pack_keys(k, gl)[:gl.C_pad], g.C_alloc, group)
-        temp = temperature.detach().reshape(1).to(torch.float32).contiguous()
-        nparts = call("triad_pairsim_nparts", g.R_pad, g.Bk)
-        rowmax = torch.empty(g.Bk, g.R_pad, dtype=torch.float32, device=dev)
-        argmax = torch.empty(g.Bk, g.R_pad, dtype=torch.int32, device=dev)
-        nn_part = torch.empty(nparts, dtype=torch.float64, device=dev)
-        diagS = torch.empty(g.Bq, g.Nq, g.Nk_pad, dtype=torch.float32, device=dev)
         need_grad = any(ctx.needs_input_grad[:3])  # (forward itself runs under no_grad)
-        CT = _rup(g.C_pad // 32, 4)
-        budget = _default_budget(dev) if ds_budget is None else int(ds_budget)
-        chunk = ds_chunk_samples(g, budget)
-        # materialise the unit dS in the forward only when it fits the budget; otherwise the
-        # backward recomputes it chunk by chunk (recompute_backward)
-        write_ds = need_grad and chunk == g.Bk
-        dS = torch.empty((g.R_pad // 32) * CT * 1024, dtype=torch.bfloat16, device=dev) if write_ds else None
-        st_part = torch.empty(nparts, dtype=torch.float64, device=dev) if write_ds else None
-        call("triad_pairsim_fwd", ptr(Qb), ptr(Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, D,
-             ptr(temp), CLAMP_LO[kind], 1, rank * Bq, ptr(rowmax), ptr(argmax), ptr(nn_part), ptr(diagS),
-             ptr(dS), CT, ptr(st_part), None, st,
-             meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, grid=nparts * 512,
-                       # algorithmic bytes: the feature operands + rowmax / argmax; the
-                       # tiled unit-dS stream the training forward also writes is NOT algorithmic
-                       # (bench.py reports it, from PMC, as traffic)
-                       bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R,
-                       ds_bytes=(2.0 * g.R_pad * g.C_pad if write_ds else 0.0)))
-        clip = torch.empty(g.Bq, g.Bk, dtype=torch.float32, device=dev)
-        qw = torch.empty(g.R, dtype=torch.float32, device=dev)
-        qm = None if q_mask is None else q_mask.to(torch.float32).contiguous()
-        call("triad_clip_reduce", ptr(rowmax), g.R_pad, g.Nq, g.Bq, g.Bk, ptr(qm), ptr(clip), ptr(qw), st)
-        dg_part = torch.empty(g.Bq, dtype=torch.float64, device=dev)
-        dgt_part = torch.empty(g.Bq, dtype=torch.float64, device=dev)
-        gdiag = torch.empty_like(diagS)
-        if kind == AV:
-            cnt = float(Bg * (g.Nq - 1) * g.Nk_eff)
-            call("triad_diag_smooth", ptr(diagS), g.Bq, g.Nq, g.Nk_pad, g.Nk_eff, cnt, ptr(dg_part), ptr(gdiag),
-                 ptr(dgt_part), st)
-        else:
-            cnt = float(Bg * g.Nk_eff)
-            call("triad_diag_sparsity", ptr(diagS), g.Bq, g.Nq, g.Nk_pad, g.Nk_eff, float(thr), cnt,
-                 ptr(dg_part), ptr(gdiag), ptr(dgt_part), st)
-        n_el = float(Bg) * Bg * g.Nq * g.Nk_eff
-        if W == 1:
-            clip_full, nn_in, n_nn, dg_in, n_dg = clip, nn_part, nparts, dg_part, g.Bq
-        else:
-            clip_full = tdist.gather_rows(clip, group)
-            sums = tdist.allreduce_sum(torch.stack([nn_part.sum(), dg_part.sum()]), group)
-            nn_in, n_nn, dg_in, n_dg = sums[0:1], 1, sums[1:2], 1
-        out = torch.empty(13, dtype=torch.float32, device=dev)
-        dclip = torch.empty(Bg, Bg, dtype=torch.float32, device=dev)
-        lse = torch.empty(2 * Bg, dtype=torch.float32, device=dev)
-        call("triad_losshead", ptr(clip_full), Bg, kind, ptr(temp), ptr(nn_in), n_nn, n_el, ptr(dg_in), n_dg,
-             cnt, float(w_sparse), ptr(out), ptr(dclip), ptr(lse), st)
-        dclip_rows = dclip[rank * Bq:(rank + 1) * Bq].contiguous() if W > 1 else dclip
-
+        h = _head_begin(q, k, temperature, kind, q_mask, group, ds_budget, need_grad)
+        st = stream_ptr(q.device)
+        _head_launch(h, st)
+        losses, stats, clip_full = _head_end(h, q_mask, thr, w_sparse, st)
         if need_grad:
-            ctx.save_for_backward(Qb, Kb, argmax, rowmax, dclip_rows, qw, gdiag, temp, dS, st_part, dgt_part)
-        ctx.geom, ctx.kind, ctx.n_el, ctx.w_sparse, ctx.nparts, ctx.CT = g, kind, n_el, float(w_sparse), nparts, CT
-        ctx.chunk = chunk
-        ctx.group, ctx.W, ctx.rank, ctx.Nk = group, W, rank, Nk
-        ctx.q_dtype, ctx.k_dtype, ctx.t_dtype = q.dtype, k.dtype, temperature.dtype
-        losses, stats = out[:4].clone(), out[4:].clone()
+            ctx.save_for_backward(*_head_saved(h))
+        ctx.head = _head_light(h)
         ctx.mark_non_differentiable(stats, clip_full)
         ctx.set_materialize_grads(False)
         return losses[0], losses[1], losses[2], losses[3], stats, clip_full
 
     @staticmethod
     def backward(ctx, g_total, g_ce, g_reg, g_aux, g_stats, g_clip):
-        none9 = (None,) * 9
         if g_total is None and g_ce is None and g_reg is None and g_aux is None:
-            return none9
-        Qb, Kb, argmax, rowmax, dclip, qw, gdiag, temp, dS, st_part, dgt_part = ctx.saved_tensors
-        g, kind, W, rank, CT = ctx.geom, ctx.kind, ctx.W, ctx.rank, ctx.CT
-        dev = Qb.device
-        st = stream_ptr(dev)
-        f32 = torch.float32
-        zero = torch.zeros((), dtype=f32, device=dev)
-        gt_, gc_, gr_, ga_ = [zero if x is None else x.to(f32) for x in (g_total, g_ce, g_reg, g_aux)]
-        c_ce = gt_ + gc_
-        c_reg = gt_ + gr_
-        c_nn = c_reg * (0.15 * 2.0 / ctx.n_el)
-        if kind == AV:
-            c_diag = 0.01 * (c_reg + ga_)   # reg = ... + 0.01*l_smooth; aux = 0.01*l_smooth
-            c_cal = 20.0 * c_reg
-        else:
-            c_diag = ctx.w_sparse * c_reg + ga_  # reg = ... + w*sparsity; aux = sparsity
-            c_cal = torch.zeros_like(c_reg)
-        has_cal = 1 if (kind == AV and rank == 0) else 0   # the l_cal term is counted once
-        fast = g_total is not None and g_ce is None and g_reg is None and g_aux is None and dS is not None
-        gq = gk = gt = None
-        if fast:
-            # dS = c_nn * (unit l_nonneg grad [written by the forward] + ratio_max * max term
-            #               + ratio_diag * diagonal term); the ratios are host constants here
-            ratio_max = ctx.n_el / 0.3
-            ratio_diag = (0.01 if kind == AV else ctx.w_sparse) * ctx.n_el / 0.3
-            nmp = 1024
-            max_part = torch.empty(nmp, dtype=torch.float64, device=dev)
-            call("triad_dS_patch", ptr(dS), CT, g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, rank * g.Bq,
-                 ptr(argmax), ptr(rowmax), ptr(dclip), ptr(qw), float(ratio_max), ptr(gdiag), float(ratio_diag),
-                 ptr(max_part), nmp, st)
-            alpha = (temp * c_nn).reshape(1).contiguous()
-            w = torch.stack([c_nn, c_ce / temp[0], c_diag / temp[0], c_cal]).contiguous()
-            parts = (st_part, ctx.nparts, max_part, nmp, dgt_part, g.Bq)
-        else:
-            # recompute form: any mix of upstream gradients, or a dS over the memory budget
-            coef = torch.stack([c_ce, c_nn, c_diag, c_cal]).contiguous()
-            dQ, dK, dt_part = recompute_backward(g, Qb, Kb, temp, kind, rank * g.Bq, argmax, dclip, qw, gdiag, coef,
-                                                 ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.chunk, st,
-                                                 ds_buf=dS)
-            w = torch.stack([torch.ones_like(c_ce), zero, zero, c_cal]).contiguous()
-            parts = (dt_part, dt_part.numel(), None, 0, None, 0)
-            if dQ is not None:
-                gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(ctx.q_dtype)
-        if fast and ctx.needs_input_grad[0]:
-            dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
-            tile_gemm(dS, CT, 0, Kb, g.R_pad, g.C_pad // 32, alpha, dQ, st,
-                      meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dQ"))
-            gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(ctx.q_dtype)
-        if ctx.needs_input_grad[1]:
-            if fast:
-                Mk = CT * 32
-                dK = torch.empty(Mk, D, dtype=torch.bfloat16, device=dev)
-                tile_gemm(dS, CT, 1, Qb, Mk, g.R_pad // 32, alpha, dK, st,
-                          meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dK"))
-            Nk_pad = g.Nk_pad
-            if W > 1:
-                from . import dist as tdist
-                dK = tdist.reduce_scatter_rows(dK, g.Bq * Nk_pad, ctx.group)  # this rank's keys, all queries
-            gk = dK[:g.Bq * Nk_pad].view(g.Bq, Nk_pad, D)[:, :ctx.Nk].to(ctx.k_dtype)
-        if ctx.needs_input_grad[2]:
-            dt = torch.empty(1, dtype=f32, device=dev)
-            p0, n0, p1, n1, p2, n2 = parts
-            call("triad_dtemp_finalize", ptr(p0), n0, ptr(p1), n1, ptr(p2), n2, ptr(temp), ptr(w), has_cal,
-                 ptr(dt), st)
-            gt = dt.reshape(()).to(ctx.t_dtype)
+            return (None,) * 9
+        gq, gk, gt = _head_backward(ctx.head, ctx.saved_tensors, ctx.needs_input_grad[:3], g_total, g_ce, g_reg,
+                                    g_aux)
         return gq, gk, gt, None, None, None, None, None, None
+
+
+class _ContrastiveHeadPair(torch.autograd.Function):
+    """The tri-modal step's AV and TV heads with ONE similarity-forward launch over both
+    (triad_pairsim_fwd_multi; BASELINE c3's fused similarity kernel over the pair losses -- the
+    reference has no audio-text loss). Everything else per head exactly as _ContrastiveHead;
+    the shared temperature's gradient is the sum of the two heads'.
+    Outputs: AV (total, ce, reg, aux, stats, clip) then TV (the same six)."""
+
+    @staticmethod
+    def forward(ctx, qa, ka, qt, kt, temperature, qt_mask, thr, w_sparse, group, ds_budget):
+        nig = ctx.needs_input_grad
+        need_grad = any(nig[:5])
+        ha = _head_begin(qa, ka, temperature, AV, None, group, ds_budget, need_grad)
+        ht = _head_begin(qt, kt, temperature, TV, qt_mask, group, ds_budget, need_grad)
+        st = stream_ptr(qa.device)
+        if (ha.dS is None) == (ht.dS is None):
+            _heads_launch([ha, ht], st)
+        else:  # one head over the dS budget: the multi launch needs one mode for both
+            _head_launch(ha, st)
+            _head_launch(ht, st)
+        la, sa, ca = _head_end(ha, None, 0.0, 0.0, st)
+        lt, stt, ct = _head_end(ht, qt_mask, thr, w_sparse, st)
+        if need_grad:
+            ctx.save_for_backward(*_head_saved(ha), *_head_saved(ht))
+        ctx.heads = (_head_light(ha), _head_light(ht))
+        ctx.mark_non_differentiable(sa, ca, stt, ct)
+        ctx.set_materialize_grads(False)
+        return la[0], la[1], la[2], la[3], sa, ca, lt[0], lt[1], lt[2], lt[3], stt, ct
+
+    @staticmethod
+    def backward(ctx, a_total, a_ce, a_reg, a_aux, _sa, _ca, t_total, t_ce, t_reg, t_aux, _st, _ct):
+        nig = ctx.needs_input_grad
+        saved = ctx.saved_tensors
+        n = len(_SAVED)
+        ha, ht = ctx.heads
+        gqa, gka, gta = _head_backward(ha, saved[:n], (nig[0], nig[1], nig[4]), a_total, a_ce, a_reg, a_aux)
+        gqt, gkt, gtt = _head_backward(ht, saved[n:], (nig[2], nig[3], nig[4]), t_total, t_ce, t_reg, t_aux)
+        gt = gta if gtt is None else (gtt if gta is None else gta + gtt)
+        return gqa, gka, gqt, gkt, gt, None, None, None, None, None
 
 
 def contrastive_head(kind, q, k, temperature, q_mask=None, threshold=0.0, sparsity_weight=0.0, group=None,
@@ -399,6 +510,16 @@ def contrastive_head(kind, q, k, temperature, q_mask=None, threshold=0.0, sparsi
     total, ce, reg, aux, stats, clip = _ContrastiveHead.apply(q, k, temperature, kind, q_mask, threshold,
                                                               sparsity_weight, group, ds_budget)
     return (total, ce, reg, aux), stats, clip
+
+
+def contrastive_heads_av_tv(audio, visual_av, text, visual_tv, temperature, text_mask, threshold=0.0,
+                            sparsity_weight=0.0, group=None, ds_budget=None):
+    """Both heads of the tri-modal step with one similarity-forward launch: equal to
+    contrastive_head(AV, audio, visual_av, ...) and contrastive_head(TV, text, visual_tv, ...).
+    Returns ((losses, stats, clip) of AV, (losses, stats, clip) of TV)."""
+    o = _ContrastiveHeadPair.apply(audio, visual_av, text, visual_tv, temperature, text_mask, threshold,
+                                   sparsity_weight, group, ds_budget)
+    return ((o[0], o[1], o[2], o[3]), o[4], o[5]), ((o[6], o[7], o[8], o[9]), o[10], o[11])
 
 
 def gather_rows(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
