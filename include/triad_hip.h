@@ -163,6 +163,10 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
  * four-wave tiles, 4 = 256 x 256 eight-wave tiles (3 / 4: M, N multiples of 256). */
 int triad_gemm_set_form(int form);
 
+/* The 256 x 256 form the size policy uses for tall outputs: 4 = eight-wave (default), 3 = four-wave
+ * (A/B knob; triad_amd/gemm.py sets it from TRIAD_GEMM_BIG_FORM). */
+int triad_gemm_set_big_form(int form);
+
 /* Fused projection head forward (model.py:32-34,68 / 81-83,116 / 253-255,326 under bf16
  * autocast): y = bf16(LN(bf16(h W1^T + b1)) W2^T + b2) for M rows of H features (H % 32 == 0);
  * also saves y1 = bf16(h W1^T + b1), ln = bf16(LN(y1)) ([M][512] bf16) and mean / rstd per row

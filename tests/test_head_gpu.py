@@ -312,7 +312,10 @@ def test_pair_launch_matches_two_heads(B, Na, Nt, Nv, budget):
     on the same tiles); and against the fp64 oracle. budget "mixed": the AV head's dS over the
     budget, TV's within it (mixed modes -> two launches, chunked recompute backward for AV)."""
     ops = _ops()
-    g = torch.Generator().manual_seed(500 + B)
+    # seed: no query's two best keys closer than 6.5e-5 in S (at seed 500 + B the (5, 300) case has
+    # two keys 2.8e-6 apart at S = 13.28, below fp32 resolution: the MFMA sum order picks the other
+    # one as the max and that row's gradient moves to it -- a legitimate tie flip, not an error)
+    g = torch.Generator().manual_seed(900 + B)
     A = _rand_feats(g, (B, Na, 512))
     T = _rand_feats(g, (B, Nt, 512))
     Va = _rand_feats(g, (B, Nv, 512))

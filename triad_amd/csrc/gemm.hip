@@ -513,6 +513,10 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
 // launch(), 1 = 128 x 128, 2 = 256 x 128 ring, 3 = 256 x 256 four-wave, 4 = 256 x 256 eight-wave
 // (when the shape allows).
 int g_gemm_form = 0;
+// The 256 x 256 form the size policy picks: 4 = eight-wave (default since round 2: 3-13 % faster
+// than the four-wave form on every c3 backbone / projection-head shape with M >= 50,944,
+// tools/gemm_backend_probe.py, profiles/r02_gemm_w8_probe.log), 3 = four-wave.
+int g_big_form = 4;
 
 
 template <bool AK, bool BK_, typename OutT>
@@ -529,6 +533,7 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
   // 2.94 -> 2.67 ms at M = 1.6 M, N = 512, K = 1536); the split-K weight gradients and the
   // shorter forward shapes keep the smaller tiles
   const bool w4_auto = AK && BK_ && splits == 1 && M >= 65536 && Kd >= 1024;
+  if (form == 0 && w4_ok && w4_auto) form = g_big_form;
   if (w4_ok && form == 4) {
     const int nwg = (M / GW_M) * (N / GW_N);
     hipLaunchKernelGGL((gemm_w8_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
@@ -582,14 +587,18 @@ int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, 
 // The backbone projections (torch's F.linear / matmul under autocast, routed here by
 // triad_amd/gemm.py): C = op(A) op(B) (+ bias[n] before the one bf16 rounding), bf16 out. Tile
 // form by shape, measured on the c3 shapes (tools/gemm_backend_probe.py,
-// profiles/r02_gemm_backend_probe.log): the 256 x 256 four-wave form when the output is tall and
-// the contraction or width large (M >= 32768 and N * Kd >= 768 * 2304), the 256 x 128 ring for
-// other tall outputs, 128 x 128 below 8192 rows. 740-990 TFLOP/s; rocBLAS's own kernels run the
-// same shapes at 300-790.
+// profiles/r02_gemm_backend_probe.log, r02_gemm_w8_probe.log): the 256 x 256 eight-wave form when
+// the output is tall (M >= 32768, M and N multiples of 256), the 256 x 128 ring for other tall
+// outputs, 128 x 128 below 8192 rows. 790-940 TFLOP/s; rocBLAS's own kernels run the same shapes
+// at 300-790.
 int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
                          int M, int N, int Kd, const float* bias, void* C, long long ldc, hipStream_t stream) {
+  // eight-wave 256 x 256 for every tall output it tiles (the four-wave form, g_big_form = 3, only
+  // where it measured faster than the 256 x 128 ring: N * Kd >= 768 * 2304)
   int form = 1;
-  if (M >= 32768 && M % GW_M == 0 && N % GW_N == 0 && (long long)N * Kd >= 768LL * 2304) form = 3;
+  if (M >= 32768 && M % GW_M == 0 && N % GW_N == 0 &&
+      (g_big_form == 4 || (long long)N * Kd >= 768LL * 2304))
+    form = g_big_form;
   else if (M >= 8192 && M % GB_M == 0) form = 2;
 #define TRIAD_GEMM_B(AK, BKC)                                                                     \
   if (!!a_kcontig == AK && !!b_kcontig == BKC)                                                    \
@@ -624,6 +633,12 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
 
 // Select the GEMM form for later calls (0 = size policy, 1 = 128 x 128, 2 = 256 x 128 ring,
 // 3 = 256 x 256 four-wave, 4 = 256 x 256 eight-wave). Process-wide tuning / test knob.
+int triad_gemm_set_big_form(int form) {
+  if (form != 3 && form != 4) return TRIAD_EINVAL;
+  g_big_form = form;
+  return TRIAD_OK;
+}
+
 int triad_gemm_set_form(int form) {
   if (form < 0 || form > 4) return TRIAD_EINVAL;
   g_gemm_form = form;
