@@ -1,6 +1,6 @@
 """Backbone forward / input-gradient GEMM shapes of the c3 step on (a) torch -> the BLAS library
 triad_amd.blas selects (rocBLAS without its hipBLASLt forwarding, by default) and (b) the HIP
-GEMM of gemm.hip in each tile form (1: 128 x 128, 2: 256 x 128 ring, 3: 256 x 256 four-wave, 4: eight-wave, 5: eight-wave 32-deep 4-slot ring),
+GEMM of gemm.hip in each tile form (1: 128 x 128, 2: 256 x 128 ring, 3: 256 x 256 four-wave, 4: eight-wave),
 bf16 out. Prints one JSON line per (shape, path): microseconds and TFLOP/s."""
 import json
 import os
@@ -50,7 +50,7 @@ def main():
         C = torch.empty(M, N, device=dev, dtype=bf)
         ref = lib().float()
         res = {"kind": kind, "M": M, "N": N, "K": K, "lib_us": round(timed(lib), 1)}
-        for form in (1, 2, 3, 4, 5):
+        for form in (1, 2, 3, 4):
             call("triad_gemm_set_form", form)
             a, lda, ak, b, ldb, bk = args
 

@@ -509,141 +509,16 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
     }
 }
 
-// ---- 256 x 256 eight-wave ring form -------------------------------------------------------------
-// The eight-wave tile with the pipeline of the head's tile GEMM (bwd_gemm.hip): stage = ONE 32-deep
-// k chunk (A [256][32] + B [256][32] = 32 KB), a 4-slot LDS ring (128 KB) with each chunk's DMA
-// issued three chunks ahead, a counted `s_waitcnt vmcnt` that leaves the two younger chunks in
-// flight, one barrier per chunk. Each wave issues exactly 4 pieces per chunk. k-contiguous
-// images have 64-B rows: chunk c of row m at c ^ ((m >> 2) & 3) (conflict-free ds_read_b128 lane
-// groups); [k][rows] images are two [32][128] halves in the n-contiguous layout (nc_off).
-constexpr int GR_BK = 32, GR_NB = 4;
-constexpr int GR_A = GW_M * GR_BK, GR_ST = GR_A + GW_N * GR_BK;  // elements per slot (32 KB)
-constexpr int GR_PIECES = 4;
-
-__device__ __forceinline__ int kc32_off(int m, int chunk) { return m * GR_BK + ((chunk ^ ((m >> 2) & 3)) << 3); }
-
-template <bool KCONTIG>
-__device__ __forceinline__ void gr_piece_one(const bf16* __restrict__ X, long long ld, int r0, int k0, bf16* img,
-                                             int inst, int lane) {
-  if (KCONTIG) {  // image [256][32]: 16 rows x 64 B per wave-instruction
-    const int m = inst * 16 + (lane >> 2), cp = lane & 3;
-    const int c = cp ^ ((m >> 2) & 3);
-    glds16(X + (size_t)(r0 + m) * ld + k0 + c * 8, img + inst * 512);
-  } else {  // X stored [k][rows]: two [32][128] halves, 4 k-rows x 256 B per wave-instruction
-    const int half = inst >> 3, ii = inst & 7;
-    const int k = ii * 4 + (lane >> 4), cp = lane & 15;
-    const int c = cp ^ ((k & 3) << 2);
-    glds16(X + (size_t)(k0 + k) * ld + r0 + half * 128 + c * 8, img + half * (GR_BK * 128) + ii * 512);
-  }
-}
-
-template <bool A_KCONTIG, bool B_KCONTIG>
-__device__ __forceinline__ void gr_piece(const bf16* __restrict__ A, long long lda, const bf16* __restrict__ B,
-                                         long long ldb, int m0, int n0, int k0, bf16* dst, int wave, int lane,
-                                         int u) {
-  if (u < 2) gr_piece_one<A_KCONTIG>(A, lda, m0, k0, dst, wave * 2 + u, lane);
-  else gr_piece_one<B_KCONTIG>(B, ldb, n0, k0, dst + GR_A, wave * 2 + (u - 2), lane);
-}
-
-template <bool KCONTIG>
-__device__ __forceinline__ bf16x8 gr_frag(const bf16* img, int row, int s, int lane) {
-  if (KCONTIG) return *(const bf16x8*)(img + kc32_off(row + (lane & 31), 2 * s + (lane >> 5)));
-  return frag_tr(img + (row >> 7) * (GR_BK * 128), row & 127, s, lane);
-}
-
-template <bool A_KCONTIG, bool B_KCONTIG, typename OutT>
-__global__ __launch_bounds__(512, 1) void gemm_w8r_kernel(const bf16* __restrict__ A, long long lda,
-                                                          const bf16* __restrict__ B, long long ldb, int M, int N,
-                                                          int Kd, const float* __restrict__ alpha_p,
-                                                          OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                          long long slab_stride, const float* __restrict__ bias) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[GR_NB * GR_ST];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int h = lane >> 5;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
-  const int ntn = N / GW_N;
-  const int m0 = (swz / ntn) * GW_M, n0 = (swz % ntn) * GW_N;
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){};
-
-  const int kbeg = blockIdx.y * k_per_split;
-  const int nk = __builtin_amdgcn_readfirstlane(max(0, min(k_per_split, Kd - kbeg)) / GR_BK);
-  C += (size_t)blockIdx.y * slab_stride;
-#pragma unroll
-  for (int p = 0; p < GR_NB - 1; ++p)
-    if (p < nk)
-#pragma unroll
-      for (int u = 0; u < GR_PIECES; ++u)
-        gr_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kbeg + p * GR_BK, lds + p * GR_ST, wave, lane, u);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int younger = min(GR_NB - 2, nk - 1 - kt);  // uniform
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GR_PIECES) : "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GR_PIECES) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const bool pf = kt + GR_NB - 1 < nk;
-    bf16* const pdst = lds + ((kt + GR_NB - 1) % GR_NB) * GR_ST;
-    const int kn = kbeg + (kt + GR_NB - 1) * GR_BK;
-    const bf16* ai = lds + (kt % GR_NB) * GR_ST;
-    const bf16* bi = ai + GR_A;
-    bf16x8 af[2][4], bfr[2][2];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) af[0][t] = gr_frag<A_KCONTIG>(ai, wm * 128 + t * 32, 0, lane);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) bfr[0][t] = gr_frag<B_KCONTIG>(bi, wn * 64 + t * 32, 0, lane);
-#pragma unroll
-    for (int s = 0; s < GR_BK / 16; ++s) {
-      const int cur = s & 1;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          acc[a][b] = mfma32(af[cur][a], bfr[cur][b], acc[a][b]);
-          const int j = a * 2 + b, mi = s * 8 + j;
-          if (s + 1 < GR_BK / 16 && j < 6) {  // step s + 1's 6 fragments between step s's MFMAs
-            __builtin_amdgcn_sched_barrier(0);
-            if (j < 4) af[cur ^ 1][j] = gr_frag<A_KCONTIG>(ai, wm * 128 + j * 32, s + 1, lane);
-            else bfr[cur ^ 1][j - 4] = gr_frag<B_KCONTIG>(bi, wn * 64 + (j - 4) * 32, s + 1, lane);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          if (mi % 4 == 1 && mi / 4 < GR_PIECES) {  // the chunk-ahead DMA: one piece per 4 MFMAs
-            __builtin_amdgcn_sched_barrier(0);
-            if (pf) gr_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, pdst, wave, lane, mi / 4);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-    }
-  }
-
-  const float alpha = alpha_p ? *alpha_p : 1.f;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int n = n0 + wn * 64 + b * 32 + (lane & 31);
-      const float bn = bias ? bias[n] : 0.f;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = m0 + wm * 128 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v] + bn);
-      }
-    }
-}
-
 // Form override for measurement and tests (triad_gemm_set_form): 0 = the size policy in
 // launch(), 1 = 128 x 128, 2 = 256 x 128 ring, 3 = 256 x 256 four-wave, 4 = 256 x 256 eight-wave
 // (when the shape allows).
 int g_gemm_form = 0;
 // The 256 x 256 form the size policy picks: 4 = eight-wave (default since round 2: 3-13 % faster
 // than the four-wave form on every c3 backbone / projection-head shape with M >= 50,944,
-// tools/gemm_backend_probe.py, profiles/r02_gemm_w8_probe.log), 3 = four-wave.
+// tools/gemm_backend_probe.py, profiles/r02_gemm_w8_probe.log), 3 = four-wave. (Measured and not
+// kept: the eight-wave tile on a 4-slot ring of 32-deep chunks with the DMA three chunks ahead,
+// 5-8 % slower than this two-slot 64-deep form on every M >= 50,944 shape,
+// profiles/r02_gemm_w8_ring_probe.log: the stage's DMA latency is not what limits it.)
 int g_big_form = 4;
 
 
@@ -662,13 +537,6 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
   // shorter forward shapes keep the smaller tiles
   const bool w4_auto = AK && BK_ && splits == 1 && M >= 65536 && Kd >= 1024;
   if (form == 0 && w4_ok && w4_auto) form = g_big_form;
-  if (w4_ok && form == 5) {
-    const int nwg = (M / GW_M) * (N / GW_N);
-    hipLaunchKernelGGL((gemm_w8r_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
-                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias);
-    TRIAD_CHECK_LAUNCH();
-    return TRIAD_OK;
-  }
   if (w4_ok && form == 4) {
     const int nwg = (M / GW_M) * (N / GW_N);
     hipLaunchKernelGGL((gemm_w8_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
@@ -769,13 +637,13 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
 // Select the GEMM form for later calls (0 = size policy, 1 = 128 x 128, 2 = 256 x 128 ring,
 // 3 = 256 x 256 four-wave, 4 = 256 x 256 eight-wave). Process-wide tuning / test knob.
 int triad_gemm_set_big_form(int form) {
-  if (form < 3 || form > 5) return TRIAD_EINVAL;
+  if (form != 3 && form != 4) return TRIAD_EINVAL;
   g_big_form = form;
   return TRIAD_OK;
 }
 
 int triad_gemm_set_form(int form) {
-  if (form < 0 || form > 5) return TRIAD_EINVAL;
+  if (form < 0 || form > 4) return TRIAD_EINVAL;
   g_gemm_form = form;
   return TRIAD_OK;
 }
