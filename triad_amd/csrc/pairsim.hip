@@ -487,7 +487,7 @@ __global__ void dtemp_finalize_kernel(const double* __restrict__ p0, int n0, con
 // (dispatch rounds of one workgroup per CU over 256 CUs) x (key samples per workgroup + the
 // query-fragment load, ~0.3 sample). Whole rounds keep the last wave of workgroups from leaving
 // CUs idle; fewer, longer workgroups amortise the query load (TV: 32 row blocks -> 8 splits of
-// 32 samples, one round; AV: 200 row blocks -> 32 splits of 8). Measured against the former fixed
+// 32 samples, one round; AV: 199 row blocks -> 9 splits of 29, 7 rounds). Measured against the former fixed
 // 2048-workgroup target: AV train forward 3.00 -> 2.96 ms, TV 0.567 -> 0.532 ms
 // (profiles/r02_fwd_grid_ab.log).
 int grid_for(int R_pad, int Bk, int* jpw, int* ysplit) {
