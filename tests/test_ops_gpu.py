@@ -416,3 +416,19 @@ def test_weight_grad_table_splits_vs_fp32(M, O, K):
     assert got.dtype == torch.bfloat16 and got.shape == (O, K)
     err = float((got.float() - ref).norm() / ref.norm())
     assert err < 4e-3, err  # bf16 output rounding (2^-9 relative) on fp32 accumulation
+
+
+@pytest.mark.parametrize("M,O,K", [(32768, 768, 768), (33024, 2304, 768), (32768, 768, 3072), (8192, 768, 768)])
+def test_linear_weight_grad_forms(M, O, K):
+    """Backbone weight gradients dW = dY^T X (triad_amd.linear.weight_grad): the eight-wave
+    256 x 256 split-K form at >= 32,768 tokens (24 / 8 / 12 splits) and the 128 x 128 table below,
+    against an fp32 torch matmul of the same bf16 operands."""
+    from triad_amd import linear
+    g = torch.Generator(device=dev).manual_seed(M + O + K)
+    dy = torch.randn(M, O, device=dev, generator=g).to(torch.bfloat16)
+    x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    form, sp = linear._form_splits(M, O, K)
+    assert form == (4 if M >= 32768 else 0)
+    dw = linear.weight_grad(dy, x)
+    ref = dy.float().t() @ x.float()
+    assert _rel(dw.float(), ref) < 4e-3

@@ -37,6 +37,7 @@ SIGNATURES = {
     "triad_gemm_bf16": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, i32, vp],
     "triad_gemm_bf16_bias": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, vp],
     "triad_gemm_bf16_splitk": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp],
+    "triad_gemm_bf16_splitk_form": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp],
     "triad_projhead_fwd": [vp, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, i64, vp, vp, vp, vp, vp],
     "triad_projhead_bwd_slabs": [i32],
     "triad_projhead_bwd": [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp],

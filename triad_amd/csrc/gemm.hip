@@ -617,14 +617,16 @@ int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void
 // Split-K form for short-and-wide outputs (weight gradients: M, N = 512 / H, Kd = tokens):
 // `splits` partial fp32 slabs in `slabs` ([splits][M][N], caller-owned), then
 // C = alpha * sum(slabs) as fp32 or bf16 (ldc == N).
-int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
-                           int M, int N, int Kd, int splits, const float* alpha, float* slabs, void* C,
-                           int out_bf16, hipStream_t stream) {
+int triad_gemm_bf16_splitk_form(const void* A, long long lda, int a_kcontig, const void* B, long long ldb,
+                                int b_kcontig, int M, int N, int Kd, int splits, const float* alpha, float* slabs,
+                                void* C, int out_bf16, int form, hipStream_t stream) {
+  if (form < 0 || form > 4) return TRIAD_EINVAL;
   const long long slab = (long long)M * N;
   int rc = TRIAD_EINVAL;
 #define TRIAD_GEMM_SK(AK, BKC)                                                                  \
   if (!!a_kcontig == AK && !!b_kcontig == BKC)                                                 \
-    rc = launch<AK, BKC, float>(A, lda, B, ldb, M, N, Kd, nullptr, slabs, N, stream, splits, slab);
+    rc = launch<AK, BKC, float>(A, lda, B, ldb, M, N, Kd, nullptr, slabs, N, stream, splits, slab, nullptr, \
+                                form ? form : g_gemm_form);
   TRIAD_GEMM_SK(true, true)
   TRIAD_GEMM_SK(true, false)
   TRIAD_GEMM_SK(false, true)
@@ -632,6 +634,13 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
 #undef TRIAD_GEMM_SK
   if (rc) return rc;
   return triad_sum_slabs(slabs, splits, slab, alpha, out_bf16, C, stream);
+}
+
+int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                           int M, int N, int Kd, int splits, const float* alpha, float* slabs, void* C,
+                           int out_bf16, hipStream_t stream) {
+  return triad_gemm_bf16_splitk_form(A, lda, a_kcontig, B, ldb, b_kcontig, M, N, Kd, splits, alpha, slabs, C,
+                                     out_bf16, 0, stream);
 }
 
 // Select the GEMM form for later calls (0 = size policy, 1 = 128 x 128, 2 = 256 x 128 ring,

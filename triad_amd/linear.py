@@ -44,15 +44,29 @@ def _splits(M, out_f, in_f):
     return min(8 if tiles <= 160 else 4, max(2, M // 2048))
 
 
+# Eight-wave 256 x 256 form for the long-token weight gradients, split counts per 256 x 256 tile
+# count (tools/dw_w8_probe.py, profiles/r02_dw_w8_probe.log, 50,944 tokens: 2304 x 768 202 vs 247 us
+# on the 128 x 128 table above, 768 x 768 98 vs 101, 3072 x 768 275 vs 298, 768 x 3072 284 vs 315;
+# at 8,192 tokens the 128 x 128 table stays faster).
+_W8_SPLITS = {27: 8, 9: 24, 36: 12}
+
+
+def _form_splits(M, out_f, in_f):
+    tiles8 = (out_f // 256) * (in_f // 256) if out_f % 256 == 0 and in_f % 256 == 0 else 0
+    if M >= 32768 and tiles8 in _W8_SPLITS:
+        return 4, _W8_SPLITS[tiles8]
+    return 0, _splits(M, out_f, in_f)
+
+
 def weight_grad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     """dW = dy2^T x2 (bf16 [O][K]) for dy2 [M][O], x2 [M][K] bf16 row-major, M % 64 == 0."""
     M, O = dy2.shape
     K = x2.shape[1]
-    sp = _splits(M, O, K)
+    form, sp = _form_splits(M, O, K)
     slabs = torch.empty(sp * O * K, dtype=torch.float32, device=dy2.device)
     dw = torch.empty(O, K, dtype=torch.bfloat16, device=dy2.device)
-    call("triad_gemm_bf16_splitk", ptr(dy2), dy2.stride(0), 0, ptr(x2), x2.stride(0), 0, O, K, M, sp, None,
-         ptr(slabs), ptr(dw), 1, stream_ptr(dy2.device), meta=dict(backbone=True))
+    call("triad_gemm_bf16_splitk_form", ptr(dy2), dy2.stride(0), 0, ptr(x2), x2.stride(0), 0, O, K, M, sp, None,
+         ptr(slabs), ptr(dw), 1, form, stream_ptr(dy2.device), meta=dict(backbone=True))
     return dw
 
 
