@@ -35,6 +35,9 @@ def main():
             shapes.append(("fwd", M, N, K))     # y = x W^T
             shapes.append(("dX", M, K, N))      # dx = dy W   (dy [M][N], W [N][K])
     one = torch.ones(1, device=dev)
+    forms = tuple(int(f) for f in os.environ.get("PROBE_FORMS", "1,2,3,4").split(","))
+    min_m = int(os.environ.get("PROBE_MIN_M", "0"))
+    shapes = [sh for sh in shapes if sh[1] >= min_m]
     for kind, M, N, K in shapes:
         fl = 2.0 * M * N * K
         if kind == "fwd":
@@ -49,8 +52,9 @@ def main():
             args = (A, K, 1, W, N, 0)
         C = torch.empty(M, N, device=dev, dtype=bf)
         ref = lib().float()
-        res = {"kind": kind, "M": M, "N": N, "K": K, "lib_us": round(timed(lib), 1)}
-        for form in (1, 2, 3, 4):
+        res = {"kind": kind, "M": M, "N": N, "K": K, "lib_us": round(timed(lib), 1) if not min_m else None,
+               "variant": os.environ.get("TRIAD_LIB_VARIANT", "default")}
+        for form in forms:
             call("triad_gemm_set_form", form)
             a, lda, ak, b, ldb, bk = args
 
@@ -67,7 +71,7 @@ def main():
         call("triad_gemm_set_form", 0)
         best = min(v for k, v in res.items() if k.endswith("_us") and v)
         res["best_TFLOPs"] = round(fl / best / 1e6, 1)
-        res["lib_TFLOPs"] = round(fl / res["lib_us"] / 1e6, 1)
+        res["lib_TFLOPs"] = round(fl / res["lib_us"] / 1e6, 1) if res["lib_us"] else None
         print(json.dumps(res), flush=True)
 
 
