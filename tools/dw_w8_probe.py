@@ -28,8 +28,14 @@ def timed(fn, iters=10):
 
 def main():
     bf = torch.bfloat16
-    for M in (50944, 8192):
-        for O, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+    spec = os.environ.get("PROBE_SHAPES")  # "M:O:K,..." (default: the HuBERT / DistilBERT shapes)
+    if spec:
+        shapes = [tuple(int(v) for v in t.split(":")) for t in spec.split(",")]
+    else:
+        shapes = [(M, O, K) for M in (50944, 8192) for O, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072))]
+    splits = tuple(int(v) for v in os.environ.get("PROBE_SPLITS", "2,4,8,12,16,24,32").split(","))
+    for M, O, K in shapes:
+        if True:
             dy = torch.randn(M, O, device="cuda", dtype=bf)
             x = torch.randn(M, K, device="cuda", dtype=bf)
             ref = (dy.float().t() @ x.float())
@@ -49,8 +55,9 @@ def main():
                 return round(us, 1), round(err, 5)
             sp0 = linear._splits(M, O, K)
             res["policy"] = (sp0,) + run(sp0, 0)
-            for sp in (2, 4, 8, 12, 16, 24, 32):
+            for sp in splits:
                 res[f"w8_s{sp}"] = run(sp, 4)
+                res[f"f1_s{sp}"] = run(sp, 1)
             print(json.dumps(res), flush=True)
 
 

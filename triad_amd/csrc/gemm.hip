@@ -419,16 +419,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
 // tiles of 32 x 32, 128 accumulators per lane), reads 6 fragments per 8 MFMAs per 16-deep step, and
 // issues 8 of the next stage's 64 DMA pieces (one after every 2nd of its first 16 MFMAs).
 constexpr int GE_PIECES = 8;
-// A/B knobs (tools/build_variants.py; defaults = the measured product form)
-#ifndef W8_PRIO
-#define W8_PRIO 0        // 1: s_setprio(1) around each 16-deep step's MFMA cluster
-#endif
-#ifndef W8_DMA_BURST
-#define W8_DMA_BURST 0   // 1: the next stage's 8 DMA pieces right after the barrier
-#endif
-#ifndef W8_YOUNG_PRIO
-#define W8_YOUNG_PRIO 0  // 1: static s_setprio(1) for waves 4-7 (the younger half) before the loop
-#endif
+// Measured and not kept (tools/build_variants.py + variant_ab.py, profiles/r02_gemm_w8_variants_ab.log,
+// 16 c3 shapes): s_setprio(1) around each step's MFMA cluster -0.4 %, a static priority for the
+// younger four waves 0.0 %, the next stage's 8 DMA pieces in a burst after the barrier +3.9 %.
 
 template <bool A_KCONTIG, bool B_KCONTIG>
 __device__ __forceinline__ void ge_piece(const bf16* __restrict__ A, long long lda, const bf16* __restrict__ B,
@@ -467,7 +460,6 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
 #pragma unroll
     for (int u = 0; u < GE_PIECES; ++u)
       ge_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kbeg, lds, wave, lane, u);
-  if (W8_YOUNG_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   for (int kt = 0; kt < nk; ++kt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -476,10 +468,6 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
     const int kn = kbeg + (kt + 1) * BK;
     const bf16* ai = lds + (kt & 1) * GW_ST;
     const bf16* bi = ai + GW_A;
-    if (W8_DMA_BURST && pf)
-#pragma unroll
-      for (int u = 0; u < GE_PIECES; ++u)
-        ge_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, u);
     bf16x8 af[2][4], bfr[2][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) af[0][t] = gw_frag<A_KCONTIG>(ai, wm * 128 + t * 32, 0, lane);
@@ -488,7 +476,6 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       const int cur = s & 1;
-      if (W8_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -501,13 +488,12 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
             else bfr[cur ^ 1][j - 4] = gw_frag<B_KCONTIG>(bi, wn * 64 + (j - 4) * 32, s + 1, lane);
             __builtin_amdgcn_sched_barrier(0);
           }
-          if (!W8_DMA_BURST && mi % 2 == 1 && mi / 2 < GE_PIECES) {
+          if (mi % 2 == 1 && mi / 2 < GE_PIECES) {
             __builtin_amdgcn_sched_barrier(0);
             if (pf) ge_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, mi / 2);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
-      if (W8_PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
 
