@@ -421,7 +421,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
 constexpr int GE_PIECES = 8;
 // Measured and not kept (tools/build_variants.py + variant_ab.py, profiles/r02_gemm_w8_variants_ab.log,
 // 16 c3 shapes): s_setprio(1) around each step's MFMA cluster -0.4 %, a static priority for the
-// younger four waves 0.0 %, the next stage's 8 DMA pieces in a burst after the barrier +3.9 %.
+// younger four waves 0.0 %, the next stage's 8 DMA pieces in a burst after the barrier +3.9 %;
+// transposed accumulators (B fragment first) with 8-byte row-run epilogue stores +10 %
+// (profiles/r02_gemm_w8_tepi_ab.log).
 
 template <bool A_KCONTIG, bool B_KCONTIG>
 __device__ __forceinline__ void ge_piece(const bf16* __restrict__ A, long long lda, const bf16* __restrict__ B,
