@@ -423,7 +423,11 @@ constexpr int GE_PIECES = 8;
 // 16 c3 shapes): s_setprio(1) around each step's MFMA cluster -0.4 %, a static priority for the
 // younger four waves 0.0 %, the next stage's 8 DMA pieces in a burst after the barrier +3.9 %;
 // transposed accumulators (B fragment first) with 8-byte row-run epilogue stores +10 %
-// (profiles/r02_gemm_w8_tepi_ab.log).
+// (profiles/r02_gemm_w8_tepi_ab.log); the bf16 tile staged through LDS and stored as 128-B row runs
+// of 16-B stores: equal (profiles/r02_gemm_w8_ldsepi_ab.log). A diagnostic build without the
+// epilogue stores ran 10 % faster (18 % on the wide K = 768 shapes, profiles/
+// r02_gemm_w8_nostore_diag.log): the cost is the output write itself, ~128 KB per workgroup
+// issued by every CU of a dispatch round at once and not overlapped with any MFMA work.
 
 template <bool A_KCONTIG, bool B_KCONTIG>
 __device__ __forceinline__ void ge_piece(const bf16* __restrict__ A, long long lda, const bf16* __restrict__ B,
