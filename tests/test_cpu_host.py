@@ -118,3 +118,32 @@ def test_reference_compile_line_leaves_the_step_methods_eager():
     for name in ("forward_audio_visual", "forward_text_visual", "forward_triad", "compute_contrastive_loss_av"):
         bound = getattr(cm, name)
         assert bound.__self__ is m and bound.__func__ is getattr(MultiModalModel, name)
+
+
+def test_pairsim_fwd_multi_rejects_bad_arguments():
+    """triad_pairsim_fwd_multi validates every problem before it launches anything (no GPU needed):
+    problem count outside 1..2, a missing array, a bad geometry, or one head writing dS while the
+    other does not -> TRIAD_EINVAL (1001)."""
+    import ctypes as C
+    from triad_amd import _lib, build
+    if not os.path.exists(_lib.LIB_PATH):
+        build.build()
+    lib = _lib.load()
+    fake = 4096  # never dereferenced: validation fails first
+
+    def prob(R_pad=256, dS=None, st_part=None):
+        return _lib.PairsimProblem(fake, fake, 200, R_pad, 50, 4, 4, 64, 60, fake, -60.0, 1, 0, fake, fake, fake,
+                                   fake, dS, 8, st_part)
+    f = lib.triad_pairsim_fwd_multi
+    two = (_lib.PairsimProblem * 2)(prob(), prob())
+    assert f(None, 1, None) == 1001
+    assert f(two, 0, None) == 1001
+    assert f(two, 3, None) == 1001
+    assert f((_lib.PairsimProblem * 1)(prob(R_pad=250)), 1, None) == 1001        # R_pad % 256
+    assert f((_lib.PairsimProblem * 1)(prob(dS=fake)), 1, None) == 1001          # dS without st_part
+    mixed = (_lib.PairsimProblem * 2)(prob(dS=fake, st_part=fake), prob())
+    assert f(mixed, 2, None) == 1001                                            # train + eval in one launch
+    nul = prob()
+    nul.rowmax = None
+    assert f((_lib.PairsimProblem * 1)(nul), 1, None) == 1001
+    assert C.sizeof(_lib.PairsimProblem) == 128
