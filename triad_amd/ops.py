@@ -756,7 +756,7 @@ class _ProjectionHeadPasses(torch.autograd.Function):
 
 
 # Measured per call, kernel time only (tools/projhead_kernels.py, profiles/r02_projhead_kernels.log):
-# "lib" fwd 142 / bwd 474 us vs "fused" 174 / 600 us at 65,536 rows; lower at every c3 / c5 row count.
+# "passes" fwd 154 / bwd 443 us vs "fused" 177 / 596 us at 65,536 rows; lower at every c3 / c5 row count.
 PROJHEAD_FORM = "passes"
 
 
