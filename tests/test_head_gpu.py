@@ -365,3 +365,25 @@ def test_pair_launch_matches_two_heads(B, Na, Nt, Nv, budget):
     for gg, rr in ((a1.grad, Ar.grad), (va1.grad, Var.grad), (t1.grad, Tr.grad), (vt1.grad, Vtr.grad)):
         _check_grad(gg, rr.numpy())
     assert _scalar_close(float(tg1.grad), float(tr.grad), 1e-3, 1e-5), (float(tg1.grad), float(tr.grad))
+
+
+@pytest.mark.parametrize("bk", [0, 1])
+def test_gemm_wide_bf16_nontemporal(bk):
+    """Eight-wave form with a wide bf16 output (2304 columns, B k-contiguous or not)
+    against an fp32 torch matmul of the same bf16 operands."""
+    from triad_amd._lib import call, ptr, stream_ptr
+    g = torch.Generator().manual_seed(11 + bk)
+    M, N, K = 512, 2304, 384
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    B = torch.randn(K, N, generator=g).to(torch.bfloat16)
+    ref = A.float() @ B.float()
+    Ad = A.to(dev)
+    Bd = (B.t().contiguous() if bk else B).to(dev)
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    call("triad_gemm_set_form", 4)
+    try:
+        call("triad_gemm_bf16", ptr(Ad), K, 1, ptr(Bd), K if bk else N, bk, M, N, K, None, ptr(C), N, 1, stream_ptr())
+        torch.cuda.synchronize()
+    finally:
+        call("triad_gemm_set_form", 0)
+    assert float((C.float().cpu() - ref).norm() / ref.norm()) < 4e-3

@@ -419,9 +419,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
 // tiles of 32 x 32, 128 accumulators per lane), reads 6 fragments per 8 MFMAs per 16-deep step, and
 // issues 8 of the next stage's 64 DMA pieces (one after every 2nd of its first 16 MFMAs).
 constexpr int GE_PIECES = 8;
-#ifndef W8_NTSTORE
-#define W8_NTSTORE 0  // A/B: non-temporal epilogue stores
-#endif
 // Measured and not kept (tools/build_variants.py + variant_ab.py, profiles/r02_gemm_w8_variants_ab.log,
 // 16 c3 shapes): s_setprio(1) around each step's MFMA cluster -0.4 %, a static priority for the
 // younger four waves 0.0 %, the next stage's 8 DMA pieces in a burst after the barrier +3.9 %;
@@ -516,11 +513,7 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int m = m0 + wm * 128 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-#if W8_NTSTORE
-        __builtin_nontemporal_store((OutT)(alpha * acc[a][b][v] + bn), C + (size_t)m * ldc + n);
-#else
         C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v] + bn);
-#endif
       }
     }
 }
