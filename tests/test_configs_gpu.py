@@ -16,8 +16,9 @@ outputs).
 
 Tolerances (north star): losses / clip / statistics 1e-4 relative (the kernels do exact fp32
 arithmetic on the bf16 features; the oracle is fp64 on the same values); feature gradients the
-bf16 bar, relative L2 < 1e-2 (dS is a bf16 MFMA operand) -- 1.5e-2 at c5, where the measured
-error sits at that line (see the test); d/dtemp 1e-3 relative.
+bf16 bar, relative L2 < 1e-2 (dS is a bf16 MFMA operand; measured 1.8e-3 - 3.0e-3 at every
+configuration, profiles/r02_config_grad_errors.log); d/dtemp 1e-3 relative. Inputs are seeded,
+SpecAugment's numpy draws included.
 """
 import math
 
@@ -197,10 +198,10 @@ def test_c5_large_backbones_per_rank_b32():
     (Na = 499), DistilBERT captions, B=32, the tri-modal step."""
     m = _model(audio_model_name="facebook/hubert-large-ls960-ft", vit_arch="dinov2_vitl14_reg")
     assert m.audio_embedder.hubert.config.hidden_size == 1024 and m.visual_embedder.model.embed_dim == 1024
-    # feature-gradient bar 1.5e-2 here: with 1369 keys per sample the bf16 dS operand (2^-9 relative
-    # per element) puts the relative L2 error of the head's feature gradients at the 1e-2 line --
-    # one box measured 1.012e-2 (profiles/r02_gpu_tests_c5.log); the per-config errors are logged
-    # (profiles/r02_config_grad_errors.log)
-    cap, v_av, v_tv = _triad_step_check(m, 32, 518, 10, 32, grad_bar=1.5e-2)
+    # feature gradients 1.8e-3 - 2.5e-3 from the oracle on the seeded inputs
+    # (profiles/r02_config_grad_errors.log); a run with unseeded SpecAugment draws once measured
+    # 1.012e-2 (profiles/r02_gpu_tests_c5.log) -- the signature of an fp32 near-tie of a row max
+    # moving one row's gradient to the other key (diagnosed in tests/test_head_gpu.py's pair test)
+    cap, v_av, v_tv = _triad_step_check(m, 32, 518, 10, 32)
     assert cap.a.shape == (32, 499, 512)
     assert 1000 < v_av.shape[1] <= 1369
