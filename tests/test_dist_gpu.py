@@ -88,6 +88,62 @@ def test_global_negatives_two_ranks_match_single_process(kind):
     assert abs(dt - float(t.grad)) <= 1e-3 * abs(float(t.grad)) + 1e-6
 
 
+def _pair_worker(rank, world, port, q_out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        q_out.put((rank,) + _pair_run(rank, world, dist.group.WORLD))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q_out.put((rank, "error", traceback.format_exc(), None, None))
+
+
+def _pair_run(rank, world, group):
+    """Both heads through ONE similarity-forward launch (ops.contrastive_heads_av_tv) on this rank's
+    slice; world = 1: the whole batch in one process."""
+    from triad_amd import ops
+    qa, ka, _ = _inputs(0, seed=21)
+    qt, kt, mask = _inputs(1, Nq=12, Nv=37, seed=22)
+    Bl = qa.shape[0] // world
+    sl = slice(rank * Bl, (rank + 1) * Bl)
+    xs = [x[sl].cuda().requires_grad_(True) for x in (qa, ka, qt, kt)]
+    t = torch.tensor(1.4, device="cuda", requires_grad=True)
+    (la, sa, _), (lt, st, _) = ops.contrastive_heads_av_tv(xs[0], xs[1], xs[2], xs[3], t, mask[sl].cuda(),
+                                                           threshold=0.01, sparsity_weight=0.2, group=group)
+    (la[0] + lt[0]).backward()
+    losses = torch.stack([x.detach() for x in list(la) + list(lt)]).cpu().numpy()
+    return losses, [x.grad.float().cpu().numpy() for x in xs], float(t.grad)
+
+
+def test_global_negatives_pair_launch_two_ranks_match_single_process():
+    """Mode G with the tri-modal step's pair launch (keys of both heads all-gathered before the one
+    launch, each head's clip rows gathered after it): 2 ranks vs the single process at B_g."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    qo = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_pair_worker, args=(r, world, port, qo)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([qo.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert not isinstance(r[1], str), r[2]
+    L, G, T = _pair_run(0, 1, None)
+    Bl = G[0].shape[0] // world
+    dt = 0.0
+    for rank, l, grads, gt in res:
+        np.testing.assert_allclose(l, L, rtol=1e-5, atol=1e-6)
+        for got, ref in zip(grads, G):
+            ref = ref[rank * Bl:(rank + 1) * Bl]
+            np.testing.assert_allclose(got, ref, rtol=0, atol=2e-2 * np.abs(ref).max())
+        dt += gt
+    assert abs(dt - T) <= 1e-3 * abs(T) + 1e-6
+
+
 # ---- Mode R: TriadTrainer itself at world size 2 ---------------------------------------
 def _mode_r_model():
     """ViT-S/14-reg + HuBERT-base + DistilBERT (c1-sized backbones), every dropout / LayerDrop /
