@@ -387,3 +387,26 @@ def test_gemm_wide_bf16_nontemporal(bk):
     finally:
         call("triad_gemm_set_form", 0)
     assert float((C.float().cpu() - ref).norm() / ref.norm()) < 4e-3
+
+
+def test_pair_launch_eval_mode_matches_two_heads():
+    """Validation / inference (no gradient): the pair launch's eval instantiation (no dS stream)
+    gives the same losses, statistics and clip matrices as the two single-head launches."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(77)
+    B, Na, Nt, Nv = 8, 99, 20, 150
+    A, T = _rand_feats(g, (B, Na, 512)), _rand_feats(g, (B, Nt, 512))
+    Va, Vt = _rand_feats(g, (B, Nv, 512)), _rand_feats(g, (B, Nv - 7, 512))
+    mask = (torch.arange(Nt)[None, :] < torch.randint(1, Nt + 1, (B, 1), generator=g)).long().to(dev)
+    xs = [x.to(dev, torch.bfloat16) for x in (A, Va, T, Vt)]
+    t = torch.tensor(1.3, device=dev)
+    with torch.no_grad():
+        (la, sa, ca), (lt, st, ct) = ops.contrastive_heads_av_tv(xs[0], xs[1], xs[2], xs[3], t, mask, threshold=0.01,
+                                                                 sparsity_weight=0.2)
+        la2, sa2, ca2 = ops.contrastive_head(ops.AV, xs[0], xs[1], t)
+        lt2, st2, ct2 = ops.contrastive_head(ops.TV, xs[2], xs[3], t, q_mask=mask, threshold=0.01, sparsity_weight=0.2)
+    for x, y in [(torch.stack(la), torch.stack(la2)), (torch.stack(lt), torch.stack(lt2)), (sa, sa2), (st, st2),
+                 (ca, ca2), (ct, ct2)]:
+        assert torch.equal(x, y)
+    total = ref_cpu.av_loss(A.double(), Va.double(), torch.tensor(1.3, dtype=torch.float64))[0]
+    assert _scalar_close(float(la[0]), float(total))
