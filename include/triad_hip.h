@@ -158,21 +158,19 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
                            int M, int N, int Kd, int splits, const float* alpha, float* slabs, void* C,
                            int out_bf16, hipStream_t stream);
 
-/* triad_gemm_bf16_splitk in an explicit tile form (1-4 as triad_gemm_set_form; 0 = the size
+/* triad_gemm_bf16_splitk in an explicit tile form (1-4 as triad_gemm_bf16_form; 0 = the size
  * policy): the backbone weight gradients at >= 32,768 tokens run the eight-wave 256 x 256 form
  * with their own split counts (triad_amd/linear.py). */
 int triad_gemm_bf16_splitk_form(const void* A, long long lda, int a_kcontig, const void* B, long long ldb,
                                 int b_kcontig, int M, int N, int Kd, int splits, const float* alpha, float* slabs,
                                 void* C, int out_bf16, int form, hipStream_t stream);
 
-/* Select the form the two GEMM entry points above use from now on (process-wide tuning / test
- * knob): 0 = size policy (default), 1 = 128 x 128 tiles, 2 = 256 x 128 LDS ring, 3 = 256 x 256
- * four-wave tiles, 4 = 256 x 256 eight-wave tiles (3 / 4: M, N multiples of 256). */
-int triad_gemm_set_form(int form);
-
-/* The 256 x 256 form the size policy uses for tall outputs: 4 = eight-wave (default), 3 = four-wave
- * (A/B knob; triad_amd/gemm.py sets it from TRIAD_GEMM_BIG_FORM). */
-int triad_gemm_set_big_form(int form);
+/* triad_gemm_bf16 in an explicit tile form, a per-call argument (there is no process-wide GEMM
+ * state): 0 = size policy (what triad_gemm_bf16 uses), 1 = 128 x 128 tiles, 2 = 256 x 128 LDS ring,
+ * 3 = 256 x 256 four-wave tiles, 4 = 256 x 256 eight-wave tiles (3 / 4: M, N multiples of 256). */
+int triad_gemm_bf16_form(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                         int M, int N, int Kd, const float* alpha, void* C, long long ldc, int out_bf16, int form,
+                         hipStream_t stream);
 
 /* Fused projection head forward (model.py:32-34,68 / 81-83,116 / 253-255,326 under bf16
  * autocast): y = bf16(LN(bf16(h W1^T + b1)) W2^T + b2) for M rows of H features (H % 32 == 0);

@@ -9,5 +9,8 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
+    # the host application's explicit BLAS opt-in (triad_amd/blas.py), before any GEMM runs
+    from triad_amd import blas
+    blas.configure()
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
     config.addinivalue_line("markers", "slow: long-running CPU test")

@@ -182,7 +182,7 @@ def _reducer_worker(rank, world, port, wire, q, skip=False):
             ((net(x, skip_w2=skip and rank == 1 and step == 1) - y) ** 2).mean().backward()
             launched = red.launched_in_backward
             red.finish()
-            out.append((space.flat_g.numpy().copy(), launched, list(red.order)))
+            out.append((space.flat_g.numpy().copy(), launched, list(red.order), space.touched.copy()))
         q.put((rank, out, len(red.buckets)))
     except Exception:
         import traceback
@@ -233,7 +233,11 @@ def test_overlapped_bucket_reducer_averages_gradients(wire, skip):
             net.w2.grad = None
             acc += space.flat_g / world
         for rank in range(world):
-            got, launched, order = res[rank][1][step]
+            got, launched, order, touched = res[rank][1][step]
+            # every parameter of every reduced bucket counts as having a gradient on EVERY rank
+            # (the optimizer then steps, counts and clips the same set everywhere), including the
+            # one rank 1 did not produce in the skip step
+            assert touched.all(), (step, rank, touched)
             err = float((torch.from_numpy(got) - acc).abs().max() / acc.abs().max())
             assert err < tol, (wire, step, rank, err)
             assert sorted(order) == list(range(nb))

@@ -196,12 +196,11 @@ def test_memory_bounded_recompute_backward(kind, B, Nq, Nv):
 @pytest.mark.parametrize("form", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("kcontig,bk", [(1, 0), (0, 0), (1, 1), (0, 1)])
 def test_gemm_layouts_vs_torch(kcontig, bk, form):
-    """triad_gemm_bf16 in each tile form (triad_gemm_set_form: size policy, 128 x 128, 256 x 128
-    ring, 256 x 256 four-wave) against a plain fp32 torch matmul of the same bf16 operands."""
+    """triad_gemm_bf16_form in each tile form (per-call argument: size policy, 128 x 128, 256 x 128
+    ring, 256 x 256 four-wave / eight-wave) against a plain fp32 torch matmul of the same bf16 operands."""
     from triad_amd._lib import call, ptr, stream_ptr
     g = torch.Generator().manual_seed(7)
     M, N, K = 512, 768, 384
-    call("triad_gemm_set_form", form)
     A = torch.randn(M, K, generator=g).to(torch.bfloat16)
     B = torch.randn(K, N, generator=g).to(torch.bfloat16)
     ref = 0.7 * (A.float() @ B.float())
@@ -209,11 +208,9 @@ def test_gemm_layouts_vs_torch(kcontig, bk, form):
     Bd = (B.t().contiguous() if bk else B).to(dev)
     alpha = torch.tensor([0.7], device=dev)
     C = torch.empty(M, N, device=dev)
-    call("triad_gemm_bf16", ptr(Ad), K if kcontig else M, kcontig, ptr(Bd), K if bk else N, bk, M, N, K, ptr(alpha),
-         ptr(C), N, 0,
-         stream_ptr())
+    call("triad_gemm_bf16_form", ptr(Ad), K if kcontig else M, kcontig, ptr(Bd), K if bk else N, bk, M, N, K,
+         ptr(alpha), ptr(C), N, 0, form, stream_ptr())
     torch.cuda.synchronize()
-    call("triad_gemm_set_form", 0)
     np.testing.assert_allclose(C.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-3)
 
 
@@ -380,12 +377,9 @@ def test_gemm_wide_bf16_nontemporal(bk):
     Ad = A.to(dev)
     Bd = (B.t().contiguous() if bk else B).to(dev)
     C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    call("triad_gemm_set_form", 4)
-    try:
-        call("triad_gemm_bf16", ptr(Ad), K, 1, ptr(Bd), K if bk else N, bk, M, N, K, None, ptr(C), N, 1, stream_ptr())
-        torch.cuda.synchronize()
-    finally:
-        call("triad_gemm_set_form", 0)
+    call("triad_gemm_bf16_form", ptr(Ad), K, 1, ptr(Bd), K if bk else N, bk, M, N, K, None, ptr(C), N, 1, 4,
+         stream_ptr())
+    torch.cuda.synchronize()
     assert float((C.float().cpu() - ref).norm() / ref.norm()) < 4e-3
 
 

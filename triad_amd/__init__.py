@@ -7,7 +7,6 @@ HIP kernels from libtriad_hip.so.
 """
 __version__ = "0.1.0"
 
-# Library GEMMs go to rocBLAS, not hipBLASLt's stream-K kernels (triad_amd/blas.py).
-from . import blas as _blas  # noqa: E402
-
-_blas.configure()
+# Importing the package changes no process-wide state. The vendor-BLAS choice for the GEMMs torch
+# still runs (rocBLAS, not hipBLASLt's stream-K kernels) is an explicit opt-in:
+# `triad_amd.blas.configure()`, which TriadTrainer and bench.py call (triad_amd/blas.py).

@@ -56,8 +56,7 @@ SIGNATURES = {
     "triad_chgn_workspace_bytes": [i32, i32, i32],
     "triad_chgn_gelu_fwd": [vp, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp],
     "triad_chgn_gelu_bwd": [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
-    "triad_gemm_set_form": [i32],
-    "triad_gemm_set_big_form": [i32],
+    "triad_gemm_bf16_form": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, i32, i32, vp],
     "triad_conv0_dw_workspace_bytes": [i32, i32, i32],
     "triad_conv0_dw": [vp, i64, vp, i32, i32, i32, i32, vp, vp, vp],
     "triad_c0gn_fwd": [vp, i64, vp, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],

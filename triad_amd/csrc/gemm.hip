@@ -518,24 +518,19 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
     }
 }
 
-// Form override for measurement and tests (triad_gemm_set_form): 0 = the size policy in
-// launch(), 1 = 128 x 128, 2 = 256 x 128 ring, 3 = 256 x 256 four-wave, 4 = 256 x 256 eight-wave
-// (when the shape allows).
-int g_gemm_form = 0;
-// The 256 x 256 form the size policy picks: 4 = eight-wave (default since round 2: 3-13 % faster
-// than the four-wave form on every c3 backbone / projection-head shape with M >= 50,944,
-// tools/gemm_backend_probe.py, profiles/r02_gemm_w8_probe.log), 3 = four-wave. (Measured and not
-// kept: the eight-wave tile on a 4-slot ring of 32-deep chunks with the DMA three chunks ahead,
-// 5-8 % slower than this two-slot 64-deep form on every M >= 50,944 shape,
-// profiles/r02_gemm_w8_ring_probe.log: the stage's DMA latency is not what limits it.)
-int g_big_form = 4;
+// The 256 x 256 form the size policy picks for tall outputs: the eight-wave form (4), 3-13 % faster
+// than the four-wave form (3) on every c3 backbone / projection-head shape with M >= 50,944
+// (profiles/r02_gemm_w8_probe.log). (Measured and not kept: the eight-wave tile on a 4-slot ring of
+// 32-deep chunks with the DMA three chunks ahead, 5-8 % slower than this two-slot 64-deep form on
+// every M >= 50,944 shape, profiles/r02_gemm_w8_ring_probe.log.) Tile forms are per-call arguments
+// (triad_gemm_bf16_form, triad_gemm_bf16_splitk_form): there is no process-wide GEMM state.
+constexpr int kBigForm = 4;
 
 
 template <bool AK, bool BK_, typename OutT>
 int launch(const void* A, long long lda, const void* B, long long ldb, int M, int N, int Kd, const float* alpha,
            void* C, long long ldc, hipStream_t st, int splits = 1, long long slab_stride = 0,
-           const float* bias = nullptr, int form = -1) {
-  if (form < 0) form = g_gemm_form;
+           const float* bias = nullptr, int form = 0) {
   if (M % BM || N % BN || Kd % BK || lda % 8 || ldb % 8 || splits < 1) return TRIAD_EINVAL;
   const int kps = ((Kd / BK + splits - 1) / splits) * BK;
   // the 256-row ring pays off on long k loops or many row tiles (conv / projection GEMMs);
@@ -545,7 +540,7 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
   // 2.94 -> 2.67 ms at M = 1.6 M, N = 512, K = 1536); the split-K weight gradients and the
   // shorter forward shapes keep the smaller tiles
   const bool w4_auto = AK && BK_ && splits == 1 && M >= 65536 && Kd >= 1024;
-  if (form == 0 && w4_ok && w4_auto) form = g_big_form;
+  if (form == 0 && w4_ok && w4_auto) form = kBigForm;
   if (w4_ok && form == 4) {
     const int nwg = (M / GW_M) * (N / GW_N);
     hipLaunchKernelGGL((gemm_w8_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
@@ -581,19 +576,28 @@ extern "C" {
 
 // C[M][N] = alpha * op(A) . op(B). a_kcontig=1: A stored [M][Kd] (lda), 0: [Kd][M].
 // b_kcontig=1: B stored [N][Kd] (ldb), 0: [Kd][N]. out_bf16 selects a bf16 or fp32 C.
-int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
-                    int M, int N, int Kd, const float* alpha, void* C, long long ldc, int out_bf16,
-                    hipStream_t stream) {
+// form: 0 = the size policy of launch(), 1 = 128 x 128, 2 = 256 x 128 ring, 3 = 256 x 256 four-wave,
+// 4 = 256 x 256 eight-wave (3 / 4 when M, N are multiples of 256; otherwise the policy's fallback).
+int triad_gemm_bf16_form(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                         int M, int N, int Kd, const float* alpha, void* C, long long ldc, int out_bf16, int form,
+                         hipStream_t stream) {
+  if (form < 0 || form > 4) return TRIAD_EINVAL;
 #define TRIAD_GEMM_CASE(AK, BKC)                                                                  \
   if (!!a_kcontig == AK && !!b_kcontig == BKC)                                                   \
-    return out_bf16 ? launch<AK, BKC, bf16>(A, lda, B, ldb, M, N, Kd, alpha, C, ldc, stream)     \
-                    : launch<AK, BKC, float>(A, lda, B, ldb, M, N, Kd, alpha, C, ldc, stream);
+    return out_bf16 ? launch<AK, BKC, bf16>(A, lda, B, ldb, M, N, Kd, alpha, C, ldc, stream, 1, 0, nullptr, form) \
+                    : launch<AK, BKC, float>(A, lda, B, ldb, M, N, Kd, alpha, C, ldc, stream, 1, 0, nullptr, form);
   TRIAD_GEMM_CASE(true, true)
   TRIAD_GEMM_CASE(true, false)
   TRIAD_GEMM_CASE(false, true)
   TRIAD_GEMM_CASE(false, false)
 #undef TRIAD_GEMM_CASE
   return TRIAD_EINVAL;
+}
+
+int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                    int M, int N, int Kd, const float* alpha, void* C, long long ldc, int out_bf16,
+                    hipStream_t stream) {
+  return triad_gemm_bf16_form(A, lda, a_kcontig, B, ldb, b_kcontig, M, N, Kd, alpha, C, ldc, out_bf16, 0, stream);
 }
 
 // The backbone projections (torch's F.linear / matmul under autocast, routed here by
@@ -605,12 +609,9 @@ int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, 
 // at 300-790.
 int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
                          int M, int N, int Kd, const float* bias, void* C, long long ldc, hipStream_t stream) {
-  // eight-wave 256 x 256 for every tall output it tiles (the four-wave form, g_big_form = 3, only
-  // where it measured faster than the 256 x 128 ring: N * Kd >= 768 * 2304)
+  // eight-wave 256 x 256 for every tall output it tiles
   int form = 1;
-  if (M >= 32768 && M % GW_M == 0 && N % GW_N == 0 &&
-      (g_big_form != 3 || (long long)N * Kd >= 768LL * 2304))
-    form = g_big_form;
+  if (M >= 32768 && M % GW_M == 0 && N % GW_N == 0) form = kBigForm;
   else if (M >= 8192 && M % GB_M == 0) form = 2;
 #define TRIAD_GEMM_B(AK, BKC)                                                                     \
   if (!!a_kcontig == AK && !!b_kcontig == BKC)                                                    \
@@ -634,8 +635,7 @@ int triad_gemm_bf16_splitk_form(const void* A, long long lda, int a_kcontig, con
   int rc = TRIAD_EINVAL;
 #define TRIAD_GEMM_SK(AK, BKC)                                                                  \
   if (!!a_kcontig == AK && !!b_kcontig == BKC)                                                 \
-    rc = launch<AK, BKC, float>(A, lda, B, ldb, M, N, Kd, nullptr, slabs, N, stream, splits, slab, nullptr, \
-                                form ? form : g_gemm_form);
+    rc = launch<AK, BKC, float>(A, lda, B, ldb, M, N, Kd, nullptr, slabs, N, stream, splits, slab, nullptr, form);
   TRIAD_GEMM_SK(true, true)
   TRIAD_GEMM_SK(true, false)
   TRIAD_GEMM_SK(false, true)
@@ -650,20 +650,6 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
                            int out_bf16, hipStream_t stream) {
   return triad_gemm_bf16_splitk_form(A, lda, a_kcontig, B, ldb, b_kcontig, M, N, Kd, splits, alpha, slabs, C,
                                      out_bf16, 0, stream);
-}
-
-// Select the GEMM form for later calls (0 = size policy, 1 = 128 x 128, 2 = 256 x 128 ring,
-// 3 = 256 x 256 four-wave, 4 = 256 x 256 eight-wave). Process-wide tuning / test knob.
-int triad_gemm_set_big_form(int form) {
-  if (form != 3 && form != 4) return TRIAD_EINVAL;
-  g_big_form = form;
-  return TRIAD_OK;
-}
-
-int triad_gemm_set_form(int form) {
-  if (form < 0 || form > 4) return TRIAD_EINVAL;
-  g_gemm_form = form;
-  return TRIAD_OK;
 }
 
 }  // extern "C"

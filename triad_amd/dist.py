@@ -212,6 +212,20 @@ class GradBucketReducer:
             if in_backward:
                 self.launched_in_backward += 1
 
+    def _mark_touched(self, b):
+        """After the reduction every trainable parameter of the bucket holds the same (possibly
+        zero) averaged gradient on every rank, whether or not THIS rank's backward produced one
+        (HuBERT LayerDrop draws differ per rank). So all of them count as having a gradient --
+        the optimizer steps them, advances their AdamW step count and includes them in the group
+        norms / clip factors -- identically on every rank, as DDP's reduced buckets do. Without
+        this a rank whose backward skipped a layer would skip that layer's update and the
+        replicas would drift apart."""
+        s, e = self.buckets[b]
+        sp = self.space
+        for i in range(s, e):
+            if sp.params[i].requires_grad:
+                sp.touched[i] = True
+
     def _range(self, b):
         s, e = self.buckets[b]
         sp = self.space
@@ -222,6 +236,7 @@ class GradBucketReducer:
         if self.expected[b] == 0:       # every parameter frozen (identically on all ranks): nothing to reduce
             self.works[b] = None
             return
+        self._mark_touched(b)
         g = self._range(b)
         scale = 1.0 / self.world if self.average else 1.0
         if not self.cuda:

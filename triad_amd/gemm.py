@@ -12,21 +12,6 @@ import torch.nn.functional as F
 from ._lib import call, ptr, stream_ptr
 
 _BF = torch.bfloat16
-_BIG_FORM_SET = False
-
-
-def _big_form():
-    """A/B knob: TRIAD_GEMM_BIG_FORM=3 makes the size policy use the four-wave 256 x 256 form
-    instead of the eight-wave one (gemm.hip g_big_form); applied once per process."""
-    global _BIG_FORM_SET
-    if not _BIG_FORM_SET:
-        import os
-        f = os.environ.get("TRIAD_GEMM_BIG_FORM")
-        if f:
-            call("triad_gemm_set_big_form", int(f))
-        _BIG_FORM_SET = True
-
-
 def _ok(M, N, K):
     return M > 0 and M % 128 == 0 and N % 128 == 0 and K % 64 == 0
 
@@ -48,7 +33,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, meta
     M = x2.shape[0]
     if not (x2.is_cuda and _ok(M, N, K)):
         return F.linear(xb, wb, None if b is None else b.to(_BF))
-    _big_form()
     wc = wb if wb.is_contiguous() else wb.contiguous()
     bias = None if b is None else b.detach().to(_BF).to(torch.float32).contiguous()
     out = torch.empty(M, N, dtype=_BF, device=x2.device)
@@ -65,7 +49,6 @@ def mm(a: torch.Tensor, b: torch.Tensor, meta=None) -> torch.Tensor:
     N = bb.shape[1]
     if not (ab.is_cuda and _ok(M, N, K)):
         return ab @ bb
-    _big_form()
     a2 = ab if ab.is_contiguous() else ab.contiguous()
     b2 = bb if bb.is_contiguous() else bb.contiguous()
     out = torch.empty(M, N, dtype=_BF, device=a2.device)

@@ -76,9 +76,9 @@ class TriadTrainer:
                  overlap_grad_reduce=True, grad_wire="fp32"):
         self.model = model
         self.device = torch.device(device)
-        if self.device.type == "cuda":  # committed library-GEMM solution choices (gemm_tuning.py)
-            from .gemm_tuning import load_gemm_tuning
-            load_gemm_tuning(self.device)
+        if self.device.type == "cuda":  # library GEMMs on rocBLAS, not hipBLASLt (explicit opt-in, blas.py)
+            from . import blas
+            blas.configure()
         self.grad_accum = gradient_accumulation_steps
         self.unfreeze = dict(audio=unfreeze_audio_step, text=unfreeze_text_step, vit=unfreeze_vit_step)
         self.av_weight_start, self.av_weight_end = av_weight_start, av_weight_end
@@ -116,8 +116,15 @@ class TriadTrainer:
         # data parallel: bucketed gradient all-reduce overlapped with backward (fused optimizer)
         self.reducer = None
         if self.world > 1 and self.space is not None and overlap_grad_reduce:
+            # its own communicator: the bucket all-reduces are issued from gradient hooks during
+            # backward, while Mode G's head issues its reduce-scatter / all-gathers inside the same
+            # backward on the model's group -- on separate communicators the two sequences can
+            # never interleave differently on different ranks
+            ranks = (dist.get_process_group_ranks(process_group) if process_group is not None
+                     else list(range(self.world)))
+            self.reducer_group = dist.new_group(ranks=ranks)
             self.reducer = tdist.GradBucketReducer(self.space, bucket_mb, grad_wire,
-                                                   average=not self.global_negatives, group=process_group)
+                                                   average=not self.global_negatives, group=self.reducer_group)
         self.total_updates = total_updates
         self.sched_others = _one_cycle(self.opt_others, learning_rate, total_updates)
         self.sched_audio = _one_cycle(self.opt_audio, learning_rate * 0.25, total_updates - unfreeze_audio_step)
@@ -163,6 +170,11 @@ class TriadTrainer:
                     tdist.allreduce_grads(p.grad.view(-1), p.grad.numel(), avg, self.pg)
             return
         tdist.allreduce_grads(self.space.flat_g, self.bucket_elems, avg, self.pg)
+        # every trainable parameter now holds the same reduced gradient on every rank (see
+        # GradBucketReducer._mark_touched): step all of them, identically everywhere
+        for i, p in enumerate(self.space.params):
+            if p.requires_grad:
+                self.space.touched[i] = True
 
     def step(self, frames, audio, text, phase="full_joint", progress=0.0, av_keep=None, tv_keep=None,
              shared_frames=True, frames_tv=None):
