@@ -327,6 +327,48 @@ def head_loss_chunked(kind, q, k, temperature, q_mask=None, threshold=0.8, weigh
     return out
 
 
+def near_ties(q, k, temperature, rel=8 * 2.0 ** -23, chunk=8, dtype=torch.float64):
+    """Where a row max of S = temp * q k^T is decided below fp32 resolution.
+
+    For every (query sample i, key sample j, query token r) the gap between the largest and the
+    second-largest S[i, j, r, :] is computed in `dtype`; a gap <= rel * |max| (8 fp32 ulps of the
+    max by default) is a near-tie: an fp32 evaluation with another summation order (the MFMA
+    kernels) may pick the other key, which moves that row's max gradient (model.py:389 / 507) from
+    one key to the other -- both answers are the reference's at fp32 precision. Returns
+    (tie_q (Bq, Nq) bool: query rows with a near-tie against any key sample, tie_k (Bk, Nk) bool:
+    keys that are the first or second candidate of one, number of near-tie rows)."""
+    Bq, Nq, _ = q.shape
+    Bk, Nk, _ = k.shape
+    Qd, Kd = q.detach().to(dtype), k.detach().to(dtype)
+    t = torch.as_tensor(temperature, dtype=dtype, device=q.device)
+    tie_q = torch.zeros(Bq, Nq, dtype=torch.bool, device=q.device)
+    tie_k = torch.zeros(Bk, Nk, dtype=torch.bool, device=q.device)
+    n = 0
+    if Nk < 2:
+        return tie_q, tie_k, 0
+    with torch.no_grad():
+        for i0 in range(0, Bq, chunk):
+            s = torch.einsum("iqd,jkd->ijqk", Qd[i0:i0 + chunk], Kd) * t
+            v, ix = s.topk(2, dim=3)
+            near = (v[..., 0] - v[..., 1]) <= rel * v[..., 0].abs()     # (c, Bk, Nq)
+            n += int(near.sum())
+            tie_q[i0:i0 + chunk] |= near.any(dim=1)
+            jj = torch.arange(Bk, device=q.device)[None, :, None].expand_as(near)
+            for c in (0, 1):
+                tie_k[jj[near], ix[..., c][near]] = True
+    return tie_q, tie_k, n
+
+
+def grad_rel(got, ref, skip_rows=None):
+    """Relative L2 error of a (B, N, D) gradient, rows flagged in skip_rows (B, N) left out."""
+    g = got.detach().double().reshape(-1, got.shape[-1])
+    r = ref.detach().double().to(g.device).reshape(-1, ref.shape[-1])
+    if skip_rows is not None:
+        keep = ~skip_rows.reshape(-1).to(g.device)
+        g, r = g[keep], r[keep]
+    return float((g - r).norm() / r.norm().clamp(min=1e-30))
+
+
 def _symmetric_ce_dev(clip):
     """_symmetric_ce on any device."""
     n = clip.shape[0]

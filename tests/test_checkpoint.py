@@ -189,3 +189,60 @@ def test_state_load_refreshes_positional_embedding_cache():
         y2 = fresh.get_intermediate_layers(x, n=1)[0]
     assert not torch.equal(y0, y1)
     assert torch.equal(y1, y2)
+
+
+class _MaskOwner:
+    """The patch-mask generator interface of ViTLoRAEmbedder (mask_generator), without a ViT."""
+
+    def __init__(self, seed):
+        self.gen = torch.Generator()
+        self.gen.manual_seed(seed)
+
+    def mask_generator(self):
+        return self.gen
+
+
+def _mask_ckpt_worker(rank, world, port, q):
+    import os
+    import types
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from triad_amd import checkpoint as ck
+        tr = types.SimpleNamespace(world=world, pg=None, global_negatives=False)
+        ve = _MaskOwner(100 + rank)
+        torch.rand(5, generator=ve.gen)                       # some draws before the save
+        saved = ck._mask_generator_state(tr, ve)              # collective
+        want = torch.rand(8, generator=ve.gen)                # what an uninterrupted run draws next
+        fresh = _MaskOwner(0)
+        ck._restore_mask_generator(tr, fresh, saved)
+        got = torch.rand(8, generator=fresh.gen)
+        single = _MaskOwner(0)                                # an old single-state checkpoint
+        ck._restore_mask_generator(tr, single, saved[0])
+        q.put((rank, len(saved), bool(torch.equal(got, want)), torch.rand(8, generator=single.gen).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_patch_mask_generator_state_per_rank():
+    """a Mode R checkpoint keeps every rank's patch-mask generator (gathered, indexed by
+    rank) and each rank resumes its own sequence; a single saved state restored on several ranks
+    re-mixes the rank in, so replicas never draw identical masks."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_mask_ckpt_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=30)
+    (_, n0, ok0, s0), (_, n1, ok1, s1) = res
+    assert n0 == n1 == 2 and ok0 and ok1
+    assert s0 != s1

@@ -17,8 +17,8 @@ outputs).
 Tolerances (north star): losses / clip / statistics 1e-4 relative (the kernels do exact fp32
 arithmetic on the bf16 features; the oracle is fp64 on the same values); feature gradients the
 bf16 bar, relative L2 < 1e-2 (dS is a bf16 MFMA operand; measured 1.8e-3 - 3.0e-3 at every
-configuration, profiles/r02_config_grad_errors.log); d/dtemp 1e-3 relative. Inputs are seeded,
-SpecAugment's numpy draws included.
+configuration, profiles/r02_config_grad_errors.log) over the rows no fp32 near-tie of a row max
+touches (oracle.ref_cpu.near_ties; those rows are counted, < 3 %); d/dtemp 1e-3 relative.
 """
 import math
 
@@ -77,6 +77,22 @@ class Capture:
         self.t, self.mask = out
 
 
+def _check_feature_grads(kind, q, k, temp, o, grad_bar, mask=None):
+    """Feature gradients at the bf16 bar, with the rows an fp32 near-tie of a row max touches left
+    out (oracle.ref_cpu.near_ties: there the kernels may legitimately take the other key's
+    gradient); the near-tied rows are counted and must stay a small minority. No seed picking: any
+    input passes or fails on the same rule."""
+    tq, tk, n = ref_cpu.near_ties(q.detach().float(), k.detach().float(), float(temp.detach()))
+    eq = ref_cpu.grad_rel(q.grad, o["dq"], tq)
+    ek = ref_cpu.grad_rel(k.grad, o["dk"], tk)
+    _log(f"{kind} feature-gradient relative L2 (near-tie rows excluded: {int(tq.sum())} query / {int(tk.sum())} "
+         f"key rows, {n} tied row maxima): dq {eq:.3e}  dk {ek:.3e}; all rows dq {_rel(q.grad, o['dq']):.3e} "
+         f"dk {_rel(k.grad, o['dk']):.3e}")
+    assert float(tq.float().mean()) < 0.03 and float(tk.float().mean()) < 0.03, (int(tq.sum()), int(tk.sum()))
+    assert eq < grad_bar, eq
+    assert ek < grad_bar, ek
+
+
 def _check_head(kind, losses, stats, q, k, temp, temp_grad, mask=None, thr=0.8, w=0.01, grad_bar=1e-2):
     o = ref_cpu.head_loss_chunked(kind, q.detach().float(), k.detach().float(), float(temp.detach()), q_mask=mask,
                                   threshold=thr, weight=w, chunk=8)
@@ -85,9 +101,7 @@ def _check_head(kind, losses, stats, q, k, temp, temp_grad, mask=None, thr=0.8, 
         assert _close(float(got), o[key]), (kind, key, float(got), o[key])
     for key, want in o["stats"].items():
         assert _close(stats[key], want, 1e-4, 1e-4), (key, stats[key], want)
-    _log(f"{kind} feature-gradient relative L2: dq {_rel(q.grad, o['dq']):.3e}  dk {_rel(k.grad, o['dk']):.3e}")
-    assert _rel(q.grad, o["dq"]) < grad_bar, _rel(q.grad, o["dq"])
-    assert _rel(k.grad, o["dk"]) < grad_bar, _rel(k.grad, o["dk"])
+    _check_feature_grads(kind, q, k, temp, o, grad_bar, mask)
     if temp_grad is not None:
         return o["dtemp"]
     return None
@@ -121,8 +135,9 @@ def base_model():
     return _model()
 
 
-def _triad_step_check(m, B, px, secs, ntok, grad_bar=1e-2):
-    np.random.seed(0)  # HuBERT's SpecAugment masks are drawn from numpy (transformers)
+def _triad_step_check(m, B, px, secs, ntok, grad_bar=1e-2, np_seed=0):
+    if np_seed is not None:
+        np.random.seed(np_seed)  # HuBERT's SpecAugment masks are drawn from numpy (transformers)
     cap = Capture(m)
     frames, audio, text = _inputs(B, px, secs, ntok)
     (av_total, av_ce, av_reg, av_sm, av_st), (tv_total, tv_st) = m.forward_triad(frames, audio, text)
@@ -140,9 +155,7 @@ def _triad_step_check(m, B, px, secs, ntok, grad_bar=1e-2):
     assert _close(float(tv_total), o["total"]), (float(tv_total), o["total"])
     for key, want in o["stats"].items():
         assert _close(tv_st[key], want, 1e-4, 1e-4), key
-    _log(f"tv feature-gradient relative L2: dq {_rel(cap.t.grad, o['dq']):.3e}  dk {_rel(v_tv.grad, o['dk']):.3e}")
-    assert _rel(cap.t.grad, o["dq"]) < grad_bar, _rel(cap.t.grad, o["dq"])
-    assert _rel(v_tv.grad, o["dk"]) < grad_bar, _rel(v_tv.grad, o["dk"])
+    _check_feature_grads("tv", cap.t, v_tv, m.temperature, o, grad_bar)
     # the temperature gets both heads' gradients (plus nothing else)
     assert _close(float(m.temperature.grad), dt_av + o["dtemp"], 1e-3, 1e-6), \
         (float(m.temperature.grad), dt_av + o["dtemp"])
@@ -188,8 +201,7 @@ def test_c1_forward_text_visual_b2():
     assert _close(float(total), o["total"])
     for key, want in o["stats"].items():
         assert _close(st[key], want, 1e-4, 1e-4), key
-    assert _rel(cap.t.grad, o["dq"]) < 1e-2
-    assert _rel(v.grad, o["dk"]) < 1e-2
+    _check_feature_grads("tv", cap.t, v, m.temperature, o, 1e-2)
     assert _close(float(m.temperature.grad), o["dtemp"], 1e-3, 1e-6)
 
 
@@ -198,10 +210,8 @@ def test_c5_large_backbones_per_rank_b32():
     (Na = 499), DistilBERT captions, B=32, the tri-modal step."""
     m = _model(audio_model_name="facebook/hubert-large-ls960-ft", vit_arch="dinov2_vitl14_reg")
     assert m.audio_embedder.hubert.config.hidden_size == 1024 and m.visual_embedder.model.embed_dim == 1024
-    # feature gradients 1.8e-3 - 2.5e-3 from the oracle on the seeded inputs
-    # (profiles/r02_config_grad_errors.log); a run with unseeded SpecAugment draws once measured
-    # 1.012e-2 (profiles/r02_gpu_tests_c5.log) -- the signature of an fp32 near-tie of a row max
-    # moving one row's gradient to the other key (diagnosed in tests/test_head_gpu.py's pair test)
-    cap, v_av, v_tv = _triad_step_check(m, 32, 518, 10, 32)
+    # SpecAugment's numpy draws are NOT seeded here: near-tied row maxima (which once moved an
+    # unseeded run to 1.012e-2, profiles/r02_gpu_tests_c5.log) are excluded by rule, not by input
+    cap, v_av, v_tv = _triad_step_check(m, 32, 518, 10, 32, np_seed=None)
     assert cap.a.shape == (32, 499, 512)
     assert 1000 < v_av.shape[1] <= 1369

@@ -29,10 +29,25 @@ def _rel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-def _check_grad(got, ref):
+def _check_grad(got, ref, skip=None):
+    """bf16 bar on a (B, N, 512) feature gradient. skip (B, N) bool: rows whose oracle row max is a
+    near-tie (ref_cpu.near_ties) are left out -- there the fp32 kernels may legitimately take the
+    other key's gradient -- and must stay a small minority."""
     got = got.detach().float().cpu().numpy()
+    ref = np.asarray(ref)
+    if skip is not None:
+        keep = ~skip.cpu().numpy().reshape(-1)
+        assert keep.mean() > 0.97, f"{(~keep).sum()} of {keep.size} rows near-tied"
+        got = got.reshape(-1, got.shape[-1])[keep]
+        ref = ref.reshape(-1, ref.shape[-1])[keep]
     assert _rel(got, ref) < 1e-2, _rel(got, ref)
     np.testing.assert_allclose(got, ref, rtol=0, atol=3e-2 * float(np.abs(ref).max()) + 1e-12)
+
+
+def _ties(q, k, temp):
+    """(query rows, key rows) touched by an fp32 near-tie of a row max (oracle.ref_cpu.near_ties)."""
+    tq, tk, _ = ref_cpu.near_ties(q.double(), k.double(), float(temp))
+    return tq, tk
 
 
 def _scalar_close(a, b, rtol=1e-4, atol=1e-5):
@@ -115,8 +130,9 @@ def test_av_head_vs_oracle_random(B, Na, Nv, pad, mix):
     lv = torch.stack([x.detach() for x in losses]).cpu().double().numpy()
     for got, want in zip(lv, (total, ce, reg, sm)):
         assert _scalar_close(float(got), float(want)), (got, float(want))
-    _check_grad(Ag.grad, Ar.grad.numpy())
-    _check_grad(Vg.grad, Vr.grad.numpy())
+    tq, tk = _ties(A, V, temp)
+    _check_grad(Ag.grad, Ar.grad.numpy(), tq)
+    _check_grad(Vg.grad, Vr.grad.numpy(), tk)
     assert _scalar_close(float(tg.grad), float(tr.grad), 1e-3, 1e-5), (float(tg.grad), float(tr.grad))
 
 
@@ -143,8 +159,9 @@ def test_tv_head_vs_oracle_random(B, Nt, Nv, mix):
     else:
         losses[0].backward()
     assert _scalar_close(float(losses[0]), float(total))
-    _check_grad(Tg.grad, Tr.grad.numpy())
-    _check_grad(Vg.grad, Vr.grad.numpy())
+    tq, tk = _ties(T, V, temp)
+    _check_grad(Tg.grad, Tr.grad.numpy(), tq)
+    _check_grad(Vg.grad, Vr.grad.numpy(), tk)
     assert _scalar_close(float(tg.grad), float(tr.grad), 1e-3, 1e-5), (float(tg.grad), float(tr.grad))
 
 
@@ -171,6 +188,7 @@ def test_memory_bounded_recompute_backward(kind, B, Nq, Nv):
     else:
         total = ref_cpu.tv_loss(Qr, Vr, mask, tr, thr, w)[0]
     total.backward()
+    tq, tk = _ties(Q, V, temp)
     geo = ops.Geometry(B, Nq, B, ((Nv + 31) // 32) * 32)
     per_sample = (geo.R_pad // 32) * (geo.Nk_pad // 32) * 2048
     res = []
@@ -182,8 +200,8 @@ def test_memory_bounded_recompute_backward(kind, B, Nq, Nv):
         losses, st, clip = ops.contrastive_head(kind, Qg, Vg, tg, ds_budget=budget, **kw)
         losses[0].backward()
         assert _scalar_close(float(losses[0]), float(total))
-        _check_grad(Qg.grad, Qr.grad.numpy())
-        _check_grad(Vg.grad, Vr.grad.numpy())
+        _check_grad(Qg.grad, Qr.grad.numpy(), tq)
+        _check_grad(Vg.grad, Vr.grad.numpy(), tk)
         assert _scalar_close(float(tg.grad), float(tr.grad), 1e-3, 1e-5), (float(tg.grad), float(tr.grad))
         res.append((Qg.grad.float().cpu(), Vg.grad.float().cpu(), float(tg.grad)))
     assert ops.ds_chunk_samples(geo, 4 * per_sample) == (4 if B > 4 else B)
@@ -236,8 +254,9 @@ def test_tv_head_any_temperature_sign(temp):
                                             sparsity_weight=w)
     losses[0].backward()
     assert _scalar_close(float(losses[0]), float(total))
-    _check_grad(Tg.grad, Tr.grad.numpy())
-    _check_grad(Vg.grad, Vr.grad.numpy())
+    tq, tk = _ties(T, V, temp)
+    _check_grad(Tg.grad, Tr.grad.numpy(), tq)
+    _check_grad(Vg.grad, Vr.grad.numpy(), tk)
     assert _scalar_close(float(tg.grad), float(tr.grad), 1e-3, 1e-5), (float(tg.grad), float(tr.grad))
 
 
@@ -261,8 +280,9 @@ def test_av_head_below_clamp_window():
     lv = torch.stack([x.detach() for x in losses]).cpu().double().numpy()
     for got, want in zip(lv, (total, ce, reg, sm)):
         assert _scalar_close(float(got), float(want)), (got, float(want))
-    _check_grad(Ag.grad, Ar.grad.numpy())
-    _check_grad(Vg.grad, Vr.grad.numpy())
+    tq, tk = _ties(A, V, 1.5)
+    _check_grad(Ag.grad, Ar.grad.numpy(), tq)
+    _check_grad(Vg.grad, Vr.grad.numpy(), tk)
     assert _scalar_close(float(tg.grad), float(tr.grad), 1e-3, 1e-5), (float(tg.grad), float(tr.grad))
 
 
@@ -306,13 +326,13 @@ def test_pair_launch_matches_two_heads(B, Na, Nt, Nv, budget):
     """contrastive_heads_av_tv (ONE similarity-forward launch over the AV and TV heads,
     triad_pairsim_fwd_multi) against the two single-head launches on the same inputs: losses,
     statistics, clip matrices and every gradient bit-identical (each workgroup runs the same code
-    on the same tiles); and against the fp64 oracle. budget "mixed": the AV head's dS over the
-    budget, TV's within it (mixed modes -> two launches, chunked recompute backward for AV)."""
+    on the same tiles); and against the fp64 oracle. budget "mixed": one dS budget for the pair
+    (ADVICE r2), AV's dS within it, TV's over what AV leaves (mixed modes -> two launches, chunked
+    recompute backward for TV)."""
     ops = _ops()
-    # seed: no query's two best keys closer than 6.5e-5 in S (at seed 500 + B the (5, 300) case has
-    # two keys 2.8e-6 apart at S = 13.28, below fp32 resolution: the MFMA sum order picks the other
-    # one as the max and that row's gradient moves to it -- a legitimate tie flip, not an error)
-    g = torch.Generator().manual_seed(900 + B)
+    # (seed 500 + B: the (5, 300) case has two keys 2.8e-6 apart at S = 13.28, below fp32
+    # resolution -- the MFMA sum order may pick either; _check_grad leaves near-tied rows out)
+    g = torch.Generator().manual_seed(500 + B)
     A = _rand_feats(g, (B, Na, 512))
     T = _rand_feats(g, (B, Nt, 512))
     Va = _rand_feats(g, (B, Nv, 512))
@@ -328,24 +348,27 @@ def test_pair_launch_matches_two_heads(B, Na, Nt, Nv, budget):
     def leaves():
         return [x.to(dev, torch.bfloat16).requires_grad_(True) for x in (A, Va, T, Vt)]
 
-    ds_budget = None
-    if budget == "mixed":  # TV's dS fits, AV's does not: two launches, AV recomputed in chunks
+    ds_budget = bud_av = bud_tv = None
+    if budget == "mixed":
+        # ONE budget for the pair: AV's whole dS fits, TV gets what AV leaves (half its dS), so TV's
+        # backward recomputes in chunks -- mixed modes -> two forward launches
         ga = ops.Geometry(B, Na, B, Va.shape[1])
         gt = ops.Geometry(B, Nt, B, Vt.shape[1])
-        ds_budget = ops.ds_bytes(gt)
-        assert ops.ds_bytes(ga) > ds_budget and ops.ds_chunk_samples(ga, ds_budget) < B
+        ds_budget = bud_av = ops.ds_bytes(ga) + ops.ds_bytes(gt) // 2
+        bud_tv = ds_budget - ops.ds_working_bytes(ga, B)
+        assert ops.ds_chunk_samples(ga, bud_av) == B and ops.ds_bytes(gt) > bud_tv
     # pair
     a1, va1, t1, vt1 = leaves()
     tg1 = torch.tensor(1.4, device=dev, requires_grad=True)
     (la, sa, ca), (lt, st, ct) = ops.contrastive_heads_av_tv(a1, va1, t1, vt1, tg1, mask.to(dev), threshold=thr,
                                                              sparsity_weight=w, ds_budget=ds_budget)
     (la[0] + lt[0]).backward()
-    # two single heads
+    # two single heads, each with the share of the budget the pair gave it
     a2, va2, t2, vt2 = leaves()
     tg2 = torch.tensor(1.4, device=dev, requires_grad=True)
-    la2, sa2, ca2 = ops.contrastive_head(ops.AV, a2, va2, tg2, ds_budget=ds_budget)
+    la2, sa2, ca2 = ops.contrastive_head(ops.AV, a2, va2, tg2, ds_budget=bud_av)
     lt2, st2, ct2 = ops.contrastive_head(ops.TV, t2, vt2, tg2, q_mask=mask.to(dev), threshold=thr, sparsity_weight=w,
-                                         ds_budget=ds_budget)
+                                         ds_budget=bud_tv)
     (la2[0] + lt2[0]).backward()
     for x, y in [(torch.stack(la), torch.stack(la2)), (torch.stack(lt), torch.stack(lt2)), (sa, sa2), (st, st2),
                  (ca, ca2), (ct, ct2), (a1.grad, a2.grad), (va1.grad, va2.grad), (t1.grad, t2.grad),
@@ -359,8 +382,11 @@ def test_pair_launch_matches_two_heads(B, Na, Nt, Nv, budget):
     tot_t = ref_cpu.tv_loss(Tr, Vtr, mask, tr, thr, w)[0]
     (tot_a + tot_t).backward()
     assert _scalar_close(float(la[0]), float(tot_a)) and _scalar_close(float(lt[0]), float(tot_t))
-    for gg, rr in ((a1.grad, Ar.grad), (va1.grad, Var.grad), (t1.grad, Tr.grad), (vt1.grad, Vtr.grad)):
-        _check_grad(gg, rr.numpy())
+    ta, tva = _ties(A, Va, 1.4)
+    tt, tvt = _ties(T, Vt, 1.4)
+    for gg, rr, sk in ((a1.grad, Ar.grad, ta), (va1.grad, Var.grad, tva), (t1.grad, Tr.grad, tt),
+                       (vt1.grad, Vtr.grad, tvt)):
+        _check_grad(gg, rr.numpy(), sk)
     assert _scalar_close(float(tg1.grad), float(tr.grad), 1e-3, 1e-5), (float(tg1.grad), float(tr.grad))
 
 

@@ -145,3 +145,27 @@ def test_audio_znorm_oracle_matches_feature_extractor(name):
     f = G.load(name)
     y = ref_cpu.audio_znorm(torch.from_numpy(f["x"]))
     np.testing.assert_allclose(y.numpy(), f["y"], rtol=1e-5, atol=2e-5)
+
+
+def test_near_ties_flags_exact_and_close_row_maxima():
+    """oracle.ref_cpu.near_ties (the parity tests' tie rule): an exactly duplicated key and a key
+    within a few fp32 ulps of the row max are flagged -- the query row and both candidate keys --,
+    a clear winner is not, and random features leave almost every row unflagged."""
+    g = torch.Generator().manual_seed(3)
+    q = torch.randn(2, 4, 512, generator=g, dtype=torch.float64)
+    k = torch.randn(2, 6, 512, generator=g, dtype=torch.float64) * 0.01
+    k[0, 1] = q[0, 2] * 0.5                   # clear max of row (0, 2) against sample 0 ...
+    k[0, 4] = k[0, 1]                         # ... duplicated: exact tie
+    k[1, 0] = q[1, 3] * 0.5
+    k[1, 5] = k[1, 0] * (1 + 2e-7)            # 0.2 ppm apart: below 8 fp32 ulps of the max
+    tq, tk, n = ref_cpu.near_ties(q, k, 1.5)
+    assert bool(tq[0, 2]) and bool(tk[0, 1]) and bool(tk[0, 4])
+    assert bool(tq[1, 3]) and bool(tk[1, 0]) and bool(tk[1, 5])
+    assert n >= 2 and int(tk.sum()) == 4
+    k[1, 5] = k[1, 0] * (1 - 1e-3)            # a clear second: no longer a tie
+    tq2, tk2, _ = ref_cpu.near_ties(q, k, 1.5)
+    assert not bool(tk2[1, 5])
+    qr = (torch.randn(4, 50, 512, generator=g) * 0.58).double()
+    kr = (torch.randn(4, 60, 512, generator=g) * 0.58).double()
+    tq3, tk3, _ = ref_cpu.near_ties(qr, kr, 1.5)
+    assert float(tq3.float().mean()) < 0.02

@@ -1,0 +1,81 @@
+"""Projection head (reference model.py:32-34,68 / 81-83,116 / 253-255,326) at the
+row counts the training step runs, through the default "passes" form the step uses:
+
+  65,536 x 768   visual head, B=256 x 256 patches (before patch dropout)   c3
+  50,944 x 768   audio head, B=256 x 199 frames                            c3
+   8,192 x 768   text head, B=256 x 32 tokens                              c3
+  43,808 x 1024  visual head of DINOv2-L at 518 px, B=32 x 1369 patches    c5
+
+At these sizes the forward GEMMs take the eight-wave 256 x 256 tile form (M >= 32,768) or the
+256 x 128 ring, and the weight gradients the split-K GEMM with 16+ splits -- code paths the
+small-row test in test_ops_gpu.py does not reach. Forward against the oracle's bf16-autocast
+emulation (oracle.ref_cpu.projection_head(amp=True)), all seven gradients against fp64 autograd of
+the unrounded head, both evaluated on the device in row chunks (plain torch; test infrastructure).
+Bars: forward within one bf16 ulp elementwise and 4e-3 relative L2; gradients 1e-2 relative L2
+(bf16 operands, fp32 accumulation)."""
+import pytest
+import torch
+import torch.nn as nn
+
+from oracle import ref_cpu
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _rel(a, b):
+    a = a.detach().double()
+    b = b.detach().double().to(a.device)
+    return float((a - b).norm() / b.norm().clamp(min=1e-30))
+
+
+@pytest.mark.parametrize("rows,H", [(65536, 768), (50944, 768), (8192, 768), (43808, 1024)])
+def test_projection_head_at_step_rows(rows, H):
+    from triad_amd import ops
+    assert ops.PROJHEAD_FORM == "passes"
+    torch.manual_seed(rows + H)
+    p1, ln, p2 = nn.Linear(H, 512), nn.LayerNorm(512), nn.Linear(512, 512)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    mods = [m.to(dev) for m in (p1, ln, p2)]
+    g = torch.Generator(device=dev).manual_seed(rows)
+    h = torch.randn(rows, H, device=dev, generator=g)
+    gy = torch.randn(rows, 512, device=dev, generator=g) * 0.01
+    # product path
+    hd = h.clone().requires_grad_(True)
+    y = ops.projection_head(hd.view(1, rows, H), *mods)
+    assert y.dtype == torch.bfloat16 and y.shape == (1, rows, 512)
+    y.float().view(rows, 512).backward(gy)
+    got = [hd.grad] + [p.grad.detach().clone() for m in mods for p in m.parameters()]
+    # splits the weight gradients used (16+ at these row counts, one round of 256 CUs)
+    Mp = (rows + 127) // 128 * 128
+    assert ops._splitk(Mp, 16) >= 16
+    # oracle forward (bf16 autocast emulation), chunked over rows
+    w = [p.detach() for m in mods for p in m.parameters()]
+    yf = y.detach().float().view(rows, 512)
+    worst, num, den = 0.0, 0.0, 0.0
+    for r0 in range(0, rows, 16384):
+        ref = ref_cpu.projection_head(h[r0:r0 + 16384], *w, amp=True)
+        d = (yf[r0:r0 + 16384] - ref).abs()
+        worst = max(worst, float((d / (ref.abs() + 2e-2)).max()))
+        num += float((d.double() ** 2).sum())
+        den += float((ref.double() ** 2).sum())
+    assert worst < 1.6e-2, worst                      # about one bf16 ulp
+    assert (num / den) ** 0.5 < 4e-3, (num / den) ** 0.5
+    # fp64 autograd of the unrounded head (the gradients' reference), chunked over rows
+    wd = [x.double().requires_grad_(True) for x in w]
+    ref_dh = torch.empty(rows, H, dtype=torch.float64, device=dev)
+    for r0 in range(0, rows, 16384):
+        hc = h[r0:r0 + 16384].double().requires_grad_(True)
+        yc = nn.functional.linear(hc, wd[0], wd[1])
+        yc = nn.functional.layer_norm(yc, (512,), wd[2], wd[3], 1e-5)
+        yc = nn.functional.linear(yc, wd[4], wd[5])
+        yc.backward(gy[r0:r0 + 16384].double())
+        ref_dh[r0:r0 + 16384] = hc.grad
+    refs = [ref_dh] + [x.grad for x in wd]
+    names = ["dh", "dW1", "db1", "dgamma", "dbeta", "dW2", "db2"]
+    errs = {n: _rel(a, b) for n, a, b in zip(names, got, refs)}
+    print(f"projection head {rows} x {H}: gradient relative L2 {errs}")
+    for n, e in errs.items():
+        assert e < 1e-2, (n, e)

@@ -85,8 +85,63 @@ def feature_encoder_case(B):
     return fn
 
 
+def model_noise(which):
+    """The tri-modal step's other streams as the noise: the DINOv2-B (+LoRA) patch encoder on the
+    current stream and / or DistilBERT on a third stream (forward under autocast, train mode)."""
+    from triad_amd.model import MultiModalModel
+    torch.manual_seed(0)
+    m = MultiModalModel(temperature=1.5, visual_dropout_prob=0.25).to(dev).train()
+    frames = torch.randn(128, 3, 224, 224, device=dev)
+    ids = torch.randint(1000, 30522, (128, 32))
+    text = {"input_ids": ids, "attention_mask": torch.ones(128, 32, dtype=torch.long)}
+    s_text = torch.cuda.Stream(device=dev)
+
+    def run():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if "text" in which:
+                s_text.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(s_text):
+                    m.text_embedder(text)
+            if "vit" in which:
+                m.visual_embedder.encode_patches(frames)
+            if "text" in which:
+                torch.cuda.current_stream(dev).wait_stream(s_text)
+    return m, run
+
+
+def audio_case(m, B):
+    x = torch.randn(B, 16000, device=dev) * 0.1
+
+    def fn():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            return m.audio_embedder(x).detach().contiguous()
+    return fn
+
+
+def feature_case(m, B):
+    x = torch.randn(B, 16000, device=dev) * 0.1
+    fe = m.audio_embedder.hubert.feature_extractor
+
+    def fn():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            return fe(m.audio_embedder.normalize(x)).detach().contiguous()
+    return fn
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "model":
+        # victim: HuBERT (feature encoder / whole audio embedder, autograd recording as in training)
+        # beside the real ViT / DistilBERT forwards
+        tot = 0
+        for which in ("vit+text", "vit", "text"):
+            m, noise = model_noise(which)
+            tot += check(f"feature encoder beside {which}", feature_case(m, 128), noise)
+            tot += check(f"audio embedder beside {which}", audio_case(m, 128), noise)
+            del m
+            torch.cuda.empty_cache()
+        print("total mismatching runs", tot)
+        sys.exit(0)
     noise = noise_fn()
     # feature encoder layer 1 at B = 128 x 1 s: frames Tp = 3200 -> M = 204,800 pair rows, K = 3 x 512
     M, C = 204800, 512

@@ -152,6 +152,8 @@ def _check_fresh():
 # Enabled by bench.py over its timed region; events are recorded on the current HIP stream,
 # which is the stream every entry point is launched on.
 TIMERS = None
+# Step watchdog (triad_amd.watchdog, armed by bench.py): notes each entry point launched per stream.
+WATCH = None
 
 
 def call(name, *args, meta=None):
@@ -166,6 +168,8 @@ def call(name, *args, meta=None):
         TIMERS[name].append((e0, e1, meta))
     else:
         rc = getattr(load(), name)(*args)
+    if WATCH is not None and name not in RESTYPES:
+        WATCH.note(name)   # event after the launch: completed <=> this entry point's kernels are done
     if name not in RESTYPES and rc != 0:
         what = "invalid argument/shape" if rc == 1001 else f"hipError_t {rc}"
         raise TriadError(f"{name} failed: {what}")

@@ -123,10 +123,10 @@ def trainer_checkpoint(trainer, epoch: int, step: int, best_loss: float = float(
                  "cuda": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else [],
                  "numpy": np.random.get_state(), "python": random.getstate()}
     ve = getattr(trainer.model, "visual_embedder", None)
-    if ve is not None and hasattr(ve, "_mask_gen"):
-        # extra key (the reference ignores it): the host generator of the patch-dropout masks,
-        # so a resumed run draws the masks an uninterrupted one would
-        rng_state["triad_patch_mask"] = ve._mask_gen.get_state()
+    if ve is not None and hasattr(ve, "mask_generator"):
+        # extra key (the reference ignores it): the host generator of the patch-dropout masks, so a
+        # resumed run draws the masks an uninterrupted one would
+        rng_state["triad_patch_mask"] = _mask_generator_state(trainer, ve)
     ck = {"epoch": epoch, "step": step, "current_batch_idx": current_batch_idx, "current_segment": current_segment,
           "rng_state": rng_state, "model_state_dict": reference_state_dict(trainer.model, trainer.space)}
     for n in _OPTS:
@@ -137,6 +137,41 @@ def trainer_checkpoint(trainer, epoch: int, step: int, best_loss: float = float(
         ck[f"sched_step_{n}"] = getattr(trainer, f"step_{n}")
     ck.update(best_loss=best_loss, config=config or {}, vis_samples_av=vis_samples_av, vis_samples_tv=vis_samples_tv)
     return ck
+
+
+def _mask_generator_state(trainer, ve):
+    """Data parallel (Mode R): every rank's own state, gathered into a list indexed by rank (a
+    collective: every rank calls this when saving); one process or Mode G (ranks share one state):
+    the state itself."""
+    st = ve.mask_generator().get_state()
+    world = getattr(trainer, "world", 1)
+    if world > 1 and not getattr(trainer, "global_negatives", False):
+        import torch.distributed as dist
+        states = [None] * world
+        dist.all_gather_object(states, st, group=getattr(trainer, "pg", None))
+        return [torch.as_tensor(x) for x in states]
+    return st
+
+
+def _restore_mask_generator(trainer, ve, saved):
+    """Per-rank patch-mask generator state: a list (one state per rank) restores this rank's; a
+    single state (a one-process checkpoint, or Mode G's shared state) restores it, and in Mode R
+    with several ranks then re-mixes the rank in -- from a seed drawn from the restored state, so
+    the result is reproducible -- instead of letting every replica draw the same masks."""
+    import torch.distributed as dist
+    gen = ve.mask_generator()
+    world = getattr(trainer, "world", 1)
+    rank = dist.get_rank(getattr(trainer, "pg", None)) if world > 1 else 0
+    if isinstance(saved, (list, tuple)):
+        st = saved[rank] if len(saved) == world else saved[0]
+        gen.set_state(torch.as_tensor(st, dtype=torch.uint8).cpu())
+        if len(saved) == world:
+            return
+    else:
+        gen.set_state(torch.as_tensor(saved, dtype=torch.uint8).cpu())
+    if world > 1 and not getattr(trainer, "global_negatives", False):
+        seed = int(torch.randint(0, 2 ** 62, (1,), generator=gen))
+        gen.manual_seed((seed + 0x9E3779B1 * rank) % (2 ** 63))
 
 
 def save_checkpoint(trainer, path, epoch: int, step: int, **kw):
@@ -186,7 +221,7 @@ def load_checkpoint(trainer, path_or_dict, restore_rng: bool = True) -> dict:
         np.random.set_state(rs["numpy"])
         random.setstate(rs["python"])
         ve = getattr(trainer.model, "visual_embedder", None)
-        if rs.get("triad_patch_mask") is not None and ve is not None and hasattr(ve, "_mask_gen"):
-            ve._mask_gen.set_state(torch.as_tensor(rs["triad_patch_mask"], dtype=torch.uint8).cpu())
+        if rs.get("triad_patch_mask") is not None and ve is not None and hasattr(ve, "mask_generator"):
+            _restore_mask_generator(trainer, ve, rs["triad_patch_mask"])
     trainer._update_frozen_params(trainer.global_step)
     return ck

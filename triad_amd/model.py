@@ -269,24 +269,36 @@ class ViTLoRAEmbedder(nn.Module):
         self.layer_norm = nn.LayerNorm(512)
         self.projection2 = nn.Linear(512, embedding_dim)
         self.patch_dropout_rate = dropout_prob
-        # host generator of the patch-dropout masks; its state is saved in trainer checkpoints
-        # (checkpoint.trainer_checkpoint) and, in Mode R, the rank is mixed into its seed so
-        # replicas seeded alike still draw different masks
+        # host generator of the patch-dropout masks; its state is saved in trainer checkpoints (one
+        # per rank, checkpoint.trainer_checkpoint). It is seeded at the FIRST draw, not here, with
+        # the data-parallel rank mixed in, so replicas seeded alike still draw different masks even
+        # when the model is built before init_process_group
         self._mask_gen = torch.Generator()
-        self._mask_gen.manual_seed((torch.initial_seed() + 0x9E3779B1 * _dist_rank()) % (2 ** 63))
+        self._mask_seed_base = torch.initial_seed()
+        self._mask_seeded = False
         self.mask_world = (1, 0)  # (W, rank): draw the global (W*B, N) mask, keep this rank's rows
+
+    def mask_generator(self) -> torch.Generator:
+        """The patch-mask generator, seeded on first use (initial seed + rank mix, or the shared
+        seed of set_global_mask)."""
+        if not self._mask_seeded:
+            self._mask_gen.manual_seed((self._mask_seed_base + 0x9E3779B1 * _dist_rank()) % (2 ** 63))
+            self._mask_seeded = True
+        return self._mask_gen
 
     def set_global_mask(self, world, rank, seed=1234):
         """Global negatives: every rank draws the same global mask from a shared seed, so the
         padded key length (the global max kept count) agrees without any communication."""
         self.mask_world = (world, rank)
         self._mask_gen.manual_seed(seed)
+        self._mask_seeded = True
 
     def draw_keep_mask(self, B, N):
         """Bernoulli(1 - drop) keep mask (model.py:282-284), drawn on the host.
         Returns (this rank's (B, N) mask, padded output length)."""
         W, r = self.mask_world
-        full = torch.bernoulli(torch.full((W * B, N), 1.0 - self.patch_dropout_rate), generator=self._mask_gen).bool()
+        full = torch.bernoulli(torch.full((W * B, N), 1.0 - self.patch_dropout_rate),
+                               generator=self.mask_generator()).bool()
         return full[r * B:(r + 1) * B], int(full.sum(1).max())
 
     def patch_dropout(self, x, drop_rate, keep_mask=None):

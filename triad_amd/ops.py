@@ -142,11 +142,31 @@ def ds_bytes(g: Geometry) -> int:
 
 def ds_chunk_samples(g: Geometry, budget: int) -> int:
     """Key samples per chunk of the memory-bounded backward: all of them when the whole dS fits
-    the budget, else the largest multiple of 4 whose dS chunk does (at least 4)."""
+    the budget, else the largest multiple of 4 whose dS chunk PLUS the recompute path's fp32 dQ
+    partial slabs (nchunks x splits x R_pad x 512 x 4 B) fit (at least 4)."""
     if ds_bytes(g) <= budget:
         return g.Bk
-    per = (g.R_pad // 32) * (g.Nk_pad // 32) * 2048
-    return max(4, (budget // per) // 4 * 4)
+    return max(4, _fit_chunk(g, budget))
+
+
+def _fit_chunk(g: Geometry, budget: int) -> int:
+    for chunk in range(g.Bk // 4 * 4, 3, -4):
+        if ds_working_bytes(g, chunk) <= budget:
+            return chunk
+    return 4
+
+
+def ds_working_bytes(g: Geometry, chunk: int) -> int:
+    """Device bytes the head's backward working set holds for dS at `chunk` key samples per chunk:
+    the whole tiled dS (chunk == Bk, materialised by the forward), or one chunk's dS plus the
+    recompute path's dQ slabs."""
+    if chunk >= g.Bk:
+        return ds_bytes(g)
+    nkb = g.Nk_pad // 32
+    per = (g.R_pad // 32) * _rup(chunk * nkb, 4) * 2048
+    nchunks = -(-g.Bk // chunk)
+    splits = _gemm_splits(g.R_pad // 128, chunk * nkb, g.R_pad)
+    return per + nchunks * splits * g.R_pad * D * 4
 
 
 def recompute_backward(g: Geometry, Qb, Kb, temp, kind, diag_off, argmax, dclip, qw, gdiag, coef, need_q, need_k,
@@ -464,8 +484,12 @@ class _ContrastiveHeadPair(torch.autograd.Function):
     def forward(ctx, qa, ka, qt, kt, temperature, qt_mask, thr, w_sparse, group, ds_budget):
         nig = ctx.needs_input_grad
         need_grad = any(nig[:5])
-        ha = _head_begin(qa, ka, temperature, AV, None, group, ds_budget, need_grad)
-        ht = _head_begin(qt, kt, temperature, TV, qt_mask, group, ds_budget, need_grad)
+        # ONE dS budget for the pair: AV takes what it needs of it, TV what AV leaves (at least
+        # its minimum chunk) -- not a full budget each
+        budget = _default_budget(qa.device) if ds_budget is None else int(ds_budget)
+        ha = _head_begin(qa, ka, temperature, AV, None, group, budget, need_grad)
+        used = ds_working_bytes(ha.g, ha.chunk) if need_grad else 0
+        ht = _head_begin(qt, kt, temperature, TV, qt_mask, group, max(0, budget - used), need_grad)
         st = stream_ptr(qa.device)
         if (ha.dS is None) == (ht.dS is None):
             _heads_launch([ha, ht], st)

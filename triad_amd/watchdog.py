@@ -110,7 +110,9 @@ class StepWatchdog:
                 head = self.pending[0] if self.pending else None
             if head is None or self.last_done_t is None:
                 continue
-            waited = now - max(self.last_done_t, head[2] if not self.durations else self.last_done_t)
+            # the stalled step could not start on the device before the previous one ended, nor
+            # before the host enqueued it
+            waited = now - max(self.last_done_t, head[2])
             if waited > self._limit():
                 self._report(head[0], waited)
                 os._exit(3)
