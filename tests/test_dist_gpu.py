@@ -266,3 +266,86 @@ def test_mode_r_trainer_two_ranks_match_accumulated_single_process(wire):
     bar = 1e-2 if wire == "fp32" else 2e-2
     for name, r in rel.items():
         assert r < bar, (name, r)
+
+
+# ---- Mode G through TriadTrainer: overlapped reducer on its own communicator, unfreeze flip ----
+def _mode_g_trainer(model, group):
+    from triad_amd.train import TriadTrainer
+    tr = TriadTrainer(model, learning_rate=1e-4, total_updates=50, gradient_accumulation_steps=1,
+                      unfreeze_audio_step=1, unfreeze_text_step=0, process_group=group, bucket_mb=16.0,
+                      global_negatives=group is not None)
+    tr.reduced = []
+    inner = tr._allreduce_grads
+
+    def snap():
+        inner()
+        tr.reduced.append(tr.space.flat_g.clone())
+    tr._allreduce_grads = snap
+    return tr
+
+
+def _mode_g_trainer_worker(rank, world, port, q_out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        m = _mode_r_model()
+        tr = _mode_g_trainer(m, dist.group.WORLD)
+        assert tr.reducer is not None and tr.reducer.group is not dist.group.WORLD
+        losses, launched = [], []
+        for step in range(2):
+            f, a, t, _, _ = _mode_r_batch(step, rank)
+            out = tr.step(f, a, t, phase="full_joint")
+            losses.append(float(out["loss"]))
+            launched.append(tr.reducer.launched_in_backward)
+        torch.cuda.synchronize()
+        q_out.put((rank, [g.cpu().numpy() for g in tr.reduced], tr.space.flat_p.cpu().numpy(), losses,
+                   tr.space.touched.copy()))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q_out.put((rank, "error", traceback.format_exc(), None, None))
+
+
+def test_mode_g_trainer_two_ranks_with_unfreeze_flip():
+    """TriadTrainer(global_negatives=True) at world size 2 (gloo on the box's one GPU): the head's
+    key all-gather / clip-row gather / dK reduce-scatter run on the model's group while the
+    overlapped bucket reducer (its own communicator) SUM-reduces the parameter
+    gradients; two steps, HuBERT unfrozen at the second (train.py:527-548), which also re-derives
+    the reducer's launch order. Both ranks compute the identical global loss and hold identical
+    parameters; the reduced gradient of each step equals ONE process running the same B_g = 4
+    batch (same global patch-dropout masks), per parameter group at the bf16 bar."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    qo = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_mode_g_trainer_worker, args=(r, world, port, qo)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([qo.get(timeout=600) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert not isinstance(r[1], str), r[2]
+    (_, g0, p0, l0, t0), (_, g1, p1, l1, t1) = res
+    assert l0 == l1                                 # the one global loss on both ranks
+    for a, b in zip(g0, g1):
+        np.testing.assert_array_equal(a, b)         # one reduced gradient on both ranks
+    np.testing.assert_array_equal(p0, p1)
+    np.testing.assert_array_equal(t0, t1)
+    # single process at B_g = 4: rank-major concatenation of the two ranks' batches, masks from the
+    # same shared seed
+    m = _mode_r_model()
+    m.visual_embedder.set_global_mask(1, 0)
+    tr = _mode_g_trainer(m, None)
+    for step in range(2):
+        b0, b1 = _mode_r_batch(step, 0), _mode_r_batch(step, 1)
+        f = torch.cat([b0[0], b1[0]])
+        a = torch.cat([b0[1], b1[1]])
+        t = list(b0[2]) + list(b1[2])
+        out = tr.step(f, a, t, phase="full_joint")
+        assert abs(float(out["loss"]) - l0[step]) <= 1e-4 * abs(l0[step]), (step, float(out["loss"]), l0[step])
+        rel = _group_rel(tr, g0[step], tr.reduced[step].cpu().numpy())
+        print(f"mode G step {step}: reduced-gradient rel error per group {rel}")
+        for name, r in rel.items():
+            assert r < 1e-2, (step, name, r)

@@ -136,6 +136,7 @@ class GradBucketReducer:
             for i in range(s, e):
                 self.bucket_of[i] = b
         self.order = None                                       # launch order (bucket ids)
+        self._trainable = None                                  # requires_grad pattern `order` was fixed for
         self.active = False
         self.comm = torch.cuda.Stream(space.device) if self.cuda else None
         self.launched_in_backward = 0                           # overlap evidence (tests, logs)
@@ -151,6 +152,13 @@ class GradBucketReducer:
         """Arm the hooks for the backward that completes an accumulation window."""
         sp = self.space
         self._arm_hooks()
+        trainable = tuple(bool(p.requires_grad) for p in sp.params)
+        if trainable != self._trainable:
+            # a staged unfreeze (train.py:527-548) changed which buckets take part: re-derive the
+            # launch order at this step (reduce after backward, record, broadcast) -- every rank
+            # flips at the same global step, so every rank resets here
+            self.order = None
+            self._trainable = trainable
         self.accumulate = accumulate
         self.expected = [0] * len(self.buckets)
         for i, p in enumerate(sp.params):
