@@ -237,11 +237,21 @@ __global__ __launch_bounds__(NT) void c0gn_kernel(const bf16* __restrict__ wave,
   const int t0 = blk * CHUNK, t1 = min(T, t0 + CHUNK);
   const int nsmp = (t1 > t0) ? C0_S * (t1 - t0 - 1) + C0_K : 0;
   for (int i = threadIdx.x; i < nsmp; i += NT) smp[i] = (float)wave[(long long)b * Lp + (long long)C0_S * t0 + i];
+  // the thread's 8 channels x 10 taps = 160 contiguous bytes at a 32-byte-aligned offset
+  // (c0 % 8 == 0), loaded as ten ALIGNED 16-byte vectors: element-wise loads let hipcc merge them
+  // into dwordx3 / dwordx4 loads at 2-byte alignment (byte offsets 14, 30, 46, ...), which were
+  // measured to return wrong data in lanes 48-63 while a 128 x 128 GEMM workgroup (LDS-DMA) shared
+  // the CU (tools/concurrency_repro.py)
   float w[8][C0_K];
+  {
+    bf16x8 wv[C0_K];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int q = 0; q < C0_K; ++q) wv[q] = *(const bf16x8*)(w0 + c0 * C0_K + 8 * q);
 #pragma unroll
-    for (int j = 0; j < C0_K; ++j) w[i][j] = (float)w0[(c0 + i) * C0_K + j];
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < C0_K; ++j) w[i][j] = (float)wv[(i * C0_K + j) >> 3][(i * C0_K + j) & 7];
+  }
   float mu[8], rs[8], g[8], be[8], s[8], q[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {

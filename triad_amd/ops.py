@@ -553,8 +553,11 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     M = idx.shape[1]
     row_bytes = src[0, 0].numel() * src.element_size()
     out = torch.empty((B, M) + tuple(src.shape[2:]), dtype=src.dtype, device=src.device)
-    call("triad_gather_rows", ptr(src.contiguous()), N, ptr(idx.to(torch.int32).contiguous()), B, M, row_bytes,
-         ptr(out), stream_ptr(src.device))
+    # keep the (possibly temporary) operands referenced across the launch: a temporary freed
+    # while the argument list is built could hand its block to the next temporary
+    srcc = src.contiguous()
+    idxc = idx.to(torch.int32).contiguous()
+    call("triad_gather_rows", ptr(srcc), N, ptr(idxc), B, M, row_bytes, ptr(out), stream_ptr(src.device))
     return out
 
 

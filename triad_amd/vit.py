@@ -82,7 +82,8 @@ class _LoRALinear(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = hipgemm.mm(dy2, w.to(torch.bfloat16))
-            call("triad_lora_update", ptr(dx), K, M, K, ptr(dt), ptr(Ab.t().contiguous()), st)
+            At = Ab.t().contiguous()   # referenced across the launch
+            call("triad_lora_update", ptr(dx), K, M, K, ptr(dt), ptr(At), st)
             dx = dx.view(*lead, K).to(x_dtype)
         dAt = torch.empty(K, r, dtype=torch.float32, device=dev)
         call("triad_lora_tn", ptr(xb), K, M, K, ptr(dt), None, None, 1.0, ptr(slabs), ptr(dAt), st)
