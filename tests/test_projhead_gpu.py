@@ -48,9 +48,9 @@ def test_projection_head_at_step_rows(rows, H):
     assert y.dtype == torch.bfloat16 and y.shape == (1, rows, 512)
     y.float().view(rows, 512).backward(gy)
     got = [hd.grad] + [p.grad.detach().clone() for m in mods for p in m.parameters()]
-    # the weight gradients' split-K factor: 16 (one round of 256 CUs) from 10,240 rows up
+    # the weight gradients' split-K factor: 16 (one round of 256 CUs) at every step row count
     Mp = (rows + 127) // 128 * 128
-    assert ops._splitk(Mp, 16) == (16 if rows >= 10240 else Mp // 640)
+    assert ops._splitk(Mp, 16) == 16
     # oracle forward (bf16 autocast emulation), chunked over rows
     w = [p.detach() for m in mods for p in m.parameters()]
     yf = y.detach().float().view(rows, 512)

@@ -609,10 +609,12 @@ int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, 
 // at 300-790.
 int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
                          int M, int N, int Kd, const float* bias, void* C, long long ldc, hipStream_t stream) {
-  // eight-wave 256 x 256 for every tall output it tiles
+  // eight-wave 256 x 256 for every tall output it tiles; the 256 x 128 ring only when its tiles
+  // fill the 256 CUs once (the 8,192-row text projection head at N = 512 has 128 such tiles, half
+  // the chip, and runs on 256 128 x 128 tiles instead)
   int form = 1;
   if (M >= 32768 && M % GW_M == 0 && N % GW_N == 0) form = kBigForm;
-  else if (M >= 8192 && M % GB_M == 0) form = 2;
+  else if (M >= 8192 && M % GB_M == 0 && (long long)(M / GB_M) * (N / BN) >= 256) form = 2;
 #define TRIAD_GEMM_B(AK, BKC)                                                                     \
   if (!!a_kcontig == AK && !!b_kcontig == BKC)                                                    \
     return launch<AK, BKC, bf16>(A, lda, B, ldb, M, N, Kd, nullptr, C, ldc, stream, 1, 0, bias, form);

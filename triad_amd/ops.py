@@ -585,12 +585,13 @@ def _pad_rows(x: torch.Tensor, rows: int) -> torch.Tensor:
 
 def _splitk(Kd, mn_tiles):
     """Split-K factor of the projection-head weight gradients (128 x 128 tiles): one round of
-    workgroups over the 256 CUs, >= 640 token rows per split. Measured (tools/dw_proj_forms.py,
+    workgroups over the 256 CUs, >= 512 token rows per split (so the 8,192-row text head also
+    fills the chip: 16 x 16 workgroups for dW2). Measured (tools/dw_proj_forms.py,
     profiles/r02_dw_proj_forms.log): fewer, longer splits beat two rounds once the slab
     reduction is counted -- dW2 at 65,536 rows 66 us (16 splits) vs 78 us (32), dW1 86 vs 96 us;
     the 256 x 256 four-wave form is no faster at its best split."""
     want = max(1, 256 // mn_tiles)
-    return max(1, min(want, Kd // 640))
+    return max(1, min(want, Kd // 512))
 
 
 def _bf16_round(t):
