@@ -144,9 +144,23 @@ def main():
     frames, audio, text = synthetic(a.batch, rank, dev)
     frames_tv = frames.roll(1, 0).contiguous() if a.separate_frames else None
 
+    # step watchdog (hang forensics): per-stream markers after every HIP entry point,
+    # a monitor thread that writes which launch is in flight and exits non-zero when a step stalls
+    wd = None
+    if os.environ.get("TRIAD_WATCHDOG", "1") != "0":
+        from triad_amd import watchdog
+        out_dir = "gpurun_out" if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else "."
+        wd = watchdog.arm(dev, os.path.join(ROOT, out_dir, f"bench_watchdog_rank{rank}.json"),
+                          ops=os.environ.get("TRIAD_WATCHDOG_OPS", "0") == "1").__enter__()
+
     def step():
-        return trainer.step(frames, audio, text, phase="full_joint", shared_frames=not a.separate_frames,
-                            frames_tv=frames_tv)
+        if wd is not None:
+            wd.step_begin()
+        out = trainer.step(frames, audio, text, phase="full_joint", shared_frames=not a.separate_frames,
+                           frames_tv=frames_tv)
+        if wd is not None:
+            wd.step_end()
+        return out
 
     for i in range(a.warmup):
         t_w = time.perf_counter()
@@ -172,6 +186,9 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     timers, _lib.TIMERS = _lib.TIMERS, None
+    if wd is not None:
+        wd.__exit__(None, None, None)
+        wd = None
     if rank == 0:
         print(f"[bench] {a.steps} timed steps: {dt:.2f} s", file=sys.stderr, flush=True)
     if world > 1:

@@ -364,6 +364,37 @@ def test_side_stream_weight_grads_bit_identical():
     assert torch.equal(gx_side, gx_main)
 
 
+def test_side_stream_weight_grads_weight_used_twice():
+    """A bf16 weight used twice in one graph (two chunks through one layer): autograd sums the two
+    dW on the main stream when the second arrives, so only the first use may go to the side stream
+    and the second must wait for it (linear.side_stream_ok). Large dW GEMMs (8192 x 2048 x 2048)
+    so that an unsynchronised sum would read an unfinished first dW."""
+    from triad_amd import linear as L
+    torch.manual_seed(4)
+    layer = torch.nn.Linear(2048, 2048).to(dev)
+    layer.weight.data = layer.weight.data.to(torch.bfloat16)
+    L.install_fast_linear(torch.nn.ModuleList([layer]))
+    xs = [torch.randn(8192, 2048, device=dev) for _ in range(2)]
+    gy = torch.randn(16384, 2048, device=dev)
+
+    def run(side):
+        L.SIDE_STREAM_DW = side
+        layer.weight.grad = None
+        layer.bias.grad = None
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = torch.cat([layer(xs[0]), layer(xs[1])])
+        (y.float() * gy).sum().backward()
+        return layer.weight.grad.clone()
+
+    try:
+        g_main = run(False)
+        g_side = [run(True) for _ in range(3)]
+    finally:
+        L.SIDE_STREAM_DW = True
+    for g in g_side:
+        assert torch.equal(g, g_main)
+
+
 def test_modality_streams_match_single_stream():
     """forward_triad with the audio / text backbones on their own streams beside the ViT (the
     bench's execution mode) against the single-stream order: one TriadTrainer step from identical

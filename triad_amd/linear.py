@@ -93,9 +93,32 @@ def _join(dev):
     return cb
 
 
-def side_stream_ok(w: torch.Tensor) -> bool:
-    return (SIDE_STREAM_DW and w.is_cuda and w.dtype == torch.bfloat16 and w.grad is None
-            and torch._C._current_graph_task_id() != -1)
+_CLAIMED = {}  # device index -> (autograd graph task, ids of the weights whose dW went to the side stream)
+
+
+def side_stream_ok(*ws: torch.Tensor) -> bool:
+    """May this backward node compute the dW of `ws` on the side stream? Only for bf16 weights
+    whose .grad is empty, inside a backward pass, and only at a weight's FIRST use in the pass:
+    a weight used twice in one graph (two chunks through one layer, tools/audio_reuse_diag.py)
+    has its two dW summed by autograd on the main stream as soon as the second arrives, so the
+    second node makes the main stream wait for the side stream (which holds the first dW) and
+    computes its dW there."""
+    task = torch._C._current_graph_task_id()
+    if not (SIDE_STREAM_DW and task != -1 and all(w.is_cuda and w.dtype == torch.bfloat16 and w.grad is None
+                                                   for w in ws)):
+        return False
+    dev = ws[0].device
+    t, seen = _CLAIMED.get(dev.index, (None, None))
+    if t != task:
+        seen = set()
+        _CLAIMED[dev.index] = (task, seen)
+    if any(id(w) in seen for w in ws):
+        if dev.index in _SIDE:
+            torch.cuda.current_stream(dev).wait_stream(_SIDE[dev.index])
+        seen.update(id(w) for w in ws)
+        return False
+    seen.update(id(w) for w in ws)
+    return True
 
 
 def on_side_stream(fn, inputs):
@@ -184,7 +207,7 @@ class _QKVFn(torch.autograd.Function):
         dx = hipgemm.mm(dy2, wb).view(*xb.shape).to(x_dtype) if ctx.needs_input_grad[0] else None
         dws = [None] * 3
         if any(ctx.needs_input_grad[i] for i in (1, 3, 5)):
-            if w_dtype == torch.bfloat16 and all(side_stream_ok(w) for w in ctx.w_refs):
+            if w_dtype == torch.bfloat16 and side_stream_ok(*ctx.w_refs):
                 # three tensors over the one buffer's storage that are not autograd views, so
                 # autograd stores each as .grad as is (a view might be cloned on the main stream)
                 dws = list(on_side_stream(lambda: _split_rows(weight_grad(dy2, x2), sizes), (dy2, x2)))
