@@ -342,6 +342,18 @@ def _embed_in_chunks(m, n):
     te.forward = types.MethodType(t_c, te)
 
 
+@torch.no_grad()
+def _load_flat_params(tr, flat):
+    """Set every optimizer-owned parameter to the fp32 values `flat` (a FlatParamSpace.flat_p
+    snapshot): the flat master buffer in place (plain parameters are views of it, so their
+    version counters move) and each bf16 model weight to its master's rounding."""
+    sp = tr.space
+    sp.flat_p.copy_(torch.from_numpy(flat).to(sp.flat_p.device))
+    for i in np.nonzero(sp.shadowed)[0]:
+        p = sp.params[int(i)]
+        p.data.copy_(sp.master(int(i)).view(p.shape).to(p.dtype))
+
+
 def _mode_g_trainer_worker(rank, world, port, q_out, unfreeze_audio=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
@@ -351,15 +363,15 @@ def _mode_g_trainer_worker(rank, world, port, q_out, unfreeze_audio=1):
         m.audio_embedder.normalize = _no_znorm
         tr = _mode_g_trainer(m, dist.group.WORLD, unfreeze_audio)
         assert tr.reducer is not None and tr.reducer.group is not dist.group.WORLD
-        losses, launched = [], []
+        losses, launched, params = [], [], []
         for step in range(2):
             f, a, t, _, _ = _mode_r_batch(step, rank)
             out = tr.step(f, a, t, phase="full_joint")
             losses.append(float(out["loss"]))
             launched.append(tr.reducer.launched_in_backward)
+            params.append(tr.space.flat_p.cpu().numpy())
         torch.cuda.synchronize()
-        q_out.put((rank, [g.cpu().numpy() for g in tr.reduced], tr.space.flat_p.cpu().numpy(), losses,
-                   tr.space.touched.copy()))
+        q_out.put((rank, [g.cpu().numpy() for g in tr.reduced], params, losses, tr.space.touched.copy()))
         dist.destroy_process_group()
     except Exception:
         import traceback
@@ -374,7 +386,10 @@ def test_mode_g_trainer_two_ranks_with_unfreeze_flip():
     the reducer's launch order. Both ranks compute the identical global loss and hold identical
     parameters; the reduced gradient of each step equals ONE process running the same B_g = 4
     batch (same global patch-dropout masks; embedders run over the ranks' halves, see
-    _embed_in_chunks), per parameter group at the bf16 bar."""
+    _embed_in_chunks), per parameter group at the bf16 bar. The second step starts the single
+    process from the ranks' parameters after the first (_load_flat_params): AdamW's first update
+    is ~lr * sign(g), so rounding-level gradient differences flip whole elements and the two runs'
+    parameters part by ~2 lr there -- which would make step 1 compare different models."""
     world = 2
     ctx = mp.get_context("spawn")
     qo = ctx.Queue()
@@ -391,7 +406,8 @@ def test_mode_g_trainer_two_ranks_with_unfreeze_flip():
     assert l0 == l1                                 # the one global loss on both ranks
     for a, b in zip(g0, g1):
         np.testing.assert_array_equal(a, b)         # one reduced gradient on both ranks
-    np.testing.assert_array_equal(p0, p1)
+    for a, b in zip(p0, p1):
+        np.testing.assert_array_equal(a, b)         # identical parameters after each step
     np.testing.assert_array_equal(t0, t1)
     # single process at B_g = 4: rank-major concatenation of the two ranks' batches, masks from the
     # same shared seed
@@ -401,6 +417,8 @@ def test_mode_g_trainer_two_ranks_with_unfreeze_flip():
     _embed_in_chunks(m, 2)
     tr = _mode_g_trainer(m, None)
     for step in range(2):
+        if step:
+            _load_flat_params(tr, p0[step - 1])
         b0, b1 = _mode_r_batch(step, 0), _mode_r_batch(step, 1)
         f = torch.cat([b0[0], b1[0]])
         a = torch.cat([b0[1], b1[1]])
