@@ -442,16 +442,21 @@ def test_modality_streams_match_single_stream():
         os.environ.pop("TRIAD_MODALITY_STREAMS", None)
     if l_multi == l_single and torch.equal(g_multi, g_single):
         return
-    num, den, first = {}, {}, None
+    num, den, first, rows = {}, {}, None, []
     for name, grp, off, n in layout:
         a, b = g_multi[off:off + n].double(), g_single[off:off + n].double()
         num[grp] = num.get(grp, 0.0) + float((a - b).square().sum())
         den[grp] = den.get(grp, 0.0) + float(b.square().sum())
-        if first is None and not torch.equal(a, b):
-            first = name
+        if not torch.equal(a, b):
+            first = first or name
+            d = (a - b).abs()
+            rows.append((float(d.norm() / b.norm().clamp(min=1e-300)), name, int((d > 0).sum()), n,
+                         int(d.argmax())))
     rel = {k: (num[k] / max(den[k], 1e-300)) ** 0.5 for k in num}
+    rows.sort(reverse=True)
     raise AssertionError(f"multi-stream step differs: losses {l_multi} vs {l_single}; reduced-gradient relative "
-                         f"L2 per group {rel}; first differing parameter {first}")
+                         f"L2 per group {rel}; first differing parameter {first}; {len(rows)} parameters differ, "
+                         f"worst (rel, name, elements differing, numel, argmax) {rows[:12]}")
 
 
 @pytest.mark.parametrize("M,O,K", [(8192, 768, 3072), (8192, 768, 768), (50944, 2304, 768)])

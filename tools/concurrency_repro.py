@@ -292,8 +292,52 @@ def c0gn_direct(noise, iters=ITERS, B=128):
     print("   quiet re-run equal to the reference:", {k: bool(torch.equal(again[k], ref[k])) for k in ref}, flush=True)
 
 
+def text_grad_case(m, B=128):
+    """DistilBERT + projection head forward AND backward (eval mode: no dropout draws), the
+    flattened gradients of every text parameter as the result."""
+    te = m.text_embedder
+    te.eval()
+    ids = torch.randint(1000, 30522, (B, 32), generator=torch.Generator().manual_seed(11))
+    text = {"input_ids": ids, "attention_mask": torch.ones(B, 32, dtype=torch.long)}
+    ps = [p for p in te.parameters() if p.requires_grad]
+    gy = None
+
+    def fn():
+        nonlocal gy
+        for p in ps:
+            p.grad = None
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = te(text)
+            y = y[0] if isinstance(y, tuple) else y
+        if gy is None:
+            gy = torch.randn(y.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(12))
+        (y.float() * gy).sum().backward()
+        return torch.cat([p.grad.float().reshape(-1) for p in ps if p.grad is not None])
+    return fn
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "text":
+        from triad_amd.model import MultiModalModel
+        m = MultiModalModel(temperature=1.5, visual_dropout_prob=0.25).to(dev).train()
+        victim = text_grad_case(m)
+
+        def rep(fn, n=6):
+            def run():
+                for _ in range(n):
+                    fn()
+            return run
+        tot = check("text fwd+bwd beside nothing", victim, lambda: None)
+        for form in (1, 2, 4):
+            tot += check(f"text fwd+bwd beside gemm form {form}", victim, rep(gemm_form_fn(33280, 3072, 768, form)))
+        for name, noise in vit_part_noises(m).items():
+            tot += check(f"text fwd+bwd beside {name}", victim, noise)
+        _, vit_fwd = model_noise("vit")
+        tot += check("text fwd+bwd beside the ViT forward", victim, vit_fwd)
+        tot += check("text fwd+bwd beside HuBERT forward", victim, rep(audio_case(m, 128), 1))
+        print("total mismatching runs", tot)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "direct":
         def rep(fn, n=6):
             def run():
