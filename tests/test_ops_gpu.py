@@ -454,7 +454,14 @@ def test_modality_streams_match_single_stream():
                          int(d.argmax())))
     rel = {k: (num[k] / max(den[k], 1e-300)) ** 0.5 for k in num}
     rows.sort(reverse=True)
-    raise AssertionError(f"multi-stream step differs: losses {l_multi} vs {l_single}; reduced-gradient relative "
+    # diagnosis only (the test has failed already): which run is the odd one out?
+    try:
+        l_again, g_again, _ = run(False)
+        odd = (f"a second single-stream run equals the first: {l_again == l_single and torch.equal(g_again, g_single)}, "
+               f"equals the multi-stream run: {l_again == l_multi and torch.equal(g_again, g_multi)}")
+    finally:
+        os.environ.pop("TRIAD_MODALITY_STREAMS", None)
+    raise AssertionError(f"multi-stream step differs ({odd}): losses {l_multi} vs {l_single}; reduced-gradient relative "
                          f"L2 per group {rel}; first differing parameter {first}; {len(rows)} parameters differ, "
                          f"worst (rel, name, elements differing, numel, argmax) {rows[:12]}")
 

@@ -316,8 +316,39 @@ def text_grad_case(m, B=128):
     return fn
 
 
+def torch_victims():
+    """PyTorch's own fp32 kernels (built with the compiler's defaults, packed-FP32 VALU ops
+    included): elementwise FMA chain, add, LayerNorm, softmax, reductions."""
+    g = torch.Generator(device=dev).manual_seed(21)
+    x = torch.randn(8192, 768, device=dev, generator=g)
+    y = torch.randn(8192, 768, device=dev, generator=g)
+    w = torch.randn(768, device=dev, generator=g)
+    b = torch.randn(768, device=dev, generator=g)
+    return {
+        "torch x*y+x (fp32)": lambda: torch.addcmul(x, x, y),
+        "torch add (fp32)": lambda: x + y,
+        "torch layer_norm (fp32)": lambda: torch.nn.functional.layer_norm(x, (768,), w, b),
+        "torch softmax (fp32)": lambda: torch.softmax(x, -1),
+        "torch sum(0) (fp32)": lambda: x.sum(0),
+        "torch gelu (fp32)": lambda: torch.nn.functional.gelu(x),
+    }
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "torchops":
+        def rep(fn, n=6):
+            def run():
+                for _ in range(n):
+                    fn()
+            return run
+        tot = 0
+        for form in (1, 2, 4):
+            noise = rep(gemm_form_fn(33280, 3072, 768, form))
+            for name, victim in torch_victims().items():
+                tot += check(f"{name} beside gemm form {form}", victim, noise)
+        print("total mismatching runs", tot)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "text":
         from triad_amd.model import MultiModalModel
         m = MultiModalModel(temperature=1.5, visual_dropout_prob=0.25).to(dev).train()

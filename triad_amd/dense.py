@@ -15,6 +15,16 @@ in `triad_amd.model.MultiModalModel`) differentiates exactly as the reference's 
   diag_smoothness   mean over the diagonal pairs of the squared step along Nq (triad_diag_smooth)
   diag_sparsity     softmax patch-usage excess on the diagonal pairs (triad_diag_sparsity)
   clip_ce           symmetric InfoNCE + similarity statistics of a (B, B) clip (triad_losshead)
+
+Deliberate deviation (precision): token_sims come back fp32 and clip / max / the regularisers are
+computed from fp32 S. In the reference, under autocast, the bf16 einsum result times the 0-dim
+fp32 temperature stays bf16 (SURVEY §2 records that promotion as measured), so its token_sims and
+everything downstream carry bf16 rounding (~2^-9 relative) and half the memory. These debug
+methods keep the fused head's arithmetic (fp32 S from fp32 MFMA accumulation, the same as
+`ops.contrastive_head`) so the two paths agree with each other. The golden fixtures were made by
+the reference on the CPU without autocast (fp32 throughout, tests/golden/gen_golden.py), and
+these methods match them at 1e-4 (`tests/test_dropin_gpu.py`); agreement with the reference's
+bf16 autocast values is bf16 rounding and is not pinned by a fixture.
 """
 from __future__ import annotations
 
