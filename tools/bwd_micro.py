@@ -14,7 +14,7 @@ from triad_amd import ops  # noqa: E402
 from triad_amd._lib import call, ptr, stream_ptr  # noqa: E402
 
 
-def run(B, Nq, Nk, dk, iters, force_sp=None):
+def run(B, Nq, Nk, dk, iters, force_sp=None, form=0):
     g = ops.Geometry(B, Nq, B, Nk)
     gen = torch.Generator(device="cuda").manual_seed(0)
     q = (torch.randn(B, Nq, 512, device="cuda", generator=gen) * 0.58).to(torch.bfloat16)
@@ -32,7 +32,8 @@ def run(B, Nq, Nk, dk, iters, force_sp=None):
     slabs = torch.empty(sp * M * 512, dtype=torch.float32, device="cuda") if sp > 1 else None
 
     def launch():
-        call("triad_tile_gemm", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream_ptr())
+        call("triad_tile_gemm_form", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), form,
+             stream_ptr())
     for _ in range(3):
         launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -52,10 +53,15 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default=os.environ.get("TRIAD_LIB_VARIANT", "default"))
     ap.add_argument("--sweep", action="store_true", help="every split count 1..8 (else the product rule)")
+    ap.add_argument("--forms", default="0", help="comma-separated triad_tile_gemm_form forms, alternated")
+    ap.add_argument("--rounds", type=int, default=1)
     a = ap.parse_args()
-    for name, Nq, Nk in (("AV", 199, 212), ("TV", 32, 212)):
-        for dk in (0, 1):
-            for fsp in (range(1, 9) if a.sweep else (None,)):
-                ms, tf, sp = run(256, Nq, Nk, dk, a.iters, fsp)
-                print(json.dumps({"tag": os.path.basename(a.tag), "head": name, "gemm": "dK" if dk else "dQ",
-                                  "splits": sp, "ms": round(ms, 4), "algo_TFLOPs": round(tf, 1)}), flush=True)
+    for r in range(a.rounds):
+        for name, Nq, Nk in (("AV", 199, 212), ("TV", 32, 212)):
+            for dk in (0, 1):
+                for fsp in (range(1, 9) if a.sweep else (None,)):
+                    for form in (int(f) for f in a.forms.split(",")):
+                        ms, tf, sp = run(256, Nq, Nk, dk, a.iters, fsp, form)
+                        print(json.dumps({"tag": os.path.basename(a.tag), "form": form, "round": r, "head": name,
+                                          "gemm": "dK" if dk else "dQ", "splits": sp, "ms": round(ms, 4),
+                                          "algo_TFLOPs": round(tf, 1)}), flush=True)

@@ -169,6 +169,130 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __re
     }
 }
 
+// Four-wave form: one wave per SIMD, each wave 128 rows x 128 columns (acc[4][4], 256
+// accumulator registers), the same 128 x 512 workgroup tile, ring and LDS-DMA stream. Per k tile a
+// wave reads 8 KB of A and 8 KB of B fragments from LDS (64 KB per workgroup) where the eight-wave
+// form reads 8 + 4 KB per wave (96 KB): every A fragment feeds four MFMAs instead of two.
+constexpr int W4_PIECES = 2 + TBK * TBN * 2 / 16 / 256;  // per thread per tile: 2 A pieces + 8 B rows
+
+template <bool DK>
+__device__ __forceinline__ void w4_piece(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ B,
+                                         int mt0, int kt, bf16* dst, int wave, int lane, int piece) {
+  if (piece < 2) {
+    const int pos = piece * 64 + lane;
+    const int c = DK ? swz_k(pos) : swz_q(pos);
+    const long long tile = DK ? ((long long)kt * CT + (mt0 + wave)) : ((long long)(mt0 + wave) * CT + kt);
+    glds16(Dt + tile * 1024 + c * 8, dst + wave * 1024 + piece * 512);
+  } else {
+    const int k = wave * 8 + piece - 2;
+    const int c = lane ^ ((k & 3) << 2);
+    glds16(B + ((long long)kt * TBK + k) * TBN + c * 8, dst + 4096 + k * TBN);
+  }
+}
+
+template <bool DK, bool SLAB>
+__global__ __launch_bounds__(256, 1) void tile_gemm_w4_kernel(const bf16* __restrict__ Dt, long long CT,
+                                                              const bf16* __restrict__ B, int M, int nkt_total,
+                                                              int kt_per_split, const float* __restrict__ alpha_p,
+                                                              void* __restrict__ Cout) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[RING_NB * RING_ST];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  const int m0 = swz * TBM, mt0 = m0 / 32;
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int nkt = __builtin_amdgcn_readfirstlane(min(kt_per_split, nkt_total - kt0));
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[t][n] = (f32x16){};
+
+#pragma unroll
+  for (int p = 0; p < RING_NB - 1; ++p)
+    if (p < nkt) {
+#pragma unroll
+      for (int u = 0; u < W4_PIECES; ++u) w4_piece<DK>(Dt, CT, B, mt0, kt0 + p, lds + p * RING_ST, wave, lane, u);
+    }
+  for (int it = 0; it < nkt; ++it) {
+    const int younger = min(RING_NB - 2, nkt - 1 - it);  // uniform
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * W4_PIECES) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W4_PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool pf = it + RING_NB - 1 < nkt;
+    bf16* const pdst = lds + ((it + RING_NB - 1) % RING_NB) * RING_ST;
+    const bf16* As = lds + (it % RING_NB) * RING_ST;
+    const bf16* Bs = As + 4096;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[4], bf[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16* tile = As + t * 1024;
+        if (!DK) {
+          af[t] = *(const bf16x8*)(tile + swz_q(2 * l32 + 64 * h + s) * 8);
+        } else {
+          const int a = 2 * (g & 1) + (p4 >> 1), hh = p4 & 1;
+          s16x4* rp = (s16x4*)&af[t];
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) {
+            const int qry = 16 * s + 8 * h + 4 * tt + q4;
+            const int c = (qry + 32 * hh) * 2 + (a >> 1);
+            rp[tt] = lds_tr16(tile + swz_k(c) * 8 + 4 * (a & 1));
+          }
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int n0 = wave * 128 + n * 32;
+        bf[n] = DK ? bfrag(Bs, 16 * s + 8 * h + q4, 4, n0, lane) : bfrag(Bs, 16 * s + 4 * h + q4, 8, n0, lane);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          acc[t][n] = mfma32(af[t], bf[n], acc[t][n]);
+          const int m = s * 16 + t * 4 + n;
+          if (m % 3 == 0 && m / 3 < W4_PIECES) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (pf) w4_piece<DK>(Dt, CT, B, mt0, kt0 + it + RING_NB - 1, pdst, wave, lane, m / 3);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+    }
+  }
+
+  const float alpha = SLAB ? 1.f : *alpha_p;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int col = wave * 128 + n * 32 + l32;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int m = m0 + t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        const float val = alpha * acc[t][n][v];
+        if (SLAB) ((float*)Cout)[((size_t)blockIdx.y * M + m) * TBN + col] = val;
+        else ((bf16*)Cout)[(size_t)m * TBN + col] = (bf16)val;
+      }
+    }
+}
+
+// form 0: policy (the four-wave form), 1: eight-wave ring, 2: four-wave
+template <bool DK, bool SLAB>
+void launch_tile(int form, dim3 grid, hipStream_t stream, const bf16* d, long long CT, const bf16* b, int M, int nkt,
+                 int kps, const float* alpha, void* out) {
+  if (form == 1)
+    hipLaunchKernelGGL((tile_gemm_ring_kernel<DK, SLAB>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
+  else
+    hipLaunchKernelGGL((tile_gemm_w4_kernel<DK, SLAB>), grid, dim3(256), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
+}
+
 }  // namespace
 
 extern "C" {
@@ -176,23 +300,28 @@ extern "C" {
 // dQ (dk = 0): M = query rows (R_pad), nkt = key tiles (C_pad / 32), B = K [C_pad][512].
 // dK (dk = 1): M = key rows (CT * 32), nkt = query tiles (R_pad / 32), B = Q [R_pad][512].
 // splits > 1: fp32 slabs [splits][M][512] in `slabs`, then C = alpha * sum (bf16).
-int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
-                    int splits, float* slabs, void* C, hipStream_t stream) {
-  if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
+int triad_tile_gemm_form(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
+                         int splits, float* slabs, void* C, int form, hipStream_t stream) {
+  if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs) || form < 0 || form > 2) return TRIAD_EINVAL;
   const int kps = (nkt + splits - 1) / splits;
   dim3 grid(M / TBM, splits);
   const bf16* d = (const bf16*)Dt;
   const bf16* b = (const bf16*)B;
   if (splits == 1) {
-    if (dk) hipLaunchKernelGGL((tile_gemm_ring_kernel<true, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
-    else hipLaunchKernelGGL((tile_gemm_ring_kernel<false, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
+    if (dk) launch_tile<true, false>(form, grid, stream, d, CT, b, M, nkt, kps, alpha, C);
+    else launch_tile<false, false>(form, grid, stream, d, CT, b, M, nkt, kps, alpha, C);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
-  if (dk) hipLaunchKernelGGL((tile_gemm_ring_kernel<true, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
-  else hipLaunchKernelGGL((tile_gemm_ring_kernel<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
+  if (dk) launch_tile<true, true>(form, grid, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
+  else launch_tile<false, true>(form, grid, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
   TRIAD_CHECK_LAUNCH();
   return triad_sum_slabs(slabs, splits, (long long)M * TBN, alpha, 1, C, stream);
+}
+
+int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
+                    int splits, float* slabs, void* C, hipStream_t stream) {
+  return triad_tile_gemm_form(Dt, CT, dk, B, M, nkt, alpha, splits, slabs, C, 0, stream);
 }
 
 // Unscaled fp32 slabs only: slabs[s][M][512] = partial (split s of nkt) of dS K (dk = 0) or
@@ -205,8 +334,8 @@ int triad_tile_gemm_slabs(const void* Dt, long long CT, int dk, const void* B, i
   dim3 grid(M / TBM, splits);
   const bf16* d = (const bf16*)Dt;
   const bf16* b = (const bf16*)B;
-  if (dk) hipLaunchKernelGGL((tile_gemm_ring_kernel<true, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
-  else hipLaunchKernelGGL((tile_gemm_ring_kernel<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  if (dk) launch_tile<true, true>(0, grid, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  else launch_tile<false, true>(0, grid, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
