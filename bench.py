@@ -123,13 +123,13 @@ def kernel_report(timers):
 
 def main():
     a = parse()
+    from triad_amd import _lib, blas
+    blas.configure()   # torch's own GEMMs on rocBLAS, before the HIP runtime starts (triad_amd/blas.py)
     world, rank, local = setup_dist()
     dev = torch.device("cuda", local)
-    from triad_amd import _lib, blas
     from triad_amd.model import MultiModalModel
     from triad_amd.train import TriadTrainer
 
-    blas.configure()   # torch's own GEMMs on rocBLAS, before any runs (triad_amd/blas.py)
     _lib.load()
     # The only MIOpen convolution left is HuBERT's positional conv (the feature encoder and the
     # patch embedding run as GEMMs, triad_amd.frontend): immediate mode, no per-shape search /

@@ -26,6 +26,13 @@ def configure() -> str:
     """Point PyTorch's BLAS dispatch at LIBRARY (process-wide, idempotent)."""
     global _configured
     if _configured != LIBRARY:
+        if torch.cuda.is_initialized():
+            # the two environment switches are read once (first addmm / first rocBLAS handle): a
+            # GEMM that ran before this call has fixed them already
+            import warnings
+            warnings.warn("triad_amd.blas.configure() called after the HIP runtime was initialised: if "
+                          "a GEMM already ran, DISABLE_ADDMM_CUDA_LT / ROCBLAS_USE_HIPBLASLT no longer take "
+                          "effect in this process (call configure() first)", RuntimeWarning, stacklevel=2)
         torch.backends.cuda.preferred_blas_library("cublas" if LIBRARY == "rocblas" else "cublaslt")
         # addmm with a bias vector (every nn.Linear under autocast) takes PyTorch's Lt path
         # (hipBLASLt gemm_and_bias) whatever the preferred library, unless this is set; PyTorch
