@@ -132,11 +132,6 @@ int triad_dtemp_finalize(const double* p0, int n0, const double* p1, int n1, con
 int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
                     int splits, float* slabs, void* C, hipStream_t stream);
 
-/* The same with the workgroup form chosen per call: 0 = policy, 1 = eight waves (each 128 rows x
- * 64 columns), 2 = four waves (each 128 x 128; a third fewer LDS fragment reads per flop). */
-int triad_tile_gemm_form(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
-                         int splits, float* slabs, void* C, int form, hipStream_t stream);
-
 /* The same GEMM into unscaled fp32 slabs [splits][M][512] only (no reduction): partial sums the
  * caller reduces with triad_sum_slabs, e.g. dQ over the key-sample chunks of the memory-bounded
  * (recompute) backward. */

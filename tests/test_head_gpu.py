@@ -294,17 +294,12 @@ def _untile_dS(dS, R_pad, CT):
     return t.reshape(R_pad, CT * 32)
 
 
-@pytest.mark.parametrize("form", [0, 1, 2])
 @pytest.mark.parametrize("panels,ct", [(16, 64), (7, 36), (400, 24), (3, 4)])
-def test_tile_gemm_vs_torch(panels, ct, form, monkeypatch):
-    """triad_tile_gemm_form (policy, 128 x 512 ring and 256 x 256 square forms, split-K slabs
-    where chosen) against fp32 torch matmuls of the untiled dS: dQ = alpha dS K, dK = alpha dS^T Q.
-    The square form needs M % 256 == 0 (the others run every case)."""
-    if form == 2 and (panels % 2 or ct % 8):
-        pytest.skip("square form: M % 256 == 0")
+def test_tile_gemm_vs_torch(panels, ct):
+    """triad_tile_gemm (ring kernel, split-K slabs where chosen) against fp32 torch matmuls of the
+    untiled dS: dQ = alpha dS K, dK = alpha dS^T Q."""
     from triad_amd._lib import stream_ptr
     ops = _ops()
-    monkeypatch.setattr(ops, "TILE_FORM", form)
     g = torch.Generator(device=dev).manual_seed(panels * 100 + ct)
     R_pad, CT = panels * 128, ct
     dS = (torch.randn(R_pad // 32 * CT * 1024, device=dev, generator=g) * 0.1).to(torch.bfloat16)
@@ -323,34 +318,6 @@ def test_tile_gemm_vs_torch(panels, ct, form, monkeypatch):
     if CT % 4 == 0:
         refK = 0.75 * dense.t() @ Q.float()
         assert _rel(dK.float().cpu(), refK.cpu()) < 5e-3
-
-
-@pytest.mark.parametrize("panels,ct,splits", [(16, 64, 1), (8, 40, 3), (398, 224, 1), (398, 224, 3), (56, 2048, 4)])
-def test_tile_gemm_forms_bit_identical(panels, ct, splits):
-    """The 256 x 256 square form accumulates every output element over the same k order as the
-    128 x 512 ring form: identical bits, dQ and dK, with and without split-K slabs (shapes with
-    M % 256 == 0 in both GEMMs)."""
-    from triad_amd._lib import call, ptr, stream_ptr
-    g = torch.Generator(device=dev).manual_seed(panels + ct)
-    R_pad, CT = panels * 128, ct
-    dS = (torch.randn(R_pad // 32 * CT * 1024, device=dev, generator=g) * 0.1).to(torch.bfloat16)
-    K = torch.randn(CT * 32, 512, device=dev, generator=g).to(torch.bfloat16)
-    Q = torch.randn(R_pad, 512, device=dev, generator=g).to(torch.bfloat16)
-    alpha = torch.tensor([0.75], device=dev)
-    outs = {}
-    for form in (1, 2):
-        for dk, B, M, nkt in ((0, K, R_pad, CT), (1, Q, CT * 32, R_pad // 32)):
-            if dk and CT % 4:
-                continue
-            out = torch.empty(M, 512, dtype=torch.bfloat16, device=dev)
-            slabs = torch.empty(splits * M * 512, device=dev) if splits > 1 else None
-            call("triad_tile_gemm_form", ptr(dS), CT, dk, ptr(B), M, nkt, ptr(alpha), splits, ptr(slabs), ptr(out),
-                 form, stream_ptr())
-            outs[(form, dk)] = out
-    torch.cuda.synchronize()
-    for dk in (0, 1):
-        if (1, dk) in outs:
-            assert torch.equal(outs[(1, dk)], outs[(2, dk)]), dk
 
 
 @pytest.mark.parametrize("B,Na,Nt,Nv,budget", [(6, 49, 16, 70, None), (16, 199, 32, 205, None),

@@ -32,8 +32,12 @@ def run(B, Nq, Nk, dk, iters, force_sp=None, form=0):
     slabs = torch.empty(sp * M * 512, dtype=torch.float32, device="cuda") if sp > 1 else None
 
     def launch():
-        call("triad_tile_gemm_form", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), form,
-             stream_ptr())
+        if form:   # a variant entry point (tools/build_variants.py builds): triad_tile_gemm_form
+            call("triad_tile_gemm_form", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), form,
+                 stream_ptr())
+        else:
+            call("triad_tile_gemm", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out),
+                 stream_ptr())
     for _ in range(3):
         launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -33,7 +33,6 @@ SIGNATURES = {
     "triad_dS_patch": [vp, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp, f32, vp, i32, vp],
     "triad_dtemp_finalize": [vp, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp],
     "triad_tile_gemm": [vp, i64, i32, vp, i32, i32, vp, i32, vp, vp, vp],
-    "triad_tile_gemm_form": [vp, i64, i32, vp, i32, i32, vp, i32, vp, vp, i32, vp],
     "triad_tile_gemm_slabs": [vp, i64, i32, vp, i32, i32, i32, vp, vp],
     "triad_gemm_bf16": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, i32, vp],
     "triad_gemm_bf16_bias": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, vp],

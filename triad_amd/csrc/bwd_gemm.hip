@@ -169,155 +169,6 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __re
     }
 }
 
-// Square form: workgroup tile 256 rows x 256 columns (8 waves: 2 row halves x 4 column quarters,
-// each 128 x 64 as in the ring form), a 5-slot ring of 32 KB stages (A 8 tiles = 16 KB, B 32 x 256
-// = 16 KB) with four stages in flight. Per k tile a workgroup ingests 32 KB for the flops the ring
-// form ingests 40 KB for (the B panel is half as wide), and holds 128 KB in flight instead of
-// 120 KB; dS is read by two workgroups (column halves) that run on the same XCD back to back, so
-// the second read is an L2 hit. Needs M % 256 == 0.
-constexpr int SQ_NB = 5, SQ_BN = 256;
-constexpr int SQ_ST = 8 * 1024 + TBK * SQ_BN;  // 32 KB
-constexpr int SQ_PIECES = 4;                    // per thread per tile: 2 A + 2 B
-
-__device__ __forceinline__ int bq_off(int k, int col) {
-  return k * SQ_BN + ((((col >> 3) ^ ((k & 3) << 2))) << 3) + (col & 7);
-}
-
-__device__ __forceinline__ bf16x8 bqfrag(const bf16* img, int r0, int dr, int n0, int lane) {
-  const int g = lane >> 4, i = lane & 15, p = i & 3;
-  const int col = n0 + 16 * (g & 1) + 4 * p;
-  bf16x8 r;
-  s16x4* rp = (s16x4*)&r;
-  rp[0] = lds_tr16(img + bq_off(r0, col));
-  rp[1] = lds_tr16(img + bq_off(r0 + dr, col));
-  return r;
-}
-
-template <bool DK>
-__device__ __forceinline__ void sq_piece(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ B,
-                                         int mt0, int n0, int kt, bf16* dst, int wave, int lane, int piece) {
-  if (piece < 2) {
-    const int pos = piece * 64 + lane;
-    const int c = DK ? swz_k(pos) : swz_q(pos);
-    const long long tile = DK ? ((long long)kt * CT + (mt0 + wave)) : ((long long)(mt0 + wave) * CT + kt);
-    glds16(Dt + tile * 1024 + c * 8, dst + wave * 1024 + piece * 512);
-  } else {
-    const int k0 = 2 * (2 * wave + piece - 2), k = k0 + (lane >> 5);
-    const int c = (lane & 31) ^ ((k & 3) << 2);
-    glds16(B + ((long long)kt * TBK + k) * TBN + n0 + c * 8, dst + 8192 + k0 * SQ_BN);
-  }
-}
-
-template <bool DK, bool SLAB>
-__global__ __launch_bounds__(512, 1) void tile_gemm_sq_kernel(const bf16* __restrict__ Dt, long long CT,
-                                                              const bf16* __restrict__ B, int M, int nkt_total,
-                                                              int kt_per_split, const float* __restrict__ alpha_p,
-                                                              void* __restrict__ Cout) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[SQ_NB * SQ_ST];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h = lane >> 5, l32 = lane & 31;
-  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-  // contiguous logical range per XCD; the two column halves of a row panel are consecutive
-  const int lg = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
-  const int m0 = (lg >> 1) * 256, mt0 = m0 / 32, n0 = (lg & 1) * SQ_BN;
-  const int kt0 = blockIdx.y * kt_per_split;
-  const int nkt = __builtin_amdgcn_readfirstlane(min(kt_per_split, nkt_total - kt0));
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) acc[t][n] = (f32x16){};
-
-#pragma unroll
-  for (int p = 0; p < SQ_NB - 1; ++p)
-    if (p < nkt) {
-#pragma unroll
-      for (int u = 0; u < SQ_PIECES; ++u) sq_piece<DK>(Dt, CT, B, mt0, n0, kt0 + p, lds + p * SQ_ST, wave, lane, u);
-    }
-  for (int it = 0; it < nkt; ++it) {
-    const int younger = min(SQ_NB - 2, nkt - 1 - it);  // uniform
-    if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * SQ_PIECES) : "memory");
-    else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * SQ_PIECES) : "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SQ_PIECES) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const bool pf = it + SQ_NB - 1 < nkt;
-    bf16* const pdst = lds + ((it + SQ_NB - 1) % SQ_NB) * SQ_ST;
-    const bf16* As = lds + (it % SQ_NB) * SQ_ST + wr * 4 * 1024;
-    const bf16* Bs = lds + (it % SQ_NB) * SQ_ST + 8192;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[4], bf[2];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf16* tile = As + t * 1024;
-        if (!DK) {
-          af[t] = *(const bf16x8*)(tile + swz_q(2 * l32 + 64 * h + s) * 8);
-        } else {
-          const int a = 2 * (g & 1) + (p4 >> 1), hh = p4 & 1;
-          s16x4* rp = (s16x4*)&af[t];
-#pragma unroll
-          for (int tt = 0; tt < 2; ++tt) {
-            const int qry = 16 * s + 8 * h + 4 * tt + q4;
-            const int c = (qry + 32 * hh) * 2 + (a >> 1);
-            rp[tt] = lds_tr16(tile + swz_k(c) * 8 + 4 * (a & 1));
-          }
-        }
-      }
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int nb = wc * 64 + n * 32;
-        bf[n] = DK ? bqfrag(Bs, 16 * s + 8 * h + q4, 4, nb, lane) : bqfrag(Bs, 16 * s + 4 * h + q4, 8, nb, lane);
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          acc[t][n] = mfma32(af[t], bf[n], acc[t][n]);
-          const int m = s * 8 + t * 2 + n;
-          if (m % 4 == 0 && m / 4 < SQ_PIECES) {
-            __builtin_amdgcn_sched_barrier(0);
-            if (pf) sq_piece<DK>(Dt, CT, B, mt0, n0, kt0 + it + SQ_NB - 1, pdst, wave, lane, m / 4);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-    }
-  }
-
-  const float alpha = SLAB ? 1.f : *alpha_p;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int col = n0 + wc * 64 + n * 32 + l32;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = m0 + wr * 128 + t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        const float val = alpha * acc[t][n][v];
-        if (SLAB) ((float*)Cout)[((size_t)blockIdx.y * M + m) * TBN + col] = val;
-        else ((bf16*)Cout)[(size_t)m * TBN + col] = (bf16)val;
-      }
-    }
-}
-
-// form 0: policy (the square form when M % 256 == 0, else the ring form), 1: 128 x 512 ring,
-// 2: 256 x 256 square (M % 256 == 0). The grid has M / 128 workgroups in either form.
-template <bool DK, bool SLAB>
-int launch_tile(int form, dim3 grid, hipStream_t stream, const bf16* d, long long CT, const bf16* b, int M, int nkt,
-                int kps, const float* alpha, void* out) {
-  if (form == 0) form = 1;  // (A/B pending)
-  if (form == 2 && M % 256) return TRIAD_EINVAL;
-  if (form == 1)
-    hipLaunchKernelGGL((tile_gemm_ring_kernel<DK, SLAB>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
-  else
-    hipLaunchKernelGGL((tile_gemm_sq_kernel<DK, SLAB>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
-  return TRIAD_OK;
-}
-
 }  // namespace
 
 extern "C" {
@@ -325,31 +176,23 @@ extern "C" {
 // dQ (dk = 0): M = query rows (R_pad), nkt = key tiles (C_pad / 32), B = K [C_pad][512].
 // dK (dk = 1): M = key rows (CT * 32), nkt = query tiles (R_pad / 32), B = Q [R_pad][512].
 // splits > 1: fp32 slabs [splits][M][512] in `slabs`, then C = alpha * sum (bf16).
-int triad_tile_gemm_form(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
-                         int splits, float* slabs, void* C, int form, hipStream_t stream) {
-  if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs) || form < 0 || form > 2) return TRIAD_EINVAL;
+int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
+                    int splits, float* slabs, void* C, hipStream_t stream) {
+  if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
   const int kps = (nkt + splits - 1) / splits;
   dim3 grid(M / TBM, splits);
   const bf16* d = (const bf16*)Dt;
   const bf16* b = (const bf16*)B;
-  int rc;
   if (splits == 1) {
-    rc = dk ? launch_tile<true, false>(form, grid, stream, d, CT, b, M, nkt, kps, alpha, C)
-            : launch_tile<false, false>(form, grid, stream, d, CT, b, M, nkt, kps, alpha, C);
-    if (rc) return rc;
+    if (dk) hipLaunchKernelGGL((tile_gemm_ring_kernel<true, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
+    else hipLaunchKernelGGL((tile_gemm_ring_kernel<false, false>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
-  rc = dk ? launch_tile<true, true>(form, grid, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs)
-          : launch_tile<false, true>(form, grid, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
-  if (rc) return rc;
+  if (dk) hipLaunchKernelGGL((tile_gemm_ring_kernel<true, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
+  else hipLaunchKernelGGL((tile_gemm_ring_kernel<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, (void*)slabs);
   TRIAD_CHECK_LAUNCH();
   return triad_sum_slabs(slabs, splits, (long long)M * TBN, alpha, 1, C, stream);
-}
-
-int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, const float* alpha,
-                    int splits, float* slabs, void* C, hipStream_t stream) {
-  return triad_tile_gemm_form(Dt, CT, dk, B, M, nkt, alpha, splits, slabs, C, 0, stream);
 }
 
 // Unscaled fp32 slabs only: slabs[s][M][512] = partial (split s of nkt) of dS K (dk = 0) or
@@ -362,9 +205,8 @@ int triad_tile_gemm_slabs(const void* Dt, long long CT, int dk, const void* B, i
   dim3 grid(M / TBM, splits);
   const bf16* d = (const bf16*)Dt;
   const bf16* b = (const bf16*)B;
-  const int rc = dk ? launch_tile<true, true>(0, grid, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs)
-                    : launch_tile<false, true>(0, grid, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
-  if (rc) return rc;
+  if (dk) hipLaunchKernelGGL((tile_gemm_ring_kernel<true, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  else hipLaunchKernelGGL((tile_gemm_ring_kernel<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

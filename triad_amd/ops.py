@@ -97,9 +97,6 @@ def colsum(x, out_dtype=torch.float32, backbone=False):
     return out
 
 
-TILE_FORM = int(__import__("os").environ.get("TRIAD_TILE_FORM", "0"))  # A/B knob (measurement)
-
-
 def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream, meta=None):
     """dQ = alpha dS K (dk=0) / dK = alpha dS^T Q (dk=1) over the tiled dS (triad_tile_gemm),
     split-K over the CUs when the row panels alone leave them idle. (A stream-K form -- one run
@@ -107,8 +104,7 @@ def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream, meta=None):
     different k offsets, so CUs of one XCD no longer share the streamed B panel in L2.)"""
     sp = _gemm_splits(M // 128, nkt, M)
     slabs = torch.empty(sp * M * D, dtype=torch.float32, device=out.device) if sp > 1 else None
-    call("triad_tile_gemm_form", ptr(dS), CT, dk, ptr(B), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), TILE_FORM,
-         stream, meta=meta)
+    call("triad_tile_gemm", ptr(dS), CT, dk, ptr(B), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream, meta=meta)
 
 
 def _gemm_splits(wgs, nkt, M, cus=256, max_splits=8, t_tile=1.0e-6, hbm=5.0e12):
