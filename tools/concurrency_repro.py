@@ -292,6 +292,29 @@ def c0gn_direct(noise, iters=ITERS, B=128):
     print("   quiet re-run equal to the reference:", {k: bool(torch.equal(again[k], ref[k])) for k in ref}, flush=True)
 
 
+def vit_train_noise(m, B=128):
+    """The ViT (+LoRA) patch encoder forward AND backward (LoRA / head gradients), train mode."""
+    frames = torch.randn(B, 3, 224, 224, device=dev)
+    ve = m.visual_embedder
+
+    def run():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = ve.encode_patches(frames)
+        y.float().square().mean().backward()
+    return run
+
+
+def audio_train_noise(m, B=128):
+    x = torch.randn(B, 16000, device=dev) * 0.1
+    ae = m.audio_embedder
+
+    def run():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = ae(x)
+        y.float().square().mean().backward()
+    return run
+
+
 def text_grad_case(m, B=128):
     """DistilBERT + projection head forward AND backward (eval mode: no dropout draws), the
     flattened gradients of every text parameter as the result."""
@@ -366,6 +389,8 @@ if __name__ == "__main__":
             tot += check(f"text fwd+bwd beside {name}", victim, noise)
         _, vit_fwd = model_noise("vit")
         tot += check("text fwd+bwd beside the ViT forward", victim, vit_fwd)
+        tot += check("text fwd+bwd beside the ViT fwd+bwd", victim, vit_train_noise(m))
+        tot += check("text fwd+bwd beside HuBERT fwd+bwd", victim, audio_train_noise(m))
         tot += check("text fwd+bwd beside HuBERT forward", victim, rep(audio_case(m, 128), 1))
         print("total mismatching runs", tot)
         sys.exit(0)
