@@ -29,14 +29,7 @@ constexpr int KT_ELEMS = 32 * D;
 constexpr int NBUF = 3;                  // key-tile LDS ring slots
 constexpr int LDSPF = 2;                 // key fragments read from LDS ahead of their MFMA
 constexpr int REGION = 2;                // k-steps per scheduling region (sched_barrier spacing)
-// Query row blocks of 32 per wave: 1 = eight waves (two per SIMD), each holding 32 rows' fragments;
-// 2 = four waves (one per SIMD), each holding 64 rows' fragments (256 VGPRs) and feeding every key
-// fragment it reads from LDS to two MFMAs -- half the LDS fragment traffic per flop.
-#ifndef TRIAD_FWD_RB
-#define TRIAD_FWD_RB 1
-#endif
-constexpr int FWD_RB = TRIAD_FWD_RB;
-static_assert(FWD_RB == 1 || FWD_RB == 2, "TRIAD_FWD_RB");
+constexpr int GLDS_PER_TILE = 32 / WAVES;  // 1-KB LDS-DMA pieces per wave per key tile (4)
 
 struct FwdArgs {
   const bf16* Q;
@@ -75,11 +68,9 @@ __device__ __forceinline__ void dma16(i32x4 rsrc, unsigned lds_addr, unsigned vo
 
 // One key tile (32 rows x 1 KB) into an LDS slot: 1-KB pieces, the row offset in soffset
 // (uniform), the source-side swizzle chunk ^ (row & 15) in voffset. Piece u of this wave's
-// 32 / W (W waves per workgroup).
-template <int W>
+// GLDS_PER_TILE.
 __device__ __forceinline__ void stage_piece(i32x4 kr, const FwdArgs& a, bf16* dst, int j, int kb, int wave,
                                             int lane, int u) {
-  constexpr int GLDS_PER_TILE = 32 / W;
   const unsigned row0 = (unsigned)(j * a.Nk_pad + kb * 32 + wave * GLDS_PER_TILE);
   const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) bf16*)dst;
   asm volatile("" : "+v"(lane));  // recompute the lane offsets here, do not keep them live
@@ -88,11 +79,10 @@ __device__ __forceinline__ void stage_piece(i32x4 kr, const FwdArgs& a, bf16* ds
         __builtin_amdgcn_readfirstlane((row0 + u) * (D * 2)));
 }
 
-template <int W>
 __device__ __forceinline__ void stage_tile(i32x4 kr, const FwdArgs& a, bf16* dst, int j, int kb, int wave,
                                            int lane) {
 #pragma unroll
-  for (int u = 0; u < 32 / W; ++u) stage_piece<W>(kr, a, dst, j, kb, wave, lane, u);
+  for (int u = 0; u < GLDS_PER_TILE; ++u) stage_piece(kr, a, dst, j, kb, wave, lane, u);
 }
 
 // 16-byte store hidden from hipcc's waitcnt bookkeeping (it would otherwise drain vmcnt(0) --
@@ -230,24 +220,16 @@ constexpr int KBUF_ELEMS = NBUF * KT_ELEMS + 16 * WAVES;
 
 // One workgroup of the forward: 256-row block bx, key-sample split by (of gx row blocks) of
 // problem a. kbuf = the workgroup's LDS (key ring + reduction scratch).
-template <bool TRAIN, int RB>
+template <bool TRAIN>
 __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int bx, const int by, const int gx) {
-  constexpr int W = WAVES / RB;              // waves per workgroup
-  constexpr int GLDS_PER_TILE = 32 / W;      // 1-KB LDS-DMA pieces per wave per key tile
   double* red = (double*)(kbuf + NBUF * KT_ELEMS);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
-  const int rbase = bx * ROWS_PER_WG + wave * 32 * RB;  // this wave's first row
-  int rows[RB];
-  bool rok[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    rows[r] = rbase + 32 * r + ql;
-    rok[r] = rows[r] < a.R;
-  }
-  const int rt = rbase / 32;
+  const int row = bx * ROWS_PER_WG + wave * 32 + ql;
+  const bool rok = row < a.R;
+  const int rt = (bx * ROWS_PER_WG + wave * 32) / 32;
 
   const int j0 = by * a.j_per_wg;
   const int j1 = min(a.Bk, j0 + a.j_per_wg);
@@ -273,7 +255,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
   int fslot = 0, cslot = 0;
   auto prefetch = [&](int b2) {
-    if (b2 < nblocks) stage_tile<W>(kr, a, kbuf + fslot * KT_ELEMS, fc.j - j0, fc.kb, wave, lane);
+    if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j - j0, fc.kb, wave, lane);
     fc.next(nkb);
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
   };
@@ -281,12 +263,11 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   prefetch(0);
   prefetch(1);
 
-  bf16x8 qf[RB][NS];
+  bf16x8 qf[NS];
+  {
+    const bf16* q0 = a.Q + (size_t)row * D + 8 * h;  // rows < R_pad: zero tail, in the allocation
 #pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    const bf16* q0 = a.Q + (size_t)rows[r] * D + 8 * h;  // rows < R_pad: zero tail, in the allocation
-#pragma unroll
-    for (int s = 0; s < NS; ++s) qf[r][s] = *(const bf16x8*)(q0 + 16 * s);
+    for (int s = 0; s < NS; ++s) qf[s] = *(const bf16x8*)(q0 + 16 * s);
   }
   // uniform (SGPR) temperature: the load completes here, not at a wait inside the loop
   const float temp = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, *a.temp)));
@@ -296,13 +277,11 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   if (!(temp > 0.f)) {
     const unsigned flip = temp < 0.f ? 0x80008000u : 0u, keep = temp == 0.f ? 0u : 0xffffffffu;
 #pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        u32x4 w = __builtin_bit_cast(u32x4, qf[r][s]);
-        w = (w & keep) ^ flip;
-        qf[r][s] = __builtin_bit_cast(bf16x8, w);
-      }
+    for (int s = 0; s < NS; ++s) {
+      u32x4 w = __builtin_bit_cast(u32x4, qf[s]);
+      w = (w & keep) ^ flip;
+      qf[s] = __builtin_bit_cast(bf16x8, w);
+    }
   }
   const f32x2 su2 = {su, su};
   const float lo = a.clamp_lo / su;  // clamp window of u
@@ -314,65 +293,58 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   // this wave's dS row block (TRAIN): tile (rt, ct) at (rt*CT + ct)*1024 elements
   bf16* const dS_w = TRAIN ? a.dS + (long long)rt * a.CT * 1024 : nullptr;
 
-  Epi e[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    e[r].m = -INFINITY;
-    e[r].am = 0;
-    e[r].at = 0;
-  }
+  Epi e;
+  e.m = -INFINITY;
+  e.am = 0;
+  e.at = 0;
 
-  f32x16 cA[RB], cB[RB];
+  f32x16 cA, cB;
 
   auto sync_tile = [&](int b) {
-    // VMEM ops younger than tile b's DMA, at least: tile b+1's pieces (if any) and, in
-    // training, one epilogue's dS stores (2 per row block, b >= 2); vmcnt counts both, in issue
-    // order (3-slot ring; a 2-slot ring has no younger tile in flight)
+    // VMEM ops younger than tile b's DMA, at least: tile b+1's 4 pieces (if any) and, in
+    // training, one epilogue's 2 dS stores (b >= 2); vmcnt counts both, in issue order
+    // (3-slot ring; a 2-slot ring has no younger tile in flight)
     const bool more = b + 1 < nblocks;
     const bool st = TRAIN && b >= 2;
-    if (more && st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_TILE + 2 * RB) : "memory");
+    if (more && st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_TILE + 2) : "memory");
     else if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_TILE) : "memory");
-    else if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RB) : "memory");
+    else if (st) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  auto epi_end = [&](const f32x16* p) {
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      Epi& er = e[r];
-      if (er.m > er.m0) er.am = ec.kb * 32 + er.at;  // the tile raised the running max
-      const float nn = er.nn2.x + er.nn2.y;
-      accd += (double)nn;
-      if (TRAIN) {
-        // some u below the window in this wave's tile: redo d (wave-uniform branch)
-        const float st = __builtin_amdgcn_ballot_w64(er.mn < lo) ? epi_fixup(er, p[r], su, lo) : nn;
-        accd2 += (double)st;
-        bf16* d = dS_w + (long long)r * a.CT * 1024 + ((long long)ec.j * nkb + ec.kb) * 1024 + lane * 16;
-        store16(d, (u32x4){er.pk[0], er.pk[1], er.pk[2], er.pk[3]});
-        store16(d + 8, (u32x4){er.pk[4], er.pk[5], er.pk[6], er.pk[7]});
+  auto epi_end = [&](const f32x16& p) {
+    if (e.m > e.m0) e.am = ec.kb * 32 + e.at;  // the tile raised the running max
+    const float nn = e.nn2.x + e.nn2.y;
+    accd += (double)nn;
+    if (TRAIN) {
+      // some u below the window in this wave's tile: redo d (wave-uniform branch)
+      const float st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup(e, p, su, lo) : nn;
+      accd2 += (double)st;
+      bf16* d = dS_w + ((long long)ec.j * nkb + ec.kb) * 1024 + lane * 16;
+      store16(d, (u32x4){e.pk[0], e.pk[1], e.pk[2], e.pk[3]});
+      store16(d + 8, (u32x4){e.pk[4], e.pk[5], e.pk[6], e.pk[7]});
+    }
+    if (ec.kb == nkb - 1) {  // end of a key sample: combine the half-waves' max / argmax
+      float m = e.m;
+      int am = e.am + 4 * h;
+      const float m2 = __shfl_xor(m, 32);
+      const int am2 = __shfl_xor(am, 32);
+      if (m2 > m || (m2 == m && am2 < am)) { m = m2; am = am2; }
+      if (h == 0 && rok) {
+        a.rowmax[(size_t)ec.j * a.R_pad + row] = su * m;  // max S = su * max u (monotone rounding)
+        a.argmax[(size_t)ec.j * a.R_pad + row] = am;
       }
-      if (ec.kb == nkb - 1) {  // end of a key sample: combine the half-waves' max / argmax
-        float m = er.m;
-        int am = er.am + 4 * h;
-        const float m2 = __shfl_xor(m, 32);
-        const int am2 = __shfl_xor(am, 32);
-        if (m2 > m || (m2 == m && am2 < am)) { m = m2; am = am2; }
-        if (h == 0 && rok[r]) {
-          a.rowmax[(size_t)ec.j * a.R_pad + rows[r]] = su * m;  // max S = su * max u (monotone rounding)
-          a.argmax[(size_t)ec.j * a.R_pad + rows[r]] = am;
-        }
-        er.m = -INFINITY;
-        er.am = 0;
-      }
+      e.m = -INFINITY;
+      e.am = 0;
     }
     ec.next(nkb);
   };
 
   // one tile iteration: chain of tile b into c (CH) with the epilogue of tile b-1 from p (EP,
   // FULL or masked), one element per two k-steps
-  auto iter = [&](auto CH, auto EP, auto FULLT, int b, f32x16* c, const f32x16* p) {
+  auto iter = [&](auto CH, auto EP, auto FULLT, int b, f32x16& c, const f32x16& p) {
     constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value, full = decltype(FULLT)::value;
     if constexpr (ch) {
       sync_tile(b);
@@ -383,21 +355,13 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       bf16x8 af[P + 1];
 #pragma unroll
       for (int s = 0; s < P; ++s) af[s] = *(const bf16x8*)(kt + xo[s & 7] + (s >> 3) * 256);
-#pragma unroll
-      for (int r = 0; r < RB; ++r) c[r] = (f32x16){};
+      c = (f32x16){};
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         if (s + P < NS) af[(s + P) % (P + 1)] = *(const bf16x8*)(kt + xo[(s + P) & 7] + ((s + P) >> 3) * 256);
-#pragma unroll
-        for (int r = 0; r < RB; ++r) c[r] = mfma32(af[s % (P + 1)], qf[r][s], c[r]);
-        // one epilogue element per two MFMAs: RB = 1 every other k-step, RB = 2 every k-step
-        // alternating the row blocks
+        c = mfma32(af[s % (P + 1)], qf[s], c);
         if constexpr (ep) {
-          if constexpr (RB == 1) {
-            if (s & 1) epi_elem<TRAIN, full>(e[0], p[0], s >> 1, su2, lo);
-          } else {
-            epi_elem<TRAIN, full>(e[s & 1], p[s & 1], s >> 1, su2, lo);
-          }
+          if (s & 1) epi_elem<TRAIN, full>(e, p, s >> 1, su2, lo);
         }
         // scheduling regions of 4 k-steps: two epilogue elements interleave and fill each
         // other's VALU->SGPR-mask wait states
@@ -405,9 +369,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       }
     } else if constexpr (ep) {
 #pragma unroll
-      for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full>(e[r], p[r], v, su2, lo);
+      for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full>(e, p, v, su2, lo);
     }
     if constexpr (ep) epi_end(p);
   };
@@ -417,27 +379,20 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   auto tile_full = [&]() {
     const int nk = a.klen ? min(a.klen[ec.j], a.Nk_eff) : a.Nk_eff;
     const int nv = __builtin_amdgcn_readfirstlane(nk - ec.kb * 32);
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      e[r].nn2 = (f32x2){0.f, 0.f};
-      e[r].mn = INFINITY;
-      e[r].m0 = e[r].m;
-      e[r].lim = (rok[r] ? min(32, nv) : 0) - 4 * h;
-    }
+    e.nn2 = (f32x2){0.f, 0.f};
+    e.mn = INFINITY;
+    e.m0 = e.m;
+    e.lim = (rok ? min(32, nv) : 0) - 4 * h;
     return nv >= 32;
   };
 
   // chain(b) accumulates into cA while the epilogue of b-1 reads cB; cB = cA after each chain
-  auto roll = [&]() {
-#pragma unroll
-    for (int r = 0; r < RB; ++r) cB[r] = cA[r];
-  };
   iter(T{}, F{}, T{}, 0, cA, cB);
-  roll();
+  cB = cA;
   for (int b = 1; b < nblocks; ++b) {
     if (tile_full()) iter(T{}, T{}, T{}, b, cA, cB);
     else iter(T{}, T{}, F{}, b, cA, cB);
-    roll();
+    cB = cA;
   }
   if (tile_full()) iter(F{}, T{}, T{}, nblocks, cA, cB);
   else iter(F{}, T{}, F{}, nblocks, cA, cB);
@@ -445,11 +400,11 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   double v = wave_sum_d(accd);
   double v2 = wave_sum_d(accd2);
   __syncthreads();
-  if (lane == 0) { red[wave] = v; red[W + wave] = v2; }
+  if (lane == 0) { red[wave] = v; red[WAVES + wave] = v2; }
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0, t2 = 0.0;
-    for (int w = 0; w < W; ++w) { t += red[w]; t2 += red[W + w]; }
+    for (int w = 0; w < WAVES; ++w) { t += red[w]; t2 += red[WAVES + w]; }
     // sum clamp(S, lo, 0)^2 = su^2 sum c^2; sum S^2/temp over [lo, 0] = temp sum u^2 there
     a.part[by * gx + bx] = t * (double)su * (double)su;
     if (a.part2) a.part2[by * gx + bx] = t2 * (double)temp;
@@ -457,9 +412,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
 }
 
 template <bool TRAIN, bool SHORTQ>
-__global__ __launch_bounds__(64 * WAVES / FWD_RB, 1) void pairsim_fwd2_kernel(FwdArgs a) {
+__global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 kbuf[KBUF_ELEMS];
-  fwd_body<TRAIN, FWD_RB>(a, kbuf, blockIdx.x, blockIdx.y, gridDim.x);
+  fwd_body<TRAIN>(a, kbuf, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // Several heads' forwards in ONE launch (the tri-modal step's AV and TV heads, model.py:470-472 /
@@ -476,13 +431,13 @@ struct MultiArgs {
 };
 
 template <bool TRAIN>
-__global__ __launch_bounds__(64 * WAVES / FWD_RB, 1) void pairsim_fwd_multi_kernel(MultiArgs m) {
+__global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd_multi_kernel(MultiArgs m) {
   __shared__ __attribute__((aligned(16))) bf16 kbuf[KBUF_ELEMS];
   const int b = blockIdx.x;
   const int q = (m.n > 1 && b >= m.first[1]) ? 1 : 0;  // uniform
   const int local = b - m.first[q];
   const int gx = m.gx[q];
-  fwd_body<TRAIN, FWD_RB>(m.p[q], kbuf, local % gx, local / gx, gx);
+  fwd_body<TRAIN>(m.p[q], kbuf, local % gx, local / gx, gx);
 }
 
 // Diagonal blocks of S for the regularisers (model.py:417-418 / 524-525):
@@ -536,7 +491,7 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
   a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part; a.klen = k_len;
   const int xw = xb * (256 / ROWS_PER_WG);  // xb counts 256-row blocks
   const bool sq = Nq <= 32;
-  const dim3 grid(xw, ys), block(64 * WAVES / FWD_RB);
+  const dim3 grid(xw, ys), block(64 * WAVES);
   if (dS && sq) hipLaunchKernelGGL((pairsim_fwd2_kernel<true, true>), grid, block, 0, stream, a);
   else if (dS) hipLaunchKernelGGL((pairsim_fwd2_kernel<true, false>), grid, block, 0, stream, a);
   else if (sq) hipLaunchKernelGGL((pairsim_fwd2_kernel<false, true>), grid, block, 0, stream, a);
@@ -574,7 +529,7 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
     m.gx[i] = xb[order[i]] * (256 / ROWS_PER_WG);
     m.first[i + 1] = m.first[i] + m.gx[i] * ys[order[i]];
   }
-  const dim3 grid(m.first[n]), block(64 * WAVES / FWD_RB);
+  const dim3 grid(m.first[n]), block(64 * WAVES);
   if (train) hipLaunchKernelGGL((pairsim_fwd_multi_kernel<true>), grid, block, 0, stream, m);
   else hipLaunchKernelGGL((pairsim_fwd_multi_kernel<false>), grid, block, 0, stream, m);
   TRIAD_CHECK_LAUNCH();
