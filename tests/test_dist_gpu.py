@@ -378,6 +378,7 @@ def _mode_g_trainer_worker(rank, world, port, q_out, unfreeze_audio=1):
         q_out.put((rank, "error", traceback.format_exc(), None, None))
 
 
+@pytest.mark.late
 def test_mode_g_trainer_two_ranks_with_unfreeze_flip():
     """TriadTrainer(global_negatives=True) at world size 2 (gloo on the box's one GPU): the head's
     key all-gather / clip-row gather / dK reduce-scatter run on the model's group while the
@@ -411,23 +412,36 @@ def test_mode_g_trainer_two_ranks_with_unfreeze_flip():
     np.testing.assert_array_equal(t0, t1)
     # single process at B_g = 4: rank-major concatenation of the two ranks' batches, masks from the
     # same shared seed
-    m = _mode_r_model()
-    m.audio_embedder.normalize = _no_znorm
-    m.visual_embedder.set_global_mask(1, 0)
-    _embed_in_chunks(m, 2)
-    tr = _mode_g_trainer(m, None)
+    def single():
+        m = _mode_r_model()
+        m.audio_embedder.normalize = _no_znorm
+        m.visual_embedder.set_global_mask(1, 0)
+        _embed_in_chunks(m, 2)
+        tr = _mode_g_trainer(m, None)
+        losses = []
+        for step in range(2):
+            if step:
+                _load_flat_params(tr, p0[step - 1])
+            b0, b1 = _mode_r_batch(step, 0), _mode_r_batch(step, 1)
+            out = tr.step(torch.cat([b0[0], b1[0]]), torch.cat([b0[1], b1[1]]), list(b0[2]) + list(b1[2]),
+                          phase="full_joint")
+            losses.append(float(out["loss"]))
+        return m, tr, losses, [g.cpu().numpy() for g in tr.reduced]
+
+    m, tr, ls, gs = single()
+    bad = []
     for step in range(2):
-        if step:
-            _load_flat_params(tr, p0[step - 1])
-        b0, b1 = _mode_r_batch(step, 0), _mode_r_batch(step, 1)
-        f = torch.cat([b0[0], b1[0]])
-        a = torch.cat([b0[1], b1[1]])
-        t = list(b0[2]) + list(b1[2])
-        out = tr.step(f, a, t, phase="full_joint")
-        assert abs(float(out["loss"]) - l0[step]) <= 1e-4 * abs(l0[step]), (step, float(out["loss"]), l0[step])
-        rel = _group_rel(tr, g0[step], tr.reduced[step].cpu().numpy())
+        assert abs(ls[step] - l0[step]) <= 1e-4 * abs(l0[step]), (step, ls[step], l0[step])
+        rel = _group_rel(tr, g0[step], gs[step])
         print(f"mode G step {step}: reduced-gradient rel error per group {rel}")
-        worst = _worst_params(m, tr, g0[step], tr.reduced[step].cpu().numpy(), tr.groups["others"])
-        print(f"mode G step {step}: worst parameters {worst}")
-        for name, r in rel.items():
-            assert r < 1e-2, (step, name, r, worst)
+        print(f"mode G step {step}: worst parameters {_worst_params(m, tr, g0[step], gs[step], tr.groups['others'])}")
+        bad += [(step, name, r, _worst_params(m, tr, g0[step], gs[step], tr.groups[name], k=4))
+                for name, r in rel.items() if not r < 1e-2]
+    if bad:
+        # diagnosis only (the test has failed): is the single process reproducible, i.e. which of
+        # the two sides is the odd one out?
+        _, _, ls2, gs2 = single()
+        same = all(np.array_equal(a, b) for a, b in zip(gs, gs2)) and ls == ls2
+        rel2 = [_group_rel(tr, g0[s], gs2[s]) for s in range(2)]
+        raise AssertionError(f"Mode G vs single process beyond the bf16 bar: {bad}; a second single-process run "
+                             f"equals the first: {same}, its errors vs the ranks per step: {rel2}")

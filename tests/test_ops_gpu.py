@@ -395,6 +395,7 @@ def test_side_stream_weight_grads_weight_used_twice():
         assert torch.equal(g, g_main)
 
 
+@pytest.mark.late
 def test_modality_streams_match_single_stream():
     """forward_triad with the audio / text backbones on their own streams beside the ViT (the
     bench's execution mode) against the single-stream order: one TriadTrainer step from identical

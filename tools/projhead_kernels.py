@@ -11,7 +11,7 @@ import os
 import sys
 
 CASES = (("visual", 65536, 768), ("audio", 50944, 768), ("text", 8192, 768), ("c5-visual", 43808, 1024))
-FORMS = ("fused", "passes")
+FORMS = tuple(os.environ.get("TRIAD_PROJHEAD_FORMS", "fused,passes").split(","))
 
 
 def run(iters):
@@ -46,7 +46,7 @@ def run(iters):
             seg += 3
 
 
-def parse(path, iters):
+def parse(path, iters, detail=False):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     marks = [(i, r) for i, r in enumerate(rows) if "l2norm_rows_kernel" in r["Kernel_Name"]]
@@ -63,6 +63,14 @@ def parse(path, iters):
             fw = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[a + 1:b]) / iters / 1e3
             bw = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[b + 1:c]) / iters / 1e3
             fl = 2.0 * M * (H * 512 + 512 * 512)
+            if detail:
+                for tag, lo, hi in (("fwd", a, b), ("bwd", b, c)):
+                    per = {}
+                    for r in rows[lo + 1:hi]:
+                        k = r["Kernel_Name"].split("(")[0][:90]
+                        per[k] = per.get(k, 0) + (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / iters / 1e3
+                    for k, us in sorted(per.items(), key=lambda kv: -kv[1]):
+                        print(f"   {form} {name} {tag} {us:8.1f} us  {k}")
             print(json.dumps({"form": form, "head": name, "M": M, "H": H, "fwd_us": round(fw, 1),
                               "fwd_TFLOPs": round(fl / fw / 1e6, 1), "bwd_us": round(bw, 1),
                               "bwd_TFLOPs": round(2 * fl / bw / 1e6, 1),
@@ -73,8 +81,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--parse")
+    ap.add_argument("--detail", action="store_true", help="per-kernel-name microseconds per call")
     a = ap.parse_args()
     if a.parse:
-        parse(a.parse, a.iters)
+        parse(a.parse, a.iters, a.detail)
     else:
         run(a.iters)
