@@ -320,6 +320,41 @@ def test_tile_gemm_vs_torch(panels, ct):
         assert _rel(dK.float().cpu(), refK.cpu()) < 5e-3
 
 
+@pytest.mark.parametrize("panels,ct,splits", [(7, 36, 1), (7, 36, 3), (16, 64, 4), (3, 4, 1), (8, 28, 4)])
+def test_tile_gemm_packed_bit_identical_to_ring(panels, ct, splits):
+    """The direct-B form (triad_bfrag_pack + triad_tile_gemm_packed / _packed_slabs: B fragments
+    straight to registers, dK with two k tiles per stage) against the ring form (B through LDS):
+    the same fragments into the same MFMA order, so bit-identical outputs and fp32 slabs -- split
+    counts whose k ranges end in a short (one-tile) stage included."""
+    from triad_amd._lib import call, ptr, stream_ptr
+    g = torch.Generator(device=dev).manual_seed(panels * 10 + ct + splits)
+    R_pad, CT = panels * 128, ct
+    dS = (torch.randn(R_pad // 32 * CT * 1024, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    K = torch.randn(CT * 32, 512, device=dev, generator=g).to(torch.bfloat16)
+    Q = torch.randn(R_pad, 512, device=dev, generator=g).to(torch.bfloat16)
+    alpha = torch.tensor([0.75], device=dev)
+    st = stream_ptr()
+    cases = [(0, K, R_pad, CT)] + ([(1, Q, CT * 32, R_pad // 32)] if CT % 4 == 0 else [])
+    for dk, Bm, M, nkt in cases:
+        Bp = torch.empty(nkt * 32 * 512, dtype=torch.bfloat16, device=dev)
+        call("triad_bfrag_pack", ptr(Bm), nkt, dk, ptr(Bp), st)
+        slabs = torch.empty(splits * M * 512, device=dev) if splits > 1 else None
+        slabs2 = torch.empty(splits * M * 512, device=dev) if splits > 1 else None
+        ring = torch.empty(M, 512, dtype=torch.bfloat16, device=dev)
+        packed = torch.empty_like(ring)
+        call("triad_tile_gemm", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), splits, ptr(slabs), ptr(ring), st)
+        call("triad_tile_gemm_packed", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), splits, ptr(slabs2), ptr(packed),
+             st)
+        torch.cuda.synchronize()
+        assert torch.equal(ring, packed), (dk, M, nkt, splits)
+        if splits > 1:
+            assert torch.equal(slabs, slabs2)
+            call("triad_tile_gemm_slabs", ptr(dS), CT, dk, ptr(Bm), M, nkt, splits, ptr(slabs), st)
+            call("triad_tile_gemm_packed_slabs", ptr(dS), CT, dk, ptr(Bp), M, nkt, splits, ptr(slabs2), st)
+            torch.cuda.synchronize()
+            assert torch.equal(slabs, slabs2), (dk, M, nkt, splits)
+
+
 @pytest.mark.parametrize("B,Na,Nt,Nv,budget", [(6, 49, 16, 70, None), (16, 199, 32, 205, None),
                                                (5, 300, 8, 40, "mixed"), (3, 2, 1, 33, None)])
 def test_pair_launch_matches_two_heads(B, Na, Nt, Nv, budget):

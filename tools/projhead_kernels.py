@@ -67,10 +67,12 @@ def parse(path, iters, detail=False):
                 for tag, lo, hi in (("fwd", a, b), ("bwd", b, c)):
                     per = {}
                     for r in rows[lo + 1:hi]:
-                        k = r["Kernel_Name"].split("(")[0][:90]
-                        per[k] = per.get(k, 0) + (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / iters / 1e3
-                    for k, us in sorted(per.items(), key=lambda kv: -kv[1]):
-                        print(f"   {form} {name} {tag} {us:8.1f} us  {k}")
+                        kn = r["Kernel_Name"].replace("void ", "")
+                        kn = kn[:kn.find("(")] if kn.find("(") > 0 else kn
+                        kn = kn[:110]
+                        per[kn] = per.get(kn, 0) + (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / iters / 1e3
+                    for kn, us in sorted(per.items(), key=lambda kv: -kv[1]):
+                        print(f"   {form} {name} {tag} {us:8.1f} us  {kn}")
             print(json.dumps({"form": form, "head": name, "M": M, "H": H, "fwd_us": round(fw, 1),
                               "fwd_TFLOPs": round(fl / fw / 1e6, 1), "bwd_us": round(bw, 1),
                               "bwd_TFLOPs": round(2 * fl / bw / 1e6, 1),

@@ -169,9 +169,220 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __re
     }
 }
 
+// ---- direct-B form ----------------------------------------------------------------------------
+// Wave w only ever multiplies columns [64w, 64w + 64) of B, so B needs no LDS: its fragments are
+// pre-arranged once per backward (bfrag_pack_kernel: the exact bf16x8 each lane takes from the
+// swizzled LDS image above, written out) and each wave streams its own 4 KB per k tile straight
+// into registers with four coalesced 16-byte loads, stages ahead. Only A (8 KB per tile,
+// shared by all eight waves) goes through LDS: one LDS-DMA piece per wave per tile instead of
+// five, and no B fragment reads from LDS.
+//   packed B: k tile kt, wave w, chunk u = 2 s + n (k-step s, 32-column block n):
+//             bf16x8 of lane L at ((kt * 8 + w) * 4 + u) * 512 + L * 8
+// KS k tiles (32 deep each) per stage and one workgroup barrier per stage; DD stages in flight
+// ahead of the one being multiplied (A ring slots = B register ring depth = DD + 1). Measured per
+// GEMM (tools/bwd_micro.py, profiles/r03_tile_gemm_db_ab.log): dQ KS = 1, DD = 3; dK KS = 2,
+// DD = 2 (the transposed A reads favour half the barriers; dQ loses 6 % with them).
+
+template <bool DK>
+__global__ __launch_bounds__(512) void bfrag_pack_kernel(const bf16* __restrict__ B, bf16* __restrict__ Bp) {
+  __shared__ __attribute__((aligned(16))) bf16 img[TBK * TBN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, q4 = (lane & 15) >> 2;
+  const long long kt = blockIdx.x;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int k = wave * 4 + r;
+    glds16(B + (kt * TBK + k) * TBN + (lane ^ ((k & 3) << 2)) * 8, img + k * TBN);
+  }
+  lds_dma_barrier();
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int n0 = wave * 64 + n * 32;
+      const bf16x8 f = DK ? bfrag(img, 16 * s + 8 * h + q4, 4, n0, lane) : bfrag(img, 16 * s + 4 * h + q4, 8, n0, lane);
+      *(bf16x8*)(Bp + ((kt * 8 + wave) * 4 + 2 * s + n) * 512 + lane * 8) = f;
+    }
+}
+
+// 16-byte global load hidden from hipcc's waitcnt bookkeeping (it would otherwise drain vmcnt(0)
+// at the first use, glds in flight): the caller's counted s_waitcnt vmcnt before the barrier
+// retires it. The destination registers are only ever read after that wait.
+__device__ __forceinline__ bf16x8 gload16(const bf16* p) {
+  bf16x8 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// one stage: k tiles kt .. kt + KS - 1 (clamped to kt_last: a short last stage re-loads its last
+// tile, so every stage issues exactly 5 KS vm ops per wave -- 4 B loads + 1 A piece per tile --
+// and the counted waits hold)
+template <bool DK, int KS>
+__device__ __forceinline__ void db_stage(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ Bp,
+                                         int mt0, int kt, int kt_last, bf16* adst, bf16x8 (&bq)[4 * KS], int wave,
+                                         int lane) {
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int ktk = min(kt + k, kt_last);
+    const bf16* src = Bp + ((long long)ktk * 8 + wave) * 2048 + lane * 8;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bq[4 * k + u] = gload16(src + u * 512);
+    const int t = wave >> 1, half = wave & 1;
+    const int pos = half * 64 + lane;
+    const int c = DK ? swz_k(pos) : swz_q(pos);
+    const long long tile = DK ? ((long long)ktk * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + ktk);
+    glds16(Dt + tile * 1024 + c * 8, adst + k * 4096 + t * 1024 + half * 512);
+  }
+}
+
+template <int OPS>
+__device__ __forceinline__ void db_wait(int younger) {
+  if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * OPS) : "memory");
+  else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPS) : "memory");
+  else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool DK, bool SLAB, int KS, int DD>
+__global__ __launch_bounds__(512, 1) void tile_gemm_db_kernel(const bf16* __restrict__ Dt, long long CT,
+                                                              const bf16* __restrict__ Bp, int M, int nkt_total,
+                                                              int kt_per_split, const float* __restrict__ alpha_p,
+                                                              void* __restrict__ Cout) {
+  static_assert(DD >= 1 && DD <= 4 && 5 * KS * (DD - 1) <= 63, "stage shape");
+  constexpr int NB = DD + 1;
+  __shared__ __attribute__((aligned(16))) bf16 lds[NB * KS * 4096];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  const int m0 = swz * TBM, mt0 = m0 / 32;
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int nkt = __builtin_amdgcn_readfirstlane(min(kt_per_split, nkt_total - kt0));
+  const int kt_last = kt0 + nkt - 1;
+  const int nst = (nkt + KS - 1) / KS;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[t][n] = (f32x16){};
+
+  bf16x8 bq[NB][4 * KS];
+#pragma unroll
+  for (int p = 0; p < DD; ++p)
+    if (p < nst) db_stage<DK, KS>(Dt, CT, Bp, mt0, kt0 + p * KS, kt_last, lds + p * KS * 4096, bq[p], wave, lane);
+  for (int st0 = 0; st0 < nst; st0 += NB) {
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int st = st0 + u;
+      if (st >= nst) break;
+      db_wait<5 * KS>(min(DD - 1, nst - 1 - st));   // uniform: stages st+1 .. stay in flight
+      __syncthreads();
+      const bool pf = st + DD < nst;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        if (st * KS + k >= nkt) break;       // a short last stage
+        const bf16* As = lds + (u * KS + k) * 4096;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 af[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const bf16* tile = As + t * 1024;
+            if (!DK) {
+              af[t] = *(const bf16x8*)(tile + swz_q(2 * l32 + 64 * h + s) * 8);
+            } else {
+              const int a = 2 * (g & 1) + (p4 >> 1), hh = p4 & 1;
+              s16x4* rp = (s16x4*)&af[t];
+#pragma unroll
+              for (int tt = 0; tt < 2; ++tt) {
+                const int qry = 16 * s + 8 * h + 4 * tt + q4;
+                const int c = (qry + 32 * hh) * 2 + (a >> 1);
+                rp[tt] = lds_tr16(tile + swz_k(c) * 8 + 4 * (a & 1));
+              }
+            }
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int n = 0; n < 2; ++n) acc[t][n] = mfma32(af[t], bq[u][4 * k + 2 * s + n], acc[t][n]);
+          if (k == 0 && s == 0 && pf) {
+            // the stage DD ahead: its A slots were last read before this stage's barrier
+            __builtin_amdgcn_sched_barrier(0);
+            db_stage<DK, KS>(Dt, CT, Bp, mt0, kt0 + (st + DD) * KS, kt_last,
+                         lds + ((u + DD) % NB) * KS * 4096, bq[(u + DD) % NB], wave, lane);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    }
+  }
+
+  const float alpha = SLAB ? 1.f : *alpha_p;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int col = wave * 64 + n * 32 + l32;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int m = m0 + t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        const float val = alpha * acc[t][n][v];
+        if (SLAB) ((float*)Cout)[((size_t)blockIdx.y * M + m) * TBN + col] = val;
+        else ((bf16*)Cout)[(size_t)m * TBN + col] = (bf16)val;
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+// Packed B fragments for the direct-B GEMM form: B [nkt * 32][512] bf16 -> Bp (same size).
+int triad_bfrag_pack(const void* B, int nkt, int dk, void* Bp, hipStream_t stream) {
+  if (nkt <= 0 || !B || !Bp) return TRIAD_EINVAL;
+  if (dk) hipLaunchKernelGGL(bfrag_pack_kernel<true>, dim3(nkt), dim3(512), 0, stream, (const bf16*)B, (bf16*)Bp);
+  else hipLaunchKernelGGL(bfrag_pack_kernel<false>, dim3(nkt), dim3(512), 0, stream, (const bf16*)B, (bf16*)Bp);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+// triad_tile_gemm over packed B fragments (triad_bfrag_pack of the same B and dk).
+int triad_tile_gemm_packed(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, const float* alpha,
+                           int splits, float* slabs, void* C, hipStream_t stream) {
+  if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
+  const int kps = (nkt + splits - 1) / splits;
+  dim3 grid(M / TBM, splits);
+  const bf16* d = (const bf16*)Dt;
+  const bf16* b = (const bf16*)Bp;
+  void* out = splits > 1 ? (void*)slabs : C;
+  if (dk) {
+    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db_kernel<true, false, 2, 2>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
+    else hipLaunchKernelGGL((tile_gemm_db_kernel<true, true, 2, 2>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
+  } else {
+    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db_kernel<false, false, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
+    else hipLaunchKernelGGL((tile_gemm_db_kernel<false, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
+  }
+  TRIAD_CHECK_LAUNCH();
+  if (splits == 1) return TRIAD_OK;
+  return triad_sum_slabs(slabs, splits, (long long)M * TBN, alpha, 1, C, stream);
+}
+
+// Unscaled fp32 slabs only, over packed B (the direct-B form of triad_tile_gemm_slabs).
+int triad_tile_gemm_packed_slabs(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, int splits,
+                                 float* slabs, hipStream_t stream) {
+  if (M % TBM || nkt <= 0 || splits < 1 || !slabs) return TRIAD_EINVAL;
+  const int kps = (nkt + splits - 1) / splits;
+  dim3 grid(M / TBM, splits);
+  const bf16* d = (const bf16*)Dt;
+  const bf16* b = (const bf16*)Bp;
+  if (dk) hipLaunchKernelGGL((tile_gemm_db_kernel<true, true, 2, 2>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  else hipLaunchKernelGGL((tile_gemm_db_kernel<false, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
 
 // dQ (dk = 0): M = query rows (R_pad), nkt = key tiles (C_pad / 32), B = K [C_pad][512].
 // dK (dk = 1): M = key rows (CT * 32), nkt = query tiles (R_pad / 32), B = Q [R_pad][512].

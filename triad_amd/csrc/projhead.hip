@@ -144,7 +144,18 @@ __global__ __launch_bounds__(256) void colsum8_kernel(const bf16* __restrict__ X
   const long long a = blockIdx.y * per, b = min(rows, a + per);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c8 * 8 < cols && rl < nrl) {
-    for (long long r = a + rl; r < b; r += nrl) {
+    // four rows' loads in flight per thread (one dependent load per iteration left the
+    // 3,072-column bias gradients at ~3 TB/s, profiles/r03_bench_kernel_stats_r03e.csv)
+    long long r = a + rl;
+    for (; r + 3 * nrl < b; r += 4 * nrl) {
+      const bf16x8 v0 = *(const bf16x8*)(X + r * ld + c8 * 8);
+      const bf16x8 v1 = *(const bf16x8*)(X + (r + nrl) * ld + c8 * 8);
+      const bf16x8 v2 = *(const bf16x8*)(X + (r + 2 * nrl) * ld + c8 * 8);
+      const bf16x8 v3 = *(const bf16x8*)(X + (r + 3 * nrl) * ld + c8 * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] += ((float)v0[i] + (float)v1[i]) + ((float)v2[i] + (float)v3[i]);
+    }
+    for (; r < b; r += nrl) {
       const bf16x8 v = *(const bf16x8*)(X + r * ld + c8 * 8);
 #pragma unroll
       for (int i = 0; i < 8; ++i) s[i] += (float)v[i];
@@ -267,7 +278,9 @@ int triad_sum_slabs(const float* slabs, int nslab, long long n, const float* alp
 int triad_colsum_splits(long long rows, int cols) {
   const int cg = cols / 8 < 256 ? cols / 8 : 256;
   const int gx = (cols / 8 + cg - 1) / cg;
-  long long s = 1024 / gx;
+  // 256 column-slab blocks fill the chip for the first pass; more slabs only lengthen the
+  // reduce's load chains (1,024 slabs: a 24 us reduce at 512 columns, profiles/r03_projhead_kernels.log)
+  long long s = 256 / gx;
   if (s > rows / 16) s = rows / 16;
   return (int)(s < 1 ? 1 : s);
 }

@@ -97,14 +97,27 @@ def colsum(x, out_dtype=torch.float32, backbone=False):
     return out
 
 
-def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream, meta=None):
-    """dQ = alpha dS K (dk=0) / dK = alpha dS^T Q (dk=1) over the tiled dS (triad_tile_gemm),
-    split-K over the CUs when the row panels alone leave them idle. (A stream-K form -- one run
-    of (row panel, k tile) units per CU, no slab round trip -- measured slower: runs start at
-    different k offsets, so CUs of one XCD no longer share the streamed B panel in L2.)"""
+def pack_b(B, nkt, dk, stream):
+    """B [nkt*32][512] bf16 -> its MFMA fragments in the direct-B GEMM's order (triad_bfrag_pack):
+    one pass over B, after which each wave of the GEMM streams its own columns into registers."""
+    Bp = torch.empty(nkt * 32 * D, dtype=torch.bfloat16, device=B.device)
+    call("triad_bfrag_pack", ptr(B), nkt, dk, ptr(Bp), stream, meta=dict(tag="bfrag-pack", flops=0.0))
+    return Bp
+
+
+def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream, meta=None, Bp=None):
+    """dQ = alpha dS K (dk=0) / dK = alpha dS^T Q (dk=1) over the tiled dS, split-K over the CUs
+    when the row panels alone leave them idle. (A stream-K form -- one run of (row panel, k tile)
+    units per CU, no slab round trip -- measured slower: runs start at different k offsets, so CUs
+    of one XCD no longer share the streamed B panel in L2.) The direct-B form
+    (triad_tile_gemm_packed over pack_b's fragments, bit-identical to triad_tile_gemm): 6-7 %
+    faster at the c3 shapes (profiles/r03_tile_gemm_db_ab.log); Bp: B already packed."""
     sp = _gemm_splits(M // 128, nkt, M)
     slabs = torch.empty(sp * M * D, dtype=torch.float32, device=out.device) if sp > 1 else None
-    call("triad_tile_gemm", ptr(dS), CT, dk, ptr(B), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream, meta=meta)
+    if Bp is None:
+        Bp = pack_b(B, nkt, dk, stream)
+    call("triad_tile_gemm_packed", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream,
+         meta=meta)
 
 
 def _gemm_splits(wgs, nkt, M, cus=256, max_splits=8, t_tile=1.0e-6, hbm=5.0e12):
@@ -175,7 +188,7 @@ def recompute_backward(g: Geometry, Qb, Kb, temp, kind, diag_off, argmax, dclip,
     triad_pairsim_dS recomputes S for those keys and writes that chunk's full dS (clamp + max +
     diagonal terms, weighted by coef), dK rows of those keys come from one tile GEMM (complete:
     a key's gradient only involves its own dS columns), and dQ accumulates the chunks' fp32 partial
-    sums (triad_tile_gemm_slabs), reduced once at the end. Peak dS memory = one chunk.
+    sums (triad_tile_gemm_packed_slabs), reduced once at the end. Peak dS memory = one chunk.
     Returns (dQ [R_pad][512] bf16 | None, dK [CT*32][512] bf16 | None, dt_part fp64)."""
     dev = Qb.device
     nkb = g.Nk_pad // 32
@@ -193,8 +206,10 @@ def recompute_backward(g: Geometry, Qb, Kb, temp, kind, diag_off, argmax, dclip,
         else:
             splits = _gemm_splits(g.R_pad // 128, chunk * nkb, g.R_pad)
             slabs = torch.empty(nchunks * splits, g.R_pad, D, dtype=torch.float32, device=dev)
+    Qp = None
     if need_k:
         dK = torch.empty(CT * 32, D, dtype=torch.bfloat16, device=dev)
+        Qp = pack_b(Qb, g.R_pad // 32, 1, stream)   # once, for every chunk's dK
     parts = []
     for c in range(nchunks):
         j0 = c * chunk
@@ -215,11 +230,12 @@ def recompute_backward(g: Geometry, Qb, Kb, temp, kind, diag_off, argmax, dclip,
                 tile_gemm(dS, ctc, 0, Kc, g.R_pad, nc * nkb, temp, dQ, stream,
                           meta=dict(kind=kind, flops=fl, what="dQ"))
             else:
-                call("triad_tile_gemm_slabs", ptr(dS), ctc, 0, ptr(Kc), g.R_pad, nc * nkb, splits,
+                Kp = pack_b(Kc, nc * nkb, 0, stream)
+                call("triad_tile_gemm_packed_slabs", ptr(dS), ctc, 0, ptr(Kp), g.R_pad, nc * nkb, splits,
                      ptr(slabs[c * splits]), stream, meta=dict(kind=kind, flops=fl, what="dQ"))
         if need_k:
             tile_gemm(dS, ctc, 1, Qb, ctc * 32, g.R_pad // 32, temp, dK[j0 * g.Nk_pad:], stream,
-                      meta=dict(kind=kind, flops=fl, what="dK"))
+                      meta=dict(kind=kind, flops=fl, what="dK"), Bp=Qp)
     if need_q and nchunks > 1:
         dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
         call("triad_sum_slabs", ptr(slabs), nchunks * splits, g.R_pad * D, ptr(temp), 1, ptr(dQ), stream)
