@@ -153,6 +153,100 @@ def test_global_negatives_pair_launch_two_ranks_match_single_process():
     assert abs(dt - T) <= 1e-3 * abs(T) + 1e-6
 
 
+# ---- c4 (Mode G at the per-rank batch of the 8-GPU config) against the fp64 oracle ---------
+C4_BL, C4_NA, C4_NV, C4_NT = 256, 199, 212, 32
+
+
+def _c4_inputs(world):
+    """Head features of a B_g = world x 256 tri-modal batch at the c3 / c4 token counts (199 audio
+    tokens, 212 visual tokens after patch dropout, 32 caption tokens with ragged masks)."""
+    Bg = world * C4_BL
+    g = torch.Generator().manual_seed(4242)
+    qa = (torch.randn(Bg, C4_NA, 512, generator=g) * 0.58).to(torch.bfloat16)
+    ka = (torch.randn(Bg, C4_NV, 512, generator=g) * 0.58).to(torch.bfloat16)
+    qt = (torch.randn(Bg, C4_NT, 512, generator=g) * 0.58).to(torch.bfloat16)
+    kt = (torch.randn(Bg, C4_NV, 512, generator=g) * 0.58).to(torch.bfloat16)
+    lens = torch.randint(C4_NT // 4, C4_NT + 1, (Bg,), generator=g)
+    mask = (torch.arange(C4_NT)[None] < lens[:, None]).long()
+    return qa, ka, qt, kt, mask
+
+
+def _c4_worker(rank, world, port, q_out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from triad_amd import ops
+        qa, ka, qt, kt, mask = _c4_inputs(world)
+        sl = slice(rank * C4_BL, (rank + 1) * C4_BL)
+        xs = [x[sl].cuda().requires_grad_(True) for x in (qa, ka, qt, kt)]
+        t = torch.tensor(1.5, device="cuda", requires_grad=True)
+        (la, sa, _), (lt, st, _) = ops.contrastive_heads_av_tv(xs[0], xs[1], xs[2], xs[3], t, mask[sl].cuda(),
+                                                               threshold=0.8, sparsity_weight=0.01,
+                                                               group=dist.group.WORLD)
+        (la[0] + lt[0]).backward()
+        # numpy (bf16 bits as int16), not tensors: a tensor in the queue is an fd of this process
+        q_out.put((rank, [float(x.detach()) for x in la], [float(x.detach()) for x in lt], sa.cpu().numpy(),
+                   st.cpu().numpy(), [x.grad.view(torch.int16).cpu().numpy() for x in xs], float(t.grad)))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q_out.put((rank, "error", traceback.format_exc(), None, None, None, None))
+
+
+def test_c4_mode_g_per_rank_batch_vs_oracle():
+    """BASELINE c4 (tri-modal B = 256 per GPU, RCCL key all-gather for global negatives) at the
+    per-rank batch it runs: two ranks of 256 triples each (gloo on the box's one GPU; c4 has eight,
+    i.e. 2,048 key samples per rank instead of 512 here), every rank through the tri-modal pair
+    launch with the keys of both heads all-gathered, clip rows gathered, key gradients
+    reduce-scattered -- against the chunked fp64 ORACLE of the reference loss at B_g = 512
+    (model.py:370-472 / 490-593): both heads' losses at 1e-4, each rank's feature gradients at the
+    bf16 bar with the near-tie rule, d/dtemp (sum over ranks) at 1e-3."""
+    from oracle import ref_cpu
+    world = 2
+    ctx = mp.get_context("spawn")
+    qo = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_c4_worker, args=(r, world, port, qo)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([qo.get(timeout=600) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert not isinstance(r[1], str), r[2]
+    qa, ka, qt, kt, mask = _c4_inputs(world)
+    temp = 1.5
+    dt_ref = 0.0
+    names = ("total", "ce", "reg", "aux")
+    for kind, q, k, m, li, gq_i, gk_i in (("av", qa, ka, None, 1, 0, 1), ("tv", qt, kt, mask, 2, 2, 3)):
+        qd, kd = q.cuda().float(), k.cuda().float()
+        o = ref_cpu.head_loss_chunked(kind, qd, kd, temp, q_mask=None if m is None else m.cuda(), threshold=0.8,
+                                      weight=0.01, chunk=4)
+        tq, tk, n = ref_cpu.near_ties(qd, kd, temp)
+        assert float(tq.float().mean()) < 0.03 and float(tk.float().mean()) < 0.03, (int(tq.sum()), int(tk.sum()))
+        dt_ref += float(o["dtemp"])
+        for rank, la, lt, sa, st, grads, gt in res:
+            losses = la if kind == "av" else lt
+            for got, key in zip(losses, names):
+                assert abs(got - o[key]) <= 1e-5 + 1e-4 * abs(o[key]), (kind, rank, key, got, o[key])
+            stats = sa if kind == "av" else st   # the statistics of the GLOBAL clip matrix on every rank
+            for got, (key, want) in zip(np.asarray(stats, dtype=np.float64).ravel()[:6], o["stats"].items()):
+                assert abs(got - want) <= 1e-4 + 1e-4 * abs(want), (kind, rank, key, got, want)
+            sl = slice(rank * C4_BL, (rank + 1) * C4_BL)
+            gq = torch.from_numpy(grads[gq_i]).view(torch.bfloat16).cuda()
+            gk = torch.from_numpy(grads[gk_i]).view(torch.bfloat16).cuda()
+            eq = ref_cpu.grad_rel(gq, o["dq"][sl], tq[sl])
+            ek = ref_cpu.grad_rel(gk, o["dk"][sl], tk[sl])
+            print(f"c4 per-rank {kind} rank {rank}: feature-gradient rel dq {eq:.3e} dk {ek:.3e} "
+                  f"(near-tie rows left out: {int(tq[sl].sum())} query / {int(tk[sl].sum())} key, {n} ties in all)")
+            assert eq < 1e-2 and ek < 1e-2, (kind, rank, eq, ek)
+        del o
+        torch.cuda.empty_cache()
+    dt = sum(r[6] for r in res)
+    assert abs(dt - dt_ref) <= 1e-3 * abs(dt_ref) + 1e-6, (dt, dt_ref)
+
+
 # ---- Mode R: TriadTrainer itself at world size 2 ---------------------------------------
 def _mode_r_model():
     """ViT-S/14-reg + HuBERT-base + DistilBERT (c1-sized backbones), every dropout / LayerDrop /
