@@ -3,7 +3,9 @@ run under rocprofv3 --kernel-trace, each (form, rows) case does `iters` forward 
 backward calls, each segment fenced by a marker launch (triad_l2norm_rows on a tiny tensor,
 rows = a segment id). Then `python tools/projhead_kernels.py --parse <kernel_trace.csv>` sums the
 kernel durations between markers (one stream, so kernels do not overlap) and prints per call
-fwd / bwd microseconds and algorithmic TFLOP/s (fwd 2 M (H 512 + 512 512), bwd twice that)."""
+fwd / bwd microseconds and algorithmic TFLOP/s (fwd 2 M (H 512 + 512 512), bwd twice that).
+Gradients are released after each backward, so no accumulation kernels are counted (round 3;
+the round-2 figures included ~45-75 us of them at 65,536 rows). --detail: per-kernel times."""
 import argparse
 import csv
 import json
@@ -41,6 +43,10 @@ def run(iters):
             mark(seg + 1)
             for y in outs:
                 y.backward(gy)
+                h.grad = None   # autograd then stores each gradient instead of adding it (no add kernels)
+                for mod in (p1, ln, p2):
+                    for prm in mod.parameters():
+                        prm.grad = None
             mark(seg + 2)
             torch.cuda.synchronize()
             seg += 3
