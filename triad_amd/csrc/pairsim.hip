@@ -197,25 +197,26 @@ __global__ __launch_bounds__(256) void clip_reduce_kernel(const float* __restric
                                                           int Nq, int Bq, int Bk,
                                                           const float* __restrict__ qmask,
                                                           float* __restrict__ clip, float* __restrict__ qw) {
+  // one wave per (i, j): every row's loads in flight at once (a wave looping over 64 rows
+  // made this a latency-bound 0.14 ms launch at B = 256)
   const int j = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int i = wave; i < Bq; i += nw) {
-    float s = 0.f, cnt = 0.f;
-    const float* rm = rowmax + (size_t)j * R_pad + (size_t)i * Nq;
+  const int lane = threadIdx.x & 63, i = blockIdx.y * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (i >= Bq) return;
+  float s = 0.f, cnt = 0.f;
+  const float* rm = rowmax + (size_t)j * R_pad + (size_t)i * Nq;
+  for (int q = lane; q < Nq; q += 64) {
+    const float w = qmask ? qmask[(size_t)i * Nq + q] : 1.f;
+    s += rm[q] * w;
+    cnt += w;
+  }
+  s = wave_sum(s);
+  cnt = wave_sum(cnt);
+  const float norm = qmask ? fmaxf(cnt, 1e-7f) : (float)Nq;
+  if (lane == 0) clip[(size_t)i * Bk + j] = s / norm;
+  if (j == 0 && qw) {
     for (int q = lane; q < Nq; q += 64) {
       const float w = qmask ? qmask[(size_t)i * Nq + q] : 1.f;
-      s += rm[q] * w;
-      cnt += w;
-    }
-    s = wave_sum(s);
-    cnt = wave_sum(cnt);
-    const float norm = qmask ? fmaxf(cnt, 1e-7f) : (float)Nq;
-    if (lane == 0) clip[(size_t)i * Bk + j] = s / norm;
-    if (j == 0 && qw) {
-      for (int q = lane; q < Nq; q += 64) {
-        const float w = qmask ? qmask[(size_t)i * Nq + q] : 1.f;
-        qw[(size_t)i * Nq + q] = w / norm;
-      }
+      qw[(size_t)i * Nq + q] = w / norm;
     }
   }
 }
@@ -224,28 +225,44 @@ __global__ __launch_bounds__(256) void clip_reduce_kernel(const float* __restric
 //   l_smooth = sum_{i,q>=1,k} (S_ii[q,k] - S_ii[q-1,k])^2 / cnt
 // Writes part[i] = the sample's sum, g[i][q][k] = d l_smooth / d S_ii[q,k] and
 // dt_part[i] = sum g * S (for d/dtemp; S = temp * S_raw).
-__global__ __launch_bounds__(256) void diag_smooth_kernel(const float* __restrict__ dS_in, int Nq, int Nk_pad,
-                                                          int Nk_eff, double inv_cnt,
-                                                          double* __restrict__ part, float* __restrict__ g,
-                                                          double* __restrict__ dt_part) {
-  __shared__ double red[4];
+__global__ __launch_bounds__(1024) void diag_smooth_kernel(const float* __restrict__ dS_in, int Nq, int Nk_pad,
+                                                           int Nk_eff, double inv_cnt,
+                                                           double* __restrict__ part, float* __restrict__ g,
+                                                           double* __restrict__ dt_part) {
+  __shared__ double red[16];
   const int i = blockIdx.x;
   const float* S = dS_in + (size_t)i * Nq * Nk_pad;
   float* G = g + (size_t)i * Nq * Nk_pad;
   double acc = 0.0, dacc = 0.0;
   const float two_inv = (float)(2.0 * inv_cnt);
-  for (int e = threadIdx.x; e < Nq * Nk_eff; e += blockDim.x) {
-    const int q = e / Nk_eff, k = e - q * Nk_eff;
-    const float s = S[(size_t)q * Nk_pad + k];
-    float grad = 0.f;
-    if (q >= 1) {
-      const float d = s - S[(size_t)(q - 1) * Nk_pad + k];
-      acc += (double)(d * d);
-      grad += two_inv * d;
+  const int n = Nq * Nk_eff;
+  // four elements per thread per pass, their loads issued together (one element per pass made
+  // this a latency-bound 0.16 ms launch at c3)
+  for (int e0 = threadIdx.x; e0 < n; e0 += 4 * blockDim.x) {
+    float s[4], sp[4], sn[4];
+    int q[4], k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = min(e0 + u * (int)blockDim.x, n - 1);
+      q[u] = e / Nk_eff;
+      k[u] = e - q[u] * Nk_eff;
+      s[u] = S[(size_t)q[u] * Nk_pad + k[u]];
+      sp[u] = q[u] >= 1 ? S[(size_t)(q[u] - 1) * Nk_pad + k[u]] : 0.f;
+      sn[u] = q[u] + 1 < Nq ? S[(size_t)(q[u] + 1) * Nk_pad + k[u]] : 0.f;
     }
-    if (q + 1 < Nq) grad -= two_inv * (S[(size_t)(q + 1) * Nk_pad + k] - s);
-    G[(size_t)q * Nk_pad + k] = grad;
-    dacc += (double)grad * (double)s;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (e0 + u * (int)blockDim.x >= n) break;
+      float grad = 0.f;
+      if (q[u] >= 1) {
+        const float d = s[u] - sp[u];
+        acc += (double)(d * d);
+        grad += two_inv * d;
+      }
+      if (q[u] + 1 < Nq) grad -= two_inv * (sn[u] - s[u]);
+      G[(size_t)q[u] * Nk_pad + k[u]] = grad;
+      dacc += (double)grad * (double)s[u];
+    }
   }
   const double t = block_sum_d(acc, red);
   const double dt = block_sum_d(dacc, red);
@@ -367,6 +384,23 @@ __global__ __launch_bounds__(256) void dS_patch_diag_kernel(bf16* __restrict__ d
 //      [4..9] pos_mean pos_std neg_mean neg_std separation hardest_negative
 //      [10] l_nonneg [11] l_cal [12] diag regulariser (l_smooth / sparsity)
 // dclip: d ce / d clip (unit upstream gradient).
+// Row (r < B) / column (r >= B) log-sum-exp of the clip matrix, one wave per line, all lines in
+// parallel (inside the one-workgroup loss head this phase was a latency-bound 0.1+ ms loop).
+__global__ __launch_bounds__(256) void clip_lse_kernel(const float* __restrict__ clip, int B,
+                                                       float* __restrict__ lse) {
+  const int lane = threadIdx.x & 63, r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= 2 * B) return;
+  const bool col = r >= B;
+  const int x = col ? r - B : r;
+  float mx = -INFINITY;
+  for (int y = lane; y < B; y += 64) mx = fmaxf(mx, col ? clip[(size_t)y * B + x] : clip[(size_t)x * B + y]);
+  mx = wave_max(mx);
+  float s = 0.f;
+  for (int y = lane; y < B; y += 64) s += expf((col ? clip[(size_t)y * B + x] : clip[(size_t)x * B + y]) - mx);
+  s = wave_sum(s);
+  if (lane == 0) lse[r] = mx + logf(s);
+}
+
 __global__ __launch_bounds__(1024) void losshead_kernel(const float* __restrict__ clip, int B, int kind,
                                                         const float* __restrict__ temp_p,
                                                         const double* __restrict__ nn_part, int n_nn,
@@ -374,23 +408,9 @@ __global__ __launch_bounds__(1024) void losshead_kernel(const float* __restrict_
                                                         const double* __restrict__ dg_part, int n_dg,
                                                         double inv_dg, float w_sparse,
                                                         float* __restrict__ out, float* __restrict__ dclip,
-                                                        float* __restrict__ lse /* [2B] scratch */) {
+                                                        const float* __restrict__ lse /* [2B], clip_lse_kernel */) {
   __shared__ double redd[16];
   __shared__ float redf[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  // row / column log-sum-exp
-  for (int r = wave; r < 2 * B; r += nw) {
-    const bool col = r >= B;
-    const int x = col ? r - B : r;
-    float mx = -INFINITY;
-    for (int y = lane; y < B; y += 64) mx = fmaxf(mx, col ? clip[(size_t)y * B + x] : clip[(size_t)x * B + y]);
-    mx = wave_max(mx);
-    float s = 0.f;
-    for (int y = lane; y < B; y += 64) s += expf((col ? clip[(size_t)y * B + x] : clip[(size_t)x * B + y]) - mx);
-    s = wave_sum(s);
-    if (lane == 0) lse[r] = mx + logf(s);
-  }
-  __syncthreads();
   double ce = 0.0, pos = 0.0, neg = 0.0;
   float hard = -INFINITY;
   for (int i = threadIdx.x; i < B; i += blockDim.x) {
@@ -399,13 +419,29 @@ __global__ __launch_bounds__(1024) void losshead_kernel(const float* __restrict_
     pos += c;
   }
   const float inv2b = 0.5f / (float)B;
-  for (size_t e = threadIdx.x; e < (size_t)B * B; e += blockDim.x) {
-    const int i = (int)(e / B), j = (int)(e - (size_t)i * B);
-    const float c = clip[e];
-    float g = expf(c - lse[i]) + expf(c - lse[B + j]);
-    if (i == j) g -= 2.f;
-    else { neg += c; hard = fmaxf(hard, c); }
-    dclip[e] = g * inv2b;
+  const int BB = B * B;
+  const int bd = blockDim.x;
+  // four elements per thread per pass, loads issued together (latency-bound otherwise)
+  for (int e0 = threadIdx.x; e0 < BB; e0 += 4 * bd) {
+    float c[4], li[4], lj[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = min(e0 + u * bd, BB - 1);
+      const int i = e / B, j = e - i * B;
+      c[u] = clip[e];
+      li[u] = lse[i];
+      lj[u] = lse[B + j];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * bd;
+      if (e >= BB) break;
+      const int i = e / B, j = e - i * B;
+      float g = expf(c[u] - li[u]) + expf(c[u] - lj[u]);
+      if (i == j) g -= 2.f;
+      else { neg += c[u]; hard = fmaxf(hard, c[u]); }
+      dclip[e] = g * inv2b;
+    }
   }
   ce = block_sum_d(ce, redd);
   pos = block_sum_d(pos, redd);
@@ -414,10 +450,18 @@ __global__ __launch_bounds__(1024) void losshead_kernel(const float* __restrict_
   const double nneg = (double)B * B - B;
   const double pm = pos / B, nm = neg / nneg;
   double pv = 0.0, nv = 0.0;
-  for (size_t e = threadIdx.x; e < (size_t)B * B; e += blockDim.x) {
-    const int i = (int)(e / B), j = (int)(e - (size_t)i * B);
-    const double d = (double)clip[e] - (i == j ? pm : nm);
-    if (i == j) pv += d * d; else nv += d * d;
+  for (int e0 = threadIdx.x; e0 < BB; e0 += 4 * bd) {
+    float c[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c[u] = clip[min(e0 + u * bd, BB - 1)];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * bd;
+      if (e >= BB) break;
+      const int i = e / B, j = e - i * B;
+      const double d = (double)c[u] - (i == j ? pm : nm);
+      if (i == j) pv += d * d; else nv += d * d;
+    }
   }
   pv = block_sum_d(pv, redd);
   nv = block_sum_d(nv, redd);
@@ -557,8 +601,8 @@ int triad_pairsim_fwd_multi(const triad_pairsim_problem* problems, int n, hipStr
 int triad_clip_reduce(const float* rowmax, int R_pad, int Nq, int Bq, int Bk, const float* qmask,
                       float* clip, float* qw, hipStream_t stream) {
   if (Bq <= 0 || Bk <= 0 || Nq <= 0) return TRIAD_EINVAL;
-  hipLaunchKernelGGL(clip_reduce_kernel, dim3(Bk), dim3(256), 0, stream, rowmax, R_pad, Nq, Bq, Bk, qmask,
-                     clip, qw);
+  hipLaunchKernelGGL(clip_reduce_kernel, dim3(Bk, (Bq + 3) / 4), dim3(256), 0, stream, rowmax, R_pad, Nq, Bq, Bk,
+                     qmask, clip, qw);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
@@ -566,7 +610,7 @@ int triad_clip_reduce(const float* rowmax, int R_pad, int Nq, int Bq, int Bk, co
 int triad_diag_smooth(const float* diagS, int Bq, int Nq, int Nk_pad, int Nk_eff, double cnt, double* part,
                       float* g, double* dt_part, hipStream_t stream) {
   if (Bq <= 0) return TRIAD_EINVAL;
-  hipLaunchKernelGGL(diag_smooth_kernel, dim3(Bq), dim3(256), 0, stream, diagS, Nq, Nk_pad, Nk_eff,
+  hipLaunchKernelGGL(diag_smooth_kernel, dim3(Bq), dim3(1024), 0, stream, diagS, Nq, Nk_pad, Nk_eff,
                      cnt > 0.0 ? 1.0 / cnt : 0.0, part, g, dt_part);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
@@ -584,10 +628,11 @@ int triad_diag_sparsity(const float* diagS, int Bq, int Nt, int Nk_pad, int Nk_e
 int triad_losshead(const float* clip, int B, int kind, const float* temp, const double* nn_part, int n_nn,
                    double n_el, const double* dg_part, int n_dg, double dg_cnt, float w_sparse, float* out,
                    float* dclip, float* lse_scratch, hipStream_t stream) {
-  if (B < 2 || (kind != 0 && kind != 1)) return TRIAD_EINVAL;
+  if (B < 2 || B > 46340 || (kind != 0 && kind != 1)) return TRIAD_EINVAL;  // B * B fits an int
   const double inv_dg = dg_cnt > 0.0 ? 1.0 / dg_cnt : NAN;
+  hipLaunchKernelGGL(clip_lse_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, stream, clip, B, lse_scratch);
   hipLaunchKernelGGL(losshead_kernel, dim3(1), dim3(1024), 0, stream, clip, B, kind, temp, nn_part, n_nn,
-                     1.0 / n_el, dg_part, n_dg, inv_dg, w_sparse, out, dclip, lse_scratch);
+                     1.0 / n_el, dg_part, n_dg, inv_dg, w_sparse, out, dclip, (const float*)lse_scratch);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
