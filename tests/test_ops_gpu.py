@@ -63,6 +63,21 @@ def test_global_znorm_matches_processor_semantics():
     np.testing.assert_allclose(y.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("offset,shape", [(0, (3, 10001)), (1, (4, 64000)), (0, (7,))])
+def test_global_znorm_vector_tail_and_unaligned(offset, shape):
+    """triad_global_znorm's 16-byte form with an element tail (numel % 4 != 0) and its element-wise
+    form for a buffer that is not 16-byte aligned (a view one float into its storage)."""
+    from triad_amd import ops
+    n = int(np.prod(shape))
+    base = torch.randn(n + offset, generator=torch.Generator().manual_seed(n)) * 0.3 + 0.7
+    x = base.to(dev)[offset:].view(shape)
+    assert (x.data_ptr() % 16 == 0) == (offset == 0)
+    ref = (base[offset:].double() - base[offset:].double().mean()) / torch.sqrt(
+        base[offset:].double().var(unbiased=False) + 1e-7)
+    y = ops.global_znorm(x, 1e-7)
+    np.testing.assert_allclose(y.cpu().numpy().ravel(), ref.numpy(), rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("name", G.names("znorm"))
 def test_global_znorm_matches_feature_extractor_fixture(name):
     """triad_global_znorm against the reference processor's own output (Wav2Vec2FeatureExtractor

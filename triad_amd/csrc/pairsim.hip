@@ -339,6 +339,9 @@ __device__ __forceinline__ long long tile_elem(long long CT, int r, long long c)
   return ((long long)(r >> 5) * CT + (c >> 5)) * 1024 + lane * 16 + v;
 }
 
+// Four elements per thread per pass with all their loads issued together, 32-bit index math:
+// one element per pass (a dependent argmax -> dS round trip each, 64-bit divisions) made the AV
+// patch a latency-bound 0.3 ms launch at c3.
 __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS, long long CT, int R, int R_pad,
                                                            int Nq, int Bk, int Nk_pad,
                                                            const int* __restrict__ argmax,
@@ -348,34 +351,59 @@ __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS
                                                            double* __restrict__ part) {
   __shared__ double red[4];
   double acc = 0.0;
-  const long long total = (long long)Bk * R;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(e / R), r = (int)(e - (long long)j * R);
-    const int i = r / Nq;
-    const float w = dclip[(size_t)i * Bk + j] * qw[r];
-    const int key = argmax[(size_t)j * R_pad + r];
-    bf16* p = dS + tile_elem(CT, r, (long long)j * Nk_pad + key);
-    *p = (bf16)((float)*p + ratio * w);
-    acc += (double)w * (double)rowmax[(size_t)j * R_pad + r];
+  const int total = Bk * R;   // < 2^31 (host check)
+  const int stride = gridDim.x * blockDim.x;
+  for (int e0 = blockIdx.x * blockDim.x + threadIdx.x; e0 < total; e0 += 4 * stride) {
+    float w[4], rm[4], old[4];
+    bf16* p[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = min(e0 + u * stride, total - 1);
+      const int j = e / R, r = e - j * R;
+      const int i = r / Nq;
+      w[u] = dclip[(size_t)i * Bk + j] * qw[r];
+      rm[u] = rowmax[(size_t)j * R_pad + r];
+      const int key = argmax[(size_t)j * R_pad + r];
+      p[u] = dS + tile_elem(CT, r, (long long)j * Nk_pad + key);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) old[u] = (float)*p[u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (e0 + u * stride >= total) break;
+      *p[u] = (bf16)(old[u] + ratio * w[u]);
+      acc += (double)w[u] * (double)rm[u];
+    }
   }
   const double t = block_sum_d(acc, red);
   if (threadIdx.x == 0) part[blockIdx.x] = t;
 }
 
-// Diagonal regulariser term: dS[i*Nq+q][(i+off)*Nk_pad + k] += ratio * g[i][q][k].
+// Diagonal regulariser term: dS[i*Nq+q][(i+off)*Nk_pad + k] += ratio * g[i][q][k] (four elements
+// per thread per pass, as above).
 __global__ __launch_bounds__(256) void dS_patch_diag_kernel(bf16* __restrict__ dS, long long CT, int Bq, int Nq,
                                                             int Nk_pad, int Nk_eff, int diag_off,
                                                             const float* __restrict__ g, float ratio) {
-  const long long total = (long long)Bq * Nq * Nk_eff;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int k = (int)(e % Nk_eff);
-    const long long iq = e / Nk_eff;
-    const int i = (int)(iq / Nq);
-    const int r = (int)iq;
-    bf16* p = dS + tile_elem(CT, r, (long long)(i + diag_off) * Nk_pad + k);
-    *p = (bf16)((float)*p + ratio * g[iq * Nk_pad + k]);
+  const int total = Bq * Nq * Nk_eff;   // < 2^31 (host check)
+  const int stride = gridDim.x * blockDim.x;
+  for (int e0 = blockIdx.x * blockDim.x + threadIdx.x; e0 < total; e0 += 4 * stride) {
+    float gv[4], old[4];
+    bf16* p[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = min(e0 + u * stride, total - 1);
+      const int k = e % Nk_eff, iq = e / Nk_eff;
+      const int i = iq / Nq;
+      gv[u] = g[(size_t)iq * Nk_pad + k];
+      p[u] = dS + tile_elem(CT, iq, (long long)(i + diag_off) * Nk_pad + k);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) old[u] = (float)*p[u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (e0 + u * stride >= total) break;
+      *p[u] = (bf16)(old[u] + ratio * gv[u]);
+    }
   }
 }
 
@@ -661,6 +689,7 @@ int triad_dS_patch(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int
                    float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
                    hipStream_t stream) {
   if (R <= 0 || Bk <= 0 || n_max_part <= 0 || CT < (long long)Bk * (Nk_pad / 32)) return TRIAD_EINVAL;
+  if ((long long)Bk * R >= (1LL << 31) || (long long)Bq * Nq * Nk_eff >= (1LL << 31)) return TRIAD_EINVAL;
   hipLaunchKernelGGL(dS_patch_max_kernel, dim3(n_max_part), dim3(256), 0, stream, (bf16*)dS, CT, R, R_pad, Nq, Bk,
                      Nk_pad, argmax, rowmax, dclip, qw, ratio_max, max_part);
   if (gdiag) {

@@ -78,25 +78,46 @@ int triad_l2norm_rows(const void* x, int rows, int D, float eps, void* y, hipStr
 
 namespace {
 
-// pass 1: per-block partial (sum, sum of squares) in double
+// pass 1: per-block partial (sum, sum of squares) in double; 16-byte loads, two in flight per
+// thread (4-byte loads with one dependent fp64 chain made the c3 audio batch a 0.2 ms pass)
+template <bool VEC>
 __global__ __launch_bounds__(256) void znorm_stats_kernel(const float* __restrict__ x, long long n,
                                                           double* __restrict__ part) {
   __shared__ double red[4];
-  double s = 0.0, q = 0.0;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const double v = x[e];
+  double s = 0.0, q = 0.0, s2 = 0.0, q2 = 0.0;
+  const long long n4 = VEC ? n / 4 : 0, stride = (long long)gridDim.x * blockDim.x;
+  const float4* x4 = (const float4*)x;
+  long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  for (; e + stride < n4; e += 2 * stride) {
+    const float4 a = x4[e], b = x4[e + stride];
+    s += ((double)a.x + (double)a.y) + ((double)a.z + (double)a.w);
+    q += ((double)a.x * a.x + (double)a.y * a.y) + ((double)a.z * a.z + (double)a.w * a.w);
+    s2 += ((double)b.x + (double)b.y) + ((double)b.z + (double)b.w);
+    q2 += ((double)b.x * b.x + (double)b.y * b.y) + ((double)b.z * b.z + (double)b.w * b.w);
+  }
+  for (; e < n4; e += stride) {
+    const float4 a = x4[e];
+    s += ((double)a.x + (double)a.y) + ((double)a.z + (double)a.w);
+    q += ((double)a.x * a.x + (double)a.y * a.y) + ((double)a.z * a.z + (double)a.w * a.w);
+  }
+  // the tail (VEC) or everything (a buffer not 16-byte aligned), element-wise
+  const long long t0 = 4 * n4, tst = VEC ? blockDim.x : stride;
+  for (long long t = t0 + (VEC ? (blockIdx.x == 0 ? threadIdx.x : n) : blockIdx.x * (long long)blockDim.x + threadIdx.x);
+       t < n; t += tst) {
+    const double v = x[t];
     s += v;
     q += v * v;
   }
-  s = block_sum_d(s, red);
-  q = block_sum_d(q, red);
+  s = block_sum_d(s + s2, red);
+  q = block_sum_d(q + q2, red);
   if (threadIdx.x == 0) {
     part[2 * blockIdx.x] = s;
     part[2 * blockIdx.x + 1] = q;
   }
 }
 
-// pass 2: every block re-reduces the partials, then normalises its slice
+// pass 2: every block re-reduces the partials, then normalises its slice (16-byte accesses)
+template <bool VEC>
 __global__ __launch_bounds__(256) void znorm_apply_kernel(const float* __restrict__ x, long long n, float eps,
                                                           const double* __restrict__ part, int nparts,
                                                           float* __restrict__ y) {
@@ -112,8 +133,17 @@ __global__ __launch_bounds__(256) void znorm_apply_kernel(const float* __restric
   const double var = q / (double)n - mean * mean;
   const float m = (float)mean;
   const float inv = (float)(1.0 / sqrt((var > 0.0 ? var : 0.0) + (double)eps));
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x)
-    y[e] = (x[e] - m) * inv;
+  const long long n4 = VEC ? n / 4 : 0, stride = (long long)gridDim.x * blockDim.x;
+  const float4* x4 = (const float4*)x;
+  float4* y4 = (float4*)y;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n4; e += stride) {
+    const float4 a = x4[e];
+    y4[e] = make_float4((a.x - m) * inv, (a.y - m) * inv, (a.z - m) * inv, (a.w - m) * inv);
+  }
+  const long long t0 = 4 * n4, tst = VEC ? blockDim.x : stride;
+  for (long long t = t0 + (VEC ? (blockIdx.x == 0 ? threadIdx.x : n) : blockIdx.x * (long long)blockDim.x + threadIdx.x);
+       t < n; t += tst)
+    y[t] = (x[t] - m) * inv;
 }
 
 }  // namespace
@@ -121,8 +151,13 @@ __global__ __launch_bounds__(256) void znorm_apply_kernel(const float* __restric
 extern "C" int triad_global_znorm(const float* x, long long n, float eps, float* y, double* part, int nblocks,
                                   hipStream_t stream) {
   if (n <= 0 || nblocks <= 0) return TRIAD_EINVAL;
-  hipLaunchKernelGGL(znorm_stats_kernel, dim3(nblocks), dim3(256), 0, stream, x, n, part);
-  hipLaunchKernelGGL(znorm_apply_kernel, dim3(nblocks), dim3(256), 0, stream, x, n, eps, part, nblocks, y);
+  if ((((size_t)x) | ((size_t)y)) % 16 == 0) {
+    hipLaunchKernelGGL(znorm_stats_kernel<true>, dim3(nblocks), dim3(256), 0, stream, x, n, part);
+    hipLaunchKernelGGL(znorm_apply_kernel<true>, dim3(nblocks), dim3(256), 0, stream, x, n, eps, part, nblocks, y);
+  } else {
+    hipLaunchKernelGGL(znorm_stats_kernel<false>, dim3(nblocks), dim3(256), 0, stream, x, n, part);
+    hipLaunchKernelGGL(znorm_apply_kernel<false>, dim3(nblocks), dim3(256), 0, stream, x, n, eps, part, nblocks, y);
+  }
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
