@@ -1,4 +1,6 @@
-# A/B of the direct-B tile GEMM stage shapes (tools/build_variants.py builds tools/variants/lib_*.so):
+# A/B of the direct-B tile GEMM stage shapes (round 3; the variants were built with
+# tools/build_variants.py from -DTRIAD_DB_KS / -DTRIAD_DB_D knobs since replaced by per-GEMM template
+# parameters in bwd_gemm.hip -- kept as the record of how profiles/r03_tile_gemm_db_ab.log was made):
 # default (1 k tile per stage, 3 stages ahead) vs 2 tiles per stage (1 / 2 stages ahead) and 1 x 4.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
