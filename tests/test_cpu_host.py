@@ -147,3 +147,25 @@ def test_pairsim_fwd_multi_rejects_bad_arguments():
     nul.rowmax = None
     assert f((_lib.PairsimProblem * 1)(nul), 1, None) == 1001
     assert C.sizeof(_lib.PairsimProblem) == 128
+
+
+def test_packed_tile_gemm_and_patch_reject_bad_arguments():
+    """The direct-B GEMM entry points, the dS patch and the loss head validate their shapes before
+    launching anything (no GPU needed) -> TRIAD_EINVAL (1001)."""
+    from triad_amd import _lib, build
+    if not os.path.exists(_lib.LIB_PATH):
+        build.build()
+    lib = _lib.load()
+    fake = 4096  # never dereferenced: validation fails first
+    assert lib.triad_bfrag_pack(fake, 0, 0, fake, None) == 1001                     # no k tiles
+    assert lib.triad_bfrag_pack(None, 4, 0, fake, None) == 1001                     # no B
+    assert lib.triad_tile_gemm_packed(fake, 8, 0, fake, 200, 8, fake, 1, None, fake, None) == 1001  # M % 128
+    assert lib.triad_tile_gemm_packed(fake, 8, 0, fake, 256, 8, fake, 2, None, fake, None) == 1001  # no slabs
+    assert lib.triad_tile_gemm_packed_slabs(fake, 8, 1, fake, 256, 0, 1, fake, None) == 1001      # nkt = 0
+    # dS patch: CT too small for Bk samples of Nk_pad keys; Bk * R past 2^31 (32-bit index math)
+    assert lib.triad_dS_patch(fake, 4, 256, 256, 32, 8, 8, 64, 60, 0, fake, fake, fake, fake, 1.0, None, 0.0,
+                              fake, 1024, None) == 1001
+    assert lib.triad_dS_patch(fake, 1 << 40, 1 << 20, 1 << 20, 32, 8, 4096, 64, 60, 0, fake, fake, fake, fake, 1.0,
+                              None, 0.0, fake, 1024, None) == 1001
+    # loss head: B * B must fit an int
+    assert lib.triad_losshead(fake, 50000, 0, fake, fake, 1, 1.0, fake, 1, 1.0, 0.0, fake, fake, fake, None) == 1001
