@@ -207,7 +207,11 @@ __global__ __launch_bounds__(512) void bfrag_pack_kernel(const bf16* __restrict_
 
 // 16-byte global load hidden from hipcc's waitcnt bookkeeping (it would otherwise drain vmcnt(0)
 // at the first use, glds in flight): the caller's counted s_waitcnt vmcnt before the barrier
-// retires it. The destination registers are only ever read after that wait.
+// retires it. The destination registers are only ever read after that wait -- and must not be
+// copied before it: the register ring is indexed statically (the stage loop is unrolled by its
+// depth) so each slot keeps one physical register range across the loop; checked in the ISA
+// (hipcc -S: no v_mov / v_accvgpr reads of the ring's ranges between a load and its wait) and by
+// test_tile_gemm_packed_bit_identical_to_ring. Re-check both after changing the stage shapes.
 __device__ __forceinline__ bf16x8 gload16(const bf16* p) {
   bf16x8 v;
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
