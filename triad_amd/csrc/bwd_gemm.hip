@@ -209,9 +209,9 @@ __global__ __launch_bounds__(512) void bfrag_pack_kernel(const bf16* __restrict_
 // at the first use, glds in flight): the caller's counted s_waitcnt vmcnt before the barrier
 // retires it. The destination registers are only ever read after that wait -- and must not be
 // copied before it: the register ring is indexed statically (the stage loop is unrolled by its
-// depth) so each slot keeps one physical register range across the loop; checked in the ISA
-// (hipcc -S: no v_mov / v_accvgpr reads of the ring's ranges between a load and its wait) and by
-// test_tile_gemm_packed_bit_identical_to_ring. Re-check both after changing the stage shapes.
+// depth) so each slot keeps one physical register range across the loop; checked on hipcc's
+// output by tests/test_isa_cpu.py (nothing touches a ring register in the straight-line code
+// after its load) and on the GPU by test_tile_gemm_packed_bit_identical_to_ring.
 __device__ __forceinline__ bf16x8 gload16(const bf16* p) {
   bf16x8 v;
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
