@@ -244,8 +244,9 @@ int triad_global_znorm(const float* x, long long n, float eps, float* y, double*
  * (the clip factor, NULL = 1); pp[3*param] = {lr/bc1, 1/sqrt(bc2), 1 - lr*wd}. shadow (may be
  * NULL): per parameter, (address of its bf16 model weight) - 2 * (flat offset), or 0; the step
  * then also writes bf16(p) there (mixed-precision model weights, the cast autocast would do).
- * triad_gather_grads: pieces = device array of {const bf16* src; int64 dst; int32 n; int32 pad};
- * g[dst + i] (+)= float(src[i]) -- bf16 weight gradients into the flat fp32 gradient buffer. */
+ * triad_gather_grads: pieces = device array of {const void* src; int64 dst; int32 n; int32 f32};
+ * g[dst + i] (+)= float(src[i]), src bf16 (f32 == 0) or fp32 (f32 == 1) -- the autograd
+ * gradients of every flat-space parameter into the flat fp32 gradient buffer. */
 int triad_grad_sumsq(const float* g, const void* chunks, int nchunks, double* out, hipStream_t stream);
 int triad_adamw_step(float* p, const float* g, float* m, float* v, const void* chunks, int nchunks,
                      const float* pp, const float* scale, float beta1, float beta2, float eps,

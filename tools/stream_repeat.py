@@ -1,0 +1,85 @@
+"""How often does the multi-stream tri-modal step differ from the single-stream one?
+
+One TriadTrainer step (c3 model, B=128, dropout / LayerDrop / SpecAugment on -- the setting of
+tests/test_ops_gpu.py::test_modality_streams_match_single_stream) from identical models and seeds:
+once single-stream as the reference, then `--reps` times with the modality streams, each compared
+bit for bit (losses and the reduced fp32 gradient buffer). Prints one line per rep (the differing
+parameters, if any) and a JSON summary. TRIAD_GATHER_FP32_GRADS=0 selects the old route of the
+fp32 gradients (autograd's add into views of the flat buffer) for an A/B.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+dev = "cuda"
+
+
+def run(streams, frames, audio, text):
+    from triad_amd.model import MultiModalModel
+    from triad_amd.train import TriadTrainer
+    os.environ["TRIAD_MODALITY_STREAMS"] = "1" if streams else "0"
+    torch.manual_seed(0)
+    m = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.8, patch_sparsity_weight=0.01,
+                        visual_dropout_prob=0.25, use_amp=True).to(dev)
+    m.train()
+    tr = TriadTrainer(m, total_updates=100, unfreeze_audio_step=0, unfreeze_text_step=0, unfreeze_vit_step=0,
+                      device=dev)
+    snap = []
+    inner = tr._allreduce_grads
+
+    def grab():
+        inner()
+        snap.append(tr.space.flat_g.clone())
+    tr._allreduce_grads = grab
+    torch.manual_seed(1)
+    np.random.seed(1)
+    out = tr.step(frames, audio, text)
+    torch.cuda.synchronize()
+    names = {id(p): n for n, p in m.named_parameters()}
+    layout = [(names[id(p)], tr.space.offsets[i], p.numel()) for i, p in enumerate(tr.space.params)]
+    return [float(out[k]) for k in ("loss", "loss_av", "loss_tv")], snap[0].cpu(), layout
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--math-sdpa", action="store_true", help="PyTorch's masked SDPA (the DistilBERT attention) "
+                    "on its math backend only")
+    ap.add_argument("--det", action="store_true", help="torch.use_deterministic_algorithms(True, warn_only=True)")
+    a = ap.parse_args()
+    if a.math_sdpa:
+        torch.backends.cuda.enable_flash_sdp(False)
+        torch.backends.cuda.enable_mem_efficient_sdp(False)
+        torch.backends.cuda.enable_math_sdp(True)
+    if a.det:
+        torch.use_deterministic_algorithms(True, warn_only=True)
+    B = 128
+    g = torch.Generator().manual_seed(5)
+    frames = torch.randn(B, 3, 224, 224, generator=g).to(dev)
+    audio = (torch.randn(B, 16000, generator=g) * 0.1).to(dev)
+    text = [f"caption number {i} of a scene" for i in range(B)]
+    l_ref, g_ref, layout = run(False, frames, audio, text)
+    bad = 0
+    for r in range(a.reps):
+        l, gm, _ = run(True, frames, audio, text)
+        diff = []
+        for name, off, n in layout:
+            x, y = gm[off:off + n], g_ref[off:off + n]
+            if not torch.equal(x, y):
+                rel = float((x.double() - y.double()).norm() / y.double().norm().clamp(min=1e-300))
+                diff.append((name, int((x != y).sum()), n, f"{rel:.2g}"))
+        ok = l == l_ref and not diff
+        bad += not ok
+        print(f"rep {r}: {'equal' if ok else 'DIFFERS'} losses_equal={l == l_ref} params={diff[:6]}", flush=True)
+    print(json.dumps({"reps": a.reps, "differing": bad, "math_sdpa": a.math_sdpa, "det": a.det,
+                      "gather_fp32": os.environ.get("TRIAD_GATHER_FP32_GRADS", "1")}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

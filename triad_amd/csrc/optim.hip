@@ -68,11 +68,11 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   }
 }
 
-struct GradPiece {  // bf16 gradient slice -> flat fp32 gradient elements [dst, dst + n)
-  const bf16* src;
+struct GradPiece {  // bf16 (f32 == 0) or fp32 (f32 == 1) gradient slice -> flat fp32 gradient [dst, dst + n)
+  const void* src;
   long long dst;
   int n;
-  int pad;
+  int f32;
 };
 
 __global__ __launch_bounds__(256) void gather_grads_kernel(const GradPiece* __restrict__ pieces,
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void gather_grads_kernel(const GradPiece* __re
   const GradPiece c = pieces[blockIdx.x];
   float* out = g + c.dst;
   for (int i = threadIdx.x; i < c.n; i += blockDim.x) {
-    const float x = (float)c.src[i];
+    const float x = c.f32 ? ((const float*)c.src)[i] : (float)((const bf16*)c.src)[i];
     out[i] = accumulate ? out[i] + x : x;
   }
 }

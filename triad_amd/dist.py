@@ -111,9 +111,9 @@ class GradBucketReducer:
     all-reduce over point-to-point xGMI is per-link bound, so buckets are sized for a few
     ms of link time each (64 MB default) rather than for latency.
 
-    Shadowed (bf16 model-weight) parameters: their bf16 autograd gradient is folded into the
-    flat fp32 buffer inside the hook (so it can join a bucket) instead of by the single
-    after-backward `gather_shadow_grads` launch.
+    Gathered parameters (FlatParamSpace.gathered: the bf16 model weights and, on a GPU, the fp32
+    ones): their autograd gradient is folded into the flat fp32 buffer inside the hook (so it can
+    join a bucket) instead of by the single after-backward `gather_shadow_grads` launch.
     """
 
     def __init__(self, space, bucket_mb: float = 64.0, wire: str = "fp32", average: bool = True, group=None):
@@ -179,7 +179,7 @@ class GradBucketReducer:
                 return
             sp = self.space
             cur = torch.cuda.current_stream(sp.device) if self.cuda else None
-            if sp.shadowed[i] and p.grad is not None:
+            if sp.gathered[i] and p.grad is not None:
                 view = sp.flat_g[sp.offsets[i]:sp.offsets[i] + p.numel()].view(p.shape)
                 if cur is not None:
                     # a bf16 weight gradient may still be in flight on the side stream

@@ -21,6 +21,7 @@ gradients are never rewritten in HBM.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Iterable, List, Sequence
 
 import numpy as np
@@ -32,7 +33,7 @@ from ._lib import TriadError, call, ptr, stream_ptr
 CHUNK = 16384
 ALIGN = 64  # elements (256 B) per parameter slot
 _CHUNK_DT = np.dtype([("off", "<i8"), ("n", "<i4"), ("param", "<i4")])
-_PIECE_DT = np.dtype([("src", "<u8"), ("dst", "<i8"), ("n", "<i4"), ("pad", "<i4")])
+_PIECE_DT = np.dtype([("src", "<u8"), ("dst", "<i8"), ("n", "<i4"), ("f32", "<i4")])
 
 
 class FlatParamSpace:
@@ -44,7 +45,13 @@ class FlatParamSpace:
     in .grad (what autocast's backward produces before casting to fp32), `gather_shadow_grads`
     moves those into the flat fp32 gradient buffer in one launch, and the AdamW launch writes
     the new bf16 weight. Only for weights consumed exactly as autocast consumes them (Linear /
-    Conv inputs), used once per backward (a second use would accumulate in bf16)."""
+    Conv inputs), used once per backward (a second use would accumulate in bf16).
+
+    On a GPU the fp32 parameters' gradients take the same route (`gathered`): .grad stays empty
+    through backward, autograd stores each gradient as it comes (no kernel), and the same one
+    gather launch adds them into the flat buffer -- instead of one PyTorch add kernel per fp32
+    parameter (biases, LayerNorm affines: ~400 launches per tri-modal step) that .grad views of
+    the flat buffer would cost. TRIAD_GATHER_FP32_GRADS=0: the views."""
 
     def __init__(self, params: Sequence[torch.nn.Parameter], device, shadow: Sequence[torch.nn.Parameter] = ()):
         self.device = torch.device(device)
@@ -52,6 +59,8 @@ class FlatParamSpace:
         self.index = {id(p): i for i, p in enumerate(self.params)}
         shadow_ids = {id(p) for p in shadow}
         self.shadowed = np.array([id(p) in shadow_ids for p in self.params], dtype=bool)
+        gather_fp32 = self.device.type == "cuda" and os.environ.get("TRIAD_GATHER_FP32_GRADS", "1") != "0"
+        self.gathered = self.shadowed | gather_fp32   # .grad empty through backward, gathered after
         offs, o = [], 0
         for p in self.params:
             offs.append(o)
@@ -80,8 +89,11 @@ class FlatParamSpace:
                     shadow_base[i] = (p.data_ptr() - 2 * offs[i]) % (1 << 64)
                 else:
                     p.data = v
-                    p.grad = self.flat_g[offs[i]:offs[i] + p.numel()].view_as(p)
-                    self._hooks.append(p.register_post_accumulate_grad_hook(self._mark(i)))
+                    if self.gathered[i]:
+                        p.grad = None
+                    else:
+                        p.grad = self.flat_g[offs[i]:offs[i] + p.numel()].view_as(p)
+                        self._hooks.append(p.register_post_accumulate_grad_hook(self._mark(i)))
         self.shadow_base = (torch.from_numpy(shadow_base.view(np.int64)).to(self.device)
                             if self.shadowed.any() else None)
         # where each shadowed bf16 model weight lived when shadow_base was taken: the AdamW
@@ -159,22 +171,24 @@ class FlatParamSpace:
 
     @torch.no_grad()
     def gather_shadow_grads(self, accumulate: bool):
-        """bf16 .grad of the shadowed parameters -> flat fp32 gradient buffer (one launch);
-        the .grad tensors are released (stream-ordered reuse by the caching allocator)."""
-        if not self.shadowed.any():
+        """.grad of the gathered parameters (bf16 for the shadowed ones, fp32 for the rest) ->
+        flat fp32 gradient buffer (one launch); the .grad tensors are released (stream-ordered
+        reuse by the caching allocator)."""
+        if not self.gathered.any():
             return
         rows, ids = [], []
-        for i in np.nonzero(self.shadowed)[0]:
+        for i in np.nonzero(self.gathered)[0]:
             p = self.params[i]
             gr = p.grad
             if gr is None:
                 continue
-            if gr.dtype != torch.bfloat16 or not gr.is_contiguous():
-                gr = gr.to(torch.bfloat16).contiguous()
+            dt = torch.bfloat16 if self.shadowed[i] else torch.float32
+            if gr.dtype != dt or not gr.is_contiguous():
+                gr = gr.to(dt).contiguous()
                 p.grad = gr
-            base, n = gr.data_ptr(), gr.numel()
+            base, n, f32 = gr.data_ptr(), gr.numel(), int(dt == torch.float32)
             for s0 in range(0, n, CHUNK):
-                rows.append((base + 2 * s0, self.offsets[i] + s0, min(CHUNK, n - s0), 0))
+                rows.append((base + (2 + 2 * f32) * s0, self.offsets[i] + s0, min(CHUNK, n - s0), f32))
             ids.append(int(i))
         if not rows:
             return
@@ -207,7 +221,7 @@ class FlatParamSpace:
             self.touched[ids] = False
             self.scale.index_fill_(0, self.index_tensor(ids), 1.0)
             for i in ids:
-                if self.shadowed[i]:
+                if self.gathered[i]:
                     self.params[i].grad = None
 
 
