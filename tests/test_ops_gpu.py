@@ -152,6 +152,33 @@ def test_fused_adamw_matches_torch_with_onecycle_and_clip():
             np.testing.assert_allclose(b.detach().cpu().numpy(), a.detach().numpy(), rtol=1e-5, atol=1e-6)
 
 
+def test_flat_space_gathers_fp32_and_bf16_grads_with_accumulation():
+    """FlatParamSpace.gathered: fp32 parameters keep .grad empty through backward and their
+    gradients join the bf16 shadowed ones in the one triad_gather_grads launch (f32 pieces);
+    a second micro-step accumulates into the flat buffer; zero_grad releases the .grad."""
+    from triad_amd import optim as fo
+    torch.manual_seed(3)
+    w32 = nn.Parameter(torch.randn(300, 17, device=dev))
+    b32 = nn.Parameter(torch.randn(5000, device=dev))
+    w16 = nn.Parameter(torch.randn(64, 70, device=dev))
+    space = fo.FlatParamSpace([w32, b32, w16], dev, shadow=[w16])
+    assert space.gathered.all() and w32.grad is None and w16.dtype == torch.bfloat16
+    gs = [[torch.randn(p.shape, device=dev) for p in (w32, b32, w16)] for _ in range(2)]
+    for k, g in enumerate(gs):
+        (w32 * g[0]).sum().add_((b32 * g[1]).sum()).add_((w16.float() * g[2]).sum()).backward()
+        assert w32.grad is not None and w32.grad.dtype == torch.float32
+        space.gather_shadow_grads(accumulate=k > 0)
+        assert w32.grad is None and b32.grad is None and w16.grad is None
+    want = [gs[0][i] + gs[1][i] for i in range(3)]
+    want[2] = gs[0][2].to(torch.bfloat16).float() + gs[1][2].to(torch.bfloat16).float()
+    for i, p in enumerate((w32, b32, w16)):
+        got = space.flat_g[space.offsets[i]:space.offsets[i] + p.numel()].view(p.shape)
+        torch.testing.assert_close(got, want[i], rtol=0, atol=0)
+    assert space.touched.all()
+    space.zero_grad([0, 1, 2])
+    assert float(space.flat_g.abs().sum()) == 0.0
+
+
 def test_trainer_step_runs_and_moves_params():
     from triad_amd.model import MultiModalModel
     from triad_amd.train import TriadTrainer
