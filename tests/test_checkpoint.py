@@ -202,7 +202,7 @@ class _MaskOwner:
         return self.gen
 
 
-def _mask_ckpt_worker(rank, world, port, q):
+def _mask_ckpt_worker(rank, world, port, q, path):
     import os
     import types
     import torch.distributed as dist
@@ -210,10 +210,18 @@ def _mask_ckpt_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from triad_amd import checkpoint as ck
-        tr = types.SimpleNamespace(world=world, pg=None, global_negatives=False)
         ve = _MaskOwner(100 + rank)
+        tr = types.SimpleNamespace(world=world, pg=None, global_negatives=False,
+                                   model=types.SimpleNamespace(visual_embedder=ve))
         torch.rand(5, generator=ve.gen)                       # some draws before the save
-        saved = ck._mask_generator_state(tr, ve)              # collective
+        saved = ck.gather_mask_states(tr)                     # collective
+        # save_checkpoint: every rank calls it (the gather inside is a collective), rank 0 writes
+        real = ck.trainer_checkpoint
+        ck.trainer_checkpoint = lambda t, e, st, **kw: {"writer": rank, "mask": ck.gather_mask_states(t)}
+        try:
+            ck.save_checkpoint(tr, path, 1, 2)
+        finally:
+            ck.trainer_checkpoint = real
         want = torch.rand(8, generator=ve.gen)                # what an uninterrupted run draws next
         fresh = _MaskOwner(0)
         ck._restore_mask_generator(tr, fresh, saved)
@@ -225,10 +233,11 @@ def _mask_ckpt_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_patch_mask_generator_state_per_rank():
+def test_patch_mask_generator_state_per_rank(tmp_path):
     """a Mode R checkpoint keeps every rank's patch-mask generator (gathered, indexed by
     rank) and each rank resumes its own sequence; a single saved state restored on several ranks
-    re-mixes the rank in, so replicas never draw identical masks."""
+    re-mixes the rank in, so replicas never draw identical masks. ADVICE r3: save_checkpoint is
+    called on every rank and only rank 0 writes the file (with both ranks' states)."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -237,7 +246,8 @@ def test_patch_mask_generator_state_per_rank():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_mask_ckpt_worker, args=(r, 2, port, q)) for r in range(2)]
+    path = str(tmp_path / "ck.pt")
+    procs = [ctx.Process(target=_mask_ckpt_worker, args=(r, 2, port, q, path)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(2)])
@@ -246,3 +256,6 @@ def test_patch_mask_generator_state_per_rank():
     (_, n0, ok0, s0), (_, n1, ok1, s1) = res
     assert n0 == n1 == 2 and ok0 and ok1
     assert s0 != s1
+    from triad_amd import checkpoint as ck
+    saved = ck.load_file(path)
+    assert saved["writer"] == 0 and len(saved["mask"]) == 2

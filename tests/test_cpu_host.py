@@ -169,3 +169,22 @@ def test_packed_tile_gemm_and_patch_reject_bad_arguments():
                               None, 0.0, fake, 1024, None) == 1001
     # loss head: B * B must fit an int
     assert lib.triad_losshead(fake, 50000, 0, fake, fake, 1, 1.0, fake, 1, 1.0, 0.0, fake, fake, fake, None) == 1001
+
+
+def test_select_subset_indices_draws_writes_and_rereads(tmp_path):
+    """retrieval.select_subset_indices (retrieval.py:9-30): python `random.shuffle` of
+    range(len(dataset)), the first `subset_size`, written as JSON; an existing file is read back
+    as is. Pinned to the reference's own draw by tests/golden/retrieval_e2e_n24.npz."""
+    import json
+    import random
+    from tests import golden_io as G
+    from triad_amd.retrieval import select_subset_indices
+    f = G.load("retrieval_e2e_n24")
+    ds = list(range(int(f["n_data"])))
+    random.seed(int(f["seed"]))
+    p = tmp_path / "sub.json"
+    got = select_subset_indices(ds, str(p), subset_size=int(f["n_sub"]))
+    assert got == [int(x) for x in f["av_idx_sub"]]
+    assert json.loads(p.read_text()) == got
+    random.seed(12345)   # a different state: the file wins
+    assert select_subset_indices(ds, str(p), subset_size=3) == got

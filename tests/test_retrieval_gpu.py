@@ -66,3 +66,74 @@ def test_retrieval_matches_reference_fixtures(name):
     pre = ("A->V", "V->A") if kind == "retrieval_av" else ("T->V", "V->T")
     assert [metrics[f"{pre[0]}_r{x}"] for x in (1, 5, 10, 20)] == list(f["recall_qk"])
     assert [metrics[f"{pre[1]}_r{x}"] for x in (1, 5, 10, 20)] == list(f["recall_kq"])
+
+
+def _near_tie_rows(ref, got):
+    """Rows whose reference rank could move under the observed matrix error (the near-tie rule of
+    DESIGN §2): some competitor j sits within twice the row's max |got - ref| of the diagonal."""
+    err = np.abs(got - ref).max(1)
+    n = ref.shape[0]
+    return [i for i in range(n) if np.abs(np.delete(ref[i], i) - ref[i, i]).min() <= 2 * err[i]]
+
+
+@pytest.mark.parametrize("kind", ["av", "tv"])
+def test_model_level_retrieval_matches_reference(kind, tmp_path):
+    """The model-level drop-in (select_subset_indices, embed_av_subset / embed_tv_subset,
+    compute_{av,tv}_retrieval_metrics -- retrieval.py:9-104, 146-188, 200-292) against the
+    reference's own functions run on the same stand-in model and datasets
+    (tests/golden/retrieval_e2e_n24.npz, made by gen_retrieval_e2e.py): subset indices exact
+    (same python `random` draw, file written and re-read); embedded per-item features with the
+    reference's padding / L2-normalisation (AV) and mask trimming (TV) -- lengths exact, values at
+    the bf16 bar; both N x N matrices within 1e-2 of the row scale; ranks exact on every row
+    without a near-tie; the result dicts' keys exact and R@k equal up to the near-tie rows."""
+    import random
+    from tests.retrieval_stub import AVStubDataset, StubModel, TVStubDataset
+    from triad_amd import retrieval as R
+    f = G.load("retrieval_e2e_n24")
+    n, n_sub = int(f["n_data"]), int(f["n_sub"])
+    seed = int(f["seed"]) + (0 if kind == "av" else 1)
+    model = StubModel().cuda()
+    ds = AVStubDataset(n) if kind == "av" else TVStubDataset(n)
+    random.seed(seed)
+    sub = R.select_subset_indices(ds, str(tmp_path / "s1.json"), subset_size=n_sub)
+    assert sub == [int(x) for x in f[kind + "_idx_sub"]]
+    assert R.select_subset_indices(ds, str(tmp_path / "s1.json"), subset_size=n_sub) == sub   # re-read
+    random.seed(seed)
+    idx = R.select_subset_indices(ds, str(tmp_path / "s2.json"), subset_size=1000)
+    assert idx == [int(x) for x in f[kind + "_idx"]]
+    if kind == "av":
+        q, k, paths = R.embed_av_subset(model, ds, idx, device="cuda", num_workers=0)
+        assert paths == [str(x) for x in f["av_paths"]]
+        keys, fq, fk, m_qk, m_kq, tol = ("a", "v"), f["av_a"], f["av_v"], f["av_a2v"], f["av_v2a"], 8e-3
+    else:
+        q, k = R.embed_tv_subset(model, ds, idx, device="cuda", num_workers=0)
+        keys, fq, fk, m_qk, m_kq, tol = ("t", "i"), f["tv_t"], f["tv_i"], f["tv_t2v"], f["tv_v2t"], 4e-3
+    assert model.training is False   # as the reference, the embed leaves the model in eval mode
+    for lst, ref, key in ((q, fq, keys[0]), (k, fk, keys[1])):
+        assert [int(t.shape[0]) for t in lst] == [int(x) for x in f[f"{kind}_{key}_len"]]
+        got = torch.cat([t.float().cpu() for t in lst]).numpy()
+        ref = ref.astype(np.float32)
+        assert np.abs(got - ref).max() <= tol * max(1.0, np.abs(ref).max()), (key, np.abs(got - ref).max())
+    temp = float(f["temp"])
+    s_qk = R.aggregated_similarity(q, k, temp).cpu().double().numpy()
+    s_kq = R.aggregated_similarity(k, q, temp).cpu().double().numpy()
+    ties = set()
+    for got, ref in ((s_qk, m_qk), (s_kq, m_kq)):
+        ref = ref.astype(np.float64)
+        assert np.abs(got - ref).max() <= 1e-2 * np.abs(ref).max(), np.abs(got - ref).max()
+        tied = _near_tie_rows(ref, got)
+        assert len(tied) <= 3, tied
+        ties.add(len(tied))
+        r_ref = ref_cpu.recall_ranks(ref)
+        r_got = R.ranks(torch.from_numpy(got)).numpy()
+        ok = [i for i in range(len(idx)) if i not in tied]
+        np.testing.assert_array_equal(r_got[ok], np.asarray(r_ref)[ok])
+    random.seed(seed)
+    fn = R.compute_av_retrieval_metrics if kind == "av" else R.compute_tv_retrieval_metrics
+    res = fn(model, ds, str(tmp_path / "s3.json"), device="cuda", num_workers=0)
+    ref_res = dict(zip([str(x) for x in f[kind + "_keys"]], [float(x) for x in f[kind + "_vals"]]))
+    assert list(res) == list(ref_res)
+    slack = max(ties) / len(idx) + 1e-12
+    for key in ref_res:
+        assert abs(res[key] - ref_res[key]) <= slack, (key, res[key], ref_res[key])
+    print(f"{kind}: near-tie rows {sorted(ties)}; recall {res}")

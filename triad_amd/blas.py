@@ -22,11 +22,15 @@ LIBRARY = "rocblas"   # "rocblas" | "hipblaslt"
 _configured = None
 
 
-def configure() -> str:
-    """Point PyTorch's BLAS dispatch at LIBRARY (process-wide, idempotent)."""
+def configure(warn_if_late: bool = True) -> str:
+    """Point PyTorch's BLAS dispatch at LIBRARY (process-wide, idempotent).
+
+    warn_if_late: warn when the HIP runtime is already up (a GEMM MAY have fixed the switches).
+    TriadTrainer passes False: a model moved to the GPU has initialised HIP without running a
+    GEMM, so the warning would fire on every ordinary construction."""
     global _configured
     if _configured != LIBRARY:
-        if torch.cuda.is_initialized():
+        if warn_if_late and torch.cuda.is_initialized():
             # the two environment switches are read once (first addmm / first rocBLAS handle): a
             # GEMM that ran before this call has fixed them already
             import warnings

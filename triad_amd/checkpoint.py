@@ -117,8 +117,13 @@ _OPTS = ("others", "audio", "text", "vit")
 
 def trainer_checkpoint(trainer, epoch: int, step: int, best_loss: float = float("inf"), config=None,
                        current_batch_idx: int = 0, current_segment: int = 0, vis_samples_av=None,
-                       vis_samples_tv=None) -> dict:
-    """The dict train.py:406-428 saves, built from a TriadTrainer."""
+                       vis_samples_tv=None, mask_states=None) -> dict:
+    """The dict train.py:406-428 saves, built from a TriadTrainer.
+
+    Data parallel (Mode R, world > 1): the patch-mask generator states of all ranks go into the
+    dict, which takes a collective. Either call this on EVERY rank, or have every rank call
+    `gather_mask_states(trainer)` and pass its result as `mask_states` to a call made on one rank
+    only (e.g. rank 0, inside `if rank == 0:`)."""
     rng_state = {"torch": torch.get_rng_state(),
                  "cuda": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else [],
                  "numpy": np.random.get_state(), "python": random.getstate()}
@@ -126,7 +131,7 @@ def trainer_checkpoint(trainer, epoch: int, step: int, best_loss: float = float(
     if ve is not None and hasattr(ve, "mask_generator"):
         # extra key (the reference ignores it): the host generator of the patch-dropout masks, so a
         # resumed run draws the masks an uninterrupted one would
-        rng_state["triad_patch_mask"] = _mask_generator_state(trainer, ve)
+        rng_state["triad_patch_mask"] = mask_states if mask_states is not None else gather_mask_states(trainer)
     ck = {"epoch": epoch, "step": step, "current_batch_idx": current_batch_idx, "current_segment": current_segment,
           "rng_state": rng_state, "model_state_dict": reference_state_dict(trainer.model, trainer.space)}
     for n in _OPTS:
@@ -139,10 +144,13 @@ def trainer_checkpoint(trainer, epoch: int, step: int, best_loss: float = float(
     return ck
 
 
-def _mask_generator_state(trainer, ve):
-    """Data parallel (Mode R): every rank's own state, gathered into a list indexed by rank (a
-    collective: every rank calls this when saving); one process or Mode G (ranks share one state):
-    the state itself."""
+def gather_mask_states(trainer):
+    """The patch-mask generator state(s) a checkpoint stores. Data parallel (Mode R): every rank's
+    own state, gathered into a list indexed by rank -- a COLLECTIVE, every rank must call it;
+    one process or Mode G (ranks share one state): the state itself."""
+    ve = getattr(trainer.model, "visual_embedder", None)
+    if ve is None or not hasattr(ve, "mask_generator"):
+        return None
     st = ve.mask_generator().get_state()
     world = getattr(trainer, "world", 1)
     if world > 1 and not getattr(trainer, "global_negatives", False):
@@ -175,7 +183,15 @@ def _restore_mask_generator(trainer, ve, saved):
 
 
 def save_checkpoint(trainer, path, epoch: int, step: int, **kw):
-    torch.save(trainer_checkpoint(trainer, epoch, step, **kw), path)
+    """train.py:398-437. Data parallel: call it on EVERY rank (the per-rank mask states are
+    gathered, a collective); only rank 0 writes `path` (the model / optimizer state is identical
+    on every rank after the reduced step). Returns the checkpoint dict on every rank."""
+    ck = trainer_checkpoint(trainer, epoch, step, **kw)
+    import torch.distributed as dist
+    rank = dist.get_rank(getattr(trainer, "pg", None)) if getattr(trainer, "world", 1) > 1 else 0
+    if rank == 0:
+        torch.save(ck, path)
+    return ck
 
 
 def _numpy_array_globals():

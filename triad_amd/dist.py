@@ -74,6 +74,37 @@ def reduce_scatter_rows(full: torch.Tensor, rows_l: int, group=None) -> torch.Te
     return out
 
 
+def agree_touched(space, group=None):
+    """After a data-parallel reduction: a parameter has a gradient iff SOME rank's backward
+    produced one (OR of the ranks' touched sets, every rank ends with the same set).
+
+    The reduced buffer then holds the same value for every parameter on every rank -- the
+    average (or sum) with zeros for ranks that did not produce it (HuBERT's LayerDrop draws
+    differ per rank) -- so those parameters are stepped, counted and clipped identically
+    everywhere, as DDP's reduced buckets are. A parameter no rank produced a gradient for (the
+    idle modality of an av_focus / tv_warmup step, or a layer every rank dropped) stays
+    untouched, so AdamW skips it exactly as torch skips a parameter whose .grad is None
+    (SajayR/TRIAD train.py:1010-1040) -- no weight decay, no momentum step, no step count.
+
+    The touched set is host state that the gradient hooks fill as backward runs on the host, so
+    the OR needs no device work: on a `gloo` group it is a host collective that does not wait for
+    the GPU (TriadTrainer passes a gloo group for an RCCL job); on an `nccl` group it goes through
+    the device and synchronises once."""
+    W, _ = world_rank(group)
+    if W <= 1:
+        return
+    import numpy as np
+    trainable = np.array([bool(p.requires_grad) for p in space.params], dtype=bool)
+    local = torch.from_numpy((space.touched & trainable).astype(np.uint8))
+    if _is_nccl(group):
+        t = local.to(space.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        local = t.cpu()
+    else:
+        dist.all_reduce(local, op=dist.ReduceOp.MAX, group=group)
+    space.touched[:] = local.numpy().astype(bool)
+
+
 def allreduce_grads(flat: torch.Tensor, bucket_elems: int, average: bool, group=None):
     """Bucketed all-reduce of a flat gradient buffer (Mode R: average, Mode G: sum)."""
     W, _ = world_rank(group)
@@ -116,10 +147,12 @@ class GradBucketReducer:
     join a bucket) instead of by the single after-backward `gather_shadow_grads` launch.
     """
 
-    def __init__(self, space, bucket_mb: float = 64.0, wire: str = "fp32", average: bool = True, group=None):
+    def __init__(self, space, bucket_mb: float = 64.0, wire: str = "fp32", average: bool = True, group=None,
+                 mask_group=None):
         if wire not in ("fp32", "bf16"):
             raise ValueError(f"wire must be 'fp32' or 'bf16', not {wire!r}")
         self.space, self.wire, self.average, self.group = space, wire, average, group
+        self.mask_group = mask_group   # host (gloo) group for the touched-set OR; None: `group`
         self.world, _ = world_rank(group)
         self.cuda = space.device.type == "cuda"
         n = len(space.params)
@@ -220,20 +253,6 @@ class GradBucketReducer:
             if in_backward:
                 self.launched_in_backward += 1
 
-    def _mark_touched(self, b):
-        """After the reduction every trainable parameter of the bucket holds the same (possibly
-        zero) averaged gradient on every rank, whether or not THIS rank's backward produced one
-        (HuBERT LayerDrop draws differ per rank). So all of them count as having a gradient --
-        the optimizer steps them, advances their AdamW step count and includes them in the group
-        norms / clip factors -- identically on every rank, as DDP's reduced buckets do. Without
-        this a rank whose backward skipped a layer would skip that layer's update and the
-        replicas would drift apart."""
-        s, e = self.buckets[b]
-        sp = self.space
-        for i in range(s, e):
-            if sp.params[i].requires_grad:
-                sp.touched[i] = True
-
     def _range(self, b):
         s, e = self.buckets[b]
         sp = self.space
@@ -244,7 +263,6 @@ class GradBucketReducer:
         if self.expected[b] == 0:       # every parameter frozen (identically on all ranks): nothing to reduce
             self.works[b] = None
             return
-        self._mark_touched(b)
         g = self._range(b)
         scale = 1.0 / self.world if self.average else 1.0
         if not self.cuda:
@@ -280,6 +298,7 @@ class GradBucketReducer:
             self.order = [int(x) for x in t.cpu()]
             self.arrival = None
         self._drain(flush=True)
+        agree_touched(self.space, self.mask_group if self.mask_group is not None else self.group)
         cur = torch.cuda.current_stream(self.space.device) if self.cuda else None
         for b in self.order:
             item = self.works.pop(b)

@@ -10,9 +10,20 @@ query masks and key lengths so padding never takes part), plus the clip reductio
   V->A: sim[i][j] = mean_v max_a  <a_j,a , v_i,v> / temp      (retrieval.py:111-114)
   T->V / V->T: same with text tokens trimmed to their attention mask (retrieval.py:243-244);
   AV features are L2-normalised first (retrieval.py:93-94), TV features are not.
+
+Model-level entry points with the reference's names, arguments and return values:
+`select_subset_indices`, `embed_av_subset`, `embed_tv_subset`, `compute_av_retrieval_metrics`,
+`compute_tv_retrieval_metrics` (retrieval.py:9-104, 146-188, 200-292). The dataset side (the
+reference's DataLoader over its video / CC3M datasets) is the caller's: any map-style dataset
+with the reference's item format works. Differences: the embedders run under the model's bf16
+autocast (the product path; the reference embeds in fp32), and the aggregation multiplies by
+1 / temperature in fp32 where the reference divides (rank-equivalent up to fp32 ties).
 """
 from __future__ import annotations
 
+import json
+import os
+import random
 from typing import Dict, List, Sequence
 
 import torch
@@ -105,3 +116,128 @@ def tv_retrieval_metrics(text_feats: List[torch.Tensor], image_feats: List[torch
     v2t = aggregated_similarity(image_feats, text_feats, temperature, device)
     rt, rv = recall_at_k(t2v), recall_at_k(v2t)
     return {**{f"T->V_{k}": v for k, v in rt.items()}, **{f"V->T_{k}": v for k, v in rv.items()}}
+
+
+# ---- model-level drop-in (retrieval.py:9-104, 146-188, 200-292) ------------------------------
+def select_subset_indices(dataset, subset_file, subset_size=1000):
+    """retrieval.py:9-30: the indices stored in `subset_file` (JSON list) if it exists, else a
+    random subset (python `random.shuffle` of range(len(dataset)), first `subset_size`), written
+    there -- the same draw as the reference from the same `random` state."""
+    if os.path.exists(subset_file):
+        with open(subset_file, "r") as f:
+            indices = json.load(f)
+        print(f"Loaded {len(indices)} subset indices from {subset_file}")
+        return indices
+    all_indices = list(range(len(dataset)))
+    random.shuffle(all_indices)
+    subset = all_indices[:subset_size]
+    with open(subset_file, "w") as f:
+        json.dump(subset, f)
+    print(f"Created new subset of size {subset_size} and wrote to {subset_file}")
+    return subset
+
+
+class _Subset(torch.utils.data.Dataset):
+    def __init__(self, base, indices, av):
+        self.base, self.indices, self.av = base, indices, av
+
+    def __len__(self):
+        return len(self.indices)
+
+    def __getitem__(self, i):
+        if self.av:   # the AV dataset's evaluation item (no augmentation), retrieval.py:75
+            return self.base.__getitem__(self.indices[i], apply_augmentation=False)
+        return self.base.__getitem__(self.indices[i])
+
+
+def _collate_av(batch):
+    """retrieval.py:46-64: stack frames, zero-pad the waveforms to the batch's longest."""
+    audios = [item["audio"] for item in batch]
+    n = max(a.shape[0] for a in audios)
+    audio = torch.zeros(len(audios), n)
+    for i, a in enumerate(audios):
+        audio[i, :a.shape[0]] = a
+    return {"frames": torch.stack([item["video_frames"] for item in batch]), "audio": audio,
+            "paths": [item["video_path"] for item in batch]}
+
+
+def _collate_tv(batch):
+    images, captions = zip(*batch)
+    return torch.stack(images), list(captions)
+
+
+def _amp(model):
+    return torch.autocast("cuda", dtype=getattr(model, "amp_dtype", torch.bfloat16),
+                          enabled=bool(getattr(model, "use_amp", True)))
+
+
+def embed_av_subset(model, dataset, subset_indices, device="cuda", batch_size=8, num_workers=4,
+                    out_device="cpu"):
+    """retrieval.py:32-104: (audio_feats_list, video_feats_list, video_paths_list), one
+    L2-normalised (N_i, 512) tensor per item (the HIP row normalisation, F.normalize's eps).
+    Like the reference this leaves the model in eval mode (no patch dropout). `out_device`:
+    where the per-item tensors go ("cpu" as the reference; the device keeps them resident for
+    compute_av_retrieval_metrics)."""
+    model.eval()
+    N = len(subset_indices)
+    a_list, v_list, p_list = [None] * N, [None] * N, [None] * N
+    loader = torch.utils.data.DataLoader(_Subset(dataset, subset_indices, True), batch_size=batch_size,
+                                         shuffle=False, num_workers=num_workers, collate_fn=_collate_av,
+                                         drop_last=False)
+    off = 0
+    with torch.no_grad():
+        for batch in loader:
+            frames = batch["frames"].to(device)
+            audio = batch["audio"].to(device)
+            with _amp(model):
+                vfeats = model.visual_embedder(frames)
+                afeats = model.audio_embedder(audio)
+            vfeats, afeats = ops.l2_normalize(vfeats), ops.l2_normalize(afeats)
+            for b in range(vfeats.shape[0]):
+                a_list[off + b] = afeats[b].to(out_device)
+                v_list[off + b] = vfeats[b].to(out_device)
+                p_list[off + b] = batch["paths"][b]
+            off += vfeats.shape[0]
+    return a_list, v_list, p_list
+
+
+def embed_tv_subset(model, dataset, subset_indices, device="cuda", batch_size=8, num_workers=4, out_device="cpu"):
+    """retrieval.py:200-248: (text_feats_list, image_feats_list); each caption's features trimmed
+    to its attention mask's token count (retrieval.py:243-244), no normalisation."""
+    model.eval()
+    N = len(subset_indices)
+    t_list, i_list = [None] * N, [None] * N
+    loader = torch.utils.data.DataLoader(_Subset(dataset, subset_indices, False), batch_size=batch_size,
+                                         shuffle=False, num_workers=num_workers, collate_fn=_collate_tv)
+    off = 0
+    with torch.no_grad():
+        for images, captions in loader:
+            images = images.to(device)
+            with _amp(model):
+                vfeats = model.visual_embedder(images)
+                tfeats, mask = model.text_embedder(captions)
+            n_tok = mask.sum(1).tolist()   # host list (one small copy per batch)
+            for b in range(vfeats.shape[0]):
+                t_list[off + b] = tfeats[b, :int(n_tok[b])].to(out_device)
+                i_list[off + b] = vfeats[b].to(out_device)
+            off += vfeats.shape[0]
+    return t_list, i_list
+
+
+def compute_av_retrieval_metrics(model, dataset, subset_file, device="cuda", subset_size=1000, batch_size=8,
+                                 num_workers=4):
+    """retrieval.py:146-188: subset -> embed -> A->V and V->A matrices (one fused-kernel launch
+    each instead of the reference's N^2 per-pair loop) -> R@1/5/10/20 with the reference's keys."""
+    indices = select_subset_indices(dataset, subset_file, subset_size=subset_size)
+    a, v, _ = embed_av_subset(model, dataset, indices, device=device, batch_size=batch_size,
+                              num_workers=num_workers, out_device=device)
+    return av_retrieval_metrics(a, v, model.temperature.item(), device)
+
+
+def compute_tv_retrieval_metrics(model, dataset, subset_file, device="cuda", subset_size=1000, batch_size=8,
+                                 num_workers=4):
+    """retrieval.py:250-292, as compute_av_retrieval_metrics with T->V / V->T keys."""
+    indices = select_subset_indices(dataset, subset_file, subset_size=subset_size)
+    t, im = embed_tv_subset(model, dataset, indices, device=device, batch_size=batch_size,
+                            num_workers=num_workers, out_device=device)
+    return tv_retrieval_metrics(t, im, model.temperature.item(), device)

@@ -78,7 +78,7 @@ class TriadTrainer:
         self.device = torch.device(device)
         if self.device.type == "cuda":  # library GEMMs on rocBLAS, not hipBLASLt (explicit opt-in, blas.py)
             from . import blas
-            blas.configure()
+            blas.configure(warn_if_late=False)
         self.grad_accum = gradient_accumulation_steps
         self.unfreeze = dict(audio=unfreeze_audio_step, text=unfreeze_text_step, vit=unfreeze_vit_step)
         self.av_weight_start, self.av_weight_end = av_weight_start, av_weight_end
@@ -113,8 +113,18 @@ class TriadTrainer:
             p.requires_grad = False
         for p in self.groups["vit_lora"]:
             p.requires_grad = True
-        # data parallel: bucketed gradient all-reduce overlapped with backward (fused optimizer)
+        # data parallel: bucketed gradient all-reduce overlapped with backward (fused optimizer).
+        # NOTE: dist.new_group is collective over the default group -- every rank of the job must
+        # construct its TriadTrainer (the usual one-trainer-per-rank script does).
         self.reducer = None
+        self.mask_group = None
+        if self.world > 1:
+            # the touched-set OR after each reduction (dist.agree_touched) runs on the host: a gloo
+            # group beside an RCCL job, so it never waits for the GPU
+            ranks = (dist.get_process_group_ranks(process_group) if process_group is not None
+                     else list(range(self.world)))
+            self.mask_group = (process_group if dist.get_backend(process_group) == "gloo"
+                               else dist.new_group(ranks=ranks, backend="gloo"))
         if self.world > 1 and self.space is not None and overlap_grad_reduce:
             # its own communicator: the bucket all-reduces are issued from gradient hooks during
             # backward, while Mode G's head issues its reduce-scatter / all-gathers inside the same
@@ -124,7 +134,8 @@ class TriadTrainer:
                      else list(range(self.world)))
             self.reducer_group = dist.new_group(ranks=ranks)
             self.reducer = tdist.GradBucketReducer(self.space, bucket_mb, grad_wire,
-                                                   average=not self.global_negatives, group=self.reducer_group)
+                                                   average=not self.global_negatives, group=self.reducer_group,
+                                                   mask_group=self.mask_group)
         self.total_updates = total_updates
         self.sched_others = _one_cycle(self.opt_others, learning_rate, total_updates)
         self.sched_audio = _one_cycle(self.opt_audio, learning_rate * 0.25, total_updates - unfreeze_audio_step)
@@ -156,8 +167,8 @@ class TriadTrainer:
     def _allreduce_grads(self):
         """Data-parallel gradient reduction over the flat gradient buffer (bucketed RCCL
         all-reduce). Mode R averages (replicas of the reference loss); Mode G sums (every rank
-        holds its share of the one global loss's gradient). Every rank runs the same phases, so
-        the set of parameters with gradients is identical across ranks by construction."""
+        holds its share of the one global loss's gradient). A parameter then has a gradient iff some
+        rank produced one (dist.agree_touched: an OR over ranks on the host)."""
         if self.world <= 1:
             return
         if self.reducer is not None:   # launched during backward; wait for the reductions
@@ -170,11 +181,9 @@ class TriadTrainer:
                     tdist.allreduce_grads(p.grad.view(-1), p.grad.numel(), avg, self.pg)
             return
         tdist.allreduce_grads(self.space.flat_g, self.bucket_elems, avg, self.pg)
-        # every trainable parameter now holds the same reduced gradient on every rank (see
-        # GradBucketReducer._mark_touched): step all of them, identically everywhere
-        for i, p in enumerate(self.space.params):
-            if p.requires_grad:
-                self.space.touched[i] = True
+        # every rank now holds the same reduced gradient; a parameter counts as having one iff
+        # some rank produced it (dist.agree_touched)
+        tdist.agree_touched(self.space, self.mask_group)
 
     def step(self, frames, audio, text, phase="full_joint", progress=0.0, av_keep=None, tv_keep=None,
              shared_frames=True, frames_tv=None):
