@@ -238,7 +238,7 @@ def recall_at_k(sim):
 
 # ---- chunked form for BASELINE-size parity checks -----------------------------------------
 def head_loss_chunked(kind, q, k, temperature, q_mask=None, threshold=0.8, weight=0.01, chunk=8,
-                      dtype=torch.float64, grads=True):
+                      dtype=torch.float64, grads=True, grad_rows=None):
     """The same values as av_loss (kind "av", model.py:370-472) / tv_loss (kind "tv",
     model.py:490-593), evaluated in chunks of query samples so the (B, B, Nq, Nk) tensor is never
     held whole (c3: 13 GB in fp32). Runs on whatever device the inputs are on (plain torch;
@@ -249,7 +249,10 @@ def head_loss_chunked(kind, q, k, temperature, q_mask=None, threshold=0.8, weigh
     Pass 2 (grads=True) re-evaluates each chunk under autograd with the surrogate
         sum(dCE/dclip * clip_chunk) + 0.15 * sum clamp(S)^2 / N_el + w_diag * diag_chunk / cnt,
     whose gradient equals the loss gradient (every term is additive over query samples, and the
-    CE enters only through clip). Returns a dict of floats / tensors (fp64)."""
+    CE enters only through clip). grad_rows=(i0, i1): pass 2 over those query samples only -- dq
+    of those rows, and dk / dtemp = the CONTRIBUTION of those rows (what one data-parallel rank
+    holding them computes before the reduce-scatter / all-reduce, SURVEY §8e Mode G; the l_cal
+    term of dtemp is included). Returns a dict of floats / tensors (fp64)."""
     av = kind == "av"
     B, Nq, _ = q.shape
     Nk = k.shape[1]
@@ -314,9 +317,10 @@ def head_loss_chunked(kind, q, k, temperature, q_mask=None, threshold=0.8, weigh
     Qg = Qd.clone().requires_grad_(True)
     Kg = Kd.clone().requires_grad_(True)
     tg = t.clone().requires_grad_(True)
-    for i0 in range(0, B, chunk):
-        c_, n_, d_ = chunk_terms(Qg[i0:i0 + chunk], Kg, tg, i0)
-        sur = (dclip[i0:i0 + chunk] * c_).sum() + 0.15 * n_ / n_el + (w_dg * d_ / cnt if cnt > 0 else 0.0)
+    g0, g1 = (0, B) if grad_rows is None else grad_rows
+    for i0 in range(g0, g1, chunk):
+        c_, n_, d_ = chunk_terms(Qg[i0:min(i0 + chunk, g1)], Kg, tg, i0)
+        sur = (dclip[i0:i0 + c_.shape[0]] * c_).sum() + 0.15 * n_ / n_el + (w_dg * d_ / cnt if cnt > 0 else 0.0)
         sur.backward()
     dtemp = tg.grad.detach().clone()
     if av:

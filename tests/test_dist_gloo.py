@@ -260,3 +260,96 @@ def test_overlapped_bucket_reducer_averages_gradients(wire, skip):
                 assert launched >= 1   # overlap: at least one bucket went out during backward
             # (skip, rank 1, step 1: the bucket of the missing gradient heads the launch order, so
             # that rank issues everything at the flush -- in the same order as rank 0)
+
+
+# ---- world 4: per-rank LayerDrop skips and a staged unfreeze ------------------------------------
+def _skip4(rank, step):
+    """w2 skipped by: step 1 ranks 1 and 3 (per-rank LayerDrop draws), step 3 every rank."""
+    return (step == 1 and rank in (1, 3)) or step == 3
+
+
+def _frozen4(step):
+    """l1 frozen before step 2, trainable from step 2 on (train.py:527-548's staged unfreeze)."""
+    return step < 2
+
+
+def _reducer_worker4(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from triad_amd import dist as tdist
+        from triad_amd import optim as fo
+        torch.manual_seed(0)
+        net = _Net()
+        params = list(net.parameters())
+        space = fo.FlatParamSpace(params, "cpu", shadow=[net.w2])
+        red = tdist.GradBucketReducer(space, bucket_mb=0.01, wire="fp32", average=True)
+        out = []
+        for step in range(5):
+            for p in net.l1.parameters():
+                p.requires_grad = not _frozen4(step)
+            space.zero_grad(list(range(len(params))))
+            x, y = _net_inputs(rank, step)
+            red.begin(accumulate=False)
+            ((net(x, skip_w2=_skip4(rank, step)) - y) ** 2).mean().backward()
+            red.finish()
+            out.append((space.flat_g.numpy().copy(), list(red.order), space.touched.copy()))
+        q.put((rank, out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucket_reducer_world4_layerdrop_and_unfreeze():
+    """GradBucketReducer on FOUR gloo ranks over five steps with per-rank LayerDrop
+    skips (step 1: ranks 1 and 3 produce no gradient for w2), a staged unfreeze (l1 trainable from
+    step 2: the launch order is re-derived at that step, identically on every rank) and a layer
+    no rank uses (step 3). Every step: the reduced buffer is the average of the four ranks'
+    gradients (zeros for the ranks that skipped), identical launch order on all ranks, and the
+    touched set = parameters SOME rank produced a gradient for (frozen l1 never; w2 at step 1 on
+    every rank, at step 3 on none)."""
+    from triad_amd import optim as fo
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reducer_worker4, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r[2]
+    torch.manual_seed(0)
+    net = _Net()
+    space = fo.FlatParamSpace(list(net.parameters()), "cpu", shadow=[net.w2])
+    i_w2 = space.index[id(net.w2)]
+    l1_ids = [space.index[id(p)] for p in net.l1.parameters()]
+    for step in range(5):
+        for p in net.l1.parameters():
+            p.requires_grad = not _frozen4(step)
+        acc = torch.zeros_like(space.flat_g)
+        for rank in range(world):
+            space.zero_grad(list(range(len(space.params))))
+            x, y = _net_inputs(rank, step)
+            ((net(x, skip_w2=_skip4(rank, step)) - y) ** 2).mean().backward()
+            if net.w2.grad is not None:
+                space.flat_g[space.offsets[i_w2]:space.offsets[i_w2] + net.w2.numel()].copy_(
+                    net.w2.grad.float().view(-1))
+            net.w2.grad = None
+            acc += space.flat_g / world
+        want = np.ones(len(space.params), dtype=bool)
+        if _frozen4(step):
+            want[l1_ids] = False
+        if step == 3:
+            want[i_w2] = False
+        for rank in range(world):
+            got, order, touched = res[rank][1][step]
+            err = float((torch.from_numpy(got) - acc).abs().max() / acc.abs().max())
+            assert err < 1e-6, (step, rank, err)
+            assert order == res[0][1][step][1], (step, rank)
+            assert (touched == want).all(), (step, rank, touched, want)

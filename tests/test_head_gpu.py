@@ -355,6 +355,36 @@ def test_tile_gemm_packed_bit_identical_to_ring(panels, ct, splits):
             assert torch.equal(slabs, slabs2), (dk, M, nkt, splits)
 
 
+@pytest.mark.parametrize("panels,ct,splits", [(2, 4, 1), (3, 7, 1), (4, 9, 3), (2, 8, 5)])
+def test_tile_gemm_mfma16_dq_matches_fp64(panels, ct, splits):
+    """The dQ GEMM on v_mfma_f32_16x16x32_bf16 (triad_bfrag_pack16 + triad_tile_gemm_packed16)
+    against an fp64 dQ = alpha dS K over the untiled dS (_untile_dS) -- within bf16 output
+    rounding -- and against the 32x32x16 form (the same sums in another fp32 order), split-K
+    slabs included."""
+    from triad_amd._lib import call, ptr, stream_ptr
+    g = torch.Generator(device=dev).manual_seed(7 * panels + ct + splits)
+    R_pad, CT = panels * 128, ct
+    dS = (torch.randn(R_pad // 32 * CT * 1024, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    K = torch.randn(CT * 32, 512, device=dev, generator=g).to(torch.bfloat16)
+    alpha = torch.tensor([0.75], device=dev)
+    st = stream_ptr()
+    M, nkt = R_pad, CT
+    Bp16 = torch.empty(nkt * 32 * 512, dtype=torch.bfloat16, device=dev)
+    call("triad_bfrag_pack16", ptr(K), nkt, 0, ptr(Bp16), st)
+    slabs = torch.empty(splits * M * 512, device=dev) if splits > 1 else None
+    out16 = torch.empty(M, 512, dtype=torch.bfloat16, device=dev)
+    ring = torch.empty_like(out16)
+    call("triad_tile_gemm_packed16", ptr(dS), CT, 0, ptr(Bp16), M, nkt, ptr(alpha), splits, ptr(slabs), ptr(out16), st)
+    call("triad_tile_gemm", ptr(dS), CT, 0, ptr(K), M, nkt, ptr(alpha), 1, None, ptr(ring), st)
+    torch.cuda.synchronize()
+    dense = _untile_dS(dS, R_pad, CT).double()
+    ref = 0.75 * dense @ K.double()
+    err = float((out16.double() - ref).abs().max() / ref.abs().max())
+    assert err < 8e-3, err
+    d = float((out16.float() - ring.float()).abs().max())
+    assert d <= 2.0 ** -7 * float(ring.float().abs().max()), d
+
+
 @pytest.mark.parametrize("B,Na,Nt,Nv,budget", [(6, 49, 16, 70, None), (16, 199, 32, 205, None),
                                                (5, 300, 8, 40, "mixed"), (3, 2, 1, 33, None)])
 def test_pair_launch_matches_two_heads(B, Na, Nt, Nv, budget):

@@ -42,9 +42,14 @@ def run(streams, frames, audio, text):
             dys[name] = g.detach().clone()
         return h
 
+    def fwd_hook(n):
+        def h(mod, inp, out):   # must return None (a returned value replaces the output)
+            if out.requires_grad:
+                out.register_hook(cap(n))
+        return h
+
     for n, mod in lin.items():
-        hooks.append(mod.register_forward_hook(lambda mod, i, o, n=n: o.register_hook(cap(n)) if o.requires_grad
-                                               else None))
+        hooks.append(mod.register_forward_hook(fwd_hook(n)))
     grads = {}
     inner = tr.space.gather_shadow_grads
 

@@ -340,6 +340,122 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db_kernel(const bf16* __rest
     }
 }
 
+// ---- v_mfma_f32_16x16x32_bf16 form of the direct-B dQ GEMM ------------------------------------
+// The same workgroup (8 waves, 128 rows x 512 columns, wave w owns columns [64w, 64w + 64)), the
+// same A stream (dS tiles through the LDS ring by one LDS-DMA piece per wave per k tile) and the
+// same register-streamed B, but each wave's 128 x 64 output is 8 x 4 blocks of 16 x 16 computed by
+// v_mfma_f32_16x16x32_bf16 (32 per 32-deep k tile instead of 16 v_mfma_f32_32x32x16): the shape
+// the microarchitecture guide measures at ~1.12-1.15x the FLOP/s of 32x32x16 on random data at
+// the clock the chip holds under load (MI355X_MICROARCH.md, 'DVFS give-back' item 7).
+//   A fragment (row block rb, lane l): query row r = 16 (rb & 1) + (l & 15) of tile rb >> 1, k
+//   chunk kc = l >> 4 = 16-byte chunk (hh = kc & 1, j = kc >> 1) of the stored dS row, i.e. keys
+//   16 j + 8 (i >> 2) + 4 hh + (i & 3), i = 0..7 -- the forward's accumulator order, read as is;
+//   B fragment (column block cb): the same 8 keys of column 64 w + 16 cb + (l & 15), packed once
+//   by bfrag_pack16_kernel at ((kt * 8 + w) * 4 + cb) * 512 + l * 8.
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(512) void bfrag_pack16_kernel(const bf16* __restrict__ B, bf16* __restrict__ Bp) {
+  __shared__ __attribute__((aligned(16))) bf16 img[TBK * TBN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long kt = blockIdx.x;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int k = wave * 4 + r;
+    glds16(B + (kt * TBK + k) * TBN + (lane ^ ((k & 3) << 2)) * 8, img + k * TBN);
+  }
+  lds_dma_barrier();
+  const int kc = lane >> 4, hh = kc & 1, j = kc >> 1;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int col = wave * 64 + cb * 16 + (lane & 15);
+    bf16x8 f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = img[b_off(16 * j + 8 * (i >> 2) + 4 * hh + (i & 3), col)];
+    *(bf16x8*)(Bp + ((kt * 8 + wave) * 4 + cb) * 512 + lane * 8) = f;
+  }
+}
+
+template <bool SLAB, int KS, int DD>
+__global__ __launch_bounds__(512, 1) void tile_gemm_db16q_kernel(const bf16* __restrict__ Dt, long long CT,
+                                                                 const bf16* __restrict__ Bp, int M, int nkt_total,
+                                                                 int kt_per_split, const float* __restrict__ alpha_p,
+                                                                 void* __restrict__ Cout) {
+  static_assert(DD >= 1 && DD <= 4 && 5 * KS * (DD - 1) <= 63, "stage shape");
+  constexpr int NB = DD + 1;
+  __shared__ __attribute__((aligned(16))) bf16 lds[NB * KS * 4096];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, kc = lane >> 4;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  const int m0 = swz * TBM, mt0 = m0 / 32;
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int nkt = __builtin_amdgcn_readfirstlane(min(kt_per_split, nkt_total - kt0));
+  const int kt_last = kt0 + nkt - 1;
+  const int nst = (nkt + KS - 1) / KS;
+  // this lane's A chunk inside a 32-row tile, per row half: stored chunk 2 (r + 32 hh) + j
+  int aoff[2];
+#pragma unroll
+  for (int rh = 0; rh < 2; ++rh) aoff[rh] = swz_q(2 * (16 * rh + l16 + 32 * (kc & 1)) + (kc >> 1)) * 8;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = (f32x4){};
+
+  bf16x8 bq[NB][4 * KS];
+#pragma unroll
+  for (int p = 0; p < DD; ++p)
+    if (p < nst) db_stage<false, KS>(Dt, CT, Bp, mt0, kt0 + p * KS, kt_last, lds + p * KS * 4096, bq[p], wave, lane);
+  for (int st0 = 0; st0 < nst; st0 += NB) {
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int st = st0 + u;
+      if (st >= nst) break;
+      db_wait<5 * KS>(min(DD - 1, nst - 1 - st));
+      __syncthreads();
+      const bool pf = st + DD < nst;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        if (st * KS + k >= nkt) break;
+        const bf16* As = lds + (u * KS + k) * 4096;
+        bf16x8 af[8];
+#pragma unroll
+        for (int rb = 0; rb < 8; ++rb) af[rb] = *(const bf16x8*)(As + (rb >> 1) * 1024 + aoff[rb & 1]);
+#pragma unroll
+        for (int rb = 0; rb < 8; ++rb) {
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = mfma16(af[rb], bq[u][4 * k + cb], acc[rb][cb]);
+          if (k == 0 && rb == 1 && pf) {
+            __builtin_amdgcn_sched_barrier(0);
+            db_stage<false, KS>(Dt, CT, Bp, mt0, kt0 + (st + DD) * KS, kt_last, lds + ((u + DD) % NB) * KS * 4096,
+                                bq[(u + DD) % NB], wave, lane);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    }
+  }
+
+  const float alpha = SLAB ? 1.f : *alpha_p;
+#pragma unroll
+  for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int col = wave * 64 + cb * 16 + l16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + rb * 16 + kc * 4 + i;
+        const float val = alpha * acc[rb][cb][i];
+        if (SLAB) ((float*)Cout)[((size_t)blockIdx.y * M + m) * TBN + col] = val;
+        else ((bf16*)Cout)[(size_t)m * TBN + col] = (bf16)val;
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -424,6 +540,32 @@ int triad_tile_gemm_slabs(const void* Dt, long long CT, int dk, const void* B, i
   else hipLaunchKernelGGL((tile_gemm_ring_kernel<false, true>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
+}
+
+// v_mfma_f32_16x16x32_bf16 forms (dQ only: dk must be 0): B's fragments in that MFMA's order.
+int triad_bfrag_pack16(const void* B, int nkt, int dk, void* Bp, hipStream_t stream) {
+  if (nkt <= 0 || !B || !Bp || dk) return TRIAD_EINVAL;
+  hipLaunchKernelGGL(bfrag_pack16_kernel, dim3(nkt), dim3(512), 0, stream, (const bf16*)B, (bf16*)Bp);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+int triad_tile_gemm_packed16(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, const float* alpha,
+                             int splits, float* slabs, void* C, hipStream_t stream) {
+  if (dk || M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
+  const int kps = (nkt + splits - 1) / splits;
+  dim3 grid(M / TBM, splits);
+  const bf16* d = (const bf16*)Dt;
+  const bf16* b = (const bf16*)Bp;
+  if (splits == 1) {
+    hipLaunchKernelGGL((tile_gemm_db16q_kernel<false, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
+    TRIAD_CHECK_LAUNCH();
+    return TRIAD_OK;
+  }
+  hipLaunchKernelGGL((tile_gemm_db16q_kernel<true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr,
+                     (void*)slabs);
+  TRIAD_CHECK_LAUNCH();
+  return triad_sum_slabs(slabs, splits, (long long)M * TBN, alpha, 1, C, stream);
 }
 
 }  // extern "C"

@@ -534,7 +534,7 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
   if (M % BM || N % BN || Kd % BK || lda % 8 || ldb % 8 || splits < 1) return TRIAD_EINVAL;
   const int kps = ((Kd / BK + splits - 1) / splits) * BK;
   // the 256-row ring pays off on long k loops or many row tiles (conv / projection GEMMs);
-  // the short split-K weight-gradient loops keep the 128 x 128 form (measured, tools/dw_variants.py)
+  // the short split-K weight-gradient loops keep the 128 x 128 form (measured, profiles/r01_dw_gemm_*.log)
   const bool w4_ok = M % GW_M == 0 && N % GW_N == 0;
   // the four-wave form measured faster on the long conv-stack GEMMs (tools/gemm_forms.py:
   // 2.94 -> 2.67 ms at M = 1.6 M, N = 512, K = 1536); the split-K weight gradients and the

@@ -4,7 +4,7 @@ The reference trains HuBERT and DistilBERT end to end after `unfreeze_*_step` (S
 train.py:527-548; model.py:29-30, 79-80) under bf16 autocast (model.py:483, 603). Their
 weight gradients dW = dy^T x contract over all B*N tokens (50,944 for HuBERT at c3) into a
 768 x 768 .. 3,072 x 768 output: too few output tiles for the library GEMM's heuristics, which
-reach 230-620 TFLOP/s on these shapes on MI355X (tools/dw_variants.py). The split-K MFMA GEMM of
+reach 230-620 TFLOP/s on these shapes on MI355X (round-1 A/B, profiles/r01_dw_gemm_*.log). The split-K MFMA GEMM of
 csrc/gemm.hip (fp32 slabs over token ranges, one bf16 rounding at the end) runs them 1.1-2.4x
 faster (c3 step: 1108 -> 1140 triples/s). Forward and dX stay on torch (hipBLASLt runs those shapes at ~1 PFLOP/s).
 
@@ -25,7 +25,7 @@ from ._lib import call, ptr, stream_ptr
 MIN_TOKENS = 4096  # DistilBERT at B=256 (8,192 tokens) still gains 1.1-1.8x
 
 
-# Split-K factors measured per output-tile count on MI355X (tools/dw_variants.py with
+# Split-K factors measured per output-tile count on MI355X (round-1 A/B with
 # TRIAD_DW_SPLITS, profiles/r01_dw_splits_{50944,8192}.log). The best factor is set by how
 # tiles x splits workgroups quantise onto the CUs' slots, not by a smooth rule: e.g. 144 tiles
 # run 7 splits (1,008 workgroups) 8-11 % faster than 8 (1,152) at 50,944 tokens, and 3 splits
@@ -99,7 +99,7 @@ _CLAIMED = {}  # device index -> (autograd graph task, ids of the weights whose 
 def side_stream_ok(*ws: torch.Tensor) -> bool:
     """May this backward node compute the dW of `ws` on the side stream? Only for bf16 weights
     whose .grad is empty, inside a backward pass, and only at a weight's FIRST use in the pass:
-    a weight used twice in one graph (two chunks through one layer, tools/audio_reuse_diag.py)
+    a weight used twice in one graph (two chunks through one layer, profiles/r03_audio_reuse_diag.log)
     has its two dW summed by autograd on the main stream as soon as the second arrives, so the
     second node makes the main stream wait for the side stream (which holds the first dW) and
     computes its dW there."""

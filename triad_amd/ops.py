@@ -602,7 +602,7 @@ def _pad_rows(x: torch.Tensor, rows: int) -> torch.Tensor:
 def _splitk(Kd, mn_tiles):
     """Split-K factor of the projection-head weight gradients (128 x 128 tiles): one round of
     workgroups over the 256 CUs, >= 512 token rows per split (so the 8,192-row text head also
-    fills the chip: 16 x 16 workgroups for dW2). Measured (tools/dw_proj_forms.py,
+    fills the chip: 16 x 16 workgroups for dW2). Measured (round-2 A/B,
     profiles/r02_dw_proj_forms.log): fewer, longer splits beat two rounds once the slab
     reduction is counted -- dW2 at 65,536 rows 66 us (16 splits) vs 78 us (32), dW1 86 vs 96 us;
     the 256 x 256 four-wave form is no faster at its best split."""
@@ -733,7 +733,7 @@ class _ProjectionHeadPasses(torch.autograd.Function):
     under autocast), the LayerNorm and its backward as single HIP row passes (triad_ln_fwd /
     triad_ln_bwd3, dgamma / dbeta / db1 column partials in the same pass), the weight gradients on
     the split-K HIP GEMM (2-4x hipBLASLt on these contraction-over-tokens shapes,
-    tools/projhead_lib_probe.py)."""
+    profiles/r02_projhead_kernels.log)."""
 
     @staticmethod
     def forward(ctx, h, w1, b1, gamma, beta, w2, b2, eps):
