@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--cpu-head-batch", type=int, default=48, help="batch of the CPU hot-path timing (extrapolated)")
     ap.add_argument("--separate-steps", type=int, default=3,
                     help="timed steps of the --separate-frames variant reported beside the headline (0 = skip)")
+    ap.add_argument("--single-stream-steps", type=int, default=3,
+                    help="timed steps with the three backbones on ONE stream, reported beside the headline "
+                         "(0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate-frames", action="store_true",
                     help="encode the AV and TV frame batches separately (2x ViT work)")
@@ -119,6 +122,12 @@ def kernel_report(timers):
             r["ds_bytes"] = r.get("ds_bytes", 0.0) + (meta or {}).get("ds_bytes", 0.0)
             r["grid"] = (meta or {}).get("grid")
     return rep
+
+
+def model_streams():
+    """Does forward_triad run the audio / text backbones on their own streams (the headline mode)?"""
+    from triad_amd.model import modality_streams_enabled
+    return modality_streams_enabled()
 
 
 def main():
@@ -223,6 +232,40 @@ def main():
         if rank == 0:
             print(f"[bench] {a.separate_steps} separate-frames steps: {dts:.2f} s", file=sys.stderr, flush=True)
 
+    single = None
+    if a.single_stream_steps > 0:
+        # the same step with the audio / text backbones on the main stream (forward_triad's
+        # TRIAD_MODALITY_STREAMS=0): the serial execution order, reported beside the headline
+        prev = os.environ.get("TRIAD_MODALITY_STREAMS")
+        os.environ["TRIAD_MODALITY_STREAMS"] = "0" if model_streams() else "1"
+        try:
+            step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+            for _ in range(a.single_stream_steps):
+                step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            dtss = time.perf_counter() - t1
+        finally:
+            if prev is None:
+                os.environ.pop("TRIAD_MODALITY_STREAMS", None)
+            else:
+                os.environ["TRIAD_MODALITY_STREAMS"] = prev
+        if world > 1:
+            t = torch.tensor([dtss], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dtss = float(t)
+        single = {"value": world * a.batch * a.single_stream_steps / dtss, "unit": "triples/s",
+                  "steps": a.single_stream_steps, "ms_per_step": dtss / a.single_stream_steps * 1e3,
+                  "modality_streams": not model_streams()}
+        if rank == 0:
+            print(f"[bench] {a.single_stream_steps} steps with modality streams "
+                  f"{'on' if single['modality_streams'] else 'off'}: {dtss:.2f} s", file=sys.stderr, flush=True)
+
     if rank == 0:
         value = world * a.batch * a.steps / dt
         # dominant hot-path kernel: the similarity forward of both heads in one launch (S = temp*Q K^T,
@@ -274,6 +317,9 @@ def main():
                      "kernels": {k: kstats(k) for k in sorted(rep) if k in head_keys}},
             "backbone_hip_gemm_ms_per_step": sum(v["ms"] for k, v in rep.items() if k not in head_keys) / a.steps,
         }
+        res["config"]["modality_streams"] = model_streams()
+        if single is not None:
+            res["other_stream_mode"] = single
         if sep is not None:
             res["separate_frames"] = {"value": sep, "unit": "triples/s", "steps": a.separate_steps,
                                       "note": "AV and TV frame batches encoded separately, as the reference's "

@@ -13,6 +13,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of a 3-step bench -> gpurun_out/<tag>_prof/
 #   pmc:<name>:<counters>  one rocprofv3 --pmc pass (counters comma-separated) of a 3-step bench
 #   py:<script args>       python <script> (tools/ micro-benchmarks)    -> gpurun_out/<tag>_py<N>.log
+#   envpy:A=1,B=2:<script args>  the same with extra environment for this step
 #   profpy:<script args>   the same under rocprofv3 --kernel-trace --stats -> gpurun_out/<tag>_profpy<N>/
 #   pmcpy:<name>:<counters>:<script args>  one rocprofv3 --pmc pass over a python script
 # environment: extra env for every step may be given as STEP_ENV="A=1 B=2" (exported first).
@@ -74,6 +75,10 @@ for step in "$@"; do
         -- python3 $script > "gpurun_out/${tag}_pmcpy_${name}.log" 2>&1 ;;
     py:*)
       timeout -k 10 600 python ${step#py:} > "gpurun_out/${tag}_py${n}.log" 2>&1 ;;
+    envpy:*)
+      # envpy:A=1,B=2:<script args>  python with extra environment for this step only
+      rest=${step#envpy:}; ev=${rest%%:*}; script=${rest#*:}
+      ( export ${ev//,/ }; timeout -k 10 600 python $script ) > "gpurun_out/${tag}_py${n}.log" 2>&1 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -1,0 +1,164 @@
+// Co-residency hazard probe (diagnostic only, not part of the product library).
+//
+// Round 3 / 4 evidence: kernels whose fp32 arithmetic is packed (v_pk_*_f32) -- PyTorch's bf16
+// sum reduction, an SLP-vectorised conv kernel -- return wrong values in some launches while one
+// of the library's MFMA GEMMs runs on another stream, and never beside rocBLAS GEMMs or alone
+// (tools/reduce_race.py). Here the aggressor is cut into its ingredients and the victims are
+// minimal kernels with a fixed instruction choice (inline asm), each checked bit for bit against
+// its solo result (tools/hazard_probe.py):
+//   aggressors: mfma_loop (v_mfma_f32_32x32x16_bf16 chains, operands in registers), dma_loop
+//               (global_load_lds_dwordx4 into an LDS ring + vmcnt / barrier, no MFMA), mix_loop
+//               (both), valu_loop (scalar fp32 FMAs: control);
+//   victims:    pk_victim (v_pk_fma_f32 chains), fma_victim (the same arithmetic as scalar
+//               v_fma_f32), pk_add_victim (v_pk_add_f32 accumulation, a reduction's inner loop).
+#include <hip/hip_runtime.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+#define LDSP(p) ((__attribute__((address_space(3))) void*)(p))
+
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)LDSP(lds_base));
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds)
+      : "memory");
+}
+
+extern "C" __global__ __launch_bounds__(256) void mfma_loop(float* out, int iters) {
+  const int t = threadIdx.x;
+  bf16x8 a, b;
+  for (int i = 0; i < 8; ++i) {
+    a[i] = (__bf16)(0.001f * ((t * 7 + i) % 13) - 0.006f);
+    b[i] = (__bf16)(0.001f * ((t * 5 + i) % 11) - 0.005f);
+  }
+  f32x16 c0 = {}, c1 = {}, c2 = {}, c3 = {};
+  for (int it = 0; it < iters; ++it) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, a, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, a, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, b, c3, 0, 0, 0);
+  }
+  float s = 0.f;
+  for (int i = 0; i < 16; ++i) s += c0[i] + c1[i] + c2[i] + c3[i];
+  out[blockIdx.x * 256 + t] = s;
+}
+
+extern "C" __global__ __launch_bounds__(256) void dma_loop(const float* src, long long n4, float* out, int iters) {
+  __shared__ __attribute__((aligned(16))) float ring[4 * 4 * 256];   // 4 slots x 4 waves x 1 KB
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  float s = 0.f;
+  for (int it = 0; it < iters; ++it) {
+    const int slot = it & 3;
+    const long long row = ((long long)(blockIdx.x * 131 + it * 17 + wave) * 64 + lane) % n4;
+    glds16(src + row * 4, ring + (slot * 4 + wave) * 256);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    s += ring[(slot * 4 + (wave ^ 1)) * 256 + lane * 4];
+    __syncthreads();
+  }
+  out[blockIdx.x * 256 + t] = s;
+}
+
+extern "C" __global__ __launch_bounds__(256) void mix_loop(const float* src, long long n4, float* out, int iters) {
+  __shared__ __attribute__((aligned(16))) float ring[4 * 4 * 256];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  bf16x8 a, b;
+  for (int i = 0; i < 8; ++i) {
+    a[i] = (__bf16)(0.001f * ((t * 7 + i) % 13) - 0.006f);
+    b[i] = (__bf16)(0.001f * ((t * 5 + i) % 11) - 0.005f);
+  }
+  f32x16 c0 = {}, c1 = {};
+  float s = 0.f;
+  for (int it = 0; it < iters; ++it) {
+    const int slot = it & 3;
+    const long long row = ((long long)(blockIdx.x * 131 + it * 17 + wave) * 64 + lane) % n4;
+    glds16(src + row * 4, ring + (slot * 4 + wave) * 256);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, a, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, a, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, b, c1, 0, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    s += ring[(slot * 4 + (wave ^ 1)) * 256 + lane * 4];
+    __syncthreads();
+  }
+  for (int i = 0; i < 16; ++i) s += c0[i] + c1[i];
+  out[blockIdx.x * 256 + t] = s;
+}
+
+extern "C" __global__ __launch_bounds__(256) void valu_loop(float* out, int iters) {
+  float x = threadIdx.x * 1e-3f, y = 1.0001f;
+  for (int it = 0; it < iters; ++it) {
+    x = fmaf(x, y, 1e-6f);
+    y = fmaf(y, 0.99999f, 1e-7f);
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = x + y;
+}
+
+// victims: 64 dependent steps per element, element = (x, y) pair
+extern "C" __global__ __launch_bounds__(256) void pk_victim(const f32x2* in, f32x2* out, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  f32x2 x = in[i];
+  const f32x2 a = {0.9990234375f, 1.0009765625f}, b = {1e-3f, -1e-3f};
+#pragma unroll 8
+  for (int k = 0; k < 64; ++k) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b));
+  out[i] = x;
+}
+
+extern "C" __global__ __launch_bounds__(256) void fma_victim(const f32x2* in, f32x2* out, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float x0 = in[i].x, x1 = in[i].y;
+#pragma unroll 8
+  for (int k = 0; k < 64; ++k) {
+    asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(x0) : "v"(0.9990234375f), "v"(1e-3f));
+    asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(x1) : "v"(1.0009765625f), "v"(-1e-3f));
+  }
+  out[i] = (f32x2){x0, x1};
+}
+
+extern "C" __global__ __launch_bounds__(256) void pk_add_victim(const f32x2* in, f32x2* out, int n, int rows) {
+  // column sums of a [rows][n] f32x2 matrix, accumulated with v_pk_add_f32
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  f32x2 acc = {0.f, 0.f};
+  for (int r = 0; r < rows; ++r) {
+    const f32x2 v = in[(long long)r * n + i];
+    asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(acc) : "v"(v));
+  }
+  out[i] = acc;
+}
+
+// host launchers (ctypes): grids sized so aggressor workgroups leave room on every CU for a victim
+extern "C" int hz_aggressor(int kind, const float* src, long long n4, float* out, int blocks, int iters,
+                            hipStream_t s) {
+  switch (kind) {
+    case 0: hipLaunchKernelGGL(mfma_loop, dim3(blocks), dim3(256), 0, s, out, iters); break;
+    case 1: hipLaunchKernelGGL(dma_loop, dim3(blocks), dim3(256), 0, s, src, n4, out, iters); break;
+    case 2: hipLaunchKernelGGL(mix_loop, dim3(blocks), dim3(256), 0, s, src, n4, out, iters); break;
+    case 3: hipLaunchKernelGGL(valu_loop, dim3(blocks), dim3(256), 0, s, out, iters); break;
+    default: return 1;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int hz_victim(int kind, const void* in, void* out, int n, int rows, hipStream_t s) {
+  const dim3 g((n + 255) / 256), b(256);
+  switch (kind) {
+    case 0: hipLaunchKernelGGL(pk_victim, g, b, 0, s, (const f32x2*)in, (f32x2*)out, n); break;
+    case 1: hipLaunchKernelGGL(fma_victim, g, b, 0, s, (const f32x2*)in, (f32x2*)out, n); break;
+    case 2: hipLaunchKernelGGL(pk_add_victim, g, b, 0, s, (const f32x2*)in, (f32x2*)out, n, rows); break;
+    default: return 1;
+  }
+  return (int)hipGetLastError();
+}

@@ -82,9 +82,23 @@ def check(name, fn, noise, noise_name):
     return bad
 
 
+def kernels_of(fn):
+    """Device kernels (and memsets) one call launches: a global (cross-workgroup) reduction shows
+    as a semaphore memset + the reduce kernel."""
+    from torch.profiler import ProfilerActivity, profile
+    fn()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    return [e.name[:90] for e in prof.events() if e.device_type.name == "CUDA"]
+
+
 def main():
     tot = 0
     vs = victims()
+    for name, fn in vs.items():
+        print(json.dumps(dict(victim=name, kernels=kernels_of(fn))), flush=True)
     noises = {"none": lambda: None, "gemm form 1 (128x128)": noise_gemm(1), "gemm form 4 (8-wave)": noise_gemm(4),
               "torch.mm (rocBLAS)": noise_torch()}
     for nn, noise in noises.items():

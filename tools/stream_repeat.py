@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--math-sdpa", action="store_true", help="PyTorch's masked SDPA (the DistilBERT attention) "
                     "on its math backend only")
     ap.add_argument("--det", action="store_true", help="torch.use_deterministic_algorithms(True, warn_only=True)")
+    ap.add_argument("--configs", default="", help="A/B within one process: 'name:VAR=val,VAR2=val;name2:...' -- "
+                    "the multi-stream reps alternate over these environments (each counted on its own)")
+    ap.add_argument("--tokens", type=int, default=6, help="caption words (6: the stream test; 32: the bench)")
     a = ap.parse_args()
     if a.math_sdpa:
         torch.backends.cuda.enable_flash_sdp(False)
@@ -63,11 +66,30 @@ def main():
     g = torch.Generator().manual_seed(5)
     frames = torch.randn(B, 3, 224, 224, generator=g).to(dev)
     audio = (torch.randn(B, 16000, generator=g) * 0.1).to(dev)
-    text = [f"caption number {i} of a scene" for i in range(B)]
+    words = ["of", "a", "scene", "with", "red", "blue", "dog", "cat", "tree", "sky", "sea", "car"]
+    text = [" ".join(["caption", "number", str(i)] + [words[(i + j) % len(words)] for j in range(a.tokens - 3)])
+            for i in range(B)]
     l_ref, g_ref, layout = run(False, frames, audio, text)
+    configs = [("default", {})]
+    if a.configs:
+        configs = []
+        for item in a.configs.split(";"):
+            name, _, kv = item.partition(":")
+            configs.append((name, dict(x.split("=", 1) for x in kv.split(",") if x)))
+    per = {n: [0, 0] for n, _ in configs}
     bad = 0
     for r in range(a.reps):
-        l, gm, _ = run(True, frames, audio, text)
+        cname, env = configs[r % len(configs)]
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            l, gm, _ = run(True, frames, audio, text)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
         diff = []
         for name, off, n in layout:
             x, y = gm[off:off + n], g_ref[off:off + n]
@@ -76,7 +98,12 @@ def main():
                 diff.append((name, int((x != y).sum()), n, f"{rel:.2g}"))
         ok = l == l_ref and not diff
         bad += not ok
-        print(f"rep {r}: {'equal' if ok else 'DIFFERS'} losses_equal={l == l_ref} params={diff[:6]}", flush=True)
+        per[cname][0] += 1
+        per[cname][1] += not ok
+        print(f"rep {r} [{cname}]: {'equal' if ok else 'DIFFERS'} losses_equal={l == l_ref} params={diff[:6]}",
+              flush=True)
+    print(json.dumps({"per_config": {n: {"reps": v[0], "differing": v[1]} for n, v in per.items()},
+                      "tokens": a.tokens}), flush=True)
     print(json.dumps({"reps": a.reps, "differing": bad, "math_sdpa": a.math_sdpa, "det": a.det,
                       "gather_fp32": os.environ.get("TRIAD_GATHER_FP32_GRADS", "1")}), flush=True)
 

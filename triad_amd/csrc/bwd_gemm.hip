@@ -104,8 +104,8 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __re
     if (p < nkt) stage_ring<DK>(Dt, CT, B, mt0, kt0 + p, lds + p * RING_ST, wave, lane);
   for (int it = 0; it < nkt; ++it) {
     const int younger = min(RING_NB - 2, nkt - 1 - it);  // uniform
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RING_PIECES) : "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING_PIECES) : "memory");
+    if (younger >= 2) TRIAD_VMCNT(2 * RING_PIECES);
+    else if (younger == 1) TRIAD_VMCNT(RING_PIECES);
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const bool pf = it + RING_NB - 1 < nkt;
@@ -241,9 +241,9 @@ __device__ __forceinline__ void db_stage(const bf16* __restrict__ Dt, long long 
 
 template <int OPS>
 __device__ __forceinline__ void db_wait(int younger) {
-  if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * OPS) : "memory");
-  else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPS) : "memory");
-  else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+  if (younger >= 3) TRIAD_VMCNT(3 * OPS);
+  else if (younger == 2) TRIAD_VMCNT(2 * OPS);
+  else if (younger == 1) TRIAD_VMCNT(OPS);
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 

@@ -33,6 +33,31 @@ __device__ __forceinline__ unsigned keep_pair(unsigned long long q, unsigned see
 }
 inline unsigned triad_drop_thr(float p) { return (unsigned)(p * 65536.f + 0.5f); }
 
+// Debug builds (tools/build_variants.py; never the product library):
+//  * TRIAD_LDS_CHECK: every LDS-DMA wave-instruction checks that its 1 KB destination (64 lanes x
+//    16 B from the wave-uniform address) lies inside the kernel's static LDS allocation, and
+//    prints the kernel's site and address if not -- a DMA beyond the allocation would land in a
+//    co-resident workgroup's LDS;
+//  * TRIAD_VMCNT0: every counted `s_waitcnt vmcnt(N)` becomes vmcnt(0). Outputs bit-identical
+//    to the product build's show that the counted waits retire everything the code reads.
+#ifdef TRIAD_LDS_CHECK
+#include <cstdio>
+__device__ __forceinline__ void lds_dma_check(unsigned lds_byte_addr, int site) {
+  const unsigned size = __builtin_amdgcn_groupstaticsize();
+  if (lds_byte_addr + 1024u > size && (threadIdx.x & 63) == 0)
+    printf("TRIAD_LDS_CHECK OOB site %d block %d,%d wave %d lds %u + 1024 > %u\n", site, (int)blockIdx.x,
+           (int)blockIdx.y, (int)(threadIdx.x >> 6), lds_byte_addr, size);
+}
+#define TRIAD_LDS_DMA_CHECK(addr, site) lds_dma_check((addr), (site))
+#else
+#define TRIAD_LDS_DMA_CHECK(addr, site) ((void)0)
+#endif
+#ifdef TRIAD_VMCNT0
+#define TRIAD_VMCNT(n) asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define TRIAD_VMCNT(n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory")
+#endif
+
 // One 16-byte global->LDS DMA per lane (global_load_lds_dwordx4). The LDS
 // destination is the wave-uniform `lds_base` + lane*16; the global source is
 // per lane (CDNA4 LDS-DMA semantics).
@@ -43,6 +68,7 @@ inline unsigned triad_drop_thr(float p) { return (unsigned)(p * 65536.f + 0.5f);
 // restored inside the statement (cdna_hip_programming.md §5.7).
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
   const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)LDS_PTR(void, lds_base));
+  TRIAD_LDS_DMA_CHECK(lds, 0);
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"

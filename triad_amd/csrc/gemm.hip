@@ -235,7 +235,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
       for (int u = 0; u < GB_PIECES; ++u)
         gb_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kbeg + p * BK, lds + p * GB_ST, wave, lane, u);
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB_PIECES) : "memory");
+    if (kt + 1 < nk) TRIAD_VMCNT(GB_PIECES);
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const bool pf = kt + GB_NB - 1 < nk;

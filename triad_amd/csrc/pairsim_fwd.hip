@@ -54,6 +54,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // Completion is counted by sync_tile's s_waitcnt vmcnt(N) + barrier. M0 = LDS destination
 // (uniform), written and restored inside the statement.
 __device__ __forceinline__ void dma16(i32x4 rsrc, unsigned lds_addr, unsigned voff, unsigned soff) {
+  TRIAD_LDS_DMA_CHECK(lds_addr, 1);
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
@@ -306,9 +307,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     // (3-slot ring; a 2-slot ring has no younger tile in flight)
     const bool more = b + 1 < nblocks;
     const bool st = TRAIN && b >= 2;
-    if (more && st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_TILE + 2) : "memory");
-    else if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLDS_PER_TILE) : "memory");
-    else if (st) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    if (more && st) TRIAD_VMCNT(GLDS_PER_TILE + 2);
+    else if (more) TRIAD_VMCNT(GLDS_PER_TILE);
+    else if (st) TRIAD_VMCNT(2);
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);

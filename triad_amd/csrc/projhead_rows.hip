@@ -79,6 +79,7 @@ __device__ __forceinline__ i32x4 ph_rsrc(const void* base, unsigned bytes) {
 // uniform LDS destination, written and restored inside the statement. Per lane only a 32-bit
 // offset: the base and the stage offset are scalars.
 __device__ __forceinline__ void ph_dma(i32x4 rsrc, unsigned lds_addr, unsigned voff, unsigned soff) {
+  TRIAD_LDS_DMA_CHECK(lds_addr, 2);
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
@@ -108,7 +109,7 @@ constexpr unsigned PH_DROP = 0xfffffff0u;   // an offset no descriptor here reac
 
 // s_waitcnt vmcnt(n) for a run-time n (clamped to the 6-bit field: waiting for fewer is safe)
 template <int K>
-__device__ __forceinline__ void ph_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory"); }
+__device__ __forceinline__ void ph_vmcnt() { TRIAD_VMCNT(K); }
 __device__ __forceinline__ void ph_vmcnt_dyn(int n) {
   switch (n < 63 ? n : 63) {
 #define PH_C(k) case k: ph_vmcnt<k>(); break;

@@ -19,6 +19,7 @@ Offline differences (documented in DESIGN.md):
 from __future__ import annotations
 
 import math
+import os
 import re
 import types
 import warnings
@@ -460,6 +461,9 @@ class MultiModalModel(nn.Module):
                 for t in (audio_feats, text_feats, attention_mask):
                     if isinstance(t, torch.Tensor) and t.is_cuda:
                         t.record_stream(main)
+                if os.environ.get("TRIAD_STREAM_HANDOFF", "1") != "0":
+                    audio_feats = _Handoff.apply(audio_feats, s_audio)
+                    text_feats = _Handoff.apply(text_feats, s_text)
         return self._triad_heads(audio_feats, v_av, text_feats, v_tv, attention_mask)
 
     def _triad_heads(self, audio_feats, v_av, text_feats, v_tv, attention_mask):
@@ -500,12 +504,38 @@ class MultiModalModel(nn.Module):
 _STREAMS = {}
 
 
+class _Handoff(torch.autograd.Function):
+    """Identity on the caller's (main) stream at a modality stream's output. Its backward runs on
+    main, where the heads produce the feature gradient; the modality's backward then consumes
+    that tensor on its own stream. The gradient is recorded for that stream (and the stream made
+    to wait), so the caching allocator cannot hand its block to another main-stream tensor while
+    the modality stream's kernels still read it -- whatever the autograd engine itself does at
+    the stream boundary."""
+
+    @staticmethod
+    def forward(ctx, x, stream):
+        ctx.stream = stream
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is not None and g.is_cuda:
+            ctx.stream.wait_stream(torch.cuda.current_stream(g.device))
+            g.record_stream(ctx.stream)
+        return g, None
+
+
+def modality_streams_enabled() -> bool:
+    """forward_triad's execution mode: audio / text backbones on their own HIP streams beside the
+    ViT (TRIAD_MODALITY_STREAMS=1) or all three on the caller's stream (=0)."""
+    import os
+    return os.environ.get("TRIAD_MODALITY_STREAMS", "1") != "0"
+
+
 def _modality_streams(frames):
     """(current, audio, text) streams for forward_triad's concurrent backbones, or None (CPU
-    tensors, or TRIAD_MODALITY_STREAMS=0)."""
-    import os
-    if not (isinstance(frames, torch.Tensor) and frames.is_cuda) or os.environ.get("TRIAD_MODALITY_STREAMS",
-                                                                                   "1") == "0":
+    tensors, or the single-stream mode)."""
+    if not (isinstance(frames, torch.Tensor) and frames.is_cuda) or not modality_streams_enabled():
         return None
     dev = frames.device
     pair = _STREAMS.get(dev.index)

@@ -784,17 +784,20 @@ class _ProjectionHeadPasses(torch.autograd.Function):
         cols = torch.empty(3, D, dtype=f32, device=dev)
         call("triad_sum_slabs", ptr(part), nb, 3 * D, None, 0, ptr(cols), st, meta=dict(tag="proj-cols", flops=0.0))
         dh = hipgemm.mm(dy1, w1b, meta=dict(tag=f"proj-dX1x{M}", flops=2.0 * M * D * H))[:M]
-        db2 = colsum(dyp, f32)
+        hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
+        # bf16 model weights (the trainer's shadowed Linear parameters): the gradients come out in
+        # bf16 straight from the reductions, as autocast's bf16 GEMM / bias gradients do
+        db2 = colsum(dyp, torch.bfloat16 if b2d == torch.bfloat16 else f32)
         sp2 = _splitk(Mp, (D // 128) * (D // 128))
         sp1 = _splitk(Mp, (D // 128) * (H // 128))
         slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
-        dw2 = torch.empty(D, D, dtype=f32, device=dev)
-        call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2), 0, st,
+        o2, o1 = int(w2d == torch.bfloat16), int(w1d == torch.bfloat16)
+        dw2 = torch.empty(D, D, dtype=torch.bfloat16 if o2 else f32, device=dev)
+        call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2), o2, st,
              meta=dict(tag=f"proj-dW2x{M}", flops=2.0 * M * D * D))
-        dw1 = torch.empty(D, H, dtype=f32, device=dev)
-        call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), 0, st,
+        dw1 = torch.empty(D, H, dtype=torch.bfloat16 if o1 else f32, device=dev)
+        call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), o1, st,
              meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
-        hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
         return (dh.view(*lead, H).to(hd), dw1.to(w1d), cols[2].to(b1d), cols[0].to(gd), cols[1].to(bd), dw2.to(w2d),
                 db2.to(b2d), None)
 

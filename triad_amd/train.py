@@ -50,16 +50,22 @@ def split_param_groups(model):
 
 
 def bf16_weight_params(model):
-    """Backbone weights autocast feeds to bf16 matmuls/convs exactly once per forward: every
-    nn.Linear / nn.Conv1d parameter of HuBERT and DistilBERT (model.py:29-30,79-80), except
-    weight-normalised convolutions (HuBERT's positional conv computes its weight from g, v in
-    fp32 before the cast). These can live as bf16 model weights over fp32 masters."""
+    """Weights autocast feeds to bf16 matmuls/convs exactly once per forward: every nn.Linear /
+    nn.Conv1d parameter of HuBERT and DistilBERT (model.py:29-30,79-80), except weight-normalised
+    convolutions (HuBERT's positional conv computes its weight from g, v in fp32 before the cast),
+    and the three projection heads' Linear layers (model.py:32-34, 81-83, 253-255; the LayerNorm
+    between them stays fp32, as autocast runs it). These can live as bf16 model weights over fp32
+    masters: the forward sees what autocast's cast would produce, and the gradients arrive in
+    bf16 as autocast's backward produces them."""
     out = []
     for root in (model.audio_embedder.hubert, model.text_embedder.encoder):
         for mod in root.modules():
             if isinstance(mod, (torch.nn.Linear, torch.nn.Conv1d)) and not hasattr(mod, "parametrizations") \
                     and not hasattr(mod, "weight_g"):
                 out.extend(p for p in mod.parameters(recurse=False) if p.dtype == torch.float32)
+    for emb in (model.audio_embedder, model.text_embedder, model.visual_embedder):
+        for mod in (emb.projection1, emb.projection2):
+            out.extend(p for p in mod.parameters(recurse=False) if p.dtype == torch.float32)
     return out
 
 
