@@ -29,7 +29,8 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "tri-modal triples/sec (whole node) + loss parity, B=256 at 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 TRACKED = ("triad_pairsim_fwd", "triad_pairsim_fwd_multi", "triad_pairsim_dS", "triad_gemm_bf16", "triad_projhead_fwd", "triad_projhead_bwd",
-           "triad_gemm_bf16_splitk", "triad_tile_gemm", "triad_tile_gemm_packed", "triad_bfrag_pack", "triad_dS_patch", "triad_clip_reduce", "triad_losshead",
+           "triad_gemm_bf16_splitk", "triad_tile_gemm", "triad_tile_gemm_packed", "triad_tile_gemm_packed16", "triad_bfrag_pack",
+           "triad_bfrag_pack16", "triad_dS_patch", "triad_clip_reduce", "triad_losshead",
            "triad_diag_smooth", "triad_diag_sparsity", "triad_dtemp_finalize", "triad_ln_bwd",
            "triad_colsum", "triad_sum_slabs", "triad_gather_rows", "triad_global_znorm",
            "triad_grad_sumsq", "triad_adamw_step", "triad_ln_fwd", "triad_ln_bwd3", "triad_gemm_bf16_bias")
@@ -47,8 +48,8 @@ def parse():
     ap.add_argument("--separate-steps", type=int, default=3,
                     help="timed steps of the --separate-frames variant reported beside the headline (0 = skip)")
     ap.add_argument("--single-stream-steps", type=int, default=3,
-                    help="timed steps with the three backbones on ONE stream, reported beside the headline "
-                         "(0 = skip)")
+                    help="timed steps in the OTHER execution mode (serial <-> concurrent streams), reported "
+                         "beside the headline (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate-frames", action="store_true",
                     help="encode the AV and TV frame batches separately (2x ViT work)")
@@ -234,10 +235,13 @@ def main():
 
     single = None
     if a.single_stream_steps > 0:
-        # the same step with the audio / text backbones on the main stream (forward_triad's
-        # TRIAD_MODALITY_STREAMS=0): the serial execution order, reported beside the headline
-        prev = os.environ.get("TRIAD_MODALITY_STREAMS")
-        os.environ["TRIAD_MODALITY_STREAMS"] = "0" if model_streams() else "1"
+        # the same step in the other execution mode, reported beside the headline: the serial
+        # default vs the concurrent opt-in (backbones on three streams + the dW side stream)
+        from triad_amd import linear as _lin
+        from triad_amd.model import set_concurrent_streams
+        prev = (os.environ.get("TRIAD_MODALITY_STREAMS"), _lin.SIDE_STREAM_DW)
+        headline_concurrent = model_streams()
+        set_concurrent_streams(not headline_concurrent)
         try:
             step()
             torch.cuda.synchronize()
@@ -251,20 +255,24 @@ def main():
                 dist.barrier()
             dtss = time.perf_counter() - t1
         finally:
-            if prev is None:
+            if prev[0] is None:
                 os.environ.pop("TRIAD_MODALITY_STREAMS", None)
             else:
-                os.environ["TRIAD_MODALITY_STREAMS"] = prev
+                os.environ["TRIAD_MODALITY_STREAMS"] = prev[0]
+            _lin.SIDE_STREAM_DW = prev[1]
         if world > 1:
             t = torch.tensor([dtss], device=dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dtss = float(t)
         single = {"value": world * a.batch * a.single_stream_steps / dtss, "unit": "triples/s",
                   "steps": a.single_stream_steps, "ms_per_step": dtss / a.single_stream_steps * 1e3,
-                  "modality_streams": not model_streams()}
+                  "concurrent_streams": not headline_concurrent,
+                  "note": ("concurrent opt-in (backbones on three streams + dW side stream): NOT bit-reproducible "
+                           "(DESIGN.md 2b), reported for reference only" if not headline_concurrent else
+                           "serial step (one stream)")}
         if rank == 0:
-            print(f"[bench] {a.single_stream_steps} steps with modality streams "
-                  f"{'on' if single['modality_streams'] else 'off'}: {dtss:.2f} s", file=sys.stderr, flush=True)
+            print(f"[bench] {a.single_stream_steps} steps with concurrent streams "
+                  f"{'on' if single['concurrent_streams'] else 'off'}: {dtss:.2f} s", file=sys.stderr, flush=True)
 
     if rank == 0:
         value = world * a.batch * a.steps / dt
@@ -317,7 +325,8 @@ def main():
                      "kernels": {k: kstats(k) for k in sorted(rep) if k in head_keys}},
             "backbone_hip_gemm_ms_per_step": sum(v["ms"] for k, v in rep.items() if k not in head_keys) / a.steps,
         }
-        res["config"]["modality_streams"] = model_streams()
+        res["config"]["execution"] = ("concurrent streams (opt-in)" if model_streams() else
+                                      "serial: one stream (the bit-reproducible default, DESIGN.md 2b)")
         if single is not None:
             res["other_stream_mode"] = single
         if sep is not None:

@@ -225,11 +225,12 @@ def test_feature_encoder_side_stream_weight_grads_bit_identical():
         (y.float() ** 2).mean().backward()
         return [layer.conv.weight.grad.clone() for layer in fe.conv_layers]
 
+    prev = L.SIDE_STREAM_DW
     try:
         g_main = run(False)
         g_side = run(True)
     finally:
-        L.SIDE_STREAM_DW = True
+        L.SIDE_STREAM_DW = prev
     for a, b in zip(g_side, g_main):
         assert a.dtype == torch.bfloat16 and a.is_contiguous()
         assert torch.equal(a, b)

@@ -139,6 +139,52 @@ extern "C" __global__ __launch_bounds__(256) void pk_add_victim(const f32x2* in,
   out[i] = acc;
 }
 
+// Second probe: the victim that IS disturbed (PyTorch's bf16 column sum, not its fp32 one) loads
+// 16-bit values; these victims do the same column sums with three load forms.
+template <int FORM>
+__global__ __launch_bounds__(256) void ld16_victim(const unsigned short* in, float* out, int npairs, int rows) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= npairs) return;
+  float a0 = 0.f, a1 = 0.f;
+  for (int r = 0; r < rows; ++r) {
+    const unsigned short* p = in + ((long long)r * npairs + i) * 2;
+    unsigned v = 0x7fc07fc0u;   // the untouched half would show up as NaN
+    if (FORM == 0) {            // d16: each load writes one half of the VGPR, the other half kept
+      asm volatile("global_load_short_d16 %0, %1, off\n\tglobal_load_short_d16_hi %0, %2, off\n\ts_waitcnt vmcnt(0)"
+                   : "+v"(v) : "v"(p), "v"(p + 1) : "memory");
+    } else if (FORM == 1) {     // two zero-extending 16-bit loads into separate VGPRs
+      unsigned lo, hi;
+      asm volatile("global_load_ushort %0, %2, off\n\tglobal_load_ushort %1, %3, off\n\ts_waitcnt vmcnt(0)"
+                   : "=&v"(lo), "=&v"(hi) : "v"(p), "v"(p + 1) : "memory");
+      v = lo | (hi << 16);
+    } else {                    // one 32-bit load of the pair
+      asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    }
+    a0 += __builtin_bit_cast(float, v << 16);
+    a1 += __builtin_bit_cast(float, v & 0xffff0000u);
+  }
+  out[2 * i] = a0;
+  out[2 * i + 1] = a1;
+}
+
+// aggressor variants: LDS-DMA beside scalar VALU instead of MFMA; buffer-form LDS-DMA beside MFMA
+extern "C" __global__ __launch_bounds__(256) void dma_valu_loop(const float* src, long long n4, float* out, int iters) {
+  __shared__ __attribute__((aligned(16))) float ring[4 * 4 * 256];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  float s = 0.f, x = t * 1e-3f, y = 1.0001f;
+  for (int it = 0; it < iters; ++it) {
+    const int slot = it & 3;
+    const long long row = ((long long)(blockIdx.x * 131 + it * 17 + wave) * 64 + lane) % n4;
+    glds16(src + row * 4, ring + (slot * 4 + wave) * 256);
+    for (int k = 0; k < 32; ++k) { x = fmaf(x, y, 1e-6f); y = fmaf(y, 0.99999f, 1e-7f); }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    s += ring[(slot * 4 + (wave ^ 1)) * 256 + lane * 4];
+    __syncthreads();
+  }
+  out[blockIdx.x * 256 + t] = s + x + y;
+}
+
 // host launchers (ctypes): grids sized so aggressor workgroups leave room on every CU for a victim
 extern "C" int hz_aggressor(int kind, const float* src, long long n4, float* out, int blocks, int iters,
                             hipStream_t s) {
@@ -147,6 +193,7 @@ extern "C" int hz_aggressor(int kind, const float* src, long long n4, float* out
     case 1: hipLaunchKernelGGL(dma_loop, dim3(blocks), dim3(256), 0, s, src, n4, out, iters); break;
     case 2: hipLaunchKernelGGL(mix_loop, dim3(blocks), dim3(256), 0, s, src, n4, out, iters); break;
     case 3: hipLaunchKernelGGL(valu_loop, dim3(blocks), dim3(256), 0, s, out, iters); break;
+    case 4: hipLaunchKernelGGL(dma_valu_loop, dim3(blocks), dim3(256), 0, s, src, n4, out, iters); break;
     default: return 1;
   }
   return (int)hipGetLastError();
@@ -158,6 +205,9 @@ extern "C" int hz_victim(int kind, const void* in, void* out, int n, int rows, h
     case 0: hipLaunchKernelGGL(pk_victim, g, b, 0, s, (const f32x2*)in, (f32x2*)out, n); break;
     case 1: hipLaunchKernelGGL(fma_victim, g, b, 0, s, (const f32x2*)in, (f32x2*)out, n); break;
     case 2: hipLaunchKernelGGL(pk_add_victim, g, b, 0, s, (const f32x2*)in, (f32x2*)out, n, rows); break;
+    case 3: hipLaunchKernelGGL(ld16_victim<0>, g, b, 0, s, (const unsigned short*)in, (float*)out, n, rows); break;
+    case 4: hipLaunchKernelGGL(ld16_victim<1>, g, b, 0, s, (const unsigned short*)in, (float*)out, n, rows); break;
+    case 5: hipLaunchKernelGGL(ld16_victim<2>, g, b, 0, s, (const unsigned short*)in, (float*)out, n, rows); break;
     default: return 1;
   }
   return (int)hipGetLastError();

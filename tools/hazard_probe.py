@@ -67,7 +67,11 @@ def main():
         "triad_gemm form 1 (128x128)": gemm(1),
         "triad_gemm form 4 (eight-wave)": gemm(4),
         "torch.mm (rocBLAS)": lambda: torch.mm(ma, mb),
+        "dma_valu_loop (global_load_lds beside scalar VALU, no MFMA)": agg(4, 256, 1000),
     }
+    if os.environ.get("AGGRESSORS"):
+        keep = os.environ["AGGRESSORS"].split("|")
+        aggressors = {k: v for k, v in aggressors.items() if any(k.startswith(x) for x in keep)}
     n = 65536
     x = torch.randn(n, 2, device=dev, generator=g)
     rows = 768
@@ -83,13 +87,30 @@ def main():
             return out
         return run
 
+    u16 = (torch.randn(rows, 2304, device=dev, generator=g) * 0.01).to(torch.bfloat16).view(torch.int16)
+
+    def vic16(kind):
+        def run():
+            out = torch.empty(2304, device=dev)
+            rc = h.hz_victim(kind, C.c_void_p(u16.data_ptr()), C.c_void_p(out.data_ptr()), 2304 // 2, rows,
+                             C.c_void_p(torch.cuda.current_stream().cuda_stream))
+            assert rc == 0, rc
+            return out
+        return run
+
     victims = {
+        "ld16_victim d16 (global_load_short_d16 / _d16_hi into one VGPR)": vic16(3),
+        "ld16_victim ushort (two zero-extending 16-bit loads)": vic16(4),
+        "ld16_victim dword (one 32-bit load)": vic16(5),
         "pk_victim (v_pk_fma_f32 chain)": vic(0, x, n),
         "fma_victim (v_fma_f32 chain)": vic(1, x, n),
         "pk_add_victim (v_pk_add_f32 column sums)": vic(2, m, 2304 // 2, rows),
         "torch bf16 sum(0) 768x2304": lambda: sb.sum(0),
         "torch fp32 sum(0) 768x2304": lambda: sb.float().sum(0),
     }
+    if os.environ.get("VICTIMS"):
+        keep = os.environ["VICTIMS"].split("|")
+        victims = {k: v for k, v in victims.items() if any(k.startswith(x) for x in keep)}
     side = torch.cuda.Stream(device=dev)
     total = 0
     for an, af in aggressors.items():

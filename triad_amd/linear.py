@@ -141,7 +141,10 @@ def on_side_stream(fn, inputs):
     return outs
 
 
-SIDE_STREAM_DW = os.environ.get("TRIAD_SIDE_STREAM_DW", "1") != "0"
+# Off by default (the serial step): on a second stream the dW GEMMs (MFMA + LDS-DMA)
+# share CUs with the main stream's PyTorch kernels, whose bf16 reductions then return wrong sums
+# in some launches. TRIAD_SIDE_STREAM_DW=1 (or model.set_concurrent_streams(True)) opts in.
+SIDE_STREAM_DW = os.environ.get("TRIAD_SIDE_STREAM_DW", "0") != "0"
 
 
 class _LinearFn(torch.autograd.Function):
