@@ -148,12 +148,15 @@ int triad_tile_gemm_packed(const void* Dt, long long CT, int dk, const void* Bp,
 /* triad_tile_gemm_slabs over packed B fragments. */
 int triad_tile_gemm_packed_slabs(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, int splits,
                                  float* slabs, hipStream_t stream);
-/* The dQ GEMM (dk = 0 only) on v_mfma_f32_16x16x32_bf16 instead of v_mfma_f32_32x32x16_bf16:
- * triad_bfrag_pack16 arranges B for that MFMA's operand order; same results up to fp32
- * summation order (reference: the dQ of S = temp Q K^T, SajayR/TRIAD model.py:384-387 / 502-505). */
+/* The same dQ / dK GEMMs on v_mfma_f32_16x16x32_bf16 instead of v_mfma_f32_32x32x16_bf16
+ * (faster at the clock the chip holds under load): triad_bfrag_pack16 arranges B for that MFMA's
+ * operand order (per dk); results equal to triad_tile_gemm_packed's (reference: the gradients of
+ * S = temp Q K^T, SajayR/TRIAD model.py:384-387 / 502-505). */
 int triad_bfrag_pack16(const void* B, int nkt, int dk, void* Bp, hipStream_t stream);
 int triad_tile_gemm_packed16(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, const float* alpha,
                              int splits, float* slabs, void* C, hipStream_t stream);
+int triad_tile_gemm_packed16_slabs(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, int splits,
+                                   float* slabs, hipStream_t stream);
 
 /* C = alpha * op(A) . op(B): A [M][Kd] (a_kcontig=1) or [Kd][M] (0); B [N][Kd] (b_kcontig=1)
  * or [Kd][N] (0); C fp32 or bf16 (out_bf16). M, N multiples of 128, Kd of 64.

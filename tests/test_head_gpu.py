@@ -355,34 +355,45 @@ def test_tile_gemm_packed_bit_identical_to_ring(panels, ct, splits):
             assert torch.equal(slabs, slabs2), (dk, M, nkt, splits)
 
 
-@pytest.mark.parametrize("panels,ct,splits", [(2, 4, 1), (3, 7, 1), (4, 9, 3), (2, 8, 5)])
-def test_tile_gemm_mfma16_dq_matches_fp64(panels, ct, splits):
-    """The dQ GEMM on v_mfma_f32_16x16x32_bf16 (triad_bfrag_pack16 + triad_tile_gemm_packed16)
-    against an fp64 dQ = alpha dS K over the untiled dS (_untile_dS) -- within bf16 output
-    rounding -- and against the 32x32x16 form (the same sums in another fp32 order), split-K
-    slabs included."""
+@pytest.mark.parametrize("panels,ct,splits", [(2, 4, 1), (3, 7, 1), (4, 8, 3), (2, 8, 5), (7, 36, 1)])
+def test_tile_gemm_mfma16_matches_ring(panels, ct, splits):
+    """dQ and dK on v_mfma_f32_16x16x32_bf16 (triad_bfrag_pack16 + triad_tile_gemm_packed16 /
+    _packed16_slabs) against the 32x32x16 ring form (bit-identical: the same fp32 sums, in an
+    order the two MFMA shapes share -- measured, not assumed) and against an fp64 product over the
+    untiled dS, split-K slabs included."""
     from triad_amd._lib import call, ptr, stream_ptr
     g = torch.Generator(device=dev).manual_seed(7 * panels + ct + splits)
     R_pad, CT = panels * 128, ct
     dS = (torch.randn(R_pad // 32 * CT * 1024, device=dev, generator=g) * 0.1).to(torch.bfloat16)
     K = torch.randn(CT * 32, 512, device=dev, generator=g).to(torch.bfloat16)
+    Q = torch.randn(R_pad, 512, device=dev, generator=g).to(torch.bfloat16)
     alpha = torch.tensor([0.75], device=dev)
     st = stream_ptr()
-    M, nkt = R_pad, CT
-    Bp16 = torch.empty(nkt * 32 * 512, dtype=torch.bfloat16, device=dev)
-    call("triad_bfrag_pack16", ptr(K), nkt, 0, ptr(Bp16), st)
-    slabs = torch.empty(splits * M * 512, device=dev) if splits > 1 else None
-    out16 = torch.empty(M, 512, dtype=torch.bfloat16, device=dev)
-    ring = torch.empty_like(out16)
-    call("triad_tile_gemm_packed16", ptr(dS), CT, 0, ptr(Bp16), M, nkt, ptr(alpha), splits, ptr(slabs), ptr(out16), st)
-    call("triad_tile_gemm", ptr(dS), CT, 0, ptr(K), M, nkt, ptr(alpha), 1, None, ptr(ring), st)
-    torch.cuda.synchronize()
     dense = _untile_dS(dS, R_pad, CT).double()
-    ref = 0.75 * dense @ K.double()
-    err = float((out16.double() - ref).abs().max() / ref.abs().max())
-    assert err < 8e-3, err
-    d = float((out16.float() - ring.float()).abs().max())
-    assert d <= 2.0 ** -7 * float(ring.float().abs().max()), d
+    cases = [(0, K, R_pad, CT, dense @ K.double())]
+    if CT % 4 == 0:
+        cases.append((1, Q, CT * 32, R_pad // 32, dense.t() @ Q.double()))
+    for dk, Bm, M, nkt, prod in cases:
+        Bp16 = torch.empty(nkt * 32 * 512, dtype=torch.bfloat16, device=dev)
+        call("triad_bfrag_pack16", ptr(Bm), nkt, dk, ptr(Bp16), st)
+        slabs = torch.empty(splits * M * 512, device=dev) if splits > 1 else None
+        slabs2 = torch.empty(splits * M * 512, device=dev) if splits > 1 else None
+        out16 = torch.empty(M, 512, dtype=torch.bfloat16, device=dev)
+        ring = torch.empty_like(out16)
+        call("triad_tile_gemm_packed16", ptr(dS), CT, dk, ptr(Bp16), M, nkt, ptr(alpha), splits, ptr(slabs), ptr(out16),
+             st)
+        call("triad_tile_gemm", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), splits, ptr(slabs2), ptr(ring), st)
+        torch.cuda.synchronize()
+        ref = 0.75 * prod
+        err = float((out16.double() - ref).abs().max() / ref.abs().max())
+        assert err < 8e-3, (dk, err)
+        assert torch.equal(out16, ring), (dk, M, nkt, splits)
+        if splits > 1:
+            assert torch.equal(slabs, slabs2), (dk, "slabs")
+            call("triad_tile_gemm_packed16_slabs", ptr(dS), CT, dk, ptr(Bp16), M, nkt, splits, ptr(slabs), st)
+            call("triad_tile_gemm_slabs", ptr(dS), CT, dk, ptr(Bm), M, nkt, splits, ptr(slabs2), st)
+            torch.cuda.synchronize()
+            assert torch.equal(slabs, slabs2), (dk, "slabs only")
 
 
 @pytest.mark.parametrize("B,Na,Nt,Nv,budget", [(6, 49, 16, 70, None), (16, 199, 32, 205, None),

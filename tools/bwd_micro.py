@@ -32,19 +32,17 @@ def run(B, Nq, Nk, dk, iters, force_sp=None, form=0):
     slabs = torch.empty(sp * M * 512, dtype=torch.float32, device="cuda") if sp > 1 else None
 
     Bp = None
-    if form == 16:   # dQ on v_mfma_f32_16x16x32_bf16 (triad_tile_gemm_packed16), vs the 32x32x16 ring form
-        if dk:
-            return None
+    if form == 16:   # on v_mfma_f32_16x16x32_bf16 (triad_tile_gemm_packed16), vs the 32x32x16 ring form
         Bp = torch.empty(nkt * 32 * 512, dtype=torch.bfloat16, device="cuda")
-        call("triad_bfrag_pack16", ptr(Bm), nkt, 0, ptr(Bp), stream_ptr())
+        call("triad_bfrag_pack16", ptr(Bm), nkt, dk, ptr(Bp), stream_ptr())
         ref = torch.empty_like(out)
         call("triad_tile_gemm", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(ref), stream_ptr())
-        call("triad_tile_gemm_packed16", ptr(dS), CT, 0, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out),
+        call("triad_tile_gemm_packed16", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out),
              stream_ptr())
         torch.cuda.synchronize()
         d = (out.float() - ref.float()).abs()
         rel = float(d.max() / ref.float().abs().max())
-        print(json.dumps({"check": "packed16 vs ring", "M": M, "max_rel": rel,
+        print(json.dumps({"check": "packed16 vs ring", "dk": dk, "M": M, "max_rel": rel,
                           "frac_differing": float((d > 0).float().mean())}), flush=True)
         assert rel < 1e-2
     if form == 9:   # direct-B form: B fragments packed once (timed apart), then triad_tile_gemm_packed
@@ -68,7 +66,7 @@ def run(B, Nq, Nk, dk, iters, force_sp=None, form=0):
 
     def launch():
         if form == 16:
-            call("triad_tile_gemm_packed16", ptr(dS), CT, 0, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out),
+            call("triad_tile_gemm_packed16", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out),
                  stream_ptr())
         elif form == 9:
             call("triad_tile_gemm_packed", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out),

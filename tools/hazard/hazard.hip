@@ -212,3 +212,71 @@ extern "C" int hz_victim(int kind, const void* in, void* out, int n, int rows, h
   }
   return (int)hipGetLastError();
 }
+
+// Third probe: every disturbed victim so far (PyTorch's reduce_kernel with its semaphore memset,
+// rocprim's look-back partition) hands data between workgroups of ONE launch; every clean one
+// (our colsum: two launches, the ld16 / pk victims) does not. Column sums of a bf16 [rows][ncols]
+// matrix in three forms:
+//   lds_colsum  (kind 6): one workgroup per 32 columns, 8 row-threads per column combined through
+//               LDS -- an LDS hand-off inside a workgroup, no cross-workgroup traffic;
+//   xblk_colsum (kind 7): grid.y row splits, partials to a staging buffer, __threadfence +
+//               atomicAdd on a per-column-group semaphore, the last workgroup sums the partials
+//               with plain loads (PyTorch's global_reduce / mark_block_finished pattern);
+//   kind 8: the same with an agent-scope acquire fence after the semaphore;
+//   kind 9: the same with the partials read by agent-scope relaxed atomic loads.
+__global__ __launch_bounds__(256) void lds_colsum(const unsigned short* in, float* out, int ncols, int rows) {
+  __shared__ float part[8][33];
+  const int cx = threadIdx.x & 31, ry = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + cx;
+  float acc = 0.f;
+  if (col < ncols)
+    for (int r = ry; r < rows; r += 8) acc += __builtin_bit_cast(float, (unsigned)in[(long long)r * ncols + col] << 16);
+  part[ry][cx] = acc;
+  __syncthreads();
+  if (ry == 0 && col < ncols) {
+    float s = 0.f;
+    for (int k = 0; k < 8; ++k) s += part[k][cx];
+    out[col] = s;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void xblk_colsum(const unsigned short* in, float* staging, int* sem, float* out,
+                                                   int ncols, int rows, int nsplit) {
+  const int col = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+  const int r0 = (int)((long long)y * rows / nsplit), r1 = (int)((long long)(y + 1) * rows / nsplit);
+  float acc = 0.f;
+  if (col < ncols)
+    for (int r = r0; r < r1; ++r) acc += __builtin_bit_cast(float, (unsigned)in[(long long)r * ncols + col] << 16);
+  if (col < ncols) staging[(long long)y * ncols + col] = acc;
+  __threadfence();
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&sem[blockIdx.x], 1) == nsplit - 1;
+  __syncthreads();
+  if (!last || col >= ncols) return;
+  if (MODE == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  float s = 0.f;
+  for (int k = 0; k < nsplit; ++k) {
+    float* p = staging + (long long)k * ncols + col;
+    s += MODE == 2 ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+  }
+  out[col] = s;
+}
+
+extern "C" int hz_victim2(int kind, const void* in, float* staging, int* sem, float* out, int ncols, int rows,
+                          int nsplit, hipStream_t s) {
+  const dim3 gx((ncols + 255) / 256, nsplit), b(256);
+  switch (kind) {
+    case 6: hipLaunchKernelGGL(lds_colsum, dim3((ncols + 31) / 32), b, 0, s, (const unsigned short*)in, out, ncols,
+                               rows); break;
+    case 7: hipLaunchKernelGGL(xblk_colsum<0>, gx, b, 0, s, (const unsigned short*)in, staging, sem, out, ncols, rows,
+                               nsplit); break;
+    case 8: hipLaunchKernelGGL(xblk_colsum<1>, gx, b, 0, s, (const unsigned short*)in, staging, sem, out, ncols, rows,
+                               nsplit); break;
+    case 9: hipLaunchKernelGGL(xblk_colsum<2>, gx, b, 0, s, (const unsigned short*)in, staging, sem, out, ncols, rows,
+                               nsplit); break;
+    default: return 1;
+  }
+  return (int)hipGetLastError();
+}

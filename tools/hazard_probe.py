@@ -6,7 +6,9 @@ launches while triad_gemm_bf16 (128 x 128 or eight-wave form) ran on another str
 beside rocBLAS GEMMs, alone, or for fp32 sums (whose inner loop is scalar). Each victim runs
 alone (reference), then `reps` times beside each aggressor (queued first on the main stream,
 the victim on a second stream so its workgroups share the CUs), compared bit for bit.
-One JSON line per (aggressor, victim): mismatching launches, worst elements."""
+One JSON line per (aggressor, victim): mismatching launches, worst elements. Third probe
+(lds_colsum / xblk_colsum*): is it the LDS hand-off inside a workgroup or the cross-workgroup
+hand-off of one launch that goes wrong (every disturbed victim has the latter)?"""
 import ctypes as C
 import json
 import os
@@ -31,6 +33,8 @@ def lib():
     h = C.CDLL(HZ)
     h.hz_aggressor.argtypes = [C.c_int, C.c_void_p, C.c_longlong, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
     h.hz_victim.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    h.hz_victim2.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                             C.c_void_p]
     return h
 
 
@@ -98,7 +102,23 @@ def main():
             return out
         return run
 
+    def vic2(kind, nsplit=8):
+        def run():   # staging / semaphores allocated per launch on the launching stream, as PyTorch does
+            out = torch.empty(2304, device=dev)
+            staging = torch.empty(nsplit * 2304, device=dev)
+            sem = torch.zeros(16, dtype=torch.int32, device=dev)
+            rc = h.hz_victim2(kind, C.c_void_p(u16.data_ptr()), C.c_void_p(staging.data_ptr()),
+                              C.c_void_p(sem.data_ptr()), C.c_void_p(out.data_ptr()), 2304, rows, nsplit,
+                              C.c_void_p(torch.cuda.current_stream().cuda_stream))
+            assert rc == 0, rc
+            return out
+        return run
+
     victims = {
+        "lds_colsum (8 row-threads per column combined through LDS, one launch, no cross-WG hand-off)": vic2(6),
+        "xblk_colsum plain (cross-WG hand-off: threadfence + atomic semaphore, last WG plain loads)": vic2(7),
+        "xblk_colsum acquire (the same + agent-scope acquire fence after the semaphore)": vic2(8),
+        "xblk_colsum atomic-load (the same, partials read by agent-scope atomic loads)": vic2(9),
         "ld16_victim d16 (global_load_short_d16 / _d16_hi into one VGPR)": vic16(3),
         "ld16_victim ushort (two zero-extending 16-bit loads)": vic16(4),
         "ld16_victim dword (one 32-bit load)": vic16(5),

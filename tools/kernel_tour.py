@@ -77,11 +77,10 @@ def tile_gemms(out):
             call("triad_bfrag_pack", ptr(Bm), nkt, dk, ptr(Bp), st)
             call("triad_tile_gemm_packed", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), splits, ptr(slabs), ptr(c), st)
             out[f"tile-packed-dk{dk}-sp{splits}"] = digest(c, Bp)
-            if dk == 0:
-                call("triad_bfrag_pack16", ptr(Bm), nkt, 0, ptr(Bp), st)
-                call("triad_tile_gemm_packed16", ptr(dS), CT, 0, ptr(Bp), M, nkt, ptr(alpha), splits, ptr(slabs),
-                     ptr(c), st)
-                out[f"tile-packed16-dk0-sp{splits}"] = digest(c, Bp)
+            call("triad_bfrag_pack16", ptr(Bm), nkt, dk, ptr(Bp), st)
+            call("triad_tile_gemm_packed16", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), splits, ptr(slabs),
+                 ptr(c), st)
+            out[f"tile-packed16-dk{dk}-sp{splits}"] = digest(c, Bp)
 
 
 def gemms(out):

@@ -340,7 +340,7 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db_kernel(const bf16* __rest
     }
 }
 
-// ---- v_mfma_f32_16x16x32_bf16 form of the direct-B dQ GEMM ------------------------------------
+// ---- v_mfma_f32_16x16x32_bf16 form of the direct-B GEMMs -----------------------------------------
 // The same workgroup (8 waves, 128 rows x 512 columns, wave w owns columns [64w, 64w + 64)), the
 // same A stream (dS tiles through the LDS ring by one LDS-DMA piece per wave per k tile) and the
 // same register-streamed B, but each wave's 128 x 64 output is 8 x 4 blocks of 16 x 16 computed by
@@ -356,6 +356,7 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+template <bool DK>
 __global__ __launch_bounds__(512) void bfrag_pack16_kernel(const bf16* __restrict__ B, bf16* __restrict__ Bp) {
   __shared__ __attribute__((aligned(16))) bf16 img[TBK * TBN];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -372,13 +373,18 @@ __global__ __launch_bounds__(512) void bfrag_pack16_kernel(const bf16* __restric
     const int col = wave * 64 + cb * 16 + (lane & 15);
     bf16x8 f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = img[b_off(16 * j + 8 * (i >> 2) + 4 * hh + (i & 3), col)];
+    for (int i = 0; i < 8; ++i)
+      f[i] = img[b_off(DK ? 8 * kc + i : 16 * j + 8 * (i >> 2) + 4 * hh + (i & 3), col)];
     *(bf16x8*)(Bp + ((kt * 8 + wave) * 4 + cb) * 512 + lane * 8) = f;
   }
 }
 
-template <bool SLAB, int KS, int DD>
-__global__ __launch_bounds__(512, 1) void tile_gemm_db16q_kernel(const bf16* __restrict__ Dt, long long CT,
+// dK (DK = true): A = dS^T, rows = keys, k = queries. Row block rb = 16 keys: tile rb >> 1, key
+// half kb = rb & 1; lane l takes keys 16 kb + (l & 15) and the queries 8 (l >> 4) .. + 7 of the
+// k tile by two ds_read_b64_tr_b16 (4 query rows each) -- natural query order, so the packed Q
+// fragment of lane l is Q[8 (l >> 4) + i][col], i = 0..7.
+template <bool DK, bool SLAB, int KS, int DD>
+__global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __restrict__ Dt, long long CT,
                                                                  const bf16* __restrict__ Bp, int M, int nkt_total,
                                                                  int kt_per_split, const float* __restrict__ alpha_p,
                                                                  void* __restrict__ Cout) {
@@ -386,7 +392,7 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16q_kernel(const bf16* __r
   constexpr int NB = DD + 1;
   __shared__ __attribute__((aligned(16))) bf16 lds[NB * KS * 4096];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int l16 = lane & 15, kc = lane >> 4;
+  const int l16 = lane & 15, kc = lane >> 4, q4 = l16 >> 2, p4 = l16 & 3;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
   const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
@@ -395,10 +401,23 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16q_kernel(const bf16* __r
   const int nkt = __builtin_amdgcn_readfirstlane(min(kt_per_split, nkt_total - kt0));
   const int kt_last = kt0 + nkt - 1;
   const int nst = (nkt + KS - 1) / KS;
-  // this lane's A chunk inside a 32-row tile, per row half: stored chunk 2 (r + 32 hh) + j
-  int aoff[2];
+  // this lane's A reads inside a 32-row tile, per row half (dQ: one chunk; dK: two transposed
+  // 4-row reads) -- offsets in elements
+  int aoff[2][2];
 #pragma unroll
-  for (int rh = 0; rh < 2; ++rh) aoff[rh] = swz_q(2 * (16 * rh + l16 + 32 * (kc & 1)) + (kc >> 1)) * 8;
+  for (int rh = 0; rh < 2; ++rh) {
+    if (!DK) {
+      aoff[rh][0] = swz_q(2 * (16 * rh + l16 + 32 * (kc & 1)) + (kc >> 1)) * 8;
+      aoff[rh][1] = 0;
+    } else {
+      const int a = 2 * rh + (p4 >> 1), hh = p4 & 1;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int qry = 8 * kc + 4 * tt + q4;
+        aoff[rh][tt] = swz_k((qry + 32 * hh) * 2 + (a >> 1)) * 8 + 4 * (a & 1);
+      }
+    }
+  }
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -409,7 +428,7 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16q_kernel(const bf16* __r
   bf16x8 bq[NB][4 * KS];
 #pragma unroll
   for (int p = 0; p < DD; ++p)
-    if (p < nst) db_stage<false, KS>(Dt, CT, Bp, mt0, kt0 + p * KS, kt_last, lds + p * KS * 4096, bq[p], wave, lane);
+    if (p < nst) db_stage<DK, KS>(Dt, CT, Bp, mt0, kt0 + p * KS, kt_last, lds + p * KS * 4096, bq[p], wave, lane);
   for (int st0 = 0; st0 < nst; st0 += NB) {
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
@@ -424,15 +443,24 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16q_kernel(const bf16* __r
         const bf16* As = lds + (u * KS + k) * 4096;
         bf16x8 af[8];
 #pragma unroll
-        for (int rb = 0; rb < 8; ++rb) af[rb] = *(const bf16x8*)(As + (rb >> 1) * 1024 + aoff[rb & 1]);
+        for (int rb = 0; rb < 8; ++rb) {
+          const bf16* tile = As + (rb >> 1) * 1024;
+          if (!DK) {
+            af[rb] = *(const bf16x8*)(tile + aoff[rb & 1][0]);
+          } else {
+            s16x4* rp = (s16x4*)&af[rb];
+            rp[0] = lds_tr16(tile + aoff[rb & 1][0]);
+            rp[1] = lds_tr16(tile + aoff[rb & 1][1]);
+          }
+        }
 #pragma unroll
         for (int rb = 0; rb < 8; ++rb) {
 #pragma unroll
           for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = mfma16(af[rb], bq[u][4 * k + cb], acc[rb][cb]);
           if (k == 0 && rb == 1 && pf) {
             __builtin_amdgcn_sched_barrier(0);
-            db_stage<false, KS>(Dt, CT, Bp, mt0, kt0 + (st + DD) * KS, kt_last, lds + ((u + DD) % NB) * KS * 4096,
-                                bq[(u + DD) % NB], wave, lane);
+            db_stage<DK, KS>(Dt, CT, Bp, mt0, kt0 + (st + DD) * KS, kt_last, lds + ((u + DD) % NB) * KS * 4096,
+                             bq[(u + DD) % NB], wave, lane);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -542,30 +570,49 @@ int triad_tile_gemm_slabs(const void* Dt, long long CT, int dk, const void* B, i
   return TRIAD_OK;
 }
 
-// v_mfma_f32_16x16x32_bf16 forms (dQ only: dk must be 0): B's fragments in that MFMA's order.
+// v_mfma_f32_16x16x32_bf16 forms: B's fragments in that MFMA's operand order (per dk).
 int triad_bfrag_pack16(const void* B, int nkt, int dk, void* Bp, hipStream_t stream) {
-  if (nkt <= 0 || !B || !Bp || dk) return TRIAD_EINVAL;
-  hipLaunchKernelGGL(bfrag_pack16_kernel, dim3(nkt), dim3(512), 0, stream, (const bf16*)B, (bf16*)Bp);
+  if (nkt <= 0 || !B || !Bp) return TRIAD_EINVAL;
+  if (dk) hipLaunchKernelGGL(bfrag_pack16_kernel<true>, dim3(nkt), dim3(512), 0, stream, (const bf16*)B, (bf16*)Bp);
+  else hipLaunchKernelGGL(bfrag_pack16_kernel<false>, dim3(nkt), dim3(512), 0, stream, (const bf16*)B, (bf16*)Bp);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
 
 int triad_tile_gemm_packed16(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, const float* alpha,
                              int splits, float* slabs, void* C, hipStream_t stream) {
-  if (dk || M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
+  if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
   const int kps = (nkt + splits - 1) / splits;
   dim3 grid(M / TBM, splits);
   const bf16* d = (const bf16*)Dt;
   const bf16* b = (const bf16*)Bp;
-  if (splits == 1) {
-    hipLaunchKernelGGL((tile_gemm_db16q_kernel<false, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, C);
-    TRIAD_CHECK_LAUNCH();
-    return TRIAD_OK;
+  void* out = splits > 1 ? (void*)slabs : C;
+  const float* al = splits > 1 ? nullptr : alpha;
+  // one k tile per stage, 3 ahead (dK with two tiles per stage, as its 32x32x16 form, would spill)
+  if (dk) {
+    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db16_kernel<true, false, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
+    else hipLaunchKernelGGL((tile_gemm_db16_kernel<true, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
+  } else {
+    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db16_kernel<false, false, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
+    else hipLaunchKernelGGL((tile_gemm_db16_kernel<false, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
   }
-  hipLaunchKernelGGL((tile_gemm_db16q_kernel<true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr,
-                     (void*)slabs);
   TRIAD_CHECK_LAUNCH();
+  if (splits == 1) return TRIAD_OK;
   return triad_sum_slabs(slabs, splits, (long long)M * TBN, alpha, 1, C, stream);
+}
+
+// Unscaled fp32 slabs over packed16 B (the memory-bounded backward's chunked dQ partials).
+int triad_tile_gemm_packed16_slabs(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, int splits,
+                                   float* slabs, hipStream_t stream) {
+  if (M % TBM || nkt <= 0 || splits < 1 || !slabs) return TRIAD_EINVAL;
+  const int kps = (nkt + splits - 1) / splits;
+  dim3 grid(M / TBM, splits);
+  const bf16* d = (const bf16*)Dt;
+  const bf16* b = (const bf16*)Bp;
+  if (dk) hipLaunchKernelGGL((tile_gemm_db16_kernel<true, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  else hipLaunchKernelGGL((tile_gemm_db16_kernel<false, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
 }
 
 }  // extern "C"

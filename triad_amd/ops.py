@@ -97,11 +97,22 @@ def colsum(x, out_dtype=torch.float32, backbone=False):
     return out
 
 
+def _m16(dk):
+    """The tile GEMMs run on v_mfma_f32_16x16x32_bf16 (triad_tile_gemm_packed16): the 32x32x16
+    form's results bit for bit, 9-12 % faster for dQ and 3-5 % for dK at the c3 shapes -- the
+    clock the chip holds under load is higher for that MFMA shape (profiles/r04_bwd_micro_mfma16.log,
+    r04_bwd_micro_mfma16_dk.log; MI355X_MICROARCH.md, DVFS item 7). TRIAD_DQ_MFMA16 / TRIAD_DK_MFMA16
+    = 0 select the 32x32x16 direct-B form (A/B only)."""
+    return MFMA16_DQ if dk == 0 else MFMA16_DK
+
+
 def pack_b(B, nkt, dk, stream):
-    """B [nkt*32][512] bf16 -> its MFMA fragments in the direct-B GEMM's order (triad_bfrag_pack):
-    one pass over B, after which each wave of the GEMM streams its own columns into registers."""
+    """B [nkt*32][512] bf16 -> its MFMA fragments in the direct-B GEMM's order (triad_bfrag_pack /
+    triad_bfrag_pack16, the form _m16 picks): one pass over B, after which each wave of the GEMM
+    streams its own columns into registers."""
     Bp = torch.empty(nkt * 32 * D, dtype=torch.bfloat16, device=B.device)
-    call("triad_bfrag_pack", ptr(B), nkt, dk, ptr(Bp), stream, meta=dict(tag="bfrag-pack", flops=0.0))
+    call("triad_bfrag_pack16" if _m16(dk) else "triad_bfrag_pack", ptr(B), nkt, dk, ptr(Bp), stream,
+         meta=dict(tag="bfrag-pack", flops=0.0))
     return Bp
 
 
@@ -109,27 +120,27 @@ def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream, meta=None, Bp=None):
     """dQ = alpha dS K (dk=0) / dK = alpha dS^T Q (dk=1) over the tiled dS, split-K over the CUs
     when the row panels alone leave them idle. (A stream-K form -- one run of (row panel, k tile)
     units per CU, no slab round trip -- measured slower: runs start at different k offsets, so CUs
-    of one XCD no longer share the streamed B panel in L2.) The direct-B form
-    (triad_tile_gemm_packed over pack_b's fragments, bit-identical to triad_tile_gemm): 6-7 %
-    faster at the c3 shapes (profiles/r03_tile_gemm_db_ab.log); Bp: B already packed."""
+    of one XCD no longer share the streamed B panel in L2.) The direct-B forms over pack_b's
+    fragments (triad_tile_gemm_packed / _packed16, bit-identical to the LDS-ring triad_tile_gemm):
+    6-7 % faster than the ring at the c3 shapes (profiles/r03_tile_gemm_db_ab.log), the 16x16x32
+    one faster again (_m16); Bp: B already packed by pack_b."""
     sp = _gemm_splits(M // 128, nkt, M)
     slabs = torch.empty(sp * M * D, dtype=torch.float32, device=out.device) if sp > 1 else None
-    if dk == 0 and Bp is None and MFMA16_DQ:
-        # dQ on v_mfma_f32_16x16x32_bf16 (triad_tile_gemm_packed16): bit-identical to the 32x32x16
-        # form and 9-12 % faster at the c3 shapes -- the clock the chip holds under load is higher
-        # for that MFMA shape (profiles/r04_bwd_micro_mfma16.log; MI355X_MICROARCH.md, DVFS item 7)
-        Bp = torch.empty(nkt * 32 * D, dtype=torch.bfloat16, device=B.device)
-        call("triad_bfrag_pack16", ptr(B), nkt, 0, ptr(Bp), stream, meta=dict(tag="bfrag-pack", flops=0.0))
-        call("triad_tile_gemm_packed16", ptr(dS), CT, 0, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out),
-             stream, meta=meta)
-        return
     if Bp is None:
         Bp = pack_b(B, nkt, dk, stream)
-    call("triad_tile_gemm_packed", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), stream,
-         meta=meta)
+    call("triad_tile_gemm_packed16" if _m16(dk) else "triad_tile_gemm_packed", ptr(dS), CT, dk, ptr(Bp), M, nkt,
+         ptr(alpha), sp, ptr(slabs), ptr(out), stream, meta=meta)
+
+
+def tile_gemm_slabs(dS, CT, dk, Bp, M, nkt, splits, slabs, stream, meta=None):
+    """Unscaled fp32 split-K partial sums only (the recompute backward's per-chunk dQ), over pack_b's
+    fragments."""
+    call("triad_tile_gemm_packed16_slabs" if _m16(dk) else "triad_tile_gemm_packed_slabs", ptr(dS), CT, dk,
+         ptr(Bp), M, nkt, splits, ptr(slabs), stream, meta=meta)
 
 
 MFMA16_DQ = __import__("os").environ.get("TRIAD_DQ_MFMA16", "1") != "0"
+MFMA16_DK = __import__("os").environ.get("TRIAD_DK_MFMA16", "1") != "0"
 
 
 def _gemm_splits(wgs, nkt, M, cus=256, max_splits=8, t_tile=1.0e-6, hbm=5.0e12):
@@ -200,7 +211,7 @@ def recompute_backward(g: Geometry, Qb, Kb, temp, kind, diag_off, argmax, dclip,
     triad_pairsim_dS recomputes S for those keys and writes that chunk's full dS (clamp + max +
     diagonal terms, weighted by coef), dK rows of those keys come from one tile GEMM (complete:
     a key's gradient only involves its own dS columns), and dQ accumulates the chunks' fp32 partial
-    sums (triad_tile_gemm_packed_slabs), reduced once at the end. Peak dS memory = one chunk.
+    sums (tile_gemm_slabs), reduced once at the end. Peak dS memory = one chunk.
     Returns (dQ [R_pad][512] bf16 | None, dK [CT*32][512] bf16 | None, dt_part fp64)."""
     dev = Qb.device
     nkb = g.Nk_pad // 32
@@ -243,8 +254,8 @@ def recompute_backward(g: Geometry, Qb, Kb, temp, kind, diag_off, argmax, dclip,
                           meta=dict(kind=kind, flops=fl, what="dQ"))
             else:
                 Kp = pack_b(Kc, nc * nkb, 0, stream)
-                call("triad_tile_gemm_packed_slabs", ptr(dS), ctc, 0, ptr(Kp), g.R_pad, nc * nkb, splits,
-                     ptr(slabs[c * splits]), stream, meta=dict(kind=kind, flops=fl, what="dQ"))
+                tile_gemm_slabs(dS, ctc, 0, Kp, g.R_pad, nc * nkb, splits, slabs[c * splits], stream,
+                                meta=dict(kind=kind, flops=fl, what="dQ"))
         if need_k:
             tile_gemm(dS, ctc, 1, Qb, ctc * 32, g.R_pad // 32, temp, dK[j0 * g.Nk_pad:], stream,
                       meta=dict(kind=kind, flops=fl, what="dK"), Bp=Qp)
