@@ -180,7 +180,8 @@ int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const vo
 
 /* triad_gemm_bf16_splitk in an explicit tile form (1-4 as triad_gemm_bf16_form; 0 = the size
  * policy): the backbone weight gradients at >= 32,768 tokens run the eight-wave 256 x 256 form
- * with their own split counts (triad_amd/linear.py). */
+ * with their own split counts (triad_amd/linear.py). form + 8: the workgroups of one split all on
+ * one XCD (each split's token slab fetched into one L2 once; splits % 8 == 0, else TRIAD_EINVAL). */
 int triad_gemm_bf16_splitk_form(const void* A, long long lda, int a_kcontig, const void* B, long long ldb,
                                 int b_kcontig, int M, int N, int Kd, int splits, const float* alpha, float* slabs,
                                 void* C, int out_bf16, int form, hipStream_t stream);

@@ -264,6 +264,40 @@ __global__ __launch_bounds__(256) void xblk_colsum(const unsigned short* in, flo
   out[col] = s;
 }
 
+// PyTorch's own form of that hand-off, as its ROCm reduce_kernel compiles for gfx950 (read from
+// the disassembly of libtorch_hip.so's gfx950 code object, at::native::reduce_kernel<128, 4,
+// ReduceOp<BFloat16 | float, sum ...>>): partials stored `sc1` (global_store_dwordx2 ... sc1),
+// s_waitcnt vmcnt(0), barrier, one lane's returning atomic add on the semaphore, and the last
+// workgroup reads the partials with PLAIN global_load_dwordx4 -- no agent-scope acquire between
+// the semaphore and those loads (MI355X_MICROARCH.md, inter-workgroup visibility: "no acquire ->
+// 24-50 % stale"). kind 10: that form; kind 11: + acquire fence after the semaphore; kind 12: the
+// partials read by sc1 loads (agent-scope relaxed atomic loads).
+template <int MODE>
+__global__ __launch_bounds__(256) void torchform_colsum(const unsigned short* in, float* staging, int* sem, float* out,
+                                                        int ncols, int rows, int nsplit) {
+  const int col = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+  const int r0 = (int)((long long)y * rows / nsplit), r1 = (int)((long long)(y + 1) * rows / nsplit);
+  float acc = 0.f;
+  if (col < ncols)
+    for (int r = r0; r < r1; ++r) acc += __builtin_bit_cast(float, (unsigned)in[(long long)r * ncols + col] << 16);
+  if (col < ncols)
+    __hip_atomic_store(staging + (long long)y * ncols + col, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&sem[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
+  __syncthreads();
+  if (!last || col >= ncols) return;
+  if (MODE == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  float s = 0.f;
+  for (int k = 0; k < nsplit; ++k) {
+    float* p = staging + (long long)k * ncols + col;
+    s += MODE == 2 ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+  }
+  out[col] = s;
+}
+
 extern "C" int hz_victim2(int kind, const void* in, float* staging, int* sem, float* out, int ncols, int rows,
                           int nsplit, hipStream_t s) {
   const dim3 gx((ncols + 255) / 256, nsplit), b(256);
@@ -276,6 +310,12 @@ extern "C" int hz_victim2(int kind, const void* in, float* staging, int* sem, fl
                                nsplit); break;
     case 9: hipLaunchKernelGGL(xblk_colsum<2>, gx, b, 0, s, (const unsigned short*)in, staging, sem, out, ncols, rows,
                                nsplit); break;
+    case 10: hipLaunchKernelGGL(torchform_colsum<0>, gx, b, 0, s, (const unsigned short*)in, staging, sem, out, ncols,
+                                rows, nsplit); break;
+    case 11: hipLaunchKernelGGL(torchform_colsum<1>, gx, b, 0, s, (const unsigned short*)in, staging, sem, out, ncols,
+                                rows, nsplit); break;
+    case 12: hipLaunchKernelGGL(torchform_colsum<2>, gx, b, 0, s, (const unsigned short*)in, staging, sem, out, ncols,
+                                rows, nsplit); break;
     default: return 1;
   }
   return (int)hipGetLastError();

@@ -119,6 +119,9 @@ def main():
         "xblk_colsum plain (cross-WG hand-off: threadfence + atomic semaphore, last WG plain loads)": vic2(7),
         "xblk_colsum acquire (the same + agent-scope acquire fence after the semaphore)": vic2(8),
         "xblk_colsum atomic-load (the same, partials read by agent-scope atomic loads)": vic2(9),
+        "torchform_colsum plain (PyTorch's form: sc1 partial stores, vmcnt(0), barrier, atomic, PLAIN loads)": vic2(10),
+        "torchform_colsum acquire (the same + agent-scope acquire after the semaphore)": vic2(11),
+        "torchform_colsum sc1-load (the same, partials read by sc1 loads)": vic2(12),
         "ld16_victim d16 (global_load_short_d16 / _d16_hi into one VGPR)": vic16(3),
         "ld16_victim ushort (two zero-extending 16-bit loads)": vic16(4),
         "ld16_victim dword (one 32-bit load)": vic16(5),

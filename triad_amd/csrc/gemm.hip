@@ -74,22 +74,39 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16* img, int n0, int s, int la
   return r;
 }
 
+// Workgroup -> (output tile, k split). Default: XCD-aware bijective remap of blockIdx.x -- blocks
+// sharing an XCD (bid % 8 under round-robin placement) get consecutive tiles, so the column tiles
+// of one row panel of A share that XCD's L2; blockIdx.y is the split. xsplit (split-K weight
+// gradients, gridDim.y % 8 == 0): every tile of one split on ONE XCD instead, so that split's
+// token slab of both operands is fetched from HBM once, into that XCD's L2, and read from there
+// by all its tiles (the default mapping puts each split's tiles on all eight XCDs: each operand
+// slab is fetched up to 8 times). Placement is a speed matter only; results do not depend on it.
+__device__ __forceinline__ void tile_split(int xsplit, int& tile, int& split) {
+  const int T = gridDim.x;
+  if (xsplit) {
+    const int L = blockIdx.y * T + blockIdx.x, c = L % 8, i = L / 8;
+    tile = i % T;
+    split = c + 8 * (i / T);
+    return;
+  }
+  const int bid = blockIdx.x, q8 = T / 8, r8 = T % 8, x = bid % 8;
+  tile = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  split = blockIdx.y;
+}
+
 template <bool A_KCONTIG, bool B_KCONTIG, typename OutT>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A, long long lda,
                                                       const bf16* __restrict__ B, long long ldb,
                                                       int M, int N, int Kd, const float* __restrict__ alpha_p,
                                                       OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                      long long slab_stride, const float* __restrict__ bias) {
+                                                      long long slab_stride, const float* __restrict__ bias, int xsplit) {
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * (A_ELEMS + B_ELEMS)];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5;
 
-  // XCD-aware bijective remap: blocks sharing an XCD (bid % 8) get consecutive tiles,
-  // so the N/BN column tiles of one row panel of A share that XCD's L2.
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  int swz, split;
+  tile_split(xsplit, swz, split);
   const int ntn = N / BN;
   const int m0 = (swz / ntn) * BM, n0 = (swz % ntn) * BN;
 
@@ -99,10 +116,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){};
 
-  // split-K: blockIdx.y owns k in [kbeg, kbeg + k_per_split) and writes its own slab of C
-  const int kbeg = blockIdx.y * k_per_split;
+  // split-K: split owns k in [kbeg, kbeg + k_per_split) and writes its own slab of C
+  const int kbeg = split * k_per_split;
   const int nk = min(k_per_split, Kd - kbeg) / BK;
-  C += (size_t)blockIdx.y * slab_stride;
+  C += (size_t)split * slab_stride;
   if (nk > 0) {
     stage_a<A_KCONTIG>(A, lda, m0, kbeg, lds, wave, lane);
     stage_b<B_KCONTIG>(B, ldb, n0, kbeg, lds + A_ELEMS, wave, lane);
@@ -208,14 +225,13 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
                                                           const bf16* __restrict__ B, long long ldb, int M, int N,
                                                           int Kd, const float* __restrict__ alpha_p,
                                                           OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                          long long slab_stride, const float* __restrict__ bias) {
+                                                          long long slab_stride, const float* __restrict__ bias, int xsplit) {
   __shared__ __attribute__((aligned(16))) bf16 lds[GB_NB * GB_ST];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  int swz, split;
+  tile_split(xsplit, swz, split);
   const int ntn = N / BN;
   const int m0 = (swz / ntn) * GB_M, n0 = (swz % ntn) * BN;
 
@@ -225,9 +241,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){};
 
-  const int kbeg = blockIdx.y * k_per_split;
+  const int kbeg = split * k_per_split;
   const int nk = __builtin_amdgcn_readfirstlane(max(0, min(k_per_split, Kd - kbeg)) / BK);
-  C += (size_t)blockIdx.y * slab_stride;
+  C += (size_t)split * slab_stride;
 #pragma unroll
   for (int p = 0; p < GB_NB - 1; ++p)
     if (p < nk)
@@ -333,14 +349,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
                                                          const bf16* __restrict__ B, long long ldb, int M, int N,
                                                          int Kd, const float* __restrict__ alpha_p,
                                                          OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                         long long slab_stride, const float* __restrict__ bias) {
+                                                         long long slab_stride, const float* __restrict__ bias, int xsplit) {
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * GW_ST];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  int swz, split;
+  tile_split(xsplit, swz, split);
   const int ntn = N / GW_N;
   const int m0 = (swz / ntn) * GW_M, n0 = (swz % ntn) * GW_N;
 
@@ -350,9 +365,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict_
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = (f32x16){};
 
-  const int kbeg = blockIdx.y * k_per_split;
+  const int kbeg = split * k_per_split;
   const int nk = __builtin_amdgcn_readfirstlane(max(0, min(k_per_split, Kd - kbeg)) / BK);
-  C += (size_t)blockIdx.y * slab_stride;
+  C += (size_t)split * slab_stride;
   if (nk > 0)
 #pragma unroll
     for (int u = 0; u < GW_PIECES; ++u)
@@ -442,14 +457,13 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
                                                          const bf16* __restrict__ B, long long ldb, int M, int N,
                                                          int Kd, const float* __restrict__ alpha_p,
                                                          OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                         long long slab_stride, const float* __restrict__ bias) {
+                                                         long long slab_stride, const float* __restrict__ bias, int xsplit) {
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * GW_ST];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int h = lane >> 5;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  int swz, split;
+  tile_split(xsplit, swz, split);
   const int ntn = N / GW_N;
   const int m0 = (swz / ntn) * GW_M, n0 = (swz % ntn) * GW_N;
 
@@ -459,9 +473,9 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16){};
 
-  const int kbeg = blockIdx.y * k_per_split;
+  const int kbeg = split * k_per_split;
   const int nk = __builtin_amdgcn_readfirstlane(max(0, min(k_per_split, Kd - kbeg)) / BK);
-  C += (size_t)blockIdx.y * slab_stride;
+  C += (size_t)split * slab_stride;
   if (nk > 0)
 #pragma unroll
     for (int u = 0; u < GE_PIECES; ++u)
@@ -525,13 +539,18 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
 // every M >= 50,944 shape, profiles/r02_gemm_w8_ring_probe.log.) Tile forms are per-call arguments
 // (triad_gemm_bf16_form, triad_gemm_bf16_splitk_form): there is no process-wide GEMM state.
 constexpr int kBigForm = 4;
+// form flag of the split-K entry points: the workgroups of one split all on one XCD (tile_split)
+constexpr int kXcdSplit = 8;
 
 
 template <bool AK, bool BK_, typename OutT>
 int launch(const void* A, long long lda, const void* B, long long ldb, int M, int N, int Kd, const float* alpha,
            void* C, long long ldc, hipStream_t st, int splits = 1, long long slab_stride = 0,
            const float* bias = nullptr, int form = 0) {
+  const int xsplit = (form & kXcdSplit) ? 1 : 0;
+  form &= ~kXcdSplit;
   if (M % BM || N % BN || Kd % BK || lda % 8 || ldb % 8 || splits < 1) return TRIAD_EINVAL;
+  if (xsplit && splits % 8) return TRIAD_EINVAL;
   const int kps = ((Kd / BK + splits - 1) / splits) * BK;
   // the 256-row ring pays off on long k loops or many row tiles (conv / projection GEMMs);
   // the short split-K weight-gradient loops keep the 128 x 128 form (measured, profiles/r01_dw_gemm_*.log)
@@ -544,14 +563,14 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
   if (w4_ok && form == 4) {
     const int nwg = (M / GW_M) * (N / GW_N);
     hipLaunchKernelGGL((gemm_w8_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
-                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias);
+                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, xsplit);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
   if (w4_ok && (form == 3 || (form == 0 && w4_auto))) {
     const int nwg = (M / GW_M) * (N / GW_N);
     hipLaunchKernelGGL((gemm_w4_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(256), 0, st, (const bf16*)A, lda,
-                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias);
+                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, xsplit);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
@@ -559,13 +578,13 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
       (form == 2 || M >= 8192 || Kd / splits >= 32768)) {
     const int nwg = (M / GB_M) * (N / BN);
     hipLaunchKernelGGL((gemm_big_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
-                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias);
+                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, xsplit);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
   const int nwg = (M / BM) * (N / BN);
   hipLaunchKernelGGL((gemm_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(256), 0, st, (const bf16*)A, lda,
-                     (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias);
+                     (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, xsplit);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
@@ -629,10 +648,12 @@ int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void
 // Split-K form for short-and-wide outputs (weight gradients: M, N = 512 / H, Kd = tokens):
 // `splits` partial fp32 slabs in `slabs` ([splits][M][N], caller-owned), then
 // C = alpha * sum(slabs) as fp32 or bf16 (ldc == N).
+// form: as triad_gemm_bf16_form, + 8 (kXcdSplit) = the workgroups of one split all on one XCD
+// (needs splits % 8 == 0).
 int triad_gemm_bf16_splitk_form(const void* A, long long lda, int a_kcontig, const void* B, long long ldb,
                                 int b_kcontig, int M, int N, int Kd, int splits, const float* alpha, float* slabs,
                                 void* C, int out_bf16, int form, hipStream_t stream) {
-  if (form < 0 || form > 4) return TRIAD_EINVAL;
+  if ((form & ~kXcdSplit) < 0 || (form & ~kXcdSplit) > 4) return TRIAD_EINVAL;
   const long long slab = (long long)M * N;
   int rc = TRIAD_EINVAL;
 #define TRIAD_GEMM_SK(AK, BKC)                                                                  \
