@@ -1,8 +1,9 @@
-"""Results must not depend on what else shares the CUs (the tri-modal step runs three backbone
-streams concurrently). Regression test of the round-2 nondeterminism: the HuBERT conv-0 +
-GroupNorm + GELU kernel (triad_c0gn_fwd), compiled with packed-FP32 VALU chains, returned wrong
-values in lanes 48-63 whenever a 128 x 128 MFMA GEMM workgroup (triad_gemm_bf16 form 1) shared its
-CU; the library is built without packed-FP32 ops since (triad_amd/build.py). Every output buffer
+"""Our kernels' results must not depend on what else shares the CUs (the opt-in concurrent step
+runs three backbone streams). Regression test of the round-2 nondeterminism: the HuBERT conv-0 +
+GroupNorm + GELU kernel (triad_c0gn_fwd) returned wrong values in lanes 48-63 whenever a 128 x 128
+MFMA GEMM workgroup (triad_gemm_bf16 form 1) shared its CU, until round 3 changed its weight loads
+and dropped packed-FP32 ops library-wide (which of the two mattered is not established, DESIGN.md
+§2b; PyTorch's bf16 reductions remain victims, hence the serial default). Every output buffer
 of c0gn, computed on a side stream while the GEMM runs on the main stream, must equal the quiet
 run bit for bit (tools/concurrency_repro.py has the wider matrix of kernel pairs)."""
 import pytest

@@ -48,9 +48,13 @@ def test_projection_head_at_step_rows(rows, H):
     assert y.dtype == torch.bfloat16 and y.shape == (1, rows, 512)
     y.float().view(rows, 512).backward(gy)
     got = [hd.grad] + [p.grad.detach().clone() for m in mods for p in m.parameters()]
-    # the weight gradients' split-K factor: 16 (one round of 256 CUs) at every step row count
+    # the weight gradients' split-K plans: 32 splits, one XCD per split, at the long token lists;
+    # one round of 16 128 x 128 splits for the 8,192-row text head
     Mp = (rows + 127) // 128 * 128
-    assert ops._splitk(Mp, 16) == 16
+    if Mp >= 32768:
+        assert ops._dw_plan(Mp, 512) == (1 | 8, 32) and ops._dw_plan(Mp, H) == (4 | 8, 32)
+    else:
+        assert ops._dw_plan(Mp, 512) == (0, 16)
     # oracle forward (bf16 autocast emulation), chunked over rows
     w = [p.detach() for m in mods for p in m.parameters()]
     yf = y.detach().float().view(rows, 512)
@@ -79,3 +83,29 @@ def test_projection_head_at_step_rows(rows, H):
     print(f"projection head {rows} x {H}: gradient relative L2 {errs}")
     for n, e in errs.items():
         assert e < 1e-2, (n, e)
+
+
+@pytest.mark.parametrize("form", [1, 4])
+def test_splitk_xcd_placement_bit_identical(form):
+    """Form flag 8 (each split's workgroups on one XCD, gemm.hip tile_split) moves workgroups, not
+    arithmetic: bit-identical to the default placement at the same form / splits, and refused
+    (TRIAD_EINVAL) when the split count is not a multiple of 8."""
+    from triad_amd._lib import TriadError, call, ptr, stream_ptr
+    M, O, K, sp = 16384, 512, 768, 16
+    g = torch.Generator(device=dev).manual_seed(form)
+    dy = (torch.randn(M, O, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    outs = []
+    for f in (form, form | 8):
+        slabs = torch.empty(sp * O * K, device=dev)
+        dw = torch.empty(O, K, device=dev)
+        call("triad_gemm_bf16_splitk_form", ptr(dy), O, 0, ptr(x), K, 0, O, K, M, sp, None, ptr(slabs), ptr(dw), 0, f,
+             stream_ptr())
+        outs.append(dw)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = dy.float().t() @ x.float()
+    assert float((outs[1] - ref).norm() / ref.norm()) < 1e-4
+    with pytest.raises(TriadError):
+        call("triad_gemm_bf16_splitk_form", ptr(dy), O, 0, ptr(x), K, 0, O, K, M, 12, None, ptr(slabs), ptr(dw), 0,
+             form | 8, stream_ptr())

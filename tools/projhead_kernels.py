@@ -14,6 +14,9 @@ import sys
 
 CASES = (("visual", 65536, 768), ("audio", 50944, 768), ("text", 8192, 768), ("c5-visual", 43808, 1024))
 FORMS = tuple(os.environ.get("TRIAD_PROJHEAD_FORMS", "fused,passes").split(","))
+# the trainer keeps bf16 shadows of projection1 / projection2 (round 4, train.py bf16_weight_params):
+# bf16 weights are the product configuration; fp32 = the round-2 / round-3 figures
+WDTYPE = os.environ.get("TRIAD_PROJHEAD_WDTYPE", "bf16")
 
 
 def run(iters):
@@ -31,6 +34,8 @@ def run(iters):
         for name, M, H in CASES:
             torch.manual_seed(0)
             p1, ln, p2 = nn.Linear(H, 512).to(dev), nn.LayerNorm(512).to(dev), nn.Linear(512, 512).to(dev)
+            if WDTYPE == "bf16":
+                p1, p2 = p1.to(torch.bfloat16), p2.to(torch.bfloat16)
             h = torch.randn(M, H, device=dev).to(torch.bfloat16).requires_grad_(True)
             gy = (torch.randn(M, 512, device=dev) * 0.01).to(torch.bfloat16)
             for _ in range(2):   # warm-up (library heuristics, allocator)

@@ -28,11 +28,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE,
          "-Wno-unused-result",
-         # no packed-FP32 VALU ops (v_pk_fma/add/mul_f32) in any kernel: a v_pk_fma_f32 chain
-         # (compiler-vectorised conv0 in frontend.hip) was measured to return wrong low halves in
-         # lanes 48-63 while a 128 x 128 MFMA GEMM workgroup shared the CU -- nondeterministic
-         # results of the concurrent-stream step (tools/concurrency_repro.py).
-         # Device-side target feature; the host compile ignores it with a warning.
+         # no packed-FP32 VALU ops (v_pk_fma/add/mul_f32) in any kernel: round 3 removed them
+         # when the compiler-vectorised conv0 in frontend.hip returned wrong values beside a
+         # co-resident MFMA GEMM; round 4's isolated v_pk_* probes were clean beside the same
+         # GEMMs (tools/hazard_probe.py), so this is kept as a neutral setting, not a proven fix
+         # (DESIGN.md §2b). Device-side target feature; the host compile ignores it with a warning.
          "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"] + os.environ.get("TRIAD_EXTRA_FLAGS", "").split()
 # per-file extras: the pipelined forward wants scalar f32 VALU beside its MFMAs (SLP-packed
 # v_pk_mul_f32 + operand moves cost more issue slots than two v_mul_f32 there)

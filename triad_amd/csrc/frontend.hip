@@ -238,10 +238,11 @@ __global__ __launch_bounds__(NT) void c0gn_kernel(const bf16* __restrict__ wave,
   const int nsmp = (t1 > t0) ? C0_S * (t1 - t0 - 1) + C0_K : 0;
   for (int i = threadIdx.x; i < nsmp; i += NT) smp[i] = (float)wave[(long long)b * Lp + (long long)C0_S * t0 + i];
   // the thread's 8 channels x 10 taps = 160 contiguous bytes at a 32-byte-aligned offset
-  // (c0 % 8 == 0), loaded as ten ALIGNED 16-byte vectors: element-wise loads let hipcc merge them
-  // into dwordx3 / dwordx4 loads at 2-byte alignment (byte offsets 14, 30, 46, ...), which were
-  // measured to return wrong data in lanes 48-63 while a 128 x 128 GEMM workgroup (LDS-DMA) shared
-  // the CU (tools/concurrency_repro.py)
+  // (c0 % 8 == 0), loaded as ten ALIGNED 16-byte vectors (element-wise loads let hipcc merge them
+  // into dwordx3 / dwordx4 loads at 2-byte alignment). Round 3 changed this load form together with
+  // the build-wide removal of packed-FP32 ops when this kernel returned wrong values in lanes 48-63
+  // beside a co-resident 128 x 128 GEMM; round 4's isolated probes of both instruction classes were
+  // clean, so neither is the established cause (the product runs one stream)
   float w[8][C0_K];
   {
     bf16x8 wv[C0_K];

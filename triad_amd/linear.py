@@ -49,12 +49,16 @@ def _splits(M, out_f, in_f):
 # on the 128 x 128 table above, 768 x 768 98 vs 101, 3072 x 768 275 vs 298, 768 x 3072 284 vs 315;
 # at 8,192 tokens the 128 x 128 table stays faster).
 _W8_SPLITS = {27: 8, 9: 24, 36: 12}
+# of those, the ones whose workgroups of one split all go to one XCD (gemm.hip tile_split, form
+# flag 8; splits % 8 == 0): 768 x 768 at 50,944 tokens 99.6 -> 86.2 us, 2304 x 768 209.6 -> 200.2
+# (profiles/r04_dw_xcd_ab.log; 3072 x 768 / 768 x 3072 keep 12 splits, faster than any 8k split)
+_W8_XCD = {27, 9}
 
 
 def _form_splits(M, out_f, in_f):
     tiles8 = (out_f // 256) * (in_f // 256) if out_f % 256 == 0 and in_f % 256 == 0 else 0
     if M >= 32768 and tiles8 in _W8_SPLITS:
-        return 4, _W8_SPLITS[tiles8]
+        return 4 | (8 if tiles8 in _W8_XCD else 0), _W8_SPLITS[tiles8]
     return 0, _splits(M, out_f, in_f)
 
 

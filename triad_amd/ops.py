@@ -633,6 +633,19 @@ def _splitk(Kd, mn_tiles):
     return max(1, min(want, Kd // 512))
 
 
+def _dw_plan(Mp, N):
+    """(form, splits) of a projection-head weight gradient [512][N] over Mp token rows. Long
+    token lists: 32 splits with each split's workgroups on one XCD (gemm.hip tile_split, form
+    flag 8) -- 128 x 128 tiles for dW2 (N = 512), the eight-wave 256 x 256 tile for dW1 (N = 768):
+    visual 65,536 rows dW2 65.9 -> 54.6 us, dW1 86.4 -> 74.2; audio 50,944 rows dW2 56.1 -> 44.9,
+    dW1 69.1 -> 63.6 (GEMM + slab reduction, profiles/r04_dw_xcd_ab.log; bit-identical to the
+    default placement at equal form / splits). Short lists (the 8,192-row text head) keep _splitk's
+    one round of 128 x 128 workgroups (faster there)."""
+    if Mp >= 32768 and N % 256 == 0:
+        return (1 if N == D else 4) | 8, 32
+    return 0, _splitk(Mp, (D // 128) * (N // 128))
+
+
 def _bf16_round(t):
     return t.detach().to(torch.bfloat16).to(torch.float32).contiguous()
 
@@ -811,16 +824,15 @@ class _ProjectionHeadPasses(torch.autograd.Function):
         # bf16 model weights (the trainer's shadowed Linear parameters): the gradients come out in
         # bf16 straight from the reductions, as autocast's bf16 GEMM / bias gradients do
         db2 = colsum(dyp, torch.bfloat16 if b2d == torch.bfloat16 else f32)
-        sp2 = _splitk(Mp, (D // 128) * (D // 128))
-        sp1 = _splitk(Mp, (D // 128) * (H // 128))
+        (f2, sp2), (f1, sp1) = _dw_plan(Mp, D), _dw_plan(Mp, H)
         slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
         o2, o1 = int(w2d == torch.bfloat16), int(w1d == torch.bfloat16)
         dw2 = torch.empty(D, D, dtype=torch.bfloat16 if o2 else f32, device=dev)
-        call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2), o2, st,
-             meta=dict(tag=f"proj-dW2x{M}", flops=2.0 * M * D * D))
+        call("triad_gemm_bf16_splitk_form", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2),
+             o2, f2, st, meta=dict(tag=f"proj-dW2x{M}", flops=2.0 * M * D * D))
         dw1 = torch.empty(D, H, dtype=torch.bfloat16 if o1 else f32, device=dev)
-        call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), o1, st,
-             meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
+        call("triad_gemm_bf16_splitk_form", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1),
+             o1, f1, st, meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
         return (dh.view(*lead, H).to(hd), dw1.to(w1d), cols[2].to(b1d), cols[0].to(gd), cols[1].to(bd), dw2.to(w2d),
                 db2.to(b2d), None)
 
