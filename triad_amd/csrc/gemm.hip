@@ -532,6 +532,10 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
     }
 }
 
+// (Measured and not kept, round 4: the eight-wave tile on v_mfma_f32_16x16x32_bf16 -- bit-identical,
+// but 2-30 % slower on every c3 projection-head / backbone shape, profiles/r04_gemm_m16_ab.log; the
+// 16 x 16 x 32 shape pays off in the similarity head's direct-B tile GEMMs, not here.)
+
 // The 256 x 256 form the size policy picks for tall outputs: the eight-wave form (4), 3-13 % faster
 // than the four-wave form (3) on every c3 backbone / projection-head shape with M >= 50,944
 // (profiles/r02_gemm_w8_probe.log). (Measured and not kept: the eight-wave tile on a 4-slot ring of
