@@ -326,6 +326,16 @@ def main():
                      "kernels": {k: kstats(k) for k in sorted(rep) if k in head_keys}},
             "backbone_hip_gemm_ms_per_step": sum(v["ms"] for k, v in rep.items() if k not in head_keys) / a.steps,
         }
+        # the three projection heads as one figure: every launch tagged proj-* /
+        # proj{H}x{M} (GEMMs, LayerNorm passes, bias column sums, slab sums) against their algorithmic
+        # flops, 6 x rows x (H x 512 + 512 x 512) per step (forward 2, backward 4)
+        pk = [k for k in head_keys if "[proj" in k]
+        p_ms = sum(rep[k]["ms"] for k in pk) / a.steps
+        p_fl = sum(rep[k]["flops"] for k in pk) / a.steps
+        if p_ms > 0:
+            res["projection_heads"] = {"ms_per_step": p_ms, "algo_TFLOP_per_step": p_fl / 1e12,
+                                       "achieved_TFLOPs": p_fl / p_ms / 1e9,
+                                       "frac": p_fl / p_ms / 1e9 / PEAK_BF16_TFLOPS, "launches": len(pk)}
         res["config"]["execution"] = ("concurrent streams (opt-in)" if model_streams() else
                                       "serial: one stream (the bit-reproducible default, DESIGN.md 2b)")
         if single is not None:

@@ -29,6 +29,10 @@ constexpr int TBM = 128, TBN = 512, TBK = 32;
 // source chunk is permuted instead).
 __device__ __forceinline__ int swz_q(int c) { return c ^ ((c >> 4) & 1); }          // dQ row reads
 __device__ __forceinline__ int swz_k(int c) { return c ^ (((c >> 6) & 1) << 3); }   // dK transposed reads
+// dK reads of the 16 x 16 x 32 form (a 32-lane half of a ds_read_b64_tr_b16 spans rows 8g + 0..7 and
+// 32 + 8g + 0..7, g = 0, 1): bit 0 also flipped by row bit 3, so the two 16-lane groups of a half land
+// on different banks (swz_k leaves them 2-way conflicting)
+__device__ __forceinline__ int swz_k16(int c) { return c ^ (((c >> 6) & 1) << 3) ^ ((c >> 4) & 1); }
 // B image [32][512], 1 KB rows: chunk c of row k at c ^ ((k & 3) << 2)
 __device__ __forceinline__ int b_off(int k, int col) { return k * TBN + ((((col >> 3) ^ ((k & 3) << 2))) << 3) + (col & 7); }
 
@@ -221,7 +225,7 @@ __device__ __forceinline__ bf16x8 gload16(const bf16* p) {
 // one stage: k tiles kt .. kt + KS - 1 (clamped to kt_last: a short last stage re-loads its last
 // tile, so every stage issues exactly 5 KS vm ops per wave -- 4 B loads + 1 A piece per tile --
 // and the counted waits hold)
-template <bool DK, int KS>
+template <bool DK, int KS, bool K16 = false>
 __device__ __forceinline__ void db_stage(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ Bp,
                                          int mt0, int kt, int kt_last, bf16* adst, bf16x8 (&bq)[4 * KS], int wave,
                                          int lane) {
@@ -233,7 +237,7 @@ __device__ __forceinline__ void db_stage(const bf16* __restrict__ Dt, long long 
     for (int u = 0; u < 4; ++u) bq[4 * k + u] = gload16(src + u * 512);
     const int t = wave >> 1, half = wave & 1;
     const int pos = half * 64 + lane;
-    const int c = DK ? swz_k(pos) : swz_q(pos);
+    const int c = DK ? (K16 ? swz_k16(pos) : swz_k(pos)) : swz_q(pos);
     const long long tile = DK ? ((long long)ktk * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + ktk);
     glds16(Dt + tile * 1024 + c * 8, adst + k * 4096 + t * 1024 + half * 512);
   }
@@ -414,7 +418,7 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         const int qry = 8 * kc + 4 * tt + q4;
-        aoff[rh][tt] = swz_k((qry + 32 * hh) * 2 + (a >> 1)) * 8 + 4 * (a & 1);
+        aoff[rh][tt] = swz_k16((qry + 32 * hh) * 2 + (a >> 1)) * 8 + 4 * (a & 1);
       }
     }
   }
@@ -428,7 +432,7 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
   bf16x8 bq[NB][4 * KS];
 #pragma unroll
   for (int p = 0; p < DD; ++p)
-    if (p < nst) db_stage<DK, KS>(Dt, CT, Bp, mt0, kt0 + p * KS, kt_last, lds + p * KS * 4096, bq[p], wave, lane);
+    if (p < nst) db_stage<DK, KS, true>(Dt, CT, Bp, mt0, kt0 + p * KS, kt_last, lds + p * KS * 4096, bq[p], wave, lane);
   for (int st0 = 0; st0 < nst; st0 += NB) {
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
@@ -459,7 +463,7 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
           for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = mfma16(af[rb], bq[u][4 * k + cb], acc[rb][cb]);
           if (k == 0 && rb == 1 && pf) {
             __builtin_amdgcn_sched_barrier(0);
-            db_stage<DK, KS>(Dt, CT, Bp, mt0, kt0 + (st + DD) * KS, kt_last, lds + ((u + DD) % NB) * KS * 4096,
+            db_stage<DK, KS, true>(Dt, CT, Bp, mt0, kt0 + (st + DD) * KS, kt_last, lds + ((u + DD) % NB) * KS * 4096,
                              bq[(u + DD) % NB], wave, lane);
             __builtin_amdgcn_sched_barrier(0);
           }

@@ -412,10 +412,299 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   }
 }
 
+// ---- the same workgroup on v_mfma_f32_16x16x32_bf16 (TRIAD_FWD_M16 build) -------------------
+// Per wave and key tile: 32 keys x 32 queries as 2 x 2 tiles of 16 x 16 (key half kb2, query half
+// qb), sixteen 32-deep k-steps of 4 MFMAs, one epilogue element of the previous tile per k-step.
+// Lane l (i = l & 15, g = l >> 4) holds queries 16 qb + i and keys 16 kb2 + 4 g + (0..3): two running
+// max / argmax per lane (one per query half), combined over the four lane groups at each sample's
+// end. The unit dS keeps the 32 x 32 tile layout the backward reads (element (q, k) at
+// (q + 32 ((k >> 2) & 1)) * 16 + (k & 3) + 4 (k >> 3)): per query half and key half a lane's four
+// keys are one 8-byte piece of a 16-element run whose other pieces lane l ^ 32 holds.
+#ifndef TRIAD_FWD_M16
+#define TRIAD_FWD_M16 0
+#endif
+constexpr int NS16 = D / 32;  // 16 k-steps
+constexpr int LDSPF16 = 2;
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+
+struct Epi16 {
+  float m[2], m0[2];  // running max of u per query half, and at the tile's start
+  int am[2], at[2];   // argmax within the sample (without 4g) / best key of the tile (valid when m > m0)
+  int lim[2];         // masked tiles: valid keys of the tile minus 4g (0 - 4g for a padded query row)
+  f32x2 nn2;
+  float mn, prev;
+  unsigned pk[8];     // unit dS, bf16 pairs: pk[4 kb2 + 2 qb + 0..1]
+};
+
+// element v = 8 kb2 + 4 qb + ii: key 16 kb2 + ii (+ 4g) of query half qb; accumulator p[v >> 2][v & 3]
+__device__ __forceinline__ constexpr int vkey16(int v) { return 16 * (v >> 3) + (v & 3); }
+
+template <bool TRAIN, bool FULL>
+__device__ __forceinline__ void epi_elem16(Epi16& e, const f32x4 (&p)[4], int v, f32x2 su2, float lo) {
+  const int qb = (v >> 2) & 1;
+  const float u = p[v >> 2][v & 3];
+  if constexpr (FULL) {
+    e.at[qb] = u > e.m[qb] ? vkey16(v) : e.at[qb];  // keys ascend with v within a query half
+    e.m[qb] = maxf(u, e.m[qb]);
+  } else {
+    PIN(e.lim[qb]);
+    const bool better = vkey16(v) < e.lim[qb] && u > e.m[qb];
+    e.m[qb] = better ? u : e.m[qb];
+    e.at[qb] = better ? vkey16(v) : e.at[qb];
+  }
+  const float c = __builtin_amdgcn_fmed3f(u, lo, 0.f);
+  if (v & 1) {
+    e.nn2.x = fma_sq(e.prev, e.nn2.x);
+    e.nn2.y = fma_sq(c, e.nn2.y);
+    PIN(e.nn2);
+    if constexpr (TRAIN) {
+      e.mn = min3f(e.mn, p[v >> 2][(v & 3) - 1], u);
+      e.pk[v >> 1] = pack_bf16x2(mulf(e.prev, su2.x), mulf(c, su2.y));
+      PIN(e.mn);
+      PIN(e.pk[v >> 1]);
+    }
+  } else {
+    e.prev = c;
+    PIN(e.prev);
+  }
+  PIN(e.m[qb]);
+  PIN(e.at[qb]);
+}
+
+__device__ __forceinline__ float epi_fixup16(Epi16& e, const f32x4 (&p)[4], float su, float lo) {
+  float st = 0.f, dp = 0.f;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const float u = p[v >> 2][v & 3];
+    const float d = (u >= lo && u <= 0.f) ? u : 0.f;
+    st = fmaf(d, d, st);
+    if (v & 1) e.pk[v >> 1] = pack_bf16x2(dp * su, d * su);
+    else dp = d;
+  }
+  return st;
+}
+
+template <bool TRAIN>
+__device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const int bx, const int by, const int gx) {
+  double* red = (double*)(kbuf + NBUF * KT_ELEMS);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i16 = lane & 15, g = lane >> 4;
+  const int row0 = bx * ROWS_PER_WG + wave * 32;
+  const int rowq[2] = {row0 + i16, row0 + 16 + i16};
+  const bool rok[2] = {rowq[0] < a.R, rowq[1] < a.R};
+  const int rt = row0 / 32;
+
+  const int j0 = by * a.j_per_wg;
+  const int j1 = min(a.Bk, j0 + a.j_per_wg);
+  const int nkb = a.Nk_pad / 32;
+  const int nblocks = (j1 - j0) * nkb;
+  if (nblocks <= 0) {
+    if (threadIdx.x == 0) {
+      a.part[by * gx + bx] = 0.0;
+      if (a.part2) a.part2[by * gx + bx] = 0.0;
+    }
+    return;
+  }
+  const unsigned long long kaddr = (unsigned long long)(a.K + (size_t)j0 * a.Nk_pad * D);
+  const i32x4 kr = {__builtin_amdgcn_readfirstlane((int)(unsigned)kaddr),
+                    __builtin_amdgcn_readfirstlane((int)((unsigned)(kaddr >> 32) & 0xffffu)),
+                    __builtin_amdgcn_readfirstlane((int)((unsigned)(j1 - j0) * a.Nk_pad * (D * 2))), 0x00020000};
+  Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
+  int fslot = 0, cslot = 0;
+  auto prefetch = [&](int b2) {
+    if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j - j0, fc.kb, wave, lane);
+    fc.next(nkb);
+    fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
+  };
+  prefetch(0);
+  prefetch(1);
+
+  bf16x8 qf[2][NS16];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const bf16* q0 = a.Q + (size_t)rowq[qb] * D + 8 * g;  // rows < R_pad: zero tail, in the allocation
+#pragma unroll
+    for (int s = 0; s < NS16; ++s) qf[qb][s] = *(const bf16x8*)(q0 + 32 * s);
+  }
+  const float temp = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, *a.temp)));
+  const float su = temp != 0.f ? fabsf(temp) : 1.f;
+  if (!(temp > 0.f)) {
+    const unsigned flip = temp < 0.f ? 0x80008000u : 0u, keep = temp == 0.f ? 0u : 0xffffffffu;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int s = 0; s < NS16; ++s) {
+        u32x4 w = __builtin_bit_cast(u32x4, qf[qb][s]);
+        w = (w & keep) ^ flip;
+        qf[qb][s] = __builtin_bit_cast(bf16x8, w);
+      }
+  }
+  const f32x2 su2 = {su, su};
+  const float lo = a.clamp_lo / su;
+  double accd = 0.0, accd2 = 0.0;
+  // swizzled LDS key-fragment offsets (bytes): key row 16 kb2 + i, chunk 4 s + g
+  int xo[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) xo[k] = i16 * (D * 2) + (((4 * k + g) ^ i16) * 16);
+  bf16* const dS_w = TRAIN ? a.dS + (long long)rt * a.CT * 1024 : nullptr;
+  // this lane's 16-byte dS run inside a 32 x 32 tile, per query half: row 16 qb + i + 32 (g & 1), half h5
+  const int h5 = g >> 1;
+  const int dso[2] = {(i16 + 32 * (g & 1)) * 16 + 8 * h5, (16 + i16 + 32 * (g & 1)) * 16 + 8 * h5};
+
+  Epi16 e;
+  e.m[0] = e.m[1] = -INFINITY;
+  e.am[0] = e.am[1] = 0;
+  e.at[0] = e.at[1] = 0;
+  f32x4 cA[4], cB[4];
+
+  auto sync_tile = [&](int b) {
+    const bool more = b + 1 < nblocks;
+    const bool st = TRAIN && b >= 2;
+    if (more && st) TRIAD_VMCNT(GLDS_PER_TILE + 2);
+    else if (more) TRIAD_VMCNT(GLDS_PER_TILE);
+    else if (st) TRIAD_VMCNT(2);
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  auto epi_end = [&](const f32x4 (&p)[4]) {
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+      if (e.m[qb] > e.m0[qb]) e.am[qb] = ec.kb * 32 + e.at[qb];
+    const float nn = e.nn2.x + e.nn2.y;
+    accd += (double)nn;
+    if (TRAIN) {
+      const float st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup16(e, p, su, lo) : nn;
+      accd2 += (double)st;
+      // lanes l and l ^ 32 hold the two halves of the same 16-element runs: swap one 8-byte
+      // piece so each lane stores one 16-byte run (h5 = 0: elements 0..7, h5 = 1: 8..15)
+      bf16* d = dS_w + ((long long)ec.j * nkb + ec.kb) * 1024;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const unsigned s0 = h5 ? e.pk[2 * qb] : e.pk[4 + 2 * qb];
+        const unsigned s1 = h5 ? e.pk[2 * qb + 1] : e.pk[4 + 2 * qb + 1];
+        const unsigned r0 = __shfl_xor(s0, 32), r1 = __shfl_xor(s1, 32);
+        const u32x4 v = h5 ? (u32x4){r0, r1, e.pk[4 + 2 * qb], e.pk[4 + 2 * qb + 1]}
+                           : (u32x4){e.pk[2 * qb], e.pk[2 * qb + 1], r0, r1};
+        store16(d + dso[qb], v);
+      }
+    }
+    if (ec.kb == nkb - 1) {  // end of a key sample: combine the four lane groups per query half
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float m = e.m[qb];
+        int am = e.am[qb] + 4 * g;
+#pragma unroll
+        for (int x = 16; x <= 32; x *= 2) {
+          const float m2 = __shfl_xor(m, x);
+          const int am2 = __shfl_xor(am, x);
+          if (m2 > m || (m2 == m && am2 < am)) { m = m2; am = am2; }
+        }
+        if (g == qb && rok[qb]) {
+          a.rowmax[(size_t)ec.j * a.R_pad + rowq[qb]] = su * m;
+          a.argmax[(size_t)ec.j * a.R_pad + rowq[qb]] = am;
+        }
+        e.m[qb] = -INFINITY;
+        e.am[qb] = 0;
+      }
+    }
+    ec.next(nkb);
+  };
+
+  auto iter = [&](auto CH, auto EP, auto FULLT, int b, f32x4 (&c)[4], const f32x4 (&p)[4]) {
+    constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value, full = decltype(FULLT)::value;
+    if constexpr (ch) {
+      sync_tile(b);
+      prefetch(b + NBUF - 1);
+      const char* kt = (const char*)kbuf + cslot * (KT_ELEMS * 2);
+      cslot = __builtin_amdgcn_readfirstlane(cslot == NBUF - 1 ? 0 : cslot + 1);
+      constexpr int P = LDSPF16;
+      bf16x8 af[P + 1][2];
+#pragma unroll
+      for (int s = 0; s < P; ++s)
+#pragma unroll
+        for (int kb2 = 0; kb2 < 2; ++kb2)
+          af[s][kb2] = *(const bf16x8*)(kt + kb2 * 16 * (D * 2) + xo[s & 3] + (s >> 2) * 256);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) c[t] = (f32x4){};
+#pragma unroll
+      for (int s = 0; s < NS16; ++s) {
+        if (s + P < NS16)
+#pragma unroll
+          for (int kb2 = 0; kb2 < 2; ++kb2)
+            af[(s + P) % (P + 1)][kb2] =
+                *(const bf16x8*)(kt + kb2 * 16 * (D * 2) + xo[(s + P) & 3] + ((s + P) >> 2) * 256);
+#pragma unroll
+        for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            c[2 * kb2 + qb] = mfma16(af[s % (P + 1)][kb2], qf[qb][s], c[2 * kb2 + qb]);
+        if constexpr (ep) epi_elem16<TRAIN, full>(e, p, s, su2, lo);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (ep) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) epi_elem16<TRAIN, full>(e, p, v, su2, lo);
+    }
+    if constexpr (ep) epi_end(p);
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  auto tile_full = [&]() {
+    const int nk = a.klen ? min(a.klen[ec.j], a.Nk_eff) : a.Nk_eff;
+    const int nv = __builtin_amdgcn_readfirstlane(nk - ec.kb * 32);
+    e.nn2 = (f32x2){0.f, 0.f};
+    e.mn = INFINITY;
+    e.m0[0] = e.m[0];
+    e.m0[1] = e.m[1];
+    e.lim[0] = (rok[0] ? min(32, nv) : 0) - 4 * g;
+    e.lim[1] = (rok[1] ? min(32, nv) : 0) - 4 * g;
+    return nv >= 32;
+  };
+  auto copy = [&]() {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) cB[t] = cA[t];
+  };
+
+  iter(T{}, F{}, T{}, 0, cA, cB);
+  copy();
+  for (int b = 1; b < nblocks; ++b) {
+    if (tile_full()) iter(T{}, T{}, T{}, b, cA, cB);
+    else iter(T{}, T{}, F{}, b, cA, cB);
+    copy();
+  }
+  if (tile_full()) iter(F{}, T{}, T{}, nblocks, cA, cB);
+  else iter(F{}, T{}, F{}, nblocks, cA, cB);
+
+  double v = wave_sum_d(accd);
+  double v2 = wave_sum_d(accd2);
+  __syncthreads();
+  if (lane == 0) { red[wave] = v; red[WAVES + wave] = v2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0, t2 = 0.0;
+    for (int w = 0; w < WAVES; ++w) { t += red[w]; t2 += red[WAVES + w]; }
+    a.part[by * gx + bx] = t * (double)su * (double)su;
+    if (a.part2) a.part2[by * gx + bx] = t2 * (double)temp;
+  }
+}
+
+template <bool TRAIN>
+__device__ __forceinline__ void fwd_any(const FwdArgs& a, bf16* kbuf, const int bx, const int by, const int gx) {
+  if constexpr (TRIAD_FWD_M16) fwd_body16<TRAIN>(a, kbuf, bx, by, gx);
+  else fwd_body<TRAIN>(a, kbuf, bx, by, gx);
+}
+
 template <bool TRAIN, bool SHORTQ>
 __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 kbuf[KBUF_ELEMS];
-  fwd_body<TRAIN>(a, kbuf, blockIdx.x, blockIdx.y, gridDim.x);
+  fwd_any<TRAIN>(a, kbuf, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // Several heads' forwards in ONE launch (the tri-modal step's AV and TV heads, model.py:470-472 /
@@ -438,7 +727,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd_multi_kernel(MultiA
   const int q = (m.n > 1 && b >= m.first[1]) ? 1 : 0;  // uniform
   const int local = b - m.first[q];
   const int gx = m.gx[q];
-  fwd_body<TRAIN>(m.p[q], kbuf, local % gx, local / gx, gx);
+  fwd_any<TRAIN>(m.p[q], kbuf, local % gx, local / gx, gx);
 }
 
 // Diagonal blocks of S for the regularisers (model.py:417-418 / 524-525):

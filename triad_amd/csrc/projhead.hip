@@ -259,7 +259,11 @@ int triad_ln_bwd3(const void* dln, const void* y1, const float* mean, const floa
 int triad_sum_slabs(const float* slabs, int nslab, long long n, const float* alpha, int out_bf16, void* out,
                     hipStream_t stream) {
   if (nslab <= 0 || n <= 0) return TRIAD_EINVAL;
-  if (nslab >= 16 && n <= (1 << 20)) {  // many slabs of a short vector: 16 slab lanes per element
+  // many slabs of a short vector (bias / LayerNorm column partials: <= 3 x 512 columns over up to
+  // 1,024 slabs): 16 slab lanes per element. Long vectors (the split-K weight-gradient slabs,
+  // 262,144-393,216 elements x 32 slabs) stream with one element per thread instead: the 64-column
+  // blocks of colsum_reduce read them at ~2 TB/s (41 us for a visual head's two dW, r04 profile)
+  if (nslab >= 16 && n <= 16384) {
     hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, stream, slabs, nslab, n,
                        alpha, 1.f, out_bf16, out);
     TRIAD_CHECK_LAUNCH();
