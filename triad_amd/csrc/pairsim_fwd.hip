@@ -412,7 +412,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   }
 }
 
-// ---- the same workgroup on v_mfma_f32_16x16x32_bf16 (TRIAD_FWD_M16 build) -------------------
+// ---- the same workgroup on v_mfma_f32_16x16x32_bf16 (the eval form's body, fwd_any) ----------
 // Per wave and key tile: 32 keys x 32 queries as 2 x 2 tiles of 16 x 16 (key half kb2, query half
 // qb), sixteen 32-deep k-steps of 4 MFMAs, one epilogue element of the previous tile per k-step.
 // Lane l (i = l & 15, g = l >> 4) holds queries 16 qb + i and keys 16 kb2 + 4 g + (0..3): two running
@@ -420,9 +420,6 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
 // end. The unit dS keeps the 32 x 32 tile layout the backward reads (element (q, k) at
 // (q + 32 ((k >> 2) & 1)) * 16 + (k & 3) + 4 (k >> 3)): per query half and key half a lane's four
 // keys are one 8-byte piece of a 16-element run whose other pieces lane l ^ 32 holds.
-#ifndef TRIAD_FWD_M16
-#define TRIAD_FWD_M16 0
-#endif
 constexpr int NS16 = D / 32;  // 16 k-steps
 constexpr int LDSPF16 = 2;
 
@@ -695,10 +692,15 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
   }
 }
 
+// Which body: measured on one box, alternated (profiles/r04_fwd_m16_ab.log, c3 shapes): the eval
+// form (no dS stream) runs 4.7 % faster on 16 x 16 x 32 MFMAs (AV 2.47 -> 2.36 ms); the training
+// form does not gain (AV 3.07 -> 3.06 ms with 8-byte dS stores, 3.10 with the runs assembled to
+// 16-byte stores by a lane swap) -- its time is the dS stream and the epilogue, not the MFMA clock.
+// Both bodies pass the same head tests (tests/test_head_gpu.py, 67 / 67 with either).
 template <bool TRAIN>
 __device__ __forceinline__ void fwd_any(const FwdArgs& a, bf16* kbuf, const int bx, const int by, const int gx) {
-  if constexpr (TRIAD_FWD_M16) fwd_body16<TRAIN>(a, kbuf, bx, by, gx);
-  else fwd_body<TRAIN>(a, kbuf, bx, by, gx);
+  if constexpr (TRAIN) fwd_body<true>(a, kbuf, bx, by, gx);
+  else fwd_body16<false>(a, kbuf, bx, by, gx);
 }
 
 template <bool TRAIN, bool SHORTQ>
