@@ -320,3 +320,21 @@ extern "C" int hz_victim2(int kind, const void* in, float* staging, int* sem, fl
   }
   return (int)hipGetLastError();
 }
+
+// Fourth probe: where does a workgroup run? (CU-masked streams, tools/cu_mask_probe.py) -- the XCC
+// id and the HW_ID register (CU / SH / SE fields) of each workgroup, read by s_getreg (a register
+// read; nothing is written through the scalar cache).
+extern "C" __global__ __launch_bounds__(64) void where_kernel(unsigned* out) {
+  unsigned xcc, hw;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = xcc;
+    out[2 * blockIdx.x + 1] = hw;
+  }
+}
+
+extern "C" int hz_where(unsigned* out, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(where_kernel, dim3(blocks), dim3(64), 0, s, out);
+  return (int)hipGetLastError();
+}
