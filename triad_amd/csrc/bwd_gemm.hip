@@ -583,6 +583,12 @@ int triad_bfrag_pack16(const void* B, int nkt, int dk, void* Bp, hipStream_t str
   return TRIAD_OK;
 }
 
+#ifndef TRIAD_DK16_KS
+#define TRIAD_DK16_KS 1
+#endif
+#ifndef TRIAD_DK16_DD
+#define TRIAD_DK16_DD 3
+#endif
 int triad_tile_gemm_packed16(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, const float* alpha,
                              int splits, float* slabs, void* C, hipStream_t stream) {
   if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
@@ -592,10 +598,11 @@ int triad_tile_gemm_packed16(const void* Dt, long long CT, int dk, const void* B
   const bf16* b = (const bf16*)Bp;
   void* out = splits > 1 ? (void*)slabs : C;
   const float* al = splits > 1 ? nullptr : alpha;
-  // one k tile per stage, 3 ahead (dK with two tiles per stage, as its 32x32x16 form, would spill)
+  // one k tile per stage, 3 ahead (dK with two tiles per stage two ahead, as its 32x32x16 form,
+  // would spill); TRIAD_DK16_KS / _DD: stage shape of dK for A/B builds (tools/build_variants.py)
   if (dk) {
-    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db16_kernel<true, false, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
-    else hipLaunchKernelGGL((tile_gemm_db16_kernel<true, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
+    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db16_kernel<true, false, TRIAD_DK16_KS, TRIAD_DK16_DD>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
+    else hipLaunchKernelGGL((tile_gemm_db16_kernel<true, true, TRIAD_DK16_KS, TRIAD_DK16_DD>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
   } else {
     if (splits == 1) hipLaunchKernelGGL((tile_gemm_db16_kernel<false, false, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
     else hipLaunchKernelGGL((tile_gemm_db16_kernel<false, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
@@ -613,7 +620,7 @@ int triad_tile_gemm_packed16_slabs(const void* Dt, long long CT, int dk, const v
   dim3 grid(M / TBM, splits);
   const bf16* d = (const bf16*)Dt;
   const bf16* b = (const bf16*)Bp;
-  if (dk) hipLaunchKernelGGL((tile_gemm_db16_kernel<true, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  if (dk) hipLaunchKernelGGL((tile_gemm_db16_kernel<true, true, TRIAD_DK16_KS, TRIAD_DK16_DD>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
   else hipLaunchKernelGGL((tile_gemm_db16_kernel<false, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
