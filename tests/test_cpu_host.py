@@ -171,6 +171,42 @@ def test_packed_tile_gemm_and_patch_reject_bad_arguments():
     assert lib.triad_losshead(fake, 50000, 0, fake, fake, 1, 1.0, fake, 1, 1.0, 0.0, fake, fake, fake, None) == 1001
 
 
+def test_round4_entry_points_reject_bad_arguments():
+    """The 16 x 16 x 32 tile GEMM forms and the split-K XCD placement flag validate before any
+    launch (no GPU needed) -> TRIAD_EINVAL (1001)."""
+    from triad_amd import _lib, build
+    if not os.path.exists(_lib.LIB_PATH):
+        build.build()
+    lib = _lib.load()
+    fake = 4096
+    assert lib.triad_bfrag_pack16(fake, 0, 1, fake, None) == 1001                   # no k tiles
+    assert lib.triad_tile_gemm_packed16(fake, 8, 0, fake, 200, 8, fake, 1, None, fake, None) == 1001  # M % 128
+    assert lib.triad_tile_gemm_packed16(fake, 8, 1, fake, 256, 8, fake, 2, None, fake, None) == 1001  # no slabs
+    assert lib.triad_tile_gemm_packed16_slabs(fake, 8, 0, fake, 256, 8, 1, None, None) == 1001       # no slabs
+    # split-K with the XCD placement flag (form | 8) needs splits % 8 == 0; forms beyond 4 refused
+    assert lib.triad_gemm_bf16_splitk_form(fake, 512, 0, fake, 768, 0, 512, 768, 65536, 12, None, fake, fake, 0,
+                                           1 | 8, None) == 1001
+    assert lib.triad_gemm_bf16_splitk_form(fake, 512, 0, fake, 768, 0, 512, 768, 65536, 16, None, fake, fake, 0,
+                                           5, None) == 1001
+
+
+def test_weight_gradient_plans():
+    """Split-K plans of the projection-head (ops._dw_plan) and backbone (linear._form_splits)
+    weight gradients: long token lists on the XCD-per-split placement with a split count that is a
+    multiple of 8; the 8,192-row text head and the 3072-wide backbone shapes keep the default."""
+    from triad_amd import linear, ops
+    for Mp in (65536, 50944, 43904):
+        f2, s2 = ops._dw_plan(Mp, 512)
+        f1, s1 = ops._dw_plan(Mp, 768)
+        assert (f2, s2) == (1 | 8, 32) and (f1, s1) == (4 | 8, 32)
+    assert ops._dw_plan(8192, 512) == (0, 16) and ops._dw_plan(8192, 768)[0] == 0
+    for O, K, xcd in ((768, 768, True), (2304, 768, True), (3072, 768, False), (768, 3072, False)):
+        form, sp = linear._form_splits(50944, O, K)
+        assert form & 7 == 4 and bool(form & 8) == xcd
+        assert not xcd or sp % 8 == 0
+    assert linear._form_splits(8192, 768, 768)[0] == 0
+
+
 def test_select_subset_indices_draws_writes_and_rereads(tmp_path):
     """retrieval.select_subset_indices (retrieval.py:9-30): python `random.shuffle` of
     range(len(dataset)), the first `subset_size`, written as JSON; an existing file is read back
