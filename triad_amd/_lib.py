@@ -162,10 +162,26 @@ TIMERS = None
 WATCH = None
 
 
+def _isolate(name):
+    """Diagnostics (tools/stream_repeat.py --configs): TRIAD_ISOLATE = comma-separated name
+    prefixes of entry points to run ALONE on the device -- a device-wide synchronisation before
+    and after the launch, so no kernel of another stream shares its CUs. Unset in
+    every product run."""
+    spec = os.environ.get("TRIAD_ISOLATE")
+    return bool(spec) and name not in RESTYPES and any(name.startswith(p) for p in spec.split(",") if p)
+
+
 def call(name, *args, meta=None):
     """Invoke an entry point; non-zero status -> TriadError (RuntimeError).
     meta: per-launch metadata (e.g. algorithmic FLOPs) recorded with the timing when enabled."""
-    if TIMERS is not None and name in TIMERS:
+    if _isolate(name):
+        import torch
+        torch.cuda.synchronize()
+        try:
+            rc = getattr(load(), name)(*args)
+        finally:
+            torch.cuda.synchronize()
+    elif TIMERS is not None and name in TIMERS:
         import torch
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
