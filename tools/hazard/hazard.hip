@@ -338,3 +338,45 @@ extern "C" int hz_where(unsigned* out, int blocks, hipStream_t s) {
   hipLaunchKernelGGL(where_kernel, dim3(blocks), dim3(64), 0, s, out);
   return (int)hipGetLastError();
 }
+
+// Fifth probe: the library's own column sum (colsum8: four 16-byte loads in flight per thread) is
+// disturbed in the tri-modal step and clean when run alone (tools/stream_repeat.py, TRIAD_ISOLATE).
+// Copy victims that only load and store: out = in, 16-byte loads, DEPTH loads in flight per thread
+// (kind 13: 1, kind 14: 4, kind 15: 4 with sc1 loads that bypass the CU's L1).
+template <int DEPTH, bool SC1>
+__global__ __launch_bounds__(256) void copy_victim(const uint4* __restrict__ in, uint4* __restrict__ out, long long n,
+                                                   int rows_per_block) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long base = (long long)blockIdx.x * 256 + threadIdx.x; base < n; base += stride * DEPTH) {
+    uint4 v[DEPTH];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const long long e = base + d * stride;
+      if (e < n) {
+        if (SC1) {
+          v[d].x = __hip_atomic_load(&in[e].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v[d].y = __hip_atomic_load(&in[e].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v[d].z = __hip_atomic_load(&in[e].z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v[d].w = __hip_atomic_load(&in[e].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          v[d] = in[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const long long e = base + d * stride;
+      if (e < n) out[e] = v[d];
+    }
+  }
+}
+
+extern "C" int hz_copy(int kind, const void* in, void* out, long long n16, int blocks, hipStream_t s) {
+  switch (kind) {
+    case 13: hipLaunchKernelGGL((copy_victim<1, false>), dim3(blocks), dim3(256), 0, s, (const uint4*)in, (uint4*)out, n16, 0); break;
+    case 14: hipLaunchKernelGGL((copy_victim<4, false>), dim3(blocks), dim3(256), 0, s, (const uint4*)in, (uint4*)out, n16, 0); break;
+    case 15: hipLaunchKernelGGL((copy_victim<4, true>), dim3(blocks), dim3(256), 0, s, (const uint4*)in, (uint4*)out, n16, 0); break;
+    default: return 1;
+  }
+  return (int)hipGetLastError();
+}

@@ -35,6 +35,7 @@ def lib():
     h.hz_victim.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
     h.hz_victim2.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                              C.c_void_p]
+    h.hz_copy.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_longlong, C.c_int, C.c_void_p]
     return h
 
 
@@ -114,7 +115,21 @@ def main():
             return out
         return run
 
+    cp_in = torch.randint(-2**31, 2**31 - 1, (768 * 2304 // 2,), dtype=torch.int32, device=dev, generator=g)
+
+    def vcopy(kind):
+        def run():   # out = in, 16-byte loads (1 or 4 in flight per thread, or sc1): any differing word is a bad load
+            out = torch.empty_like(cp_in)
+            rc = h.hz_copy(kind, C.c_void_p(cp_in.data_ptr()), C.c_void_p(out.data_ptr()), cp_in.numel() // 4, 256,
+                           C.c_void_p(torch.cuda.current_stream().cuda_stream))
+            assert rc == 0, rc
+            return out
+        return run
+
     victims = {
+        "copy16 depth1 (one 16-byte load per thread in flight)": vcopy(13),
+        "copy16 depth4 (four 16-byte loads in flight, as colsum8)": vcopy(14),
+        "copy16 depth4 sc1 (the same, loads bypass L1)": vcopy(15),
         "lds_colsum (8 row-threads per column combined through LDS, one launch, no cross-WG hand-off)": vic2(6),
         "xblk_colsum plain (cross-WG hand-off: threadfence + atomic semaphore, last WG plain loads)": vic2(7),
         "xblk_colsum acquire (the same + agent-scope acquire fence after the semaphore)": vic2(8),
