@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--configs", default="", help="A/B within one process: 'name:VAR=val,VAR2=val;name2:...' -- "
                     "the multi-stream reps alternate over these environments (each counted on its own)")
     ap.add_argument("--tokens", type=int, default=6, help="caption words (6: the stream test; 32: the bench)")
+    ap.add_argument("--ref-per-config", action="store_true", help="each config against its own single-stream "
+                    "reference (for configs that change the arithmetic)")
     a = ap.parse_args()
     if a.math_sdpa:
         torch.backends.cuda.enable_flash_sdp(False)
@@ -77,19 +79,27 @@ def main():
             name, _, kv = item.partition(":")
             configs.append((name, dict(x.split("=", 1) for x in kv.split(",") if x)))
     per = {n: [0, 0] for n, _ in configs}
-    bad = 0
-    for r in range(a.reps):
-        cname, env = configs[r % len(configs)]
+    refs = {}
+
+    def under(env, streams):
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:
-            l, gm, _ = run(True, frames, audio, text)
+            return run(streams, frames, audio, text)
         finally:
             for k, v in saved.items():
                 if v is None:
                     os.environ.pop(k, None)
                 else:
                     os.environ[k] = v
+    bad = 0
+    for r in range(a.reps):
+        cname, env = configs[r % len(configs)]
+        if a.ref_per_config:
+            if cname not in refs:   # this config's own single-stream reference (its arithmetic may differ)
+                refs[cname] = under(env, False)[:2]
+            l_ref, g_ref = refs[cname]
+        l, gm, _ = under(env, True)
         diff = []
         for name, off, n in layout:
             x, y = gm[off:off + n], g_ref[off:off + n]

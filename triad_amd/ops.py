@@ -12,6 +12,8 @@ import math
 from dataclasses import dataclass
 from typing import Optional
 
+import os
+
 import torch
 
 from . import _lib
@@ -104,6 +106,29 @@ def _m16(dk):
     r04_bwd_micro_mfma16_dk.log; MI355X_MICROARCH.md, DVFS item 7). TRIAD_DQ_MFMA16 / TRIAD_DK_MFMA16
     = 0 select the 32x32x16 direct-B form (A/B only)."""
     return MFMA16_DQ if dk == 0 else MFMA16_DK
+
+
+_ONES = {}
+
+
+def bias_grad(x, out_dtype=torch.float32):
+    """Column sums of a bf16 [rows][cols] matrix for the BACKBONE bias gradients. TRIAD_DB_GEMM=1
+    (experiment): on the split-K MFMA GEMM as x^T . ones (column 0 of a
+    [cols][128] product) instead of triad_colsum -- the co-residency experiments found the column
+    sum disturbed beside the concurrent backbones and the LDS-DMA GEMMs not."""
+    rows, cols = x.shape
+    if os.environ.get("TRIAD_DB_GEMM", "0") == "0" or cols % 128 or rows % 64 or x.stride(1) != 1:
+        return colsum(x, out_dtype, backbone=True)
+    dev = x.device
+    ones = _ONES.get(dev.index)
+    if ones is None or ones.shape[0] < rows:
+        ones = _ONES[dev.index] = torch.ones(max(rows, 65536), 128, dtype=torch.bfloat16, device=dev)
+    sp = max(1, min(16, rows // 2048))
+    slabs = torch.empty(sp * cols * 128, dtype=torch.float32, device=dev)
+    c = torch.empty(cols, 128, dtype=torch.float32, device=dev)
+    call("triad_gemm_bf16_splitk_form", ptr(x), x.stride(0), 0, ptr(ones), 128, 0, cols, 128, rows, sp, None,
+         ptr(slabs), ptr(c), 0, 1, stream_ptr(dev), meta=dict(backbone=True))
+    return c[:, 0].to(out_dtype)
 
 
 def pack_b(B, nkt, dk, stream):
