@@ -459,8 +459,8 @@ class _PosConv(torch.autograd.Function):
                                                      False, [0, 0], G, [False, True, False])[1]
             dw = dw.squeeze(2).to(ctx.dtypes[1])
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            from .ops import colsum
-            db = colsum(dyb.view(B * T, C), torch.float32, backbone=True).to(ctx.dtypes[2])
+            from .ops import bias_grad
+            db = bias_grad(dyb.view(B * T, C), torch.float32).to(ctx.dtypes[2])
         return dx, dw, db, None, None
 
 
@@ -516,6 +516,34 @@ def _hubert_pos_conv_forward(self, hidden_states):
     return _hip_act(self.activation)(y)
 
 
+class _SpecMask(torch.autograd.Function):
+    """torch.where(mask[..., None], emb, h) with emb's gradient (the sum of h's gradient over the
+    masked frames) taken by ops.bias_grad instead of PyTorch's bf16 reduction (TRIAD_DB_GEMM=1
+    experiment)."""
+
+    @staticmethod
+    def forward(ctx, h, m, emb):
+        ctx.save_for_backward(m)
+        ctx.emb_dtype = emb.dtype
+        return torch.where(m[..., None], emb.to(h.dtype), h)
+
+    @staticmethod
+    def backward(ctx, g):
+        (m,) = ctx.saved_tensors
+        from .ops import bias_grad
+        mm = m[..., None]
+        gm = torch.where(mm, g, torch.zeros((), dtype=g.dtype, device=g.device))
+        demb = bias_grad(gm.reshape(-1, g.shape[-1]).to(torch.bfloat16).contiguous(), torch.float32)
+        return torch.where(mm, torch.zeros((), dtype=g.dtype, device=g.device), g), None, demb.to(ctx.emb_dtype)
+
+
+def _spec_where(m, emb, h):
+    import os
+    if os.environ.get("TRIAD_DB_GEMM", "0") != "0" and h.dtype == torch.bfloat16 and emb.requires_grad:
+        return _SpecMask.apply(h, m, emb)
+    return torch.where(m[..., None], emb.to(h.dtype), h)
+
+
 def _hubert_mask_hidden_states(self, hidden_states, mask_time_indices=None, attention_mask=None):
     """transformers HubertModel._mask_hidden_states (SpecAugment in training) without host syncs:
     the numpy-drawn masks go up through pinned memory and are applied with torch.where instead of
@@ -529,14 +557,13 @@ def _hubert_mask_hidden_states(self, hidden_states, mask_time_indices=None, atte
     B, T, C = hidden_states.shape
     dev = hidden_states.device
     if mask_time_indices is not None:
-        emb = self.masked_spec_embed.to(hidden_states.dtype)
-        hidden_states = torch.where(mask_time_indices[..., None].to(dev), emb, hidden_states)
+        hidden_states = _spec_where(mask_time_indices.to(dev), self.masked_spec_embed, hidden_states)
     elif cfg.mask_time_prob > 0 and self.training:
-        emb = self.masked_spec_embed.to(hidden_states.dtype)  # exists only when masking is configured
+        # masked_spec_embed exists only when masking is configured
         m = _compute_mask_indices((B, T), mask_prob=cfg.mask_time_prob, mask_length=cfg.mask_time_length,
                                   attention_mask=attention_mask, min_masks=cfg.mask_time_min_masks)
         m = _lib.h2d(torch.from_numpy(m).to(torch.bool), dev)
-        hidden_states = torch.where(m[..., None], emb, hidden_states)
+        hidden_states = _spec_where(m, self.masked_spec_embed, hidden_states)
     if cfg.mask_feature_prob > 0 and self.training:
         mf = _compute_mask_indices((B, C), mask_prob=cfg.mask_feature_prob, mask_length=cfg.mask_feature_length,
                                    min_masks=cfg.mask_feature_min_masks)

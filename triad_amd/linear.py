@@ -180,8 +180,8 @@ class _LinearFn(torch.autograd.Function):
             else:
                 dw = weight_grad(dy2, x2).to(w_dtype)
         if b_dtype is not None and ctx.needs_input_grad[2]:
-            from .ops import colsum
-            db = colsum(dy2, torch.bfloat16 if b_dtype == torch.bfloat16 else torch.float32, backbone=True).to(b_dtype)
+            from .ops import bias_grad
+            db = bias_grad(dy2, torch.bfloat16 if b_dtype == torch.bfloat16 else torch.float32).to(b_dtype)
         return dx, dw, db
 
 
@@ -222,8 +222,8 @@ class _QKVFn(torch.autograd.Function):
                 dws = [t.to(w_dtype) for t in weight_grad(dy2, x2).split(sizes)]
         dbs = [None] * 3
         if b_dtype is not None and any(ctx.needs_input_grad[i] for i in (2, 4, 6)):
-            from .ops import colsum
-            db = colsum(dy2, torch.bfloat16 if b_dtype == torch.bfloat16 else torch.float32, backbone=True).to(b_dtype)
+            from .ops import bias_grad
+            db = bias_grad(dy2, torch.bfloat16 if b_dtype == torch.bfloat16 else torch.float32).to(b_dtype)
             dbs = list(db.split(sizes))
         return dx, dws[0], dbs[0], dws[1], dbs[1], dws[2], dbs[2]
 

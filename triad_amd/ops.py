@@ -108,6 +108,29 @@ def _m16(dk):
     return MFMA16_DQ if dk == 0 else MFMA16_DK
 
 
+_ONES = {}
+
+
+def bias_grad(x, out_dtype=torch.float32):
+    """Column sums of a bf16 [rows][cols] matrix for the BACKBONE bias gradients. TRIAD_DB_GEMM=1
+    (experiment): on the split-K MFMA GEMM as x^T . ones (column 0 of a
+    [cols][128] product) instead of triad_colsum -- the co-residency experiments found the column
+    sum disturbed beside the concurrent backbones and the LDS-DMA GEMMs not."""
+    rows, cols = x.shape
+    if os.environ.get("TRIAD_DB_GEMM", "0") == "0" or cols % 128 or rows % 64 or x.stride(1) != 1:
+        return colsum(x, out_dtype, backbone=True)
+    dev = x.device
+    ones = _ONES.get(dev.index)
+    if ones is None or ones.shape[0] < rows:
+        ones = _ONES[dev.index] = torch.ones(max(rows, 65536), 128, dtype=torch.bfloat16, device=dev)
+    sp = max(1, min(16, rows // 2048))
+    slabs = torch.empty(sp * cols * 128, dtype=torch.float32, device=dev)
+    c = torch.empty(cols, 128, dtype=torch.float32, device=dev)
+    call("triad_gemm_bf16_splitk_form", ptr(x), x.stride(0), 0, ptr(ones), 128, 0, cols, 128, rows, sp, None,
+         ptr(slabs), ptr(c), 0, 1, stream_ptr(dev), meta=dict(backbone=True))
+    return c[:, 0].to(out_dtype)
+
+
 def pack_b(B, nkt, dk, stream):
     """B [nkt*32][512] bf16 -> its MFMA fragments in the direct-B GEMM's order (triad_bfrag_pack /
     triad_bfrag_pack16, the form _m16 picks): one pass over B, after which each wave of the GEMM
@@ -141,8 +164,8 @@ def tile_gemm_slabs(dS, CT, dk, Bp, M, nkt, splits, slabs, stream, meta=None):
          ptr(Bp), M, nkt, splits, ptr(slabs), stream, meta=meta)
 
 
-MFMA16_DQ = os.environ.get("TRIAD_DQ_MFMA16", "1") != "0"
-MFMA16_DK = os.environ.get("TRIAD_DK_MFMA16", "1") != "0"
+MFMA16_DQ = __import__("os").environ.get("TRIAD_DQ_MFMA16", "1") != "0"
+MFMA16_DK = __import__("os").environ.get("TRIAD_DK_MFMA16", "1") != "0"
 
 
 def _gemm_splits(wgs, nkt, M, cus=256, max_splits=8, t_tile=1.0e-6, hbm=5.0e12):
