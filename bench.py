@@ -268,9 +268,8 @@ def main():
         single = {"value": world * a.batch * a.single_stream_steps / dtss, "unit": "triples/s",
                   "steps": a.single_stream_steps, "ms_per_step": dtss / a.single_stream_steps * 1e3,
                   "concurrent_streams": not headline_concurrent,
-                  "note": ("concurrent opt-in (backbones on three streams + dW side stream): NOT bit-reproducible "
-                           "(DESIGN.md 2b), reported for reference only" if not headline_concurrent else
-                           "serial step (one stream)")}
+                  "note": ("concurrent streams (backbones on three streams + dW side stream)" if not headline_concurrent
+                           else "serial step (one stream), bit-identical results")}
         if rank == 0:
             print(f"[bench] {a.single_stream_steps} steps with concurrent streams "
                   f"{'on' if single['concurrent_streams'] else 'off'}: {dtss:.2f} s", file=sys.stderr, flush=True)
@@ -336,8 +335,9 @@ def main():
             res["projection_heads"] = {"ms_per_step": p_ms, "algo_TFLOP_per_step": p_fl / 1e12,
                                        "achieved_TFLOPs": p_fl / p_ms / 1e9,
                                        "frac": p_fl / p_ms / 1e9 / PEAK_BF16_TFLOPS, "launches": len(pk)}
-        res["config"]["execution"] = ("concurrent streams (opt-in)" if model_streams() else
-                                      "serial: one stream (the bit-reproducible default, DESIGN.md 2b)")
+        res["config"]["execution"] = ("concurrent streams: audio / text backbones and the backbone dW on their own "
+                                      "streams (the default; bit-identical to the serial step, DESIGN.md 2b)"
+                                      if model_streams() else "serial: one stream")
         if single is not None:
             res["other_stream_mode"] = single
         if sep is not None:

@@ -441,64 +441,66 @@ def test_side_stream_weight_grads_weight_used_twice():
 
 
 @pytest.mark.late
-def test_serial_step_bit_reproducible():
-    """The shipped execution mode (serial: the three backbones and every weight gradient on the
-    caller's stream) is bit-reproducible: two TriadTrainer steps from identical
-    models / seeds (dropout, LayerDrop and SpecAugment ON) give BIT-IDENTICAL losses and reduced
-    gradient buffers. One attempt, no retry.
-
-    The concurrent opt-in (TRIAD_MODALITY_STREAMS=1 + the dW side stream) is not held to this: on
-    MI355X, PyTorch's bf16 sum-reduction kernel returns wrong partial sums in 20-90 % of launches
-    while a kernel mixing MFMA with LDS-DMA (every GEMM of this library) shares its CU, and the
-    concurrent step puts the text bias gradients / HuBERT's masked_spec_embed (such reductions)
-    beside those GEMMs -- the ~10-60 % residual of rounds 2-3 (tools/reduce_race.py,
-    tools/hazard_probe.py, profiles/r04_hazard_probe.log)."""
+def test_step_bit_identical_serial_and_concurrent():
+    """The shipped execution mode (concurrent: audio / text backbones on their own streams beside
+    the ViT, backbone weight gradients on a side stream) gives BIT-IDENTICAL losses and reduced
+    gradient buffers to the serial step, run after run: one serial TriadTrainer step and three
+    concurrent ones from identical models / seeds (dropout, LayerDrop and SpecAugment ON) must all
+    agree. One attempt, no retry. What makes it hold: every column
+    sum of the step runs on the MFMA GEMM (ops.bias_grad) -- column-sum reductions, ours and
+    PyTorch's, returned disturbed sums beside another stream's GEMMs (21-38 of 80 concurrent
+    steps differing with them, 0 of 490 without, tools/stream_repeat.py)."""
     from triad_amd import linear as L
-    from triad_amd.model import MultiModalModel, modality_streams_enabled
+    from triad_amd.model import MultiModalModel, modality_streams_enabled, set_concurrent_streams
     from triad_amd.train import TriadTrainer, split_param_groups
-    assert not modality_streams_enabled() and not L.SIDE_STREAM_DW   # the defaults
+    assert modality_streams_enabled() and L.SIDE_STREAM_DW   # the defaults
     B = 128
     g = torch.Generator().manual_seed(5)
     frames = torch.randn(B, 3, 224, 224, generator=g).to(dev)
     audio = (torch.randn(B, 16000, generator=g) * 0.1).to(dev)
     text = [f"caption number {i} of a scene" for i in range(B)]
 
-    def run():
-        torch.manual_seed(0)
-        m = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.8, patch_sparsity_weight=0.01,
-                            visual_dropout_prob=0.25, use_amp=True).to(dev)
-        m.train()
-        tr = TriadTrainer(m, total_updates=100, unfreeze_audio_step=0, unfreeze_text_step=0, unfreeze_vit_step=0,
-                          device=dev)
-        snap = []
-        inner = tr._allreduce_grads
+    def run(concurrent):
+        set_concurrent_streams(concurrent)
+        try:
+            torch.manual_seed(0)
+            m = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.8, patch_sparsity_weight=0.01,
+                                visual_dropout_prob=0.25, use_amp=True).to(dev)
+            m.train()
+            tr = TriadTrainer(m, total_updates=100, unfreeze_audio_step=0, unfreeze_text_step=0,
+                              unfreeze_vit_step=0, device=dev)
+            snap = []
+            inner = tr._allreduce_grads
 
-        def grab():   # the reduced gradient before clipping / AdamW / zero_grad
-            inner()
-            snap.append(tr.space.flat_g.clone())
-        tr._allreduce_grads = grab
-        torch.manual_seed(1)
-        np.random.seed(1)  # SpecAugment masks (transformers' _compute_mask_indices draws from numpy)
-        out = tr.step(frames, audio, text)
-        torch.cuda.synchronize()
+            def grab():   # the reduced gradient before clipping / AdamW / zero_grad
+                inner()
+                snap.append(tr.space.flat_g.clone())
+            tr._allreduce_grads = grab
+            torch.manual_seed(1)
+            np.random.seed(1)  # SpecAugment masks (transformers' _compute_mask_indices draws from numpy)
+            out = tr.step(frames, audio, text)
+            torch.cuda.synchronize()
+        finally:
+            set_concurrent_streams(True)
         names = {id(p): n for n, p in m.named_parameters()}
         groups = {id(p): k for k, ps in split_param_groups(m).items() for p in ps}
         layout = [(names[id(p)], groups[id(p)], tr.space.offsets[i], p.numel()) for i, p in enumerate(tr.space.params)]
         return {k: float(out[k]) for k in ("loss", "loss_av", "loss_tv")}, snap[0].cpu(), layout
 
-    l_a, g_a, layout = run()
-    l_b, g_b, _ = run()
-    if l_a == l_b and torch.equal(g_a, g_b):
-        return
-    rows = []
-    for name, grp, off, n in layout:
-        a, b = g_b[off:off + n].double(), g_a[off:off + n].double()
-        if not torch.equal(a, b):
-            d = (a - b).abs()
-            rows.append((float(d.norm() / b.norm().clamp(min=1e-300)), name, int((d > 0).sum()), n))
-    rows.sort(reverse=True)
-    raise AssertionError(f"serial step not reproducible: losses {l_b} vs {l_a}; {len(rows)} parameters differ, "
-                         f"worst (rel, name, elements differing, numel) {rows[:12]}")
+    l_s, g_s, layout = run(False)
+    for rep in range(3):
+        l_c, g_c, _ = run(True)
+        if l_c == l_s and torch.equal(g_c, g_s):
+            continue
+        rows = []
+        for name, grp, off, n in layout:
+            a, b = g_c[off:off + n].double(), g_s[off:off + n].double()
+            if not torch.equal(a, b):
+                d = (a - b).abs()
+                rows.append((float(d.norm() / b.norm().clamp(min=1e-300)), name, int((d > 0).sum()), n))
+        rows.sort(reverse=True)
+        raise AssertionError(f"concurrent step {rep} differs from the serial one: losses {l_c} vs {l_s}; {len(rows)} "
+                             f"parameters differ, worst (rel, name, elements differing, numel) {rows[:12]}")
 
 
 @pytest.mark.parametrize("M,O,K", [(8192, 768, 3072), (8192, 768, 768), (50944, 2304, 768)])
@@ -531,3 +533,19 @@ def test_linear_weight_grad_forms(M, O, K):
     dw = linear.weight_grad(dy, x)
     ref = dy.float().t() @ x.float()
     assert _rel(dw.float(), ref) < 4e-3
+
+
+@pytest.mark.parametrize("rows,cols", [(768, 768), (8192, 2304), (50944, 3072), (200, 768)])
+def test_bias_grad_on_gemm_matches_column_sum(rows, cols):
+    """ops.bias_grad (the step's column sums on the split-K MFMA GEMM, x^T . ones) against an fp32
+    torch column sum of the same bf16 matrix; shapes the GEMM does not tile (rows % 64) take
+    triad_colsum."""
+    from triad_amd import ops
+    g = torch.Generator(device=dev).manual_seed(rows + cols)
+    x = (torch.randn(rows, cols, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    ref = x.float().sum(0)
+    for dt in (torch.float32, torch.bfloat16):
+        got = ops.bias_grad(x, dt)
+        assert got.dtype == dt and got.shape == (cols,)
+        tol = 1e-5 if dt == torch.float32 else 8e-3
+        assert float((got.float() - ref).norm() / ref.norm()) < tol

@@ -518,8 +518,8 @@ def _hubert_pos_conv_forward(self, hidden_states):
 
 class _SpecMask(torch.autograd.Function):
     """torch.where(mask[..., None], emb, h) with emb's gradient (the sum of h's gradient over the
-    masked frames) taken by ops.bias_grad instead of PyTorch's bf16 reduction (TRIAD_DB_GEMM=1
-    experiment)."""
+    masked frames) taken by ops.bias_grad instead of PyTorch's bf16 reduction, which returned
+    disturbed sums beside the concurrent streams' GEMMs."""
 
     @staticmethod
     def forward(ctx, h, m, emb):
@@ -539,7 +539,7 @@ class _SpecMask(torch.autograd.Function):
 
 def _spec_where(m, emb, h):
     import os
-    if os.environ.get("TRIAD_DB_GEMM", "0") != "0" and h.dtype == torch.bfloat16 and emb.requires_grad:
+    if os.environ.get("TRIAD_DB_GEMM", "1") != "0" and h.dtype == torch.bfloat16 and emb.requires_grad:
         return _SpecMask.apply(h, m, emb)
     return torch.where(m[..., None], emb.to(h.dtype), h)
 

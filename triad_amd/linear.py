@@ -145,10 +145,9 @@ def on_side_stream(fn, inputs):
     return outs
 
 
-# Off by default (the serial step): on a second stream the dW GEMMs (MFMA + LDS-DMA)
-# share CUs with the main stream's PyTorch kernels, whose bf16 reductions then return wrong sums
-# in some launches. TRIAD_SIDE_STREAM_DW=1 (or model.set_concurrent_streams(True)) opts in.
-SIDE_STREAM_DW = os.environ.get("TRIAD_SIDE_STREAM_DW", "0") != "0"
+# On by default (with the modality streams; model.set_concurrent_streams / TRIAD_SIDE_STREAM_DW=0
+# turn it off): safe since every bias sum runs on the GEMM (ops.bias_grad).
+SIDE_STREAM_DW = os.environ.get("TRIAD_SIDE_STREAM_DW", "1") != "0"
 
 
 class _LinearFn(torch.autograd.Function):
@@ -258,7 +257,10 @@ def _eligible(mod: nn.Linear, x: torch.Tensor) -> bool:
     if not (x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
         return False
     M = x.numel() // max(1, x.shape[-1])
-    return M >= MIN_TOKENS and M % 64 == 0 and mod.in_features % 128 == 0 and mod.out_features % 128 == 0
+    # every size when the bias sums run on the GEMM (ops.bias_grad, the default): no bias gradient
+    # may fall back to PyTorch's reduction kernels beside another stream's GEMMs
+    low = 64 if os.environ.get("TRIAD_DB_GEMM", "1") != "0" else MIN_TOKENS
+    return M >= low and M % 64 == 0 and mod.in_features % 128 == 0 and mod.out_features % 128 == 0
 
 
 class TriadLinear(nn.Linear):

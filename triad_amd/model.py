@@ -526,20 +526,18 @@ class _Handoff(torch.autograd.Function):
 
 
 def modality_streams_enabled() -> bool:
-    """forward_triad's execution mode: all three backbones on the caller's stream (default,
-    TRIAD_MODALITY_STREAMS unset or 0) or audio / text on their own HIP streams beside the ViT
-    (TRIAD_MODALITY_STREAMS=1, opt-in). The concurrent mode is NOT bit-reproducible: while one of
-    the library's GEMMs (MFMA + LDS-DMA) shares a CU with PyTorch's bf16 sum-reduction kernel, that
-    kernel returns wrong partial sums in 20-90 % of launches (tools/hazard_probe.py),
-    and the concurrent backbones put exactly those kernels side by side (the bias gradients of
-    DistilBERT's stock linears, HuBERT's masked_spec_embed)."""
-    return os.environ.get("TRIAD_MODALITY_STREAMS", "0") != "0"
+    """forward_triad's execution mode: audio / text on their own HIP streams beside the ViT
+    (default, TRIAD_MODALITY_STREAMS unset or 1) or all three backbones on the caller's stream
+    (TRIAD_MODALITY_STREAMS=0). Both modes give bit-identical results
+    (test_ops_gpu.py::test_step_bit_identical_serial_and_concurrent): every column-sum reduction of
+    the step runs on the MFMA GEMM (ops.bias_grad) -- the reductions were what co-running streams
+    disturbed."""
+    return os.environ.get("TRIAD_MODALITY_STREAMS", "1") != "0"
 
 
 def set_concurrent_streams(on: bool):
-    """Switch the step between the serial default and the concurrent opt-in: the modality
-    streams of forward_triad AND the weight-gradient side stream (triad_amd.linear), which
-    otherwise puts the same GEMMs beside the main stream's PyTorch kernels."""
+    """Switch the step between the concurrent default and the serial mode: the modality streams
+    of forward_triad AND the weight-gradient side stream (triad_amd.linear)."""
     from . import linear
     os.environ["TRIAD_MODALITY_STREAMS"] = "1" if on else "0"
     linear.SIDE_STREAM_DW = bool(on)

@@ -111,14 +111,19 @@ def _m16(dk):
 _ONES = {}
 
 
-def bias_grad(x, out_dtype=torch.float32):
-    """Column sums of a bf16 [rows][cols] matrix for the BACKBONE bias gradients. TRIAD_DB_GEMM=1
-    (experiment): on the split-K MFMA GEMM as x^T . ones (column 0 of a
-    [cols][128] product) instead of triad_colsum -- the co-residency experiments found the column
-    sum disturbed beside the concurrent backbones and the LDS-DMA GEMMs not."""
+def bias_grad(x, out_dtype=torch.float32, meta=None):
+    """Column sums of a bf16 [rows][cols] matrix for the BACKBONE bias gradients (and SpecAugment's
+    masked_spec_embed), on the split-K MFMA GEMM as x^T . ones (column 0 of a [cols][128]
+    product, fp32 accumulation). Why not triad_colsum / PyTorch's sum: with the backbones on
+    concurrent streams, column-sum reductions beside the library's MFMA + LDS-DMA GEMMs returned
+    disturbed partial sums in some launches (16-column groups off by ~1 %), while the same sums on
+    the GEMM stayed bit-identical to the serial step in every one of 490 concurrent steps against
+    21-38 of 80 with the reductions (tools/stream_repeat.py, profiles/r04_stream_repeat_*.log,
+    DESIGN.md §2b). TRIAD_DB_GEMM=0: triad_colsum (A/B only). Shapes the GEMM does not tile
+    (cols % 128, rows % 64) fall back to triad_colsum. meta: launch tag (default: backbone work)."""
     rows, cols = x.shape
-    if os.environ.get("TRIAD_DB_GEMM", "0") == "0" or cols % 128 or rows % 64 or x.stride(1) != 1:
-        return colsum(x, out_dtype, backbone=True)
+    if os.environ.get("TRIAD_DB_GEMM", "1") == "0" or cols % 128 or rows % 64 or x.stride(1) != 1:
+        return colsum(x, out_dtype, backbone=meta is None)
     dev = x.device
     ones = _ONES.get(dev.index)
     if ones is None or ones.shape[0] < rows:
@@ -127,7 +132,7 @@ def bias_grad(x, out_dtype=torch.float32):
     slabs = torch.empty(sp * cols * 128, dtype=torch.float32, device=dev)
     c = torch.empty(cols, 128, dtype=torch.float32, device=dev)
     call("triad_gemm_bf16_splitk_form", ptr(x), x.stride(0), 0, ptr(ones), 128, 0, cols, 128, rows, sp, None,
-         ptr(slabs), ptr(c), 0, 1, stream_ptr(dev), meta=dict(backbone=True))
+         ptr(slabs), ptr(c), 0, 1, stream_ptr(dev), meta=meta if meta is not None else dict(backbone=True))
     return c[:, 0].to(out_dtype)
 
 
@@ -848,7 +853,9 @@ class _ProjectionHeadPasses(torch.autograd.Function):
         hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
         # bf16 model weights (the trainer's shadowed Linear parameters): the gradients come out in
         # bf16 straight from the reductions, as autocast's bf16 GEMM / bias gradients do
-        db2 = colsum(dyp, torch.bfloat16 if b2d == torch.bfloat16 else f32)
+        # (on the GEMM like every bias sum of the step: the audio / text heads' backward runs on the
+        # concurrent backbone streams)
+        db2 = bias_grad(dyp, torch.bfloat16 if b2d == torch.bfloat16 else f32, meta=dict(tag="proj-bias", flops=0.0))
         (f2, sp2), (f1, sp1) = _dw_plan(Mp, D), _dw_plan(Mp, H)
         slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
         o2, o1 = int(w2d == torch.bfloat16), int(w1d == torch.bfloat16)
