@@ -128,11 +128,16 @@ def bias_grad(x, out_dtype=torch.float32, meta=None):
     ones = _ONES.get(dev.index)
     if ones is None or ones.shape[0] < rows:
         ones = _ONES[dev.index] = torch.ones(max(rows, 65536), 128, dtype=torch.bfloat16, device=dev)
-    sp = max(1, min(16, rows // 2048))
+    # one round of >= 256 workgroups (cols / 128 output tiles x splits), splits a multiple of 8 with
+    # each split's workgroups on one XCD (gemm.hip tile_split), >= 512 rows per split
+    tiles = cols // 128
+    sp = min(-(-256 // tiles), rows // 512)
+    sp = (sp + 4) // 8 * 8 if sp >= 8 else max(1, sp)
+    form = 1 | (8 if sp % 8 == 0 else 0)
     slabs = torch.empty(sp * cols * 128, dtype=torch.float32, device=dev)
     c = torch.empty(cols, 128, dtype=torch.float32, device=dev)
     call("triad_gemm_bf16_splitk_form", ptr(x), x.stride(0), 0, ptr(ones), 128, 0, cols, 128, rows, sp, None,
-         ptr(slabs), ptr(c), 0, 1, stream_ptr(dev), meta=meta if meta is not None else dict(backbone=True))
+         ptr(slabs), ptr(c), 0, form, stream_ptr(dev), meta=meta if meta is not None else dict(backbone=True))
     return c[:, 0].to(out_dtype)
 
 
