@@ -235,6 +235,13 @@ int triad_colsum_splits(long long rows, int cols);
 int triad_colsum(const void* X, long long rows, int cols, long long ld, float* part, float alpha, int out_bf16,
                  void* out, hipStream_t stream);
 
+/* The same column sums with the rows staged by 16-byte LDS-DMA (cols % 256 == 0): the form the
+ * step's bias gradients use (beside concurrent streams' GEMMs, plain-load column sums returned
+ * disturbed values). part: triad_colsum_dma_splits(rows, cols) * cols floats. */
+int triad_colsum_dma_splits(long long rows, int cols);
+int triad_colsum_dma(const void* X, long long rows, int cols, long long ld, float* part, float alpha, int out_bf16,
+                     void* out, hipStream_t stream);
+
 /* out[e] = alpha * sum_i slabs[i][e] (alpha may be NULL = 1), fp32 or bf16 out. */
 int triad_sum_slabs(const float* slabs, int nslab, long long n, const float* alpha, int out_bf16, void* out,
                     hipStream_t stream);

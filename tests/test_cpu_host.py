@@ -188,6 +188,10 @@ def test_round4_entry_points_reject_bad_arguments():
                                            1 | 8, None) == 1001
     assert lib.triad_gemm_bf16_splitk_form(fake, 512, 0, fake, 768, 0, 512, 768, 65536, 16, None, fake, fake, 0,
                                            5, None) == 1001
+    # LDS-DMA column sums: 256-column tiles only, scratch required
+    assert lib.triad_colsum_dma(fake, 1024, 640, 640, fake, 1.0, 0, fake, None) == 1001
+    assert lib.triad_colsum_dma(fake, 1024, 768, 768, None, 1.0, 0, fake, None) == 1001
+    assert lib.triad_colsum_dma_splits(50944, 768) == 86 and lib.triad_colsum_dma_splits(256, 768) == 4
 
 
 def test_weight_gradient_plans():

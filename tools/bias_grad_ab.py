@@ -27,7 +27,13 @@ for rows, cols in ((50944, 768), (50944, 2304), (50944, 3072), (65536, 768), (65
                    (8192, 3072), (65536, 512)):
     x = (torch.randn(rows, cols, device="cuda") * 0.05).to(torch.bfloat16)
     for r in range(2):
-        os.environ["TRIAD_DB_GEMM"] = "1"
+        os.environ["TRIAD_DB_FORM"] = "gemm"
         a = bench(lambda: ops.bias_grad(x))
+        os.environ["TRIAD_DB_FORM"] = "dma"
+        d = bench(lambda: ops.bias_grad(x))
+        ref = x.float().sum(0)
+        err = float((ops.bias_grad(x).float() - ref).norm() / ref.norm())
+        os.environ["TRIAD_DB_FORM"] = "gemm"
         b = bench(lambda: ops.colsum(x, backbone=True))
-        print(json.dumps(dict(rows=rows, cols=cols, round=r, gemm_ms=round(a, 4), colsum_ms=round(b, 4))), flush=True)
+        print(json.dumps(dict(rows=rows, cols=cols, round=r, gemm_ms=round(a, 4), dma_ms=round(d, 4),
+                              colsum_ms=round(b, 4), dma_rel_err=err)), flush=True)

@@ -53,6 +53,8 @@ SIGNATURES = {
     "triad_sum_slabs": [vp, i32, i64, vp, i32, vp, vp],
     "triad_colsum_splits": [i64, i32],
     "triad_colsum": [vp, i64, i32, i64, vp, f32, i32, vp, vp],
+    "triad_colsum_dma_splits": [i64, i32],
+    "triad_colsum_dma": [vp, i64, i32, i64, vp, f32, i32, vp, vp],
     "triad_global_znorm": [vp, i64, f32, vp, vp, i32, vp],
     "triad_grad_sumsq": [vp, vp, i32, vp, vp],
     "triad_adamw_step": [vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, vp, vp],
@@ -103,7 +105,7 @@ RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_l
             "triad_conv0_dw_workspace_bytes": C.c_longlong, "triad_gelu_table_bytes": C.c_longlong,
             "triad_posconv_dw_part_bytes": C.c_longlong,
             "triad_lora_tn_blocks": C.c_int, "triad_dropaddln_bwd_blocks": C.c_int,
-            "triad_colsum_splits": C.c_int, "triad_dense_nparts": C.c_int,
+            "triad_colsum_splits": C.c_int, "triad_colsum_dma_splits": C.c_int, "triad_dense_nparts": C.c_int,
             "triad_projhead_bwd_slabs": C.c_int}
 
 

@@ -224,6 +224,85 @@ __global__ __launch_bounds__(256) void sum_slabs_kernel(const float* __restrict_
   }
 }
 
+// ---- column sums through LDS-DMA (the step's bias gradients) -----------------
+// Rows stream into LDS by 16-byte LDS-DMA (global_load_lds, as the GEMMs load their operands),
+// double-buffered chunks of 16 rows x 512 bytes of one column tile; the sums are VALU over LDS.
+// Pass 1: bf16 X, 256-column tiles x row splits -> fp32 partials [splits][cols]; pass 2: the
+// partials (fp32, 128-column tiles, one split) -> out. A thread owns 4 bytes of a row (two bf16
+// columns / one fp32 column) and every other row of a chunk; the two row halves meet in LDS.
+constexpr int CD_ROWS = 16;    // rows per chunk (16 x 512 B = 8 KB = 8 one-KB LDS-DMA pieces)
+
+template <bool F32>
+__global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict__ Xv, long long rows, long long ld,
+                                                         long long per, float alpha, int out_mode,
+                                                         void* __restrict__ out, long long out_ld) {
+  __shared__ __attribute__((aligned(16))) char buf[2][CD_ROWS * 512];
+  __shared__ float fin[2][128][2];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  constexpr int TILE = F32 ? 128 : 256;                 // columns per 512-byte row slice
+  const long long c0 = (long long)blockIdx.x * TILE;
+  const long long r0 = (long long)blockIdx.y * per, r1 = r0 + per < rows ? r0 + per : rows;
+  const char* X = (const char*)Xv;
+  const int esz = F32 ? 4 : 2;
+  const int nchunk = r1 > r0 ? (int)((r1 - r0 + CD_ROWS - 1) / CD_ROWS) : 0;
+  // wave w issues pieces 2w, 2w + 1 of a chunk: piece p = rows 2p, 2p + 1, lane L -> row 2p + (L >> 5),
+  // 16 bytes at column offset (L & 31) * 16 B; rows past the range re-read the last row (not summed)
+  auto issue = [&](int c, int slot) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = 2 * wave + u;
+      long long r = r0 + (long long)c * CD_ROWS + 2 * p + (lane >> 5);
+      r = r < r1 ? r : r1 - 1;
+      glds16(X + (r * ld + c0) * esz + (lane & 31) * 16, buf[slot] + p * 1024);
+    }
+  };
+  const int cp = t & 127, rh = t >> 7;                  // 4-byte column slot, row parity
+  float a0 = 0.f, a1 = 0.f;
+  if (nchunk > 0) issue(0, 0);
+  for (int c = 0; c < nchunk; ++c) {
+    if (c + 1 < nchunk) {
+      issue(c + 1, (c + 1) & 1);
+      TRIAD_VMCNT(2);                                   // this chunk's 2 pieces done, the next 2 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const char* b = buf[c & 1];
+    const int nr = (int)((r1 - r0 - (long long)c * CD_ROWS) < CD_ROWS ? (r1 - r0 - (long long)c * CD_ROWS) : CD_ROWS);
+#pragma unroll
+    for (int k = 0; k < CD_ROWS / 2; ++k) {
+      const int rr = 2 * k + rh;
+      if (rr < nr) {
+        const unsigned v = *(const unsigned*)(b + rr * 512 + cp * 4);
+        if (F32) {
+          a0 += __builtin_bit_cast(float, v);
+        } else {
+          a0 += __builtin_bit_cast(float, v << 16);
+          a1 += __builtin_bit_cast(float, v & 0xffff0000u);
+        }
+      }
+    }
+    __syncthreads();                                    // slot c & 1 is refilled by chunk c + 2's DMA
+  }
+  fin[rh][cp][0] = a0;
+  fin[rh][cp][1] = a1;
+  __syncthreads();
+  if (rh == 0) {
+    const float s0 = fin[0][cp][0] + fin[1][cp][0], s1 = fin[0][cp][1] + fin[1][cp][1];
+    if (F32) {
+      const long long col = c0 + cp;
+      const float v = alpha * s0;
+      if (out_mode == 2) ((bf16*)out)[col] = (bf16)v;
+      else ((float*)out)[(long long)blockIdx.y * out_ld + col] = v;
+    } else {
+      const long long col = c0 + 2 * cp;
+      float* o = (float*)out + (long long)blockIdx.y * out_ld + col;   // fp32 partials of this split
+      o[0] = s0;
+      o[1] = s1;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -287,6 +366,30 @@ int triad_colsum_splits(long long rows, int cols) {
   long long s = 256 / gx;
   if (s > rows / 16) s = rows / 16;
   return (int)(s < 1 ? 1 : s);
+}
+
+// Column sums through LDS-DMA: part = triad_colsum_dma_splits(rows, cols) * cols floats of scratch.
+int triad_colsum_dma_splits(long long rows, int cols) {
+  if (cols <= 0 || cols % 256) return 0;
+  const long long tiles = cols / 256;
+  long long s = (256 + tiles - 1) / tiles;              // one round of >= 256 workgroups
+  const long long cap = rows / (4 * CD_ROWS);           // >= 4 chunks per split
+  if (s > cap) s = cap;
+  return (int)(s < 1 ? 1 : s);
+}
+
+int triad_colsum_dma(const void* X, long long rows, int cols, long long ld, float* part, float alpha, int out_bf16,
+                     void* out, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || cols % 256 || ld % 8 || ld < cols || !part) return TRIAD_EINVAL;
+  const int S = triad_colsum_dma_splits(rows, cols);
+  long long per = (rows + S - 1) / S;
+  hipLaunchKernelGGL(colsum_dma_kernel<false>, dim3(cols / 256, S), dim3(256), 0, stream, X, rows, ld, per, 1.f, 0,
+                     (void*)part, (long long)cols);
+  TRIAD_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_dma_kernel<true>, dim3(cols / 128, 1), dim3(256), 0, stream, (const void*)part,
+                     (long long)S, (long long)cols, (long long)S, alpha, out_bf16 ? 2 : 1, out, 0LL);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
 }
 
 int triad_colsum(const void* X, long long rows, int cols, long long ld, float* part, float alpha, int out_bf16,

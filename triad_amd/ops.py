@@ -122,6 +122,13 @@ def bias_grad(x, out_dtype=torch.float32, meta=None):
     DESIGN.md §2b). TRIAD_DB_GEMM=0: triad_colsum (A/B only). Shapes the GEMM does not tile
     (cols % 128, rows % 64) fall back to triad_colsum. meta: launch tag (default: backbone work)."""
     rows, cols = x.shape
+    if os.environ.get("TRIAD_DB_FORM", "gemm") == "dma" and cols % 256 == 0 and x.stride(1) == 1:
+        # the rows staged by LDS-DMA, sums on the VALU (no MFMA work wasted on 127 dead columns)
+        part = torch.empty(call("triad_colsum_dma_splits", rows, cols) * cols, dtype=torch.float32, device=x.device)
+        out = torch.empty(cols, dtype=out_dtype, device=x.device)
+        call("triad_colsum_dma", ptr(x), rows, cols, x.stride(0), ptr(part), 1.0, int(out_dtype == torch.bfloat16),
+             ptr(out), stream_ptr(x.device), meta=meta if meta is not None else dict(backbone=True))
+        return out
     if os.environ.get("TRIAD_DB_GEMM", "1") == "0" or cols % 128 or rows % 64 or x.stride(1) != 1:
         return colsum(x, out_dtype, backbone=meta is None)
     dev = x.device
@@ -132,7 +139,7 @@ def bias_grad(x, out_dtype=torch.float32, meta=None):
     # each split's workgroups on one XCD (gemm.hip tile_split), >= 512 rows per split
     tiles = cols // 128
     sp = min(-(-256 // tiles), rows // 512)
-    sp = (sp + 4) // 8 * 8 if sp >= 8 else max(1, sp)
+    sp = (sp + 7) // 8 * 8 if sp >= 8 else max(1, sp)
     form = 1 | (8 if sp % 8 == 0 else 0)
     slabs = torch.empty(sp * cols * 128, dtype=torch.float32, device=dev)
     c = torch.empty(cols, 128, dtype=torch.float32, device=dev)
