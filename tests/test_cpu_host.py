@@ -191,7 +191,7 @@ def test_round4_entry_points_reject_bad_arguments():
     # LDS-DMA column sums: 256-column tiles only, scratch required
     assert lib.triad_colsum_dma(fake, 1024, 640, 640, fake, 1.0, 0, fake, None) == 1001
     assert lib.triad_colsum_dma(fake, 1024, 768, 768, None, 1.0, 0, fake, None) == 1001
-    assert lib.triad_colsum_dma_splits(50944, 768) == 86 and lib.triad_colsum_dma_splits(256, 768) == 4
+    assert lib.triad_colsum_dma_splits(50944, 768) == 171 and lib.triad_colsum_dma_splits(256, 768) == 4
 
 
 def test_weight_gradient_plans():

@@ -535,12 +535,16 @@ def test_linear_weight_grad_forms(M, O, K):
     assert _rel(dw.float(), ref) < 4e-3
 
 
-@pytest.mark.parametrize("rows,cols", [(768, 768), (8192, 2304), (50944, 3072), (200, 768)])
-def test_bias_grad_on_gemm_matches_column_sum(rows, cols):
-    """ops.bias_grad (the step's column sums on the split-K MFMA GEMM, x^T . ones) against an fp32
-    torch column sum of the same bf16 matrix; shapes the GEMM does not tile (rows % 64) take
-    triad_colsum."""
+@pytest.mark.parametrize("form", ["dma", "gemm"])
+@pytest.mark.parametrize("rows,cols", [(768, 768), (8192, 2304), (50944, 3072), (200, 768), (37, 512),
+                                       (65536, 512), (1000, 256)])
+def test_bias_grad_forms_match_column_sum(rows, cols, form, monkeypatch):
+    """ops.bias_grad -- the step's column sums by LDS-DMA (triad_colsum_dma, default) or on the
+    split-K MFMA GEMM (x^T . ones) -- against an fp32 torch column sum of the same bf16 matrix,
+    ragged row counts included (the DMA ring's last chunk; shapes the GEMM does not tile take
+    triad_colsum); a strided view (ld > cols) gives the same sums."""
     from triad_amd import ops
+    monkeypatch.setenv("TRIAD_DB_FORM", form)
     g = torch.Generator(device=dev).manual_seed(rows + cols)
     x = (torch.randn(rows, cols, device=dev, generator=g) * 0.05).to(torch.bfloat16)
     ref = x.float().sum(0)
@@ -549,3 +553,6 @@ def test_bias_grad_on_gemm_matches_column_sum(rows, cols):
         assert got.dtype == dt and got.shape == (cols,)
         tol = 1e-5 if dt == torch.float32 else 8e-3
         assert float((got.float() - ref).norm() / ref.norm()) < tol
+    wide = torch.zeros(rows, cols + 256, device=dev, dtype=torch.bfloat16)
+    wide[:, :cols] = x
+    assert torch.equal(ops.bias_grad(wide[:, :cols]), ops.bias_grad(x))

@@ -226,17 +226,28 @@ __global__ __launch_bounds__(256) void sum_slabs_kernel(const float* __restrict_
 
 // ---- column sums through LDS-DMA (the step's bias gradients) -----------------
 // Rows stream into LDS by 16-byte LDS-DMA (global_load_lds, as the GEMMs load their operands),
-// double-buffered chunks of 16 rows x 512 bytes of one column tile; the sums are VALU over LDS.
+// chunks of 16 rows x 512 bytes of one column tile in a CD_SLOTS ring (CD_SLOTS - 1 chunks in
+// flight while one is summed: 8 KB per chunk is too little to cover HBM latency on its own);
+// the sums are VALU over LDS.
 // Pass 1: bf16 X, 256-column tiles x row splits -> fp32 partials [splits][cols]; pass 2: the
 // partials (fp32, 128-column tiles, one split) -> out. A thread owns 4 bytes of a row (two bf16
 // columns / one fp32 column) and every other row of a chunk; the two row halves meet in LDS.
 constexpr int CD_ROWS = 16;    // rows per chunk (16 x 512 B = 8 KB = 8 one-KB LDS-DMA pieces)
+#ifndef TRIAD_CD_SLOTS
+#define TRIAD_CD_SLOTS 4
+#endif
+#ifndef TRIAD_CD_WG
+#define TRIAD_CD_WG 512
+#endif
+constexpr int CD_SLOTS = TRIAD_CD_SLOTS;   // LDS ring depth (2..4)
+constexpr int CD_WG = TRIAD_CD_WG;         // first-pass workgroup target (2 per CU)
+static_assert(CD_SLOTS >= 2 && CD_SLOTS <= 4, "ring depth");
 
 template <bool F32>
 __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict__ Xv, long long rows, long long ld,
                                                          long long per, float alpha, int out_mode,
                                                          void* __restrict__ out, long long out_ld) {
-  __shared__ __attribute__((aligned(16))) char buf[2][CD_ROWS * 512];
+  __shared__ __attribute__((aligned(16))) char buf[CD_SLOTS][CD_ROWS * 512];
   __shared__ float fin[2][128][2];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   constexpr int TILE = F32 ? 128 : 256;                 // columns per 512-byte row slice
@@ -258,16 +269,21 @@ __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict_
   };
   const int cp = t & 127, rh = t >> 7;                  // 4-byte column slot, row parity
   float a0 = 0.f, a1 = 0.f;
-  if (nchunk > 0) issue(0, 0);
+  constexpr int AHEAD = CD_SLOTS - 1;
+#pragma unroll
+  for (int c = 0; c < AHEAD; ++c)
+    if (c < nchunk) issue(c, c);
   for (int c = 0; c < nchunk; ++c) {
-    if (c + 1 < nchunk) {
-      issue(c + 1, (c + 1) & 1);
-      TRIAD_VMCNT(2);                                   // this chunk's 2 pieces done, the next 2 in flight
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // chunk c + AHEAD refills the slot chunk c - 1 left (free since the last barrier); then wait for
+    // chunk c's 2 pieces per wave while the chunks issued after it stay in flight
+    if (c + AHEAD < nchunk) issue(c + AHEAD, (c + AHEAD) % CD_SLOTS);
+    const int later = nchunk - 1 - c < AHEAD ? nchunk - 1 - c : AHEAD;
+    if (later >= 3) TRIAD_VMCNT(6);
+    else if (later == 2) TRIAD_VMCNT(4);
+    else if (later == 1) TRIAD_VMCNT(2);
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const char* b = buf[c & 1];
+    const char* b = buf[c % CD_SLOTS];
     const int nr = (int)((r1 - r0 - (long long)c * CD_ROWS) < CD_ROWS ? (r1 - r0 - (long long)c * CD_ROWS) : CD_ROWS);
 #pragma unroll
     for (int k = 0; k < CD_ROWS / 2; ++k) {
@@ -282,7 +298,7 @@ __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict_
         }
       }
     }
-    __syncthreads();                                    // slot c & 1 is refilled by chunk c + 2's DMA
+    __syncthreads();                                    // slot c % CD_SLOTS is refilled next iteration
   }
   fin[rh][cp][0] = a0;
   fin[rh][cp][1] = a1;
@@ -372,7 +388,7 @@ int triad_colsum_splits(long long rows, int cols) {
 int triad_colsum_dma_splits(long long rows, int cols) {
   if (cols <= 0 || cols % 256) return 0;
   const long long tiles = cols / 256;
-  long long s = (256 + tiles - 1) / tiles;              // one round of >= 256 workgroups
+  long long s = (CD_WG + tiles - 1) / tiles;            // one round of >= CD_WG workgroups
   const long long cap = rows / (4 * CD_ROWS);           // >= 4 chunks per split
   if (s > cap) s = cap;
   return (int)(s < 1 ? 1 : s);

@@ -112,17 +112,22 @@ _ONES = {}
 
 
 def bias_grad(x, out_dtype=torch.float32, meta=None):
-    """Column sums of a bf16 [rows][cols] matrix for the BACKBONE bias gradients (and SpecAugment's
-    masked_spec_embed), on the split-K MFMA GEMM as x^T . ones (column 0 of a [cols][128]
-    product, fp32 accumulation). Why not triad_colsum / PyTorch's sum: with the backbones on
-    concurrent streams, column-sum reductions beside the library's MFMA + LDS-DMA GEMMs returned
-    disturbed partial sums in some launches (16-column groups off by ~1 %), while the same sums on
-    the GEMM stayed bit-identical to the serial step in every one of 490 concurrent steps against
-    21-38 of 80 with the reductions (tools/stream_repeat.py, profiles/r04_stream_repeat_*.log,
-    DESIGN.md §2b). TRIAD_DB_GEMM=0: triad_colsum (A/B only). Shapes the GEMM does not tile
-    (cols % 128, rows % 64) fall back to triad_colsum. meta: launch tag (default: backbone work)."""
+    """Column sums of a bf16 [rows][cols] matrix for the BACKBONE and head bias gradients (and
+    SpecAugment's masked_spec_embed), fp32 accumulation. Why not triad_colsum / PyTorch's sum: with
+    the backbones on concurrent streams, column-sum REDUCTIONS beside the library's MFMA + LDS-DMA
+    GEMMs returned disturbed partial sums in some launches (16-column groups off by ~1 %, 21-38 of
+    80 concurrent steps differing from the serial one), while sums whose rows arrive by LDS-DMA
+    stayed bit-identical in every concurrent step (tools/stream_repeat.py,
+    profiles/r04_stream_repeat_*.log). Forms (TRIAD_DB_FORM):
+      dma  (default, cols % 256 == 0): triad_colsum_dma -- rows staged by LDS-DMA, VALU sums, a
+           second pass over the per-split partials; HBM-bound, 4.8 TB/s at 50,944 x 2,304
+           (profiles/r04_colsum_dma_ring.log) and no MFMA time taken from the other stream;
+      gemm (and shapes dma does not take when cols % 128 == 0, rows % 64 == 0): the split-K MFMA
+           GEMM as x^T . ones, column 0 of a [cols][128] product (127 of 128 MFMA columns dead);
+    TRIAD_DB_GEMM=0 or any other shape: triad_colsum. meta: launch tag (default: backbone work)."""
     rows, cols = x.shape
-    if os.environ.get("TRIAD_DB_FORM", "gemm") == "dma" and cols % 256 == 0 and x.stride(1) == 1:
+    if (os.environ.get("TRIAD_DB_FORM", "dma") == "dma" and cols % 256 == 0 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0):
         # the rows staged by LDS-DMA, sums on the VALU (no MFMA work wasted on 127 dead columns)
         part = torch.empty(call("triad_colsum_dma_splits", rows, cols) * cols, dtype=torch.float32, device=x.device)
         out = torch.empty(cols, dtype=out_dtype, device=x.device)
