@@ -209,6 +209,14 @@ def test_weight_gradient_plans():
         assert form & 7 == 4 and bool(form & 8) == xcd
         assert not xcd or sp % 8 == 0
     assert linear._form_splits(8192, 768, 768)[0] == 0
+    # HuBERT conv stack (frontend._conv_dw_plan): eight-wave tiles, one round of <= 256 workgroups
+    from triad_amd.frontend import _conv_dw_plan
+    for M, N in ((1638400, 1536), (204800, 1536), (102400, 1024), (51200, 1024), (4096, 1536)):
+        form, sp = _conv_dw_plan(M, 512, N)
+        assert form & 7 == 4 and 1 <= sp and sp * (512 // 256) * (N // 256) <= 256 and M // sp >= 2048
+        assert not form & 8 or sp % 8 == 0
+    assert _conv_dw_plan(1638400, 512, 1536) == (4, 21) and _conv_dw_plan(102400, 512, 1024) == (12, 32)
+    assert _conv_dw_plan(65536, 512, 384) == (0, 8)
 
 
 def test_select_subset_indices_draws_writes_and_rereads(tmp_path):

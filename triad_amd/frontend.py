@@ -169,15 +169,27 @@ def _gemm_rows(a, a_row, lda, M, K, b, out, out_row, ldc):
         out.as_strided((M, N), (ldc, 1), out.storage_offset() + out_row * ldc).copy_(torch.mm(A, b.t()))
 
 
+def _conv_dw_plan(M, O, N):
+    """(form, splits) of a conv-stack weight gradient ([O][N] over M frame-pair rows): the
+    eight-wave 256 x 256 tile with one round of <= 256 workgroups (21 splits at N = 1536, 32 with
+    each split on one XCD at N = 1024), >= 2,048 rows per split. 965 against 720 TFLOP/s for the
+    former 8 splits of 256 x 128 tiles (192 workgroups) at 1.6 M rows x 1,536 -- 3.6 -> 2.65 ms per
+    call, ~1.9 ms per c3 step over the conv stack (tools/conv_dw_ab.py, profiles/r04_conv_dw_ab.log)."""
+    if O % 256 or N % 256:
+        return 0, 8
+    sp = max(1, min(256 // ((O // 256) * (N // 256)), M // 2048))
+    return (4 | 8 if sp % 8 == 0 else 4), sp
+
+
 def _weight_grad_rows(dy, M, x, ldx, N):
     """fp32 [O][N] = sum_r dy[r][o] X[r][n] over r < M, X[r][n] = x.flat[r * ldx + n] (overlapping)."""
     O = dy.shape[1]
     if M % 64 == 0 and O % 128 == 0 and N % 128 == 0 and ldx % 8 == 0:
-        sp = 8
+        form, sp = _conv_dw_plan(M, O, N)
         slabs = torch.empty(sp * O * N, dtype=torch.float32, device=dy.device)
         out = torch.empty(O, N, dtype=torch.float32, device=dy.device)
-        call("triad_gemm_bf16_splitk", ptr(dy), O, 0, ptr(x), ldx, 0, O, N, M, sp, None, ptr(slabs), ptr(out), 0,
-             stream_ptr(dy.device), meta=dict(backbone=True))
+        call("triad_gemm_bf16_splitk_form", ptr(dy), O, 0, ptr(x), ldx, 0, O, N, M, sp, None, ptr(slabs), ptr(out), 0,
+             form, stream_ptr(dy.device), meta=dict(backbone=True))
         return out
     X = x.as_strided((M, N), (ldx, 1), x.storage_offset())
     return torch.mm(dy[:M].t(), X, out_dtype=torch.float32)
