@@ -239,15 +239,28 @@ constexpr int CD_ROWS = 16;    // rows per chunk (16 x 512 B = 8 KB = 8 one-KB L
 #ifndef TRIAD_CD_WG
 #define TRIAD_CD_WG 512
 #endif
-constexpr int CD_SLOTS = TRIAD_CD_SLOTS;   // LDS ring depth (2..4)
+constexpr int CD_SLOTS = TRIAD_CD_SLOTS;   // LDS ring depth (2..4: two workgroups per CU)
 constexpr int CD_WG = TRIAD_CD_WG;         // first-pass workgroup target (2 per CU)
+// (Measured and not kept: a 12-slot ring for the second pass, all its chunks in flight at once --
+// 26.5 -> 26.2 us at 50,944 x 768, 15.6 -> 17.1 at 8,192 x 768, profiles/r04_colsum_dma_pass2.log.)
 static_assert(CD_SLOTS >= 2 && CD_SLOTS <= 4, "ring depth");
 
-template <bool F32>
+// s_waitcnt with an immediate for `later` (0..L) outstanding chunks of 2 pieces per wave
+template <int L>
+__device__ __forceinline__ void cd_wait(int later) {
+  if constexpr (L == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (later >= L) TRIAD_VMCNT(2 * L);
+    else cd_wait<L - 1>(later);
+  }
+}
+
+template <bool F32, int SLOTS>
 __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict__ Xv, long long rows, long long ld,
                                                          long long per, float alpha, int out_mode,
                                                          void* __restrict__ out, long long out_ld) {
-  __shared__ __attribute__((aligned(16))) char buf[CD_SLOTS][CD_ROWS * 512];
+  __shared__ __attribute__((aligned(16))) char buf[SLOTS][CD_ROWS * 512];
   __shared__ float fin[2][128][2];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   constexpr int TILE = F32 ? 128 : 256;                 // columns per 512-byte row slice
@@ -269,21 +282,17 @@ __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict_
   };
   const int cp = t & 127, rh = t >> 7;                  // 4-byte column slot, row parity
   float a0 = 0.f, a1 = 0.f;
-  constexpr int AHEAD = CD_SLOTS - 1;
+  constexpr int AHEAD = SLOTS - 1;
 #pragma unroll
   for (int c = 0; c < AHEAD; ++c)
     if (c < nchunk) issue(c, c);
   for (int c = 0; c < nchunk; ++c) {
     // chunk c + AHEAD refills the slot chunk c - 1 left (free since the last barrier); then wait for
     // chunk c's 2 pieces per wave while the chunks issued after it stay in flight
-    if (c + AHEAD < nchunk) issue(c + AHEAD, (c + AHEAD) % CD_SLOTS);
-    const int later = nchunk - 1 - c < AHEAD ? nchunk - 1 - c : AHEAD;
-    if (later >= 3) TRIAD_VMCNT(6);
-    else if (later == 2) TRIAD_VMCNT(4);
-    else if (later == 1) TRIAD_VMCNT(2);
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (c + AHEAD < nchunk) issue(c + AHEAD, (c + AHEAD) % SLOTS);
+    cd_wait<AHEAD>(nchunk - 1 - c < AHEAD ? nchunk - 1 - c : AHEAD);
     __syncthreads();
-    const char* b = buf[c % CD_SLOTS];
+    const char* b = buf[c % SLOTS];
     const int nr = (int)((r1 - r0 - (long long)c * CD_ROWS) < CD_ROWS ? (r1 - r0 - (long long)c * CD_ROWS) : CD_ROWS);
 #pragma unroll
     for (int k = 0; k < CD_ROWS / 2; ++k) {
@@ -298,7 +307,7 @@ __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict_
         }
       }
     }
-    __syncthreads();                                    // slot c % CD_SLOTS is refilled next iteration
+    __syncthreads();                                    // slot c % SLOTS is refilled next iteration
   }
   fin[rh][cp][0] = a0;
   fin[rh][cp][1] = a1;
@@ -399,10 +408,10 @@ int triad_colsum_dma(const void* X, long long rows, int cols, long long ld, floa
   if (rows <= 0 || cols <= 0 || cols % 256 || ld % 8 || ld < cols || !part) return TRIAD_EINVAL;
   const int S = triad_colsum_dma_splits(rows, cols);
   long long per = (rows + S - 1) / S;
-  hipLaunchKernelGGL(colsum_dma_kernel<false>, dim3(cols / 256, S), dim3(256), 0, stream, X, rows, ld, per, 1.f, 0,
+  hipLaunchKernelGGL((colsum_dma_kernel<false, CD_SLOTS>), dim3(cols / 256, S), dim3(256), 0, stream, X, rows, ld, per, 1.f, 0,
                      (void*)part, (long long)cols);
   TRIAD_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_dma_kernel<true>, dim3(cols / 128, 1), dim3(256), 0, stream, (const void*)part,
+  hipLaunchKernelGGL((colsum_dma_kernel<true, CD_SLOTS>), dim3(cols / 128, 1), dim3(256), 0, stream, (const void*)part,
                      (long long)S, (long long)cols, (long long)S, alpha, out_bf16 ? 2 : 1, out, 0LL);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;

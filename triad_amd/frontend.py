@@ -162,8 +162,12 @@ def _gemm_rows(a, a_row, lda, M, K, b, out, out_row, ldc):
     a.flat[(a_row + m) * lda + k] (rows may overlap), b [N][K] contiguous bf16."""
     N = b.shape[0]
     if M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and lda % 8 == 0 and ldc % 8 == 0:
-        call("triad_gemm_bf16", _addr(a, a_row, lda), lda, 1, ptr(b), K, 1, M, N, K, None, _addr(out, out_row, ldc), ldc,
-             1, stream_ptr(a.device), meta=dict(backbone=True))
+        # the eight-wave 256 x 256 tile for every tall product, K = 512 included (the size policy's
+        # 256 x 128 ring ran the 512-deep input gradients at 605-690 TFLOP/s, this form 745-815;
+        # bit-identical, tools/conv_gemm_ab.py, profiles/r04_conv_gemm_ab.log)
+        form = 4 if M >= 32768 and M % 256 == 0 and N % 256 == 0 else 0
+        call("triad_gemm_bf16_form", _addr(a, a_row, lda), lda, 1, ptr(b), K, 1, M, N, K, None,
+             _addr(out, out_row, ldc), ldc, 1, form, stream_ptr(a.device), meta=dict(backbone=True))
     else:  # same product through torch (it copies the overlapping operand)
         A = a.as_strided((M, K), (lda, 1), a.storage_offset() + a_row * lda)
         out.as_strided((M, N), (ldc, 1), out.storage_offset() + out_row * ldc).copy_(torch.mm(A, b.t()))
