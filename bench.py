@@ -248,6 +248,7 @@ def main():
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
+            _lib.TIMERS = {k: [] for k in TRACKED}
             t1 = time.perf_counter()
             for _ in range(a.single_stream_steps):
                 step()
@@ -255,6 +256,7 @@ def main():
             if world > 1:
                 dist.barrier()
             dtss = time.perf_counter() - t1
+            timers_other, _lib.TIMERS = _lib.TIMERS, None
         finally:
             if prev[0] is None:
                 os.environ.pop("TRIAD_MODALITY_STREAMS", None)
@@ -270,6 +272,19 @@ def main():
                   "concurrent_streams": not headline_concurrent,
                   "note": ("concurrent streams (backbones on three streams + dW side stream)" if not headline_concurrent
                            else "serial step (one stream), bit-identical results")}
+        # per-kernel figures of this mode too: on concurrent streams a launch shares the CUs with the
+        # other streams' kernels, so its duration (and fraction of peak) reads lower than alone
+        rep_o = kernel_report(timers_other)
+        single["kernels_frac"] = {k: v["flops"] / max(1, v["launches"]) / (v["ms"] / max(1, v["launches"]) * 1e-3)
+                                  / 1e12 / PEAK_BF16_TFLOPS
+                                  for k, v in sorted(rep_o.items()) if v["flops"] and not k.endswith("[backbone]")
+                                  and ("pairsim" in k or "tile_gemm" in k)}
+        pko = [k for k in rep_o if "[proj" in k]
+        po_ms = sum(rep_o[k]["ms"] for k in pko) / a.single_stream_steps
+        po_fl = sum(rep_o[k]["flops"] for k in pko) / a.single_stream_steps
+        if po_ms > 0:
+            single["projection_heads"] = {"ms_per_step": po_ms, "achieved_TFLOPs": po_fl / po_ms / 1e9,
+                                          "frac": po_fl / po_ms / 1e9 / PEAK_BF16_TFLOPS}
         if rank == 0:
             print(f"[bench] {a.single_stream_steps} steps with concurrent streams "
                   f"{'on' if single['concurrent_streams'] else 'off'}: {dtss:.2f} s", file=sys.stderr, flush=True)
