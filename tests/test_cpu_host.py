@@ -194,6 +194,13 @@ def test_round4_entry_points_reject_bad_arguments():
     assert lib.triad_colsum_dma_splits(50944, 768) == 171 and lib.triad_colsum_dma_splits(256, 768) == 4
 
 
+def test_side_stream_tables_key_by_device_ordinal():
+    """linear._dev_index: "cuda:N" -> N without touching a GPU (index None -> the current device,
+    GPU-tested in test_ops_gpu.py::test_side_stream_is_one_stream_per_device)."""
+    from triad_amd.linear import _dev_index
+    assert _dev_index("cuda:3") == 3 and _dev_index(torch.device("cuda", 1)) == 1
+
+
 def test_weight_gradient_plans():
     """Split-K plans of the projection-head (ops._dw_plan) and backbone (linear._form_splits)
     weight gradients: long token lists on the XCD-per-split placement with a split count that is a

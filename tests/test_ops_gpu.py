@@ -369,6 +369,19 @@ def test_colsum_matches_torch(rows, cols):
     assert gb.dtype == torch.bfloat16 and torch.allclose(gb.float(), got, rtol=8e-3, atol=1e-2)
 
 
+def test_side_stream_is_one_stream_per_device():
+    """The reducer's fold (dist.py, keyed by the trainer's device, "cuda" by default) and the
+    backward nodes (keyed by their tensors' device, "cuda:0") must get the SAME side stream: with
+    two, the fold of a side-stream weight gradient waited on the wrong one and read it unfinished
+    (the two-rank Mode G test's audio conv dW, profiles/r04_gpu_tests_modeg_nan.log)."""
+    from triad_amd.linear import _dev_index, _side_stream
+    cur = torch.cuda.current_device()
+    assert _dev_index(torch.device("cuda")) == cur == _dev_index(f"cuda:{cur}")
+    assert _side_stream(torch.device("cuda")) is _side_stream(torch.device("cuda", cur))
+    x = torch.ones(4, device="cuda")
+    assert _side_stream(x.device) is _side_stream(torch.device("cuda"))
+
+
 def test_side_stream_weight_grads_bit_identical():
     """Weight gradients of bf16 (mixed-precision shadow) Linear / fused-qkv weights computed on
     the side stream (linear.on_side_stream, joined at the end of the backward pass) equal the

@@ -84,10 +84,22 @@ _SIDE = {}
 _JOIN_TASK = {}  # device index -> autograd graph task that already has a join callback queued
 
 
+def _dev_index(dev) -> int:
+    """The ordinal of a CUDA device given as torch.device("cuda") (index None: the current
+    device) or "cuda:N". Every per-device table here is keyed by it: a trainer built with
+    device="cuda" asks for the side stream under index None while the backward nodes ask under
+    the tensors' index 0 -- two different streams, and the reducer's fold of a side-stream weight
+    gradient then waited on the wrong one (the two-rank Mode G test's audio conv dW,
+    profiles/r04_gpu_tests_modeg_nan.log)."""
+    dev = torch.device(dev)
+    return dev.index if dev.index is not None else torch.cuda.current_device()
+
+
 def _side_stream(dev):
-    s = _SIDE.get(dev.index)
+    i = _dev_index(dev)
+    s = _SIDE.get(i)
     if s is None:
-        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+        s = _SIDE[i] = torch.cuda.Stream(device=i)
     return s
 
 
@@ -112,13 +124,14 @@ def side_stream_ok(*ws: torch.Tensor) -> bool:
                                                    for w in ws)):
         return False
     dev = ws[0].device
-    t, seen = _CLAIMED.get(dev.index, (None, None))
+    di = _dev_index(dev)
+    t, seen = _CLAIMED.get(di, (None, None))
     if t != task:
         seen = set()
-        _CLAIMED[dev.index] = (task, seen)
+        _CLAIMED[di] = (task, seen)
     if any(id(w) in seen for w in ws):
-        if dev.index in _SIDE:
-            torch.cuda.current_stream(dev).wait_stream(_SIDE[dev.index])
+        if di in _SIDE:
+            torch.cuda.current_stream(dev).wait_stream(_SIDE[di])
         seen.update(id(w) for w in ws)
         return False
     seen.update(id(w) for w in ws)
@@ -139,8 +152,8 @@ def on_side_stream(fn, inputs):
     for o in (outs if isinstance(outs, (list, tuple)) else (outs,)):
         o.record_stream(main)
     task = torch._C._current_graph_task_id()
-    if _JOIN_TASK.get(dev.index) != task:  # once per backward pass (robust to an aborted one)
-        _JOIN_TASK[dev.index] = task
+    if _JOIN_TASK.get(_dev_index(dev)) != task:  # once per backward pass (robust to an aborted one)
+        _JOIN_TASK[_dev_index(dev)] = task
         torch.autograd.Variable._execution_engine.queue_callback(_join(dev))
     return outs
 
