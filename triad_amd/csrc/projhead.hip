@@ -241,6 +241,8 @@ constexpr int CD_ROWS = 16;    // rows per chunk (16 x 512 B = 8 KB = 8 one-KB L
 #endif
 constexpr int CD_SLOTS = TRIAD_CD_SLOTS;   // LDS ring depth (2..4: two workgroups per CU)
 constexpr int CD_WG = TRIAD_CD_WG;         // first-pass workgroup target (2 per CU)
+// (Sweep, profiles/r04_colsum_dma_ring_variants.log: at 256 workgroups a 4-slot ring is no faster
+// than 2 slots; 512 workgroups take 50,944 x 2,304 from 84 to 49 us; 1,024 are slower again.)
 // (Measured and not kept: a 12-slot ring for the second pass, all its chunks in flight at once --
 // 26.5 -> 26.2 us at 50,944 x 768, 15.6 -> 17.1 at 8,192 x 768, profiles/r04_colsum_dma_pass2.log.)
 static_assert(CD_SLOTS >= 2 && CD_SLOTS <= 4, "ring depth");
