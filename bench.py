@@ -28,12 +28,12 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "tri-modal triples/sec (whole node) + loss parity, B=256 at 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
-TRACKED = ("triad_pairsim_fwd", "triad_pairsim_fwd_multi", "triad_pairsim_dS", "triad_gemm_bf16", "triad_projhead_fwd", "triad_projhead_bwd",
-           "triad_gemm_bf16_splitk", "triad_gemm_bf16_splitk_form", "triad_tile_gemm", "triad_tile_gemm_packed", "triad_tile_gemm_packed16", "triad_tile_gemm_packed_slabs",
-           "triad_tile_gemm_packed16_slabs", "triad_bfrag_pack",
+TRACKED = ("triad_pairsim_fwd", "triad_pairsim_fwd_multi", "triad_pairsim_dS", "triad_gemm_bf16", "triad_projhead_ln_fwd", "triad_rowgemm_bias", "triad_projhead_ln_bwd", "triad_wpack",
+           "triad_gemm_bf16_splitk", "triad_gemm_bf16_splitk_form", "triad_tile_gemm", "triad_tile_gemm_packed16",
+           "triad_tile_gemm_packed16_slabs",
            "triad_bfrag_pack16", "triad_dS_patch", "triad_clip_reduce", "triad_losshead",
-           "triad_diag_smooth", "triad_diag_sparsity", "triad_dtemp_finalize", "triad_ln_bwd",
-           "triad_colsum", "triad_sum_slabs", "triad_gather_rows", "triad_global_znorm",
+           "triad_diag_smooth", "triad_diag_sparsity", "triad_dtemp_finalize",
+           "triad_colsum_dma", "triad_sum_slabs", "triad_gather_rows", "triad_global_znorm",
            "triad_grad_sumsq", "triad_adamw_step", "triad_ln_fwd", "triad_ln_bwd3", "triad_gemm_bf16_bias")
 
 
@@ -52,6 +52,8 @@ def parse():
                     help="timed steps in the OTHER execution mode (serial <-> concurrent streams), reported "
                          "beside the headline (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stream-check", dest="stream_check", action="store_false",
+                    help="skip the serial-vs-concurrent bit-identity check at the product shape (N = 1)")
     ap.add_argument("--separate-frames", action="store_true",
                     help="encode the AV and TV frame batches separately (2x ViT work)")
     return ap.parse_args()
@@ -130,6 +132,52 @@ def model_streams():
     """Does forward_triad run the audio / text backbones on their own streams (the headline mode)?"""
     from triad_amd.model import modality_streams_enabled
     return modality_streams_enabled()
+
+
+def stream_bit_identity(dev, frames, audio, text):
+    """the concurrent default must give the serial step's results bit for bit at the
+    PRODUCT shape (c3, B = 256), not only at the tests' B = 128. Two fresh models / trainers from
+    the same seed, one step each (dropout, LayerDrop, SpecAugment and patch dropout drawn from the
+    same seeds), serial then concurrent; the losses and the reduced flat gradient (taken before
+    clipping / AdamW) are compared bit for bit."""
+    import numpy as np
+    from triad_amd.model import MultiModalModel, modality_streams_enabled, set_concurrent_streams
+    from triad_amd.train import TriadTrainer
+
+    def run(concurrent):
+        set_concurrent_streams(concurrent)
+        torch.manual_seed(4321)
+        m = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.80, patch_sparsity_weight=0.01,
+                            visual_dropout_prob=0.25, use_amp=True).to(dev)
+        m.train()
+        tr = TriadTrainer(m, learning_rate=1e-4, total_updates=100000, unfreeze_audio_step=0,
+                          unfreeze_text_step=0, unfreeze_vit_step=0, device=dev)
+        snap = []
+
+        def grab():   # the reduced gradient, then no optimizer step (the models are discarded)
+            tr._allreduce_grads()
+            snap.append(tr.space.flat_g.clone())
+            return {}
+        tr._optimizer_step = grab
+        torch.manual_seed(1)
+        np.random.seed(1)   # SpecAugment masks (transformers draws them from numpy)
+        out = tr.step(frames, audio, text, phase="full_joint")
+        torch.cuda.synchronize()
+        loss = torch.stack([out["loss"], out["loss_av"], out["loss_tv"]]).clone()
+        del tr, m
+        return loss, snap[0]
+
+    prev = modality_streams_enabled()
+    try:
+        l_s, g_s = run(False)
+        l_c, g_c = run(True)
+    finally:
+        set_concurrent_streams(prev)
+    diff = int((g_s != g_c).sum())
+    return {"equal": bool(torch.equal(l_s, l_c) and diff == 0), "B": int(frames.shape[0]),
+            "losses_serial": [float(x) for x in l_s], "losses_concurrent": [float(x) for x in l_c],
+            "gradient_elements": int(g_s.numel()), "differing_elements": diff,
+            "max_abs": float((g_s - g_c).abs().max())}
 
 
 def main():
@@ -234,10 +282,23 @@ def main():
         if rank == 0:
             print(f"[bench] {a.separate_steps} separate-frames steps: {dts:.2f} s", file=sys.stderr, flush=True)
 
+    rcheck = None
+    if world > 1 and trainer.reducer is not None:
+        # correctness gate of the overlapped gradient reduction: one more step with
+        # every bucket's pre-reduction gradient snapshotted; after it the same buckets are
+        # all-reduced again from the snapshots, one at a time with the device otherwise idle, and
+        # compared bit for bit with what the all-reduces overlapped with backward produced
+        trainer.reducer.check = True
+        step()
+        torch.cuda.synchronize()
+        rcheck = trainer.reducer.check_result
+        if rank == 0:
+            print(f"[bench] reducer check: {rcheck}", file=sys.stderr, flush=True)
+
     single = None
     if a.single_stream_steps > 0:
-        # the same step in the other execution mode, reported beside the headline: the serial
-        # default vs the concurrent opt-in (backbones on three streams + the dW side stream)
+        # the same step in the other execution mode, reported beside the headline: the serial step
+        # (one stream) beside the concurrent default (backbones on three streams + the dW side stream)
         from triad_amd import linear as _lin
         from triad_amd.model import set_concurrent_streams
         prev = (os.environ.get("TRIAD_MODALITY_STREAMS"), _lin.SIDE_STREAM_DW)
@@ -353,12 +414,20 @@ def main():
         res["config"]["execution"] = ("concurrent streams: audio / text backbones and the backbone dW on their own "
                                       "streams (the default; bit-identical to the serial step, DESIGN.md 2b)"
                                       if model_streams() else "serial: one stream")
+        if rcheck is not None:
+            res["reducer_check"] = rcheck
         if single is not None:
             res["other_stream_mode"] = single
         if sep is not None:
             res["separate_frames"] = {"value": sep, "unit": "triples/s", "steps": a.separate_steps,
                                       "note": "AV and TV frame batches encoded separately, as the reference's "
                                               "two data loaders do (2x ViT work)"}
+        if world == 1 and a.stream_check:
+            del trainer, model
+            torch.cuda.empty_cache()
+            bit = stream_bit_identity(dev, frames, audio, text)
+            res["stream_bit_identity"] = bit
+            print(f"[bench] serial vs concurrent step at B={a.batch}: {bit}", file=sys.stderr, flush=True)
         if world == 1 and not a.no_cpu_baseline:
             from oracle import cpu_step
             # the threads this process may use: torch's intra-op pool honours OMP_NUM_THREADS (the GPU box
@@ -393,6 +462,11 @@ def main():
                                                         "(Na=199, Nv=205, Nt=32); B^2-extrapolated to the bench batch "
                                                         "(EXTRAPOLATED, not measured at that size)"}}
         print(json.dumps(res), flush=True)
+        if not res.get("stream_bit_identity", {"equal": True})["equal"]:
+            print("[bench] ERROR: the concurrent step's results differ from the serial step's at the product "
+                  "shape (stream_bit_identity); the default execution mode is not trustworthy", file=sys.stderr,
+                  flush=True)
+            sys.exit(1)
     if world > 1:
         dist.destroy_process_group()
 

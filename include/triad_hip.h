@@ -138,20 +138,11 @@ int triad_tile_gemm(const void* Dt, long long CT, int dk, const void* B, int M, 
 int triad_tile_gemm_slabs(const void* Dt, long long CT, int dk, const void* B, int M, int nkt, int splits,
                           float* slabs, hipStream_t stream);
 
-/* Direct-B form of triad_tile_gemm: B's MFMA fragments pre-arranged once (triad_bfrag_pack,
- * B [nkt*32][512] bf16 -> Bp of the same size, per dk) so each wave streams its own columns into
- * registers and only dS goes through LDS (6-7 % faster at the c3 shapes). Same results, bit for bit,
- * as triad_tile_gemm, which stays the workspace-free form. */
-int triad_bfrag_pack(const void* B, int nkt, int dk, void* Bp, hipStream_t stream);
-int triad_tile_gemm_packed(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, const float* alpha,
-                           int splits, float* slabs, void* C, hipStream_t stream);
-/* triad_tile_gemm_slabs over packed B fragments. */
-int triad_tile_gemm_packed_slabs(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, int splits,
-                                 float* slabs, hipStream_t stream);
-/* The same dQ / dK GEMMs on v_mfma_f32_16x16x32_bf16 instead of v_mfma_f32_32x32x16_bf16
- * (faster at the clock the chip holds under load): triad_bfrag_pack16 arranges B for that MFMA's
- * operand order (per dk); results equal to triad_tile_gemm_packed's (reference: the gradients of
- * S = temp Q K^T, SajayR/TRIAD model.py:384-387 / 502-505). */
+/* Direct-B form of triad_tile_gemm on v_mfma_f32_16x16x32_bf16: B's MFMA fragments pre-arranged
+ * once (triad_bfrag_pack16, B [nkt*32][512] bf16 -> Bp of the same size, per dk) so each wave
+ * streams its own columns into registers and only dS goes through LDS; faster at the c3 shapes
+ * than the workspace-free triad_tile_gemm, results equal to fp32 accumulation order of the tile
+ * (reference: the gradients of S = temp Q K^T, SajayR/TRIAD model.py:384-387 / 502-505). */
 int triad_bfrag_pack16(const void* B, int nkt, int dk, void* Bp, hipStream_t stream);
 int triad_tile_gemm_packed16(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, const float* alpha,
                              int splits, float* slabs, void* C, hipStream_t stream);
@@ -188,30 +179,33 @@ int triad_gemm_bf16_splitk_form(const void* A, long long lda, int a_kcontig, con
 
 /* triad_gemm_bf16 in an explicit tile form, a per-call argument (there is no process-wide GEMM
  * state): 0 = size policy (what triad_gemm_bf16 uses), 1 = 128 x 128 tiles, 2 = 256 x 128 LDS ring,
- * 3 = 256 x 256 four-wave tiles, 4 = 256 x 256 eight-wave tiles (3 / 4: M, N multiples of 256). */
+ * 4 = 256 x 256 eight-wave tiles (3, the retired four-wave tile, runs as 4; M, N multiples of 256). */
 int triad_gemm_bf16_form(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
                          int M, int N, int Kd, const float* alpha, void* C, long long ldc, int out_bf16, int form,
                          hipStream_t stream);
 
-/* Fused projection head forward (model.py:32-34,68 / 81-83,116 / 253-255,326 under bf16
- * autocast): y = bf16(LN(bf16(h W1^T + b1)) W2^T + b2) for M rows of H features (H % 32 == 0);
- * also saves y1 = bf16(h W1^T + b1), ln = bf16(LN(y1)) ([M][512] bf16) and mean / rstd per row
- * for the backward. W1 [512][H], W2 [512][512] bf16 (nn.Linear layout); b1, b2 (bf16-valued),
- * gamma, beta fp32. Persistent row-panel kernel: each wave owns 32 rows x 512 features. */
-int triad_projhead_fwd(const void* h, int M, int H, const void* W1, const float* b1, const float* gamma,
-                       const float* beta, float eps, const void* W2, const float* b2, void* y, long long ldy,
-                       void* y1, void* ln, float* mean, float* rstd, hipStream_t stream);
-
-/* Fused projection head backward, row part (autograd of the head under autocast, H % 256 == 0):
- * dln = bf16(dy W2), dy1 = bf16(LN'(dln)) (fp32 LayerNorm backward at y1 / mean / rstd / gamma),
- * dh = bf16(dy1 W1) into dh (row stride ldh); dy1 [M][512] written for the weight gradients.
- * W2t = W2^T [512][512], W1t = W1^T [H][512] bf16. colpart: triad_projhead_bwd_slabs(M) slabs of
- * [3][512] fp32 partial column sums (dgamma, dbeta, db1), reduced by triad_sum_slabs.
- * dW2 = dy^T ln, dW1 = dy1^T h and db2 = colsum(dy) are the caller's (split-K GEMM, triad_colsum). */
-int triad_projhead_bwd_slabs(int M);
-int triad_projhead_bwd(const void* dy, int M, int H, const void* W2t, const void* W1t, const void* y1,
-                       const float* mean, const float* rstd, const float* gamma, void* dy1, void* dh, long long ldh,
-                       float* colpart, hipStream_t stream);
+/* Projection head on row-panel GEMMs (model.py:32-34,68 / 81-83,116 / 253-255,326 under bf16
+ * autocast; csrc/rowgemm.hip): a workgroup owns 128 token rows x all 512 columns, so the LayerNorm
+ * and its backward run in the GEMM epilogues. Weights are pre-arranged in MFMA-fragment order:
+ * triad_wpack(W, K, Bp) for C = A W^T with W [512][K] bf16 (Bp: K * 512 bf16). Outputs have
+ * triad_rowpanel_count(M) * 128 rows (rows >= M written as zeros).
+ *   ln_fwd: y1 = bf16(h W1^T + b1), mean / rstd (fp32, biased variance + eps) of y1's rows,
+ *           ln = bf16((y1 - mean) rstd gamma + beta); h row r at
+ *           h + (r / n_per) * bstride + (r % n_per) * lda (a strided view read in place);
+ *   rowgemm_bias: C = bf16(A W^T + bias) (projection2);
+ *   ln_bwd: dln = bf16(dy W2) (W2p = triad_bfrag_pack16(W2, 16, 1, .)), dy1 = bf16(rstd (g -
+ *           mean(g) - xh mean(g xh))), g = dln gamma, and part [panels][3][512] column sums of
+ *           dln xh (dgamma), dln (dbeta), dy1 (db1) per panel (reduce with triad_sum_slabs).
+ * b1 / b2 fp32 holding bf16 values (autocast casts the bias), gamma / beta fp32. */
+int triad_wpack(const void* W, int K, void* Bp, hipStream_t stream);
+int triad_rowpanel_count(long long M);
+int triad_projhead_ln_fwd(const void* h, long long M, int H, long long lda, long long n_per, long long bstride,
+                          const void* W1p, const float* b1, const float* gamma, const float* beta, float eps, void* y1,
+                          void* ln, float* mean, float* rstd, hipStream_t stream);
+int triad_rowgemm_bias(const void* A, long long M, int K, long long lda, const void* Bp, const float* bias, void* C,
+                       hipStream_t stream);
+int triad_projhead_ln_bwd(const void* dy, long long M, const void* W2p, const void* y1, const float* mean,
+                          const float* rstd, const float* gamma, void* dy1, float* part, hipStream_t stream);
 
 /* LayerNorm(512) forward of the library-GEMM projection head (model.py:68/116/326 under
  * autocast): ln = bf16((y1 - mean) rstd gamma + beta) over bf16 y1 [M][512], fp32 statistics
@@ -224,20 +218,18 @@ int triad_ln_fwd(const void* y1, int M, const float* gamma, const float* beta, f
 int triad_ln_bwd3(const void* dln, const void* y1, const float* mean, const float* rstd, const float* gamma, int M,
                   void* dy1, float* part, int nblocks, hipStream_t stream);
 
-/* LayerNorm(512) backward: dy1 (bf16) from dln (fp32), y1, mean, rstd, gamma; per-block
- * column partials of dgamma / dbeta in dgb_part [nblocks][2][512]. */
-int triad_ln_bwd(const float* dln, const void* y1, const float* mean, const float* rstd, const float* gamma, int M,
-                 void* dy1, float* dgb_part, int nblocks, hipStream_t stream);
-
 /* out[c] = alpha * sum_r X[r][c] over bf16 X [rows][ld] (cols % 8 == 0), fp32 or bf16 out, at HBM rate:
  * row slices x 8-column 16-byte loads, partials in part (triad_colsum_splits(rows, cols) * cols floats). */
 int triad_colsum_splits(long long rows, int cols);
 int triad_colsum(const void* X, long long rows, int cols, long long ld, float* part, float alpha, int out_bf16,
                  void* out, hipStream_t stream);
 
-/* The same column sums with the rows staged by 16-byte LDS-DMA (cols % 256 == 0): the form the
- * step's bias gradients use (beside concurrent streams' GEMMs, plain-load column sums returned
- * disturbed values). part: triad_colsum_dma_splits(rows, cols) * cols floats. */
+/* The same column sums with the rows staged by 16-byte LDS-DMA (cols % 8 == 0, X 16-byte aligned;
+ * the last 256-column tile masked): the form EVERY column sum of the step uses -- the bias
+ * gradients of the heads and backbones, SpecAugment's masked_spec_embed (beside concurrent
+ * streams' GEMMs, plain-load column sums returned disturbed values; reference:
+ * autograd's bias gradients of model.py:32-34 / 81-83 / 253-255 and the backbones' Linear layers).
+ * part: triad_colsum_dma_splits(rows, cols) * cols floats. */
 int triad_colsum_dma_splits(long long rows, int cols);
 int triad_colsum_dma(const void* X, long long rows, int cols, long long ld, float* part, float alpha, int out_bf16,
                      void* out, hipStream_t stream);

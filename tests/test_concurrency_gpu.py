@@ -1,9 +1,10 @@
-"""Our kernels' results must not depend on what else shares the CUs (the opt-in concurrent step
+"""Our kernels' results must not depend on what else shares the CUs (the default concurrent step
 runs three backbone streams). Regression test of the round-2 nondeterminism: the HuBERT conv-0 +
 GroupNorm + GELU kernel (triad_c0gn_fwd) returned wrong values in lanes 48-63 whenever a 128 x 128
 MFMA GEMM workgroup (triad_gemm_bf16 form 1) shared its CU, until round 3 changed its weight loads
 and dropped packed-FP32 ops library-wide (which of the two mattered is not established, DESIGN.md
-§2b; PyTorch's bf16 reductions remain victims, hence the serial default). Every output buffer
+§2b; plain-load bf16 column-sum reductions were victims, so every column sum of the step now reads
+its rows by LDS-DMA). Every output buffer
 of c0gn, computed on a side stream while the GEMM runs on the main stream, must equal the quiet
 run bit for bit (tools/concurrency_repro.py has the wider matrix of kernel pairs)."""
 import pytest

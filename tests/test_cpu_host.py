@@ -157,11 +157,11 @@ def test_packed_tile_gemm_and_patch_reject_bad_arguments():
         build.build()
     lib = _lib.load()
     fake = 4096  # never dereferenced: validation fails first
-    assert lib.triad_bfrag_pack(fake, 0, 0, fake, None) == 1001                     # no k tiles
-    assert lib.triad_bfrag_pack(None, 4, 0, fake, None) == 1001                     # no B
-    assert lib.triad_tile_gemm_packed(fake, 8, 0, fake, 200, 8, fake, 1, None, fake, None) == 1001  # M % 128
-    assert lib.triad_tile_gemm_packed(fake, 8, 0, fake, 256, 8, fake, 2, None, fake, None) == 1001  # no slabs
-    assert lib.triad_tile_gemm_packed_slabs(fake, 8, 1, fake, 256, 0, 1, fake, None) == 1001      # nkt = 0
+    assert lib.triad_bfrag_pack16(fake, 0, 0, fake, None) == 1001                   # no k tiles
+    assert lib.triad_bfrag_pack16(None, 4, 0, fake, None) == 1001                   # no B
+    assert lib.triad_tile_gemm_packed16(fake, 8, 0, fake, 200, 8, fake, 1, None, fake, None) == 1001  # M % 128
+    assert lib.triad_tile_gemm_packed16(fake, 8, 0, fake, 256, 8, fake, 2, None, fake, None) == 1001  # no slabs
+    assert lib.triad_tile_gemm_packed16_slabs(fake, 8, 1, fake, 256, 0, 1, fake, None) == 1001      # nkt = 0
     # dS patch: CT too small for Bk samples of Nk_pad keys; Bk * R past 2^31 (32-bit index math)
     assert lib.triad_dS_patch(fake, 4, 256, 256, 32, 8, 8, 64, 60, 0, fake, fake, fake, fake, 1.0, None, 0.0,
                               fake, 1024, None) == 1001
@@ -188,10 +188,13 @@ def test_round4_entry_points_reject_bad_arguments():
                                            1 | 8, None) == 1001
     assert lib.triad_gemm_bf16_splitk_form(fake, 512, 0, fake, 768, 0, 512, 768, 65536, 16, None, fake, fake, 0,
                                            5, None) == 1001
-    # LDS-DMA column sums: 256-column tiles only, scratch required
-    assert lib.triad_colsum_dma(fake, 1024, 640, 640, fake, 1.0, 0, fake, None) == 1001
+    # LDS-DMA column sums: cols % 8, a 16-byte aligned X, ld >= cols and scratch required
+    assert lib.triad_colsum_dma(fake, 1024, 644, 648, fake, 1.0, 0, fake, None) == 1001   # cols % 8
+    assert lib.triad_colsum_dma(fake + 2, 1024, 640, 640, fake, 1.0, 0, fake, None) == 1001   # misaligned
+    assert lib.triad_colsum_dma(fake, 1024, 640, 632, fake, 1.0, 0, fake, None) == 1001   # ld < cols
     assert lib.triad_colsum_dma(fake, 1024, 768, 768, None, 1.0, 0, fake, None) == 1001
     assert lib.triad_colsum_dma_splits(50944, 768) == 171 and lib.triad_colsum_dma_splits(256, 768) == 4
+    assert lib.triad_colsum_dma_splits(50944, 640) == 171 and lib.triad_colsum_dma_splits(50944, 12) == 0
 
 
 def test_side_stream_tables_key_by_device_ordinal():
@@ -243,3 +246,81 @@ def test_select_subset_indices_draws_writes_and_rereads(tmp_path):
     assert json.loads(p.read_text()) == got
     random.seed(12345)   # a different state: the file wins
     assert select_subset_indices(ds, str(p), subset_size=3) == got
+
+
+@pytest.mark.parametrize("rows,cols,view", [(50944, 768, None), (8192, 3072, None), (37, 520, None),
+                                            (200, 776, None), (63, 13, None), (5, 1000, None),
+                                            (100, 768, "wide"), (100, 768, "shifted"), (0, 64, None)])
+def test_bias_grad_takes_only_the_lds_dma_form(rows, cols, view, monkeypatch):
+    """every column sum of the step goes to triad_colsum_dma -- no shape falls back
+    to triad_colsum or a PyTorch reduction (the measured victims of DESIGN.md §2b). Host routing
+    only (the C-ABI calls are recorded, nothing runs): the DMA entry point gets an aligned,
+    row-stride % 8 == 0, cols % 8 == 0 operand; other shapes are first copied into one."""
+    from triad_amd import ops
+    seen = []
+
+    def fake_call(name, *args, **kw):
+        seen.append((name, args))
+        return 2 if name.endswith("_splits") else 0
+
+    monkeypatch.setattr(ops, "call", fake_call)
+    monkeypatch.setattr(ops, "stream_ptr", lambda *a: None)
+    base = torch.zeros(rows, cols + 16, dtype=torch.bfloat16)
+    x = {"wide": base[:, :cols], "shifted": base[:, 1:cols + 1]}.get(view, base[:, :cols].contiguous())
+    out = ops.bias_grad(x, torch.float32)
+    assert out.shape == (cols,)
+    names = {n for n, _ in seen}
+    assert names <= {"triad_colsum_dma_splits", "triad_colsum_dma"}, names
+    if rows:
+        (_, (xp, r, c, ld, *_)), = [s for s in seen if s[0] == "triad_colsum_dma"]
+        assert r == rows and c % 8 == 0 and ld % 8 == 0 and (xp.value or 0) % 16 == 0
+
+
+def test_triad_linear_takes_every_token_count():
+    """No backbone Linear falls back to nn.Linear (whose bias gradient is PyTorch's reduction) for
+    a token count: only widths the split-K GEMM does not tile do (no backbone Linear with a bias)."""
+    from triad_amd import linear
+
+    class _X:   # what _eligible reads of the input
+        is_cuda = True
+
+        def __init__(self, n, k):
+            self.shape = (n, k)
+
+        def numel(self):
+            return self.shape[0] * self.shape[1]
+
+    lin = torch.nn.Linear(768, 768)
+    orig = torch.is_autocast_enabled, torch.get_autocast_dtype
+    try:
+        torch.is_autocast_enabled = lambda *a: True
+        torch.get_autocast_dtype = lambda *a: torch.bfloat16
+        for n in (1, 63, 100, 4095, 8192, 50944):
+            assert linear._eligible(lin, _X(n, 768)), n
+        assert not linear._eligible(torch.nn.Linear(768, 8), _X(100, 768))
+    finally:
+        torch.is_autocast_enabled, torch.get_autocast_dtype = orig
+
+
+def test_vit_embedder_mirrors_the_reference_surface():
+    """`from model import ViTEmbedder` (model.py:120-205): the constructor's arguments, the
+    attributes the reference reads (model, projection1, layer_norm, projection2,
+    patch_dropout_rate), every parameter trainable, no LoRA, no register tokens by default;
+    patch_dropout leaves the input alone in eval mode / at rate 0 (no GPU needed)."""
+    import inspect
+    import warnings
+    from triad_amd.model import ViTEmbedder
+    sig = inspect.signature(ViTEmbedder.__init__)
+    assert list(sig.parameters)[1:] == ["model_name", "arch", "embedding_dim", "dropout_prob"]
+    assert sig.parameters["arch"].default == "dinov2_vitb14" and sig.parameters["dropout_prob"].default == 0.1
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        emb = ViTEmbedder(arch="dinov2_vits14", embedding_dim=512)
+    names = [n for n, _ in emb.named_parameters()]
+    assert not any("lora" in n for n in names)
+    assert {n.split(".")[0] for n in names} == {"model", "projection1", "layer_norm", "projection2"}
+    assert all(p.requires_grad for p in emb.parameters())
+    assert emb.model.num_register_tokens == 0 and emb.projection1.in_features == 384
+    assert emb.patch_dropout_rate == 0.1
+    x = torch.zeros(2, 5, 512)
+    assert emb.eval().patch_dropout(x, 0.1) is x and emb.train().patch_dropout(x, 0) is x

@@ -170,7 +170,20 @@ def _skips(skip, rank, step):
     return step == 1 and (skip == "both" or (skip == "one" and rank == 1))
 
 
-def _reducer_worker(rank, world, port, wire, q, skip=False):
+class _PerturbedCheck:
+    """A reducer whose check reference differs from what the overlapped reduction saw (its
+    snapshot perturbed in one element): the gate must report it."""
+
+    @staticmethod
+    def make(tdist, *a, **kw):
+        class R(tdist.GradBucketReducer):
+            def _check_reference(self):
+                self._snap_range(self.order[0])[0] += 1e-3
+                super()._check_reference()
+        return R(*a, **kw)
+
+
+def _reducer_worker(rank, world, port, wire, q, skip=False, check=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -180,17 +193,21 @@ def _reducer_worker(rank, world, port, wire, q, skip=False):
         net = _Net()
         params = list(net.parameters())
         space = fo.FlatParamSpace(params, "cpu", shadow=[net.w2])
-        red = tdist.GradBucketReducer(space, bucket_mb=0.01, wire=wire, average=True)   # ~2.6k elems per bucket
-        out = []
+        mk = _PerturbedCheck.make if check == "perturbed" else (lambda t, *a, **kw: t.GradBucketReducer(*a, **kw))
+        red = mk(tdist, space, bucket_mb=0.01, wire=wire, average=True)   # ~2.6k elems per bucket
+        out, checks = [], []
         for step in range(3):
             space.zero_grad(list(range(len(params))))
             x, y = _net_inputs(rank, step)
+            red.check = check is not None and step == 2
             red.begin(accumulate=False)
             ((net(x, skip_w2=_skips(skip, rank, step)) - y) ** 2).mean().backward()
             launched = red.launched_in_backward
             red.finish()
             out.append((space.flat_g.numpy().copy(), launched, list(red.order), space.touched.copy()))
-        q.put((rank, out, len(red.buckets)))
+            checks.append(red.check_result)
+            red.check_result = None
+        q.put((rank, out, len(red.buckets), checks))
     except Exception:
         import traceback
         q.put((rank, "error", traceback.format_exc()))
@@ -260,6 +277,37 @@ def test_overlapped_bucket_reducer_averages_gradients(wire, skip):
                 assert launched >= 1   # overlap: at least one bucket went out during backward
             # (skip, rank 1, step 1: the bucket of the missing gradient heads the launch order, so
             # that rank issues everything at the flush -- in the same order as rank 0)
+
+
+@pytest.mark.parametrize("wire,check", [("fp32", "clean"), ("bf16", "clean"), ("fp32", "perturbed")])
+def test_reducer_check_gate(wire, check):
+    """the reducer's correctness gate (bench.py --gpus N > 1 prints its result).
+    With `check` set for a step, every bucket's pre-reduction gradient is snapshotted, the same
+    buckets are all-reduced again from the snapshots after backward, in the same order, and the
+    two results are compared bit for bit (max over ranks): equal on a clean run (fp32 and bf16
+    wire), and a difference in one element is reported (equal False, its size as max_abs)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reducer_worker, args=(r, world, port, wire, q, False, check)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r[2]
+    for rank in range(world):
+        checks = res[rank][3]
+        assert checks[0] is None and checks[1] is None
+        c = checks[2]
+        assert c["world_size"] == world and c["backend"] == "gloo" and c["buckets"] == res[rank][2]
+        assert c["launched_in_backward"] >= 1
+        if check == "clean":
+            assert c["equal"] and c["max_abs"] == 0.0, c
+        else:
+            assert not c["equal"] and c["max_abs"] > 0, c
 
 
 # ---- world 4: per-rank LayerDrop skips and a staged unfreeze ------------------------------------

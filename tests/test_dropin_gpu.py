@@ -215,3 +215,46 @@ def test_debug_and_fused_paths_agree():
     assert _rel(Ad.grad.cpu(), A2.grad.float().cpu()) < 1e-2
     assert _rel(Vd.grad.cpu(), V2.grad.float().cpu()) < 1e-2
     assert _close(float(m.temperature.grad), float(t2.grad), 1e-3, 1e-6)
+
+
+@pytest.mark.parametrize("name", G.names("dropout"))
+def test_vit_embedder_patch_dropout_matches_reference(name):
+    """ViTEmbedder (model.py:120-205; the non-LoRA visual embedder) drops patches with the same
+    algorithm as ViTLoRAEmbedder (model.py:143-183 == 268-308): against the reference's own
+    patch_dropout outputs (the golden fixtures) with the fixture's keep mask injected."""
+    from triad_amd.model import ViTEmbedder
+    f = G.load(name)
+    emb = ViTEmbedder(arch="dinov2_vits14").to(dev).train()
+    x = G.bf16(f["x"]).to(dev, torch.bfloat16)
+    out = emb.patch_dropout(x, 0.25, torch.from_numpy(f["keep"]))
+    np.testing.assert_array_equal(out.float().cpu().numpy(), G.bf16(f["out"]).numpy())
+    emb.eval()
+    assert emb.patch_dropout(x, 0.25) is x   # eval / drop 0: unchanged (model.py:150-151)
+
+
+def test_vit_embedder_forward_is_backbone_head_dropout():
+    """ViTEmbedder.forward = DINOv2 patch tokens (get_intermediate_layers(x, n=1)[0]) -> projection
+    head (HIP) -> patch dropout (HIP gather), every parameter trainable: against the same steps
+    composed by hand (the head through the oracle's bf16-autocast emulation), and gradients reach
+    the backbone (no frozen base, model.py:136-141)."""
+    from triad_amd.model import ViTEmbedder
+    torch.manual_seed(3)
+    emb = ViTEmbedder(arch="dinov2_vits14", dropout_prob=0.25).to(dev).train()
+    x = torch.randn(3, 3, 224, 224, device=dev)
+    keep = torch.rand(3, 256, generator=torch.Generator().manual_seed(4)) > 0.25
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = emb(x, keep_mask=keep)
+        patches = emb.model.get_intermediate_layers(x, n=1)[0]
+    assert patches.shape == (3, 256, 384)
+    w = [p.detach() for m in (emb.projection1, emb.layer_norm, emb.projection2) for p in m.parameters()]
+    head = ref_cpu.projection_head(patches.detach().float(), *w, amp=True)
+    ref = torch.zeros(3, int(keep.sum(1).max()), 512, device=dev)
+    for b in range(3):
+        kept = keep[b].nonzero().flatten().to(dev)
+        ref[b, :len(kept)] = head[b, kept]
+    assert out.shape == ref.shape and out.dtype == torch.bfloat16
+    np.testing.assert_allclose(out.float().cpu().numpy(), ref.cpu().numpy(), rtol=1.6e-2, atol=2e-2)
+    out.float().sum().backward()
+    assert all(p.requires_grad for p in emb.parameters())
+    assert emb.model.blocks[0].attn.qkv.weight.grad is not None
+    assert float(emb.model.patch_embed.proj.weight.grad.abs().sum()) > 0

@@ -20,8 +20,8 @@ def _rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
-@pytest.mark.parametrize("form", ["fused", "passes"])
-@pytest.mark.parametrize("rows,H", [(130, 768), (256, 384), (64 * 5 + 3, 1024)])
+@pytest.mark.parametrize("form", ["rows", "passes"])
+@pytest.mark.parametrize("rows,H", [(130, 768), (256, 384), (64 * 5 + 3, 1024), (1, 768)])
 def test_projection_head_fwd_bwd(rows, H, form):
     from triad_amd import ops
     torch.manual_seed(rows + H)
@@ -358,15 +358,16 @@ def test_backbone_gemm_vs_fp32(M, N, K, bias, dx):
 
 @pytest.mark.parametrize("rows,cols", [(50944, 768), (8192, 3072), (100, 8), (65536, 512), (7, 2304)])
 def test_colsum_matches_torch(rows, cols):
-    """triad_colsum (bias gradients) against an fp64 torch column sum of the same bf16 matrix."""
-    from triad_amd import ops
+    """The library's plain-load column sum (triad_colsum, C-ABI only: the step no longer calls it,
+    DESIGN.md §2b) against an fp64 torch column sum of the same bf16 matrix."""
+    from triad_amd._lib import call, ptr, stream_ptr
     x = torch.randn(rows, cols, device=dev).to(torch.bfloat16)
     ref = x.double().sum(0)
-    got = ops.colsum(x)
-    assert got.dtype == torch.float32
+    part = torch.empty(call("triad_colsum_splits", rows, cols) * cols, device=dev)
+    got = torch.empty(cols, device=dev)
+    call("triad_colsum", ptr(x), rows, cols, cols, ptr(part), 1.0, 0, ptr(got), stream_ptr())
+    torch.cuda.synchronize()
     assert float((got.double() - ref).abs().max()) <= 1e-5 * float(x.double().abs().sum(0).max()) + 1e-6
-    gb = ops.colsum(x, torch.bfloat16)
-    assert gb.dtype == torch.bfloat16 and torch.allclose(gb.float(), got, rtol=8e-3, atol=1e-2)
 
 
 def test_side_stream_is_one_stream_per_device():
@@ -460,9 +461,10 @@ def test_step_bit_identical_serial_and_concurrent():
     gradient buffers to the serial step, run after run: one serial TriadTrainer step and three
     concurrent ones from identical models / seeds (dropout, LayerDrop and SpecAugment ON) must all
     agree. One attempt, no retry. What makes it hold: every column
-    sum of the step runs on the MFMA GEMM (ops.bias_grad) -- column-sum reductions, ours and
-    PyTorch's, returned disturbed sums beside another stream's GEMMs (21-38 of 80 concurrent
-    steps differing with them, 0 of 490 without, tools/stream_repeat.py)."""
+    sum of the step reads its rows by LDS-DMA (ops.bias_grad -> triad_colsum_dma, every shape) --
+    plain-load column-sum reductions, ours and PyTorch's, returned disturbed sums beside another
+    stream's MFMA + LDS-DMA GEMMs (21-38 of 80 concurrent steps differing with them, 0 of 490 on
+    the GEMM form, 0 of 160 on the LDS-DMA form, tools/stream_repeat.py)."""
     from triad_amd import linear as L
     from triad_amd.model import MultiModalModel, modality_streams_enabled, set_concurrent_streams
     from triad_amd.train import TriadTrainer, split_param_groups
@@ -548,16 +550,15 @@ def test_linear_weight_grad_forms(M, O, K):
     assert _rel(dw.float(), ref) < 4e-3
 
 
-@pytest.mark.parametrize("form", ["dma", "gemm"])
 @pytest.mark.parametrize("rows,cols", [(768, 768), (8192, 2304), (50944, 3072), (200, 768), (37, 512),
-                                       (65536, 512), (1000, 256)])
-def test_bias_grad_forms_match_column_sum(rows, cols, form, monkeypatch):
-    """ops.bias_grad -- the step's column sums by LDS-DMA (triad_colsum_dma, default) or on the
-    split-K MFMA GEMM (x^T . ones) -- against an fp32 torch column sum of the same bf16 matrix,
-    ragged row counts included (the DMA ring's last chunk; shapes the GEMM does not tile take
-    triad_colsum); a strided view (ld > cols) gives the same sums."""
+                                       (65536, 512), (1000, 256), (777, 8), (129, 520), (4096, 1000),
+                                       (63, 13), (5000, 776), (1, 264)])
+def test_bias_grad_matches_column_sum(rows, cols):
+    """ops.bias_grad -- every column sum of the step, by LDS-DMA (triad_colsum_dma) -- against an
+    fp32 torch column sum of the same bf16 matrix: ragged row counts (the DMA ring's last chunk),
+    column counts that are not a multiple of the 256-column tile (the masked last tile) or not of 8
+    (the padded copy); a strided view (ld > cols) and a misaligned view give the same sums."""
     from triad_amd import ops
-    monkeypatch.setenv("TRIAD_DB_FORM", form)
     g = torch.Generator(device=dev).manual_seed(rows + cols)
     x = (torch.randn(rows, cols, device=dev, generator=g) * 0.05).to(torch.bfloat16)
     ref = x.float().sum(0)
@@ -566,6 +567,9 @@ def test_bias_grad_forms_match_column_sum(rows, cols, form, monkeypatch):
         assert got.dtype == dt and got.shape == (cols,)
         tol = 1e-5 if dt == torch.float32 else 8e-3
         assert float((got.float() - ref).norm() / ref.norm()) < tol
-    wide = torch.zeros(rows, cols + 256, device=dev, dtype=torch.bfloat16)
+    wide = torch.zeros(rows, cols + 264, device=dev, dtype=torch.bfloat16)
     wide[:, :cols] = x
     assert torch.equal(ops.bias_grad(wide[:, :cols]), ops.bias_grad(x))
+    shifted = wide[:, 1:cols + 1]          # data_ptr 2 bytes past an aligned row start
+    shifted.copy_(x)
+    assert torch.equal(ops.bias_grad(shifted), ops.bias_grad(x))

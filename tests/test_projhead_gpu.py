@@ -1,5 +1,6 @@
 """Projection head (reference model.py:32-34,68 / 81-83,116 / 253-255,326) at the
-row counts the training step runs, through the default "passes" form the step uses:
+row counts the training step runs, through both forms: "passes" (tiled GEMMs + LayerNorm row
+passes) and "rows" (row-panel GEMMs with the LayerNorm and its backward in the epilogues):
 
   65,536 x 768   visual head, B=256 x 256 patches (before patch dropout)   c3
   50,944 x 768   audio head, B=256 x 199 frames                            c3
@@ -29,10 +30,10 @@ def _rel(a, b):
     return float((a - b).norm() / b.norm().clamp(min=1e-30))
 
 
+@pytest.mark.parametrize("form", ["passes", "rows"])
 @pytest.mark.parametrize("rows,H", [(65536, 768), (50944, 768), (8192, 768), (43808, 1024)])
-def test_projection_head_at_step_rows(rows, H):
+def test_projection_head_at_step_rows(rows, H, form):
     from triad_amd import ops
-    assert ops.PROJHEAD_FORM == "passes"
     torch.manual_seed(rows + H)
     p1, ln, p2 = nn.Linear(H, 512), nn.LayerNorm(512), nn.Linear(512, 512)
     with torch.no_grad():
@@ -44,7 +45,7 @@ def test_projection_head_at_step_rows(rows, H):
     gy = torch.randn(rows, 512, device=dev, generator=g) * 0.01
     # product path
     hd = h.clone().requires_grad_(True)
-    y = ops.projection_head(hd.view(1, rows, H), *mods)
+    y = ops.projection_head(hd.view(1, rows, H), *mods, form=form)
     assert y.dtype == torch.bfloat16 and y.shape == (1, rows, 512)
     y.float().view(rows, 512).backward(gy)
     got = [hd.grad] + [p.grad.detach().clone() for m in mods for p in m.parameters()]
@@ -109,3 +110,29 @@ def test_splitk_xcd_placement_bit_identical(form):
     with pytest.raises(TriadError):
         call("triad_gemm_bf16_splitk_form", ptr(dy), O, 0, ptr(x), K, 0, O, K, M, 12, None, ptr(slabs), ptr(dw), 0,
              form | 8, stream_ptr())
+
+
+def test_rows_form_reads_a_strided_view_in_place():
+    """The row-panel head reads the ViT's patch tokens as they lie -- a strided view of
+    (B, 5 + N, H) behind the CLS / register tokens, model.py:325 -- with two-level row addressing
+    (no packing copy): outputs and every gradient equal, bit for bit, to the same head on a
+    contiguous copy of the view, the gradient landing in the view's rows only."""
+    from triad_amd import ops
+    torch.manual_seed(5)
+    B, N, H = 24, 256, 768
+    p1, ln, p2 = (m.to(dev) for m in (nn.Linear(H, 512), nn.LayerNorm(512), nn.Linear(512, 512)))
+    full = torch.randn(B, 5 + N, H, device=dev).to(torch.bfloat16).requires_grad_(True)
+    gy = (torch.randn(B, N, 512, device=dev) * 0.01).to(torch.bfloat16)
+    y = ops.projection_head(full[:, 5:], p1, ln, p2, form="rows")
+    y.backward(gy)
+    got = [y.detach(), full.grad[:, 5:].clone()] + [p.grad.clone() for m in (p1, ln, p2) for p in m.parameters()]
+    assert float(full.grad[:, :5].abs().max()) == 0.0
+    for m in (p1, ln, p2):
+        for p in m.parameters():
+            p.grad = None
+    hc = full.detach()[:, 5:].contiguous().requires_grad_(True)
+    y2 = ops.projection_head(hc, p1, ln, p2, form="rows")
+    y2.backward(gy)
+    ref = [y2.detach(), hc.grad] + [p.grad for m in (p1, ln, p2) for p in m.parameters()]
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)

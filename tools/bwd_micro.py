@@ -45,31 +45,9 @@ def run(B, Nq, Nk, dk, iters, force_sp=None, form=0):
         print(json.dumps({"check": "packed16 vs ring", "dk": dk, "M": M, "max_rel": rel,
                           "frac_differing": float((d > 0).float().mean())}), flush=True)
         assert rel < 1e-2
-    if form == 9:   # direct-B form: B fragments packed once (timed apart), then triad_tile_gemm_packed
-        Bp = torch.empty(nkt * 32 * 512, dtype=torch.bfloat16, device="cuda")
-        call("triad_bfrag_pack", ptr(Bm), nkt, dk, ptr(Bp), stream_ptr())
-        ref = torch.empty_like(out)
-        call("triad_tile_gemm", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(ref), stream_ptr())
-        call("triad_tile_gemm_packed", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out),
-             stream_ptr())
-        torch.cuda.synchronize()
-        same = bool(torch.equal(out, ref))
-        print(json.dumps({"check": "packed == ring", "dk": dk, "M": M, "bit_identical": same}), flush=True)
-        assert same
-        p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        p0.record()
-        for _ in range(iters):
-            call("triad_bfrag_pack", ptr(Bm), nkt, dk, ptr(Bp), stream_ptr())
-        p1.record()
-        torch.cuda.synchronize()
-        print(json.dumps({"pack_ms": round(p0.elapsed_time(p1) / iters, 4), "dk": dk, "nkt": nkt}), flush=True)
-
     def launch():
         if form == 16:
             call("triad_tile_gemm_packed16", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out),
-                 stream_ptr())
-        elif form == 9:
-            call("triad_tile_gemm_packed", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out),
                  stream_ptr())
         elif form:   # a variant entry point (tools/build_variants.py builds): triad_tile_gemm_form
             call("triad_tile_gemm_form", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), sp, ptr(slabs), ptr(out), form,

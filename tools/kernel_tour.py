@@ -74,9 +74,6 @@ def tile_gemms(out):
             call("triad_tile_gemm", ptr(dS), CT, dk, ptr(Bm), M, nkt, ptr(alpha), splits, ptr(slabs), ptr(c), st)
             out[f"tile-ring-dk{dk}-sp{splits}"] = digest(c)
             Bp = torch.empty(nkt * 32 * 512, dtype=torch.bfloat16, device=dev)
-            call("triad_bfrag_pack", ptr(Bm), nkt, dk, ptr(Bp), st)
-            call("triad_tile_gemm_packed", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), splits, ptr(slabs), ptr(c), st)
-            out[f"tile-packed-dk{dk}-sp{splits}"] = digest(c, Bp)
             call("triad_bfrag_pack16", ptr(Bm), nkt, dk, ptr(Bp), st)
             call("triad_tile_gemm_packed16", ptr(dS), CT, dk, ptr(Bp), M, nkt, ptr(alpha), splits, ptr(slabs),
                  ptr(c), st)
@@ -114,7 +111,7 @@ def projheads(out):
     for H, M in ((768, 8192), (1024, 4096)):
         p1, ln, p2 = torch.nn.Linear(H, 512).to(dev), torch.nn.LayerNorm(512).to(dev), torch.nn.Linear(512, 512).to(dev)
         h = feats((M // 64, 64, H), 32, 1.0).requires_grad_(True)
-        for form in ("passes", "fused"):
+        for form in ("passes", "rows"):
             for p in (*p1.parameters(), *ln.parameters(), *p2.parameters()):
                 p.grad = None
             h.grad = None

@@ -12,8 +12,9 @@ import json
 import os
 import sys
 
-CASES = (("visual", 65536, 768), ("audio", 50944, 768), ("text", 8192, 768), ("c5-visual", 43808, 1024))
-FORMS = tuple(os.environ.get("TRIAD_PROJHEAD_FORMS", "fused,passes").split(","))
+CASES = (("visual", 65536, 768), ("audio", 50944, 768), ("text", 8192, 768), ("c5-visual", 43808, 1024),
+         ("visual-view", 65536, 768))   # the ViT's patch tokens as a strided view of (256, 261, 768)
+FORMS = tuple(os.environ.get("TRIAD_PROJHEAD_FORMS", "rows,passes").split(","))
 # the trainer keeps bf16 shadows of projection1 / projection2 (round 4, train.py bf16_weight_params):
 # bf16 weights are the product configuration; fp32 = the round-2 / round-3 figures
 WDTYPE = os.environ.get("TRIAD_PROJHEAD_WDTYPE", "bf16")
@@ -36,8 +37,12 @@ def run(iters):
             p1, ln, p2 = nn.Linear(H, 512).to(dev), nn.LayerNorm(512).to(dev), nn.Linear(512, 512).to(dev)
             if WDTYPE == "bf16":
                 p1, p2 = p1.to(torch.bfloat16), p2.to(torch.bfloat16)
-            h = torch.randn(M, H, device=dev).to(torch.bfloat16).requires_grad_(True)
-            gy = (torch.randn(M, 512, device=dev) * 0.01).to(torch.bfloat16)
+            if name.endswith("-view"):
+                full = torch.randn(M // 256, 261, H, device=dev).to(torch.bfloat16).requires_grad_(True)
+                h = full[:, 5:]
+            else:
+                h = torch.randn(M, H, device=dev).to(torch.bfloat16).requires_grad_(True)
+            gy = (torch.randn(*h.shape[:-1], 512, device=dev) * 0.01).to(torch.bfloat16)
             for _ in range(2):   # warm-up (library heuristics, allocator)
                 ops.projection_head(h, p1, ln, p2, form=form).backward(gy)
             outs = []
@@ -48,7 +53,7 @@ def run(iters):
             mark(seg + 1)
             for y in outs:
                 y.backward(gy)
-                h.grad = None   # autograd then stores each gradient instead of adding it (no add kernels)
+                (full if name.endswith("-view") else h).grad = None   # stored, not added (no add kernels)
                 for mod in (p1, ln, p2):
                     for prm in mod.parameters():
                         prm.grad = None

@@ -34,9 +34,6 @@ SIGNATURES = {
     "triad_dtemp_finalize": [vp, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp],
     "triad_tile_gemm": [vp, i64, i32, vp, i32, i32, vp, i32, vp, vp, vp],
     "triad_tile_gemm_slabs": [vp, i64, i32, vp, i32, i32, i32, vp, vp],
-    "triad_bfrag_pack": [vp, i32, i32, vp, vp],
-    "triad_tile_gemm_packed": [vp, i64, i32, vp, i32, i32, vp, i32, vp, vp, vp],
-    "triad_tile_gemm_packed_slabs": [vp, i64, i32, vp, i32, i32, i32, vp, vp],
     "triad_bfrag_pack16": [vp, i32, i32, vp, vp],
     "triad_tile_gemm_packed16": [vp, i64, i32, vp, i32, i32, vp, i32, vp, vp, vp],
     "triad_tile_gemm_packed16_slabs": [vp, i64, i32, vp, i32, i32, i32, vp, vp],
@@ -44,10 +41,11 @@ SIGNATURES = {
     "triad_gemm_bf16_bias": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, vp],
     "triad_gemm_bf16_splitk": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp],
     "triad_gemm_bf16_splitk_form": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp],
-    "triad_projhead_fwd": [vp, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, i64, vp, vp, vp, vp, vp],
-    "triad_projhead_bwd_slabs": [i32],
-    "triad_projhead_bwd": [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp],
-    "triad_ln_bwd": [vp, vp, vp, vp, vp, i32, vp, vp, i32, vp],
+    "triad_wpack": [vp, i32, vp, vp],
+    "triad_rowpanel_count": [i64],
+    "triad_projhead_ln_fwd": [vp, i64, i32, i64, i64, i64, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp],
+    "triad_rowgemm_bias": [vp, i64, i32, i64, vp, vp, vp, vp],
+    "triad_projhead_ln_bwd": [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp],
     "triad_ln_fwd": [vp, i32, vp, vp, f32, vp, vp, vp, vp],
     "triad_ln_bwd3": [vp, vp, vp, vp, vp, i32, vp, vp, i32, vp],
     "triad_sum_slabs": [vp, i32, i64, vp, i32, vp, vp],
@@ -106,7 +104,7 @@ RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_l
             "triad_posconv_dw_part_bytes": C.c_longlong,
             "triad_lora_tn_blocks": C.c_int, "triad_dropaddln_bwd_blocks": C.c_int,
             "triad_colsum_splits": C.c_int, "triad_colsum_dma_splits": C.c_int, "triad_dense_nparts": C.c_int,
-            "triad_projhead_bwd_slabs": C.c_int}
+            "triad_rowpanel_count": C.c_int}
 
 
 

@@ -19,6 +19,8 @@
 // once); wave w owns columns [64w, 64w+64): 4 x 2 tiles of 32 x 32 accumulators; A and B
 // through a 4-slot LDS ring by 16-byte LDS-DMA with source-side swizzles (conflict-free reads).
 // Optional split-K over grid.y with fp32 slabs.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -173,189 +175,23 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_ring_kernel(const bf16* __re
     }
 }
 
-// ---- direct-B form ----------------------------------------------------------------------------
+// ---- direct-B form on v_mfma_f32_16x16x32_bf16 (the product backward GEMM) ----------------------
 // Wave w only ever multiplies columns [64w, 64w + 64) of B, so B needs no LDS: its fragments are
-// pre-arranged once per backward (bfrag_pack_kernel: the exact bf16x8 each lane takes from the
-// swizzled LDS image above, written out) and each wave streams its own 4 KB per k tile straight
-// into registers with four coalesced 16-byte loads, stages ahead. Only A (8 KB per tile,
-// shared by all eight waves) goes through LDS: one LDS-DMA piece per wave per tile instead of
-// five, and no B fragment reads from LDS.
-//   packed B: k tile kt, wave w, chunk u = 2 s + n (k-step s, 32-column block n):
-//             bf16x8 of lane L at ((kt * 8 + w) * 4 + u) * 512 + L * 8
-// KS k tiles (32 deep each) per stage and one workgroup barrier per stage; DD stages in flight
-// ahead of the one being multiplied (A ring slots = B register ring depth = DD + 1). Measured per
-// GEMM (tools/bwd_micro.py, profiles/r03_tile_gemm_db_ab.log): dQ KS = 1, DD = 3; dK KS = 2,
-// DD = 2 (the transposed A reads favour half the barriers; dQ loses 6 % with them).
-
-template <bool DK>
-__global__ __launch_bounds__(512) void bfrag_pack_kernel(const bf16* __restrict__ B, bf16* __restrict__ Bp) {
-  __shared__ __attribute__((aligned(16))) bf16 img[TBK * TBN];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 5, q4 = (lane & 15) >> 2;
-  const long long kt = blockIdx.x;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int k = wave * 4 + r;
-    glds16(B + (kt * TBK + k) * TBN + (lane ^ ((k & 3) << 2)) * 8, img + k * TBN);
-  }
-  lds_dma_barrier();
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int n0 = wave * 64 + n * 32;
-      const bf16x8 f = DK ? bfrag(img, 16 * s + 8 * h + q4, 4, n0, lane) : bfrag(img, 16 * s + 4 * h + q4, 8, n0, lane);
-      *(bf16x8*)(Bp + ((kt * 8 + wave) * 4 + 2 * s + n) * 512 + lane * 8) = f;
-    }
-}
-
-// 16-byte global load hidden from hipcc's waitcnt bookkeeping (it would otherwise drain vmcnt(0)
-// at the first use, glds in flight): the caller's counted s_waitcnt vmcnt before the barrier
-// retires it. The destination registers are only ever read after that wait -- and must not be
-// copied before it: the register ring is indexed statically (the stage loop is unrolled by its
-// depth) so each slot keeps one physical register range across the loop; checked on hipcc's
-// output by tests/test_isa_cpu.py (nothing touches a ring register in the straight-line code
-// after its load) and on the GPU by test_tile_gemm_packed_bit_identical_to_ring.
-__device__ __forceinline__ bf16x8 gload16(const bf16* p) {
-  bf16x8 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-
-// one stage: k tiles kt .. kt + KS - 1 (clamped to kt_last: a short last stage re-loads its last
-// tile, so every stage issues exactly 5 KS vm ops per wave -- 4 B loads + 1 A piece per tile --
-// and the counted waits hold)
-template <bool DK, int KS, bool K16 = false>
-__device__ __forceinline__ void db_stage(const bf16* __restrict__ Dt, long long CT, const bf16* __restrict__ Bp,
-                                         int mt0, int kt, int kt_last, bf16* adst, bf16x8 (&bq)[4 * KS], int wave,
-                                         int lane) {
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    const int ktk = min(kt + k, kt_last);
-    const bf16* src = Bp + ((long long)ktk * 8 + wave) * 2048 + lane * 8;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) bq[4 * k + u] = gload16(src + u * 512);
-    const int t = wave >> 1, half = wave & 1;
-    const int pos = half * 64 + lane;
-    const int c = DK ? (K16 ? swz_k16(pos) : swz_k(pos)) : swz_q(pos);
-    const long long tile = DK ? ((long long)ktk * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + ktk);
-    glds16(Dt + tile * 1024 + c * 8, adst + k * 4096 + t * 1024 + half * 512);
-  }
-}
-
-template <int OPS>
-__device__ __forceinline__ void db_wait(int younger) {
-  if (younger >= 3) TRIAD_VMCNT(3 * OPS);
-  else if (younger == 2) TRIAD_VMCNT(2 * OPS);
-  else if (younger == 1) TRIAD_VMCNT(OPS);
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <bool DK, bool SLAB, int KS, int DD>
-__global__ __launch_bounds__(512, 1) void tile_gemm_db_kernel(const bf16* __restrict__ Dt, long long CT,
-                                                              const bf16* __restrict__ Bp, int M, int nkt_total,
-                                                              int kt_per_split, const float* __restrict__ alpha_p,
-                                                              void* __restrict__ Cout) {
-  static_assert(DD >= 1 && DD <= 4 && 5 * KS * (DD - 1) <= 63, "stage shape");
-  constexpr int NB = DD + 1;
-  __shared__ __attribute__((aligned(16))) bf16 lds[NB * KS * 4096];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h = lane >> 5, l32 = lane & 31;
-  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-  const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
-  const int m0 = swz * TBM, mt0 = m0 / 32;
-  const int kt0 = blockIdx.y * kt_per_split;
-  const int nkt = __builtin_amdgcn_readfirstlane(min(kt_per_split, nkt_total - kt0));
-  const int kt_last = kt0 + nkt - 1;
-  const int nst = (nkt + KS - 1) / KS;
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) acc[t][n] = (f32x16){};
-
-  bf16x8 bq[NB][4 * KS];
-#pragma unroll
-  for (int p = 0; p < DD; ++p)
-    if (p < nst) db_stage<DK, KS>(Dt, CT, Bp, mt0, kt0 + p * KS, kt_last, lds + p * KS * 4096, bq[p], wave, lane);
-  for (int st0 = 0; st0 < nst; st0 += NB) {
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int st = st0 + u;
-      if (st >= nst) break;
-      db_wait<5 * KS>(min(DD - 1, nst - 1 - st));   // uniform: stages st+1 .. stay in flight
-      __syncthreads();
-      const bool pf = st + DD < nst;
-#pragma unroll
-      for (int k = 0; k < KS; ++k) {
-        if (st * KS + k >= nkt) break;       // a short last stage
-        const bf16* As = lds + (u * KS + k) * 4096;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          bf16x8 af[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const bf16* tile = As + t * 1024;
-            if (!DK) {
-              af[t] = *(const bf16x8*)(tile + swz_q(2 * l32 + 64 * h + s) * 8);
-            } else {
-              const int a = 2 * (g & 1) + (p4 >> 1), hh = p4 & 1;
-              s16x4* rp = (s16x4*)&af[t];
-#pragma unroll
-              for (int tt = 0; tt < 2; ++tt) {
-                const int qry = 16 * s + 8 * h + 4 * tt + q4;
-                const int c = (qry + 32 * hh) * 2 + (a >> 1);
-                rp[tt] = lds_tr16(tile + swz_k(c) * 8 + 4 * (a & 1));
-              }
-            }
-          }
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int n = 0; n < 2; ++n) acc[t][n] = mfma32(af[t], bq[u][4 * k + 2 * s + n], acc[t][n]);
-          if (k == 0 && s == 0 && pf) {
-            // the stage DD ahead: its A slots were last read before this stage's barrier
-            __builtin_amdgcn_sched_barrier(0);
-            db_stage<DK, KS>(Dt, CT, Bp, mt0, kt0 + (st + DD) * KS, kt_last,
-                         lds + ((u + DD) % NB) * KS * 4096, bq[(u + DD) % NB], wave, lane);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-    }
-  }
-
-  const float alpha = SLAB ? 1.f : *alpha_p;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int col = wave * 64 + n * 32 + l32;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = m0 + t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        const float val = alpha * acc[t][n][v];
-        if (SLAB) ((float*)Cout)[((size_t)blockIdx.y * M + m) * TBN + col] = val;
-        else ((bf16*)Cout)[(size_t)m * TBN + col] = (bf16)val;
-      }
-    }
-}
-
-// ---- v_mfma_f32_16x16x32_bf16 form of the direct-B GEMMs -----------------------------------------
-// The same workgroup (8 waves, 128 rows x 512 columns, wave w owns columns [64w, 64w + 64)), the
-// same A stream (dS tiles through the LDS ring by one LDS-DMA piece per wave per k tile) and the
-// same register-streamed B, but each wave's 128 x 64 output is 8 x 4 blocks of 16 x 16 computed by
-// v_mfma_f32_16x16x32_bf16 (32 per 32-deep k tile instead of 16 v_mfma_f32_32x32x16): the shape
-// the microarchitecture guide measures at ~1.12-1.15x the FLOP/s of 32x32x16 on random data at
-// the clock the chip holds under load (MI355X_MICROARCH.md, 'DVFS give-back' item 7).
+// pre-arranged once per backward (bfrag_pack16_kernel) and each wave streams its own 4 KB per k
+// tile straight into registers with four coalesced 16-byte loads, stages ahead. Only A (dS, 8 KB
+// per tile, shared by all eight waves) goes through LDS: one LDS-DMA piece per wave per tile.
+// Each wave's 128 x 64 output is 8 x 4 blocks of 16 x 16 computed by v_mfma_f32_16x16x32_bf16 (32
+// per 32-deep k tile): the shape the microarchitecture guide measures at ~1.12-1.15x the FLOP/s of
+// 32x32x16 at the clock the chip holds under load (MI355X_MICROARCH.md, 'DVFS give-back' item 7).
 //   A fragment (row block rb, lane l): query row r = 16 (rb & 1) + (l & 15) of tile rb >> 1, k
 //   chunk kc = l >> 4 = 16-byte chunk (hh = kc & 1, j = kc >> 1) of the stored dS row, i.e. keys
 //   16 j + 8 (i >> 2) + 4 hh + (i & 3), i = 0..7 -- the forward's accumulator order, read as is;
 //   B fragment (column block cb): the same 8 keys of column 64 w + 16 cb + (l & 15), packed once
 //   by bfrag_pack16_kernel at ((kt * 8 + w) * 4 + cb) * 512 + l * 8.
+// dK (DK = true): A = dS^T, rows = keys, k = queries. Row block rb = 16 keys: tile rb >> 1, key
+// half kb = rb & 1; lane l takes keys 16 kb + (l & 15) and the queries 8 (l >> 4) .. + 7 of the
+// k tile by two ds_read_b64_tr_b16 (4 query rows each) -- natural query order, so the packed Q
+// fragment of lane l is Q[8 (l >> 4) + i][col], i = 0..7.
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -383,18 +219,58 @@ __global__ __launch_bounds__(512) void bfrag_pack16_kernel(const bf16* __restric
   }
 }
 
-// dK (DK = true): A = dS^T, rows = keys, k = queries. Row block rb = 16 keys: tile rb >> 1, key
-// half kb = rb & 1; lane l takes keys 16 kb + (l & 15) and the queries 8 (l >> 4) .. + 7 of the
-// k tile by two ds_read_b64_tr_b16 (4 query rows each) -- natural query order, so the packed Q
-// fragment of lane l is Q[8 (l >> 4) + i][col], i = 0..7.
-template <bool DK, bool SLAB, int KS, int DD>
+// B fragment load: an ORDINARY 16-byte load that hipcc counts (round 5). Rounds 3-4
+// hid it in an inline-asm global_load_dwordx4 with a "=v" output so hipcc would not drain the
+// prefetches at the first use; hipcc then took the destination as written at ;;#ASMEND, and a
+// build with more register pressure (the TRIAD_LDS_CHECK printf build) spilled ring registers
+// right after their loads and reused them while the loads were in flight: the aperture violation
+// of gpurun_out/r04d_py5.log (tile_gemm_db_kernel<true,true,2,2>, private_seg_size 120; its
+// -save-temps output shows `global_load_dwordx4 v[134:137]` followed by a spill of v[134:137] and
+// three more loads into the same range). A counted load is correct under ANY register allocation:
+// hipcc waits for it before any copy, spill or reuse. What made hipcc drain the ring before was
+// control flow, not the load: a conditional prologue / prefetch and a `break` out of the unrolled
+// stage loop let the loop header merge paths with different loads in flight. So: every stage
+// issues the same loads (a stage past the end re-loads the last tile, clamped in-bounds, into a
+// slot nobody reads again), the main loop runs whole groups of NB stages with no exit inside, and
+// the last nst % NB stages follow it in straight-line code. The packed B pointer is not
+// __restrict__: with it, hipcc sank each prefetch down to the stage that consumes it (the
+// LDS-DMA asm in between no longer ordered it). tests/test_isa_cpu.py checks the emitted waits.
+__device__ __forceinline__ bf16x8 bload16(const bf16* p) { return *(const bf16x8*)p; }
+
+// one stage = one 32-deep k tile kt (clamped to kt_last): 4 B loads + 1 A LDS-DMA piece per wave
+template <bool DK>
+__device__ __forceinline__ void db_stage(const bf16* __restrict__ Dt, long long CT, const bf16* Bp, int mt0, int kt,
+                                         int kt_last, bf16* adst, bf16x8 (&bq)[4], int wave, int lane) {
+  const int ktk = min(kt, kt_last);
+  const bf16* src = Bp + ((long long)ktk * 8 + wave) * 2048 + lane * 8;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) bq[u] = bload16(src + u * 512);
+  const int t = wave >> 1, half = wave & 1;
+  const int pos = half * 64 + lane;
+  const int c = DK ? swz_k16(pos) : swz_q(pos);
+  const long long tile = DK ? ((long long)ktk * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + ktk);
+  glds16(Dt + tile * 1024 + c * 8, adst + t * 1024 + half * 512);
+}
+
+template <int U, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (U < N) {
+    f(std::integral_constant<int, U>{});
+    static_for<U + 1, N>(f);
+  }
+}
+
+// DD stages in flight ahead of the one being multiplied (A ring slots = B register ring depth =
+// NB = DD + 1); one workgroup barrier per stage. DD = 3 for dQ and dK (dK with two k tiles per
+// stage, as its 32x32x16 form had, would spill).
+template <bool DK, bool SLAB, int DD>
 __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __restrict__ Dt, long long CT,
-                                                                 const bf16* __restrict__ Bp, int M, int nkt_total,
+                                                                 const bf16* Bp, int M, int nkt_total,
                                                                  int kt_per_split, const float* __restrict__ alpha_p,
                                                                  void* __restrict__ Cout) {
-  static_assert(DD >= 1 && DD <= 4 && 5 * KS * (DD - 1) <= 63, "stage shape");
+  static_assert(DD >= 1 && DD <= 4 && 5 * (DD - 1) <= 63, "stage shape");
   constexpr int NB = DD + 1;
-  __shared__ __attribute__((aligned(16))) bf16 lds[NB * KS * 4096];
+  __shared__ __attribute__((aligned(16))) bf16 lds[NB * 4096];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, kc = lane >> 4, q4 = l16 >> 2, p4 = l16 & 3;
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -402,9 +278,8 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
   const int swz = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
   const int m0 = swz * TBM, mt0 = m0 / 32;
   const int kt0 = blockIdx.y * kt_per_split;
-  const int nkt = __builtin_amdgcn_readfirstlane(min(kt_per_split, nkt_total - kt0));
-  const int kt_last = kt0 + nkt - 1;
-  const int nst = (nkt + KS - 1) / KS;
+  const int nst = __builtin_amdgcn_readfirstlane(min(kt_per_split, nkt_total - kt0));   // k tiles = stages
+  const int kt_last = kt0 + nst - 1;
   // this lane's A reads inside a 32-row tile, per row half (dQ: one chunk; dK: two transposed
   // 4-row reads) -- offsets in elements
   int aoff[2][2];
@@ -429,47 +304,54 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = (f32x4){};
 
-  bf16x8 bq[NB][4 * KS];
+  bf16x8 bq[NB][4];
+  // stage st in ring slot u = st % NB: wait for its A piece (the counted vmcnt: the DD - 1 younger
+  // stages, 5 ops each, stay in flight; hipcc waits for its B loads itself), barrier, 32 MFMAs with
+  // the prefetch of stage st + DD (into slot (u + DD) % NB, read for the last time by stage st - 1,
+  // before this barrier) issued after the first two row blocks
+  auto stage = [&](auto U, int st) {
+    constexpr int u = decltype(U)::value;
+    TRIAD_VMCNT(5 * (DD - 1));
+    __syncthreads();
+    const bf16* As = lds + u * 4096;
+    bf16x8 af[8];
 #pragma unroll
-  for (int p = 0; p < DD; ++p)
-    if (p < nst) db_stage<DK, KS, true>(Dt, CT, Bp, mt0, kt0 + p * KS, kt_last, lds + p * KS * 4096, bq[p], wave, lane);
-  for (int st0 = 0; st0 < nst; st0 += NB) {
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int st = st0 + u;
-      if (st >= nst) break;
-      db_wait<5 * KS>(min(DD - 1, nst - 1 - st));
-      __syncthreads();
-      const bool pf = st + DD < nst;
-#pragma unroll
-      for (int k = 0; k < KS; ++k) {
-        if (st * KS + k >= nkt) break;
-        const bf16* As = lds + (u * KS + k) * 4096;
-        bf16x8 af[8];
-#pragma unroll
-        for (int rb = 0; rb < 8; ++rb) {
-          const bf16* tile = As + (rb >> 1) * 1024;
-          if (!DK) {
-            af[rb] = *(const bf16x8*)(tile + aoff[rb & 1][0]);
-          } else {
-            s16x4* rp = (s16x4*)&af[rb];
-            rp[0] = lds_tr16(tile + aoff[rb & 1][0]);
-            rp[1] = lds_tr16(tile + aoff[rb & 1][1]);
-          }
-        }
-#pragma unroll
-        for (int rb = 0; rb < 8; ++rb) {
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = mfma16(af[rb], bq[u][4 * k + cb], acc[rb][cb]);
-          if (k == 0 && rb == 1 && pf) {
-            __builtin_amdgcn_sched_barrier(0);
-            db_stage<DK, KS, true>(Dt, CT, Bp, mt0, kt0 + (st + DD) * KS, kt_last, lds + ((u + DD) % NB) * KS * 4096,
-                             bq[(u + DD) % NB], wave, lane);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
+    for (int rb = 0; rb < 8; ++rb) {
+      const bf16* tile = As + (rb >> 1) * 1024;
+      if (!DK) {
+        af[rb] = *(const bf16x8*)(tile + aoff[rb & 1][0]);
+      } else {
+        s16x4* rp = (s16x4*)&af[rb];
+        rp[0] = lds_tr16(tile + aoff[rb & 1][0]);
+        rp[1] = lds_tr16(tile + aoff[rb & 1][1]);
       }
     }
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = mfma16(af[rb], bq[u][cb], acc[rb][cb]);
+      if (rb == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        db_stage<DK>(Dt, CT, Bp, mt0, kt0 + st + DD, kt_last, lds + ((u + DD) % NB) * 4096, bq[(u + DD) % NB],
+                     wave, lane);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  if (nst > 0) {   // (an empty split leaves its slab zero)
+    static_for<0, DD>([&](auto P) {
+      constexpr int p = decltype(P)::value;
+      db_stage<DK>(Dt, CT, Bp, mt0, kt0 + p, kt_last, lds + p * 4096, bq[p], wave, lane);
+    });
+    const int ngroups = nst / NB;
+    for (int g = 0; g < ngroups; ++g)
+      static_for<0, NB>([&](auto U) { stage(U, g * NB + decltype(U)::value); });
+    const int rem = nst - ngroups * NB, base = ngroups * NB;
+    static_for<0, NB - 1>([&](auto U) {
+      if (decltype(U)::value < rem) stage(U, base + decltype(U)::value);
+    });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the past-the-end stages' LDS-DMA lands before exit
   }
 
   const float alpha = SLAB ? 1.f : *alpha_p;
@@ -491,50 +373,6 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
 }  // namespace
 
 extern "C" {
-
-// Packed B fragments for the direct-B GEMM form: B [nkt * 32][512] bf16 -> Bp (same size).
-int triad_bfrag_pack(const void* B, int nkt, int dk, void* Bp, hipStream_t stream) {
-  if (nkt <= 0 || !B || !Bp) return TRIAD_EINVAL;
-  if (dk) hipLaunchKernelGGL(bfrag_pack_kernel<true>, dim3(nkt), dim3(512), 0, stream, (const bf16*)B, (bf16*)Bp);
-  else hipLaunchKernelGGL(bfrag_pack_kernel<false>, dim3(nkt), dim3(512), 0, stream, (const bf16*)B, (bf16*)Bp);
-  TRIAD_CHECK_LAUNCH();
-  return TRIAD_OK;
-}
-
-// triad_tile_gemm over packed B fragments (triad_bfrag_pack of the same B and dk).
-int triad_tile_gemm_packed(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, const float* alpha,
-                           int splits, float* slabs, void* C, hipStream_t stream) {
-  if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
-  const int kps = (nkt + splits - 1) / splits;
-  dim3 grid(M / TBM, splits);
-  const bf16* d = (const bf16*)Dt;
-  const bf16* b = (const bf16*)Bp;
-  void* out = splits > 1 ? (void*)slabs : C;
-  if (dk) {
-    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db_kernel<true, false, 2, 2>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
-    else hipLaunchKernelGGL((tile_gemm_db_kernel<true, true, 2, 2>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
-  } else {
-    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db_kernel<false, false, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
-    else hipLaunchKernelGGL((tile_gemm_db_kernel<false, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, alpha, out);
-  }
-  TRIAD_CHECK_LAUNCH();
-  if (splits == 1) return TRIAD_OK;
-  return triad_sum_slabs(slabs, splits, (long long)M * TBN, alpha, 1, C, stream);
-}
-
-// Unscaled fp32 slabs only, over packed B (the direct-B form of triad_tile_gemm_slabs).
-int triad_tile_gemm_packed_slabs(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, int splits,
-                                 float* slabs, hipStream_t stream) {
-  if (M % TBM || nkt <= 0 || splits < 1 || !slabs) return TRIAD_EINVAL;
-  const int kps = (nkt + splits - 1) / splits;
-  dim3 grid(M / TBM, splits);
-  const bf16* d = (const bf16*)Dt;
-  const bf16* b = (const bf16*)Bp;
-  if (dk) hipLaunchKernelGGL((tile_gemm_db_kernel<true, true, 2, 2>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
-  else hipLaunchKernelGGL((tile_gemm_db_kernel<false, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
-  TRIAD_CHECK_LAUNCH();
-  return TRIAD_OK;
-}
 
 // dQ (dk = 0): M = query rows (R_pad), nkt = key tiles (C_pad / 32), B = K [C_pad][512].
 // dK (dk = 1): M = key rows (CT * 32), nkt = query tiles (R_pad / 32), B = Q [R_pad][512].
@@ -583,12 +421,6 @@ int triad_bfrag_pack16(const void* B, int nkt, int dk, void* Bp, hipStream_t str
   return TRIAD_OK;
 }
 
-#ifndef TRIAD_DK16_KS
-#define TRIAD_DK16_KS 1
-#endif
-#ifndef TRIAD_DK16_DD
-#define TRIAD_DK16_DD 3
-#endif
 int triad_tile_gemm_packed16(const void* Dt, long long CT, int dk, const void* Bp, int M, int nkt, const float* alpha,
                              int splits, float* slabs, void* C, hipStream_t stream) {
   if (M % TBM || nkt <= 0 || splits < 1 || (splits > 1 && !slabs)) return TRIAD_EINVAL;
@@ -598,14 +430,12 @@ int triad_tile_gemm_packed16(const void* Dt, long long CT, int dk, const void* B
   const bf16* b = (const bf16*)Bp;
   void* out = splits > 1 ? (void*)slabs : C;
   const float* al = splits > 1 ? nullptr : alpha;
-  // one k tile per stage, 3 ahead (dK with two tiles per stage two ahead, as its 32x32x16 form,
-  // would spill); TRIAD_DK16_KS / _DD: stage shape of dK for A/B builds (tools/build_variants.py)
   if (dk) {
-    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db16_kernel<true, false, TRIAD_DK16_KS, TRIAD_DK16_DD>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
-    else hipLaunchKernelGGL((tile_gemm_db16_kernel<true, true, TRIAD_DK16_KS, TRIAD_DK16_DD>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
+    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db16_kernel<true, false, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
+    else hipLaunchKernelGGL((tile_gemm_db16_kernel<true, true, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
   } else {
-    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db16_kernel<false, false, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
-    else hipLaunchKernelGGL((tile_gemm_db16_kernel<false, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
+    if (splits == 1) hipLaunchKernelGGL((tile_gemm_db16_kernel<false, false, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
+    else hipLaunchKernelGGL((tile_gemm_db16_kernel<false, true, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, al, out);
   }
   TRIAD_CHECK_LAUNCH();
   if (splits == 1) return TRIAD_OK;
@@ -620,8 +450,8 @@ int triad_tile_gemm_packed16_slabs(const void* Dt, long long CT, int dk, const v
   dim3 grid(M / TBM, splits);
   const bf16* d = (const bf16*)Dt;
   const bf16* b = (const bf16*)Bp;
-  if (dk) hipLaunchKernelGGL((tile_gemm_db16_kernel<true, true, TRIAD_DK16_KS, TRIAD_DK16_DD>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
-  else hipLaunchKernelGGL((tile_gemm_db16_kernel<false, true, 1, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  if (dk) hipLaunchKernelGGL((tile_gemm_db16_kernel<true, true, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
+  else hipLaunchKernelGGL((tile_gemm_db16_kernel<false, true, 3>), grid, dim3(512), 0, stream, d, CT, b, M, nkt, kps, nullptr, (void*)slabs);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

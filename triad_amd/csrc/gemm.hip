@@ -301,19 +301,15 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
     }
 }
 
-// ---- 256 x 256 four-wave form ------------------------------------------------------------------
-// Workgroup = 4 waves (2 x 2), each owning a 128 x 128 output (4 x 4 tiles of 32 x 32, 256 fp32
-// accumulators per lane in AGPRs), tile 256 x 256 x 64 per stage, two 64 KB LDS slots. Per
-// 16-deep k step a wave reads 8 fragments for 16 MFMAs (the 64 x 64-per-wave forms read 4 for 4),
-// halving the LDS bytes per MFMA. Each wave issues the 16 DMA pieces of the next stage in the
-// first half of the current one (one after every 2nd MFMA; every 4th measured 5 % slower), and
-// waits with vmcnt(0) + barrier at the top of the next. Measured bounds (tools/gemm_forms.py,
-// profiles/r01_gemm_w4_bounds.log): without the fragment reads the conv GEMM runs 3 % faster,
-// without the DMA 25 % faster -- the LDS-DMA fill rate (~64 KB per CU per stage), not the LDS
-// reads, is what holds it under the MFMA rate; a 32-deep 4-slot ring with more lead was slower.
+// ---- 256 x 256 tile: LDS images and staging (the eight-wave form below) -------------------------
+// Tile 256 x 256 x 64 per stage, two 64 KB LDS slots, the next stage's DMA pieces issued in the
+// first half of the current one, vmcnt(0) + barrier at the top of the next. (Round 1 ran this tile
+// on four waves, 128 x 128 each; measured bounds, profiles/r01_gemm_w4_bounds.log: without the
+// fragment reads 3 % faster, without the DMA 25 % faster -- the LDS-DMA fill rate (~64 KB per CU per
+// stage) holds it under the MFMA rate. The eight-wave form replaced it in round 2, 3-13 % faster;
+// the four-wave kernel was deleted in round 5.)
 constexpr int GW_M = 256, GW_N = 256;
 constexpr int GW_A = GW_M * BK, GW_ST = GW_A + GW_N * BK;  // elements per stage (64 KB)
-constexpr int GW_PIECES = 16;
 
 template <bool KCONTIG>
 __device__ __forceinline__ void gw_piece_one(const bf16* __restrict__ X, long long ld, int r0, int k0, bf16* img,
@@ -330,106 +326,14 @@ __device__ __forceinline__ void gw_piece_one(const bf16* __restrict__ X, long lo
   }
 }
 
-template <bool A_KCONTIG, bool B_KCONTIG>
-__device__ __forceinline__ void gw_piece(const bf16* __restrict__ A, long long lda, const bf16* __restrict__ B,
-                                         long long ldb, int m0, int n0, int k0, bf16* dst, int wave, int lane,
-                                         int u) {
-  if (u < 8) gw_piece_one<A_KCONTIG>(A, lda, m0, k0, dst, wave * 8 + u, lane);
-  else gw_piece_one<B_KCONTIG>(B, ldb, n0, k0, dst + GW_A, wave * 8 + (u - 8), lane);
-}
-
 template <bool KCONTIG>
 __device__ __forceinline__ bf16x8 gw_frag(const bf16* img, int row, int s, int lane) {
   if (KCONTIG) return *(const bf16x8*)(img + kc_off(row + (lane & 31), 2 * s + (lane >> 5)));
   return frag_tr(img + (row >> 7) * (BK * 128), row & 127, s, lane);
 }
 
-template <bool A_KCONTIG, bool B_KCONTIG, typename OutT>
-__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const bf16* __restrict__ A, long long lda,
-                                                         const bf16* __restrict__ B, long long ldb, int M, int N,
-                                                         int Kd, const float* __restrict__ alpha_p,
-                                                         OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                         long long slab_stride, const float* __restrict__ bias, int xsplit) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * GW_ST];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int h = lane >> 5;
-  int swz, split;
-  tile_split(xsplit, swz, split);
-  const int ntn = N / GW_N;
-  const int m0 = (swz / ntn) * GW_M, n0 = (swz % ntn) * GW_N;
-
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x16){};
-
-  const int kbeg = split * k_per_split;
-  const int nk = __builtin_amdgcn_readfirstlane(max(0, min(k_per_split, Kd - kbeg)) / BK);
-  C += (size_t)split * slab_stride;
-  if (nk > 0)
-#pragma unroll
-    for (int u = 0; u < GW_PIECES; ++u)
-      gw_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kbeg, lds, wave, lane, u);
-  for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const bool pf = kt + 1 < nk;
-    bf16* const nb = lds + ((kt + 1) & 1) * GW_ST;
-    const int kn = kbeg + (kt + 1) * BK;
-    const bf16* ai = lds + (kt & 1) * GW_ST;
-    const bf16* bi = ai + GW_A;
-    // fragments double-buffered across the four 16-deep steps: step s + 1's 8 LDS reads are
-    // issued between step s's first 8 MFMAs (only step 0's reads are exposed per stage)
-    bf16x8 af[2][4], bfr[2][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      af[0][t] = gw_frag<A_KCONTIG>(ai, wm * 128 + t * 32, 0, lane);
-      bfr[0][t] = gw_frag<B_KCONTIG>(bi, wn * 128 + t * 32, 0, lane);
-    }
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      const int cur = s & 1;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          acc[a][b] = mfma32(af[cur][a], bfr[cur][b], acc[a][b]);
-          const int j = a * 4 + b, mi = s * 16 + j;
-          if (s + 1 < BK / 16 && j < 8) {
-            __builtin_amdgcn_sched_barrier(0);
-            const int t = j >> 1;
-            if (j & 1) bfr[cur ^ 1][t] = gw_frag<B_KCONTIG>(bi, wn * 128 + t * 32, s + 1, lane);
-            else af[cur ^ 1][t] = gw_frag<A_KCONTIG>(ai, wm * 128 + t * 32, s + 1, lane);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          if (mi % 2 == 1 && mi / 2 < GW_PIECES) {  // all 16 pieces in the stage's first 32 MFMAs
-            __builtin_amdgcn_sched_barrier(0);
-            if (pf) gw_piece<A_KCONTIG, B_KCONTIG>(A, lda, B, ldb, m0, n0, kn, nb, wave, lane, mi / 2);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-    }
-  }
-
-  const float alpha = alpha_p ? *alpha_p : 1.f;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int n = n0 + wn * 128 + b * 32 + (lane & 31);
-      const float bn = bias ? bias[n] : 0.f;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = m0 + wm * 128 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-        C[(size_t)m * ldc + n] = (OutT)(alpha * acc[a][b][v] + bn);
-      }
-    }
-}
-
 // ---- 256 x 256 eight-wave form -----------------------------------------------------------------
-// The four-wave form's tile, LDS images and staging with 8 waves (two per SIMD: one wave's DMA
+// The 256 x 256 tile, LDS images and staging with 8 waves (two per SIMD: one wave's DMA
 // issue and barrier waits overlap the other's MFMAs): wave (wm, wn) of 2 x 4 owns 128 x 64 (4 x 2
 // tiles of 32 x 32, 128 accumulators per lane), reads 6 fragments per 8 MFMAs per 16-deep step, and
 // issues 8 of the next stage's 64 DMA pieces (one after every 2nd of its first 16 MFMAs).
@@ -564,16 +468,9 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
   // shorter forward shapes keep the smaller tiles
   const bool w4_auto = AK && BK_ && splits == 1 && M >= 65536 && Kd >= 1024;
   if (form == 0 && w4_ok && w4_auto) form = kBigForm;
-  if (w4_ok && form == 4) {
+  if (w4_ok && (form == 4 || form == 3)) {   // (form 3, the four-wave 256 x 256 tile, was retired in round 5)
     const int nwg = (M / GW_M) * (N / GW_N);
     hipLaunchKernelGGL((gemm_w8_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
-                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, xsplit);
-    TRIAD_CHECK_LAUNCH();
-    return TRIAD_OK;
-  }
-  if (w4_ok && (form == 3 || (form == 0 && w4_auto))) {
-    const int nwg = (M / GW_M) * (N / GW_N);
-    hipLaunchKernelGGL((gemm_w4_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(256), 0, st, (const bf16*)A, lda,
                        (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, xsplit);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
@@ -599,7 +496,7 @@ extern "C" {
 
 // C[M][N] = alpha * op(A) . op(B). a_kcontig=1: A stored [M][Kd] (lda), 0: [Kd][M].
 // b_kcontig=1: B stored [N][Kd] (ldb), 0: [Kd][N]. out_bf16 selects a bf16 or fp32 C.
-// form: 0 = the size policy of launch(), 1 = 128 x 128, 2 = 256 x 128 ring, 3 = 256 x 256 four-wave,
+// form: 0 = the size policy of launch(), 1 = 128 x 128, 2 = 256 x 128 ring, 3 = (retired four-wave, runs as 4),
 // 4 = 256 x 256 eight-wave (3 / 4 when M, N are multiples of 256; otherwise the policy's fallback).
 int triad_gemm_bf16_form(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
                          int M, int N, int Kd, const float* alpha, void* C, long long ldc, int out_bf16, int form,

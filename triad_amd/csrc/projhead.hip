@@ -1,55 +1,11 @@
-// Projection-head helpers (the head itself is csrc/projhead_rows.hip): the standalone LayerNorm
-// backward (heads whose width does not tile the fused backward), column sums (bias gradients,
-// also of the backbones) and the split-K slab reduce.
+// Projection-head helpers: the LayerNorm forward / backward row passes of the "passes" head form
+// (the "rows" form runs them in its GEMM epilogues, csrc/rowgemm.hip), column sums (bias
+// gradients, also of the backbones) and the split-K slab reduce.
 #include "common.h"
 
 namespace {
 
 constexpr int PN = 512;       // projection width
-
-// LayerNorm backward, one wave per row (512 features, 8 per lane):
-//   xh = (y1 - mean) * rstd;  g = dln * gamma
-//   dy1 = rstd * (g - mean(g) - xh * mean(g * xh))     (bf16 out)
-// plus per-workgroup column partials of dgamma = sum dln*xh and dbeta = sum dln.
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dln, const bf16* __restrict__ y1,
-                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                     const float* __restrict__ gamma, int M, bf16* __restrict__ dy1,
-                                                     float* __restrict__ dgb_part /* [grid][2][512] */) {
-  __shared__ float sg[4][PN], sb[4][PN];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float pg[8], pb[8], gm[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { pg[k] = 0.f; pb[k] = 0.f; gm[k] = gamma[lane * 8 + k]; }
-  for (int r = blockIdx.x * 4 + wave; r < M; r += gridDim.x * 4) {
-    const float mu = mean[r], rs = rstd[r];
-    const float* d = dln + (size_t)r * PN + lane * 8;
-    const bf16x8 yv = *(const bf16x8*)(y1 + (size_t)r * PN + lane * 8);
-    float xh[8], g[8], s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      xh[k] = ((float)yv[k] - mu) * rs;
-      const float dv = d[k];
-      g[k] = dv * gm[k];
-      s1 += g[k];
-      s2 += g[k] * xh[k];
-      pg[k] += dv * xh[k];
-      pb[k] += dv;
-    }
-    s1 = wave_sum(s1) * (1.f / PN);
-    s2 = wave_sum(s2) * (1.f / PN);
-    bf16x8 o;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = (bf16)(rs * (g[k] - s1 - xh[k] * s2));
-    *(bf16x8*)(dy1 + (size_t)r * PN + lane * 8) = o;
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { sg[wave][lane * 8 + k] = pg[k]; sb[wave][lane * 8 + k] = pb[k]; }
-  __syncthreads();
-  for (int n = threadIdx.x; n < PN; n += blockDim.x) {
-    dgb_part[(size_t)blockIdx.x * 2 * PN + n] = sg[0][n] + sg[1][n] + sg[2][n] + sg[3][n];
-    dgb_part[(size_t)blockIdx.x * 2 * PN + PN + n] = sb[0][n] + sb[1][n] + sb[2][n] + sb[3][n];
-  }
-}
 
 // LayerNorm(512) forward of the library-GEMM projection head, one wave per row (8 features per
 // lane): mean / biased variance in fp32 over the bf16 y1 row (F.layer_norm under autocast runs in
@@ -258,9 +214,12 @@ __device__ __forceinline__ void cd_wait(int later) {
   }
 }
 
+// Any column count that is a multiple of 8 (16 bytes of bf16): the last column tile is masked --
+// its lanes past `cols` re-read the tile's last valid 16 bytes (in bounds, never summed into an
+// output) and only columns < cols are written.
 template <bool F32, int SLOTS>
 __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict__ Xv, long long rows, long long ld,
-                                                         long long per, float alpha, int out_mode,
+                                                         long long cols, long long per, float alpha, int out_mode,
                                                          void* __restrict__ out, long long out_ld) {
   __shared__ __attribute__((aligned(16))) char buf[SLOTS][CD_ROWS * 512];
   __shared__ float fin[2][128][2];
@@ -273,13 +232,16 @@ __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict_
   const int nchunk = r1 > r0 ? (int)((r1 - r0 + CD_ROWS - 1) / CD_ROWS) : 0;
   // wave w issues pieces 2w, 2w + 1 of a chunk: piece p = rows 2p, 2p + 1, lane L -> row 2p + (L >> 5),
   // 16 bytes at column offset (L & 31) * 16 B; rows past the range re-read the last row (not summed)
+  constexpr int PER16 = F32 ? 4 : 8;                    // columns per 16-byte piece
+  const long long last16 = cols - c0 - PER16;           // the tile's last valid piece (cols % PER16 == 0)
+  const long long off16 = (lane & 31) * PER16 <= last16 ? (lane & 31) * PER16 : last16;
   auto issue = [&](int c, int slot) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int p = 2 * wave + u;
       long long r = r0 + (long long)c * CD_ROWS + 2 * p + (lane >> 5);
       r = r < r1 ? r : r1 - 1;
-      glds16(X + (r * ld + c0) * esz + (lane & 31) * 16, buf[slot] + p * 1024);
+      glds16(X + (r * ld + c0 + off16) * esz, buf[slot] + p * 1024);
     }
   };
   const int cp = t & 127, rh = t >> 7;                  // 4-byte column slot, row parity
@@ -314,7 +276,7 @@ __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict_
   fin[rh][cp][0] = a0;
   fin[rh][cp][1] = a1;
   __syncthreads();
-  if (rh == 0) {
+  if (rh == 0 && c0 + (F32 ? 1 : 2) * cp < cols) {
     const float s0 = fin[0][cp][0] + fin[1][cp][0], s1 = fin[0][cp][1] + fin[1][cp][1];
     if (F32) {
       const long long col = c0 + cp;
@@ -333,15 +295,6 @@ __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict_
 }  // namespace
 
 extern "C" {
-
-int triad_ln_bwd(const float* dln, const void* y1, const float* mean, const float* rstd, const float* gamma, int M,
-                 void* dy1, float* dgb_part, int nblocks, hipStream_t stream) {
-  if (M <= 0 || nblocks <= 0) return TRIAD_EINVAL;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(nblocks), dim3(256), 0, stream, dln, (const bf16*)y1, mean, rstd, gamma, M,
-                     (bf16*)dy1, dgb_part);
-  TRIAD_CHECK_LAUNCH();
-  return TRIAD_OK;
-}
 
 int triad_ln_fwd(const void* y1, int M, const float* gamma, const float* beta, float eps, void* ln, float* mean,
                  float* rstd, hipStream_t stream) {
@@ -396,9 +349,10 @@ int triad_colsum_splits(long long rows, int cols) {
 }
 
 // Column sums through LDS-DMA: part = triad_colsum_dma_splits(rows, cols) * cols floats of scratch.
+// Any cols % 8 == 0 (a 256-column tile count rounded up, the last tile masked); X 16-byte aligned.
 int triad_colsum_dma_splits(long long rows, int cols) {
-  if (cols <= 0 || cols % 256) return 0;
-  const long long tiles = cols / 256;
+  if (cols <= 0 || cols % 8) return 0;
+  const long long tiles = (cols + 255) / 256;
   long long s = (CD_WG + tiles - 1) / tiles;            // one round of >= CD_WG workgroups
   const long long cap = rows / (4 * CD_ROWS);           // >= 4 chunks per split
   if (s > cap) s = cap;
@@ -407,14 +361,17 @@ int triad_colsum_dma_splits(long long rows, int cols) {
 
 int triad_colsum_dma(const void* X, long long rows, int cols, long long ld, float* part, float alpha, int out_bf16,
                      void* out, hipStream_t stream) {
-  if (rows <= 0 || cols <= 0 || cols % 256 || ld % 8 || ld < cols || !part) return TRIAD_EINVAL;
+  if (rows <= 0 || cols <= 0 || cols % 8 || ld % 8 || ld < cols || !part || !X || !out ||
+      ((uintptr_t)X & 15))
+    return TRIAD_EINVAL;
   const int S = triad_colsum_dma_splits(rows, cols);
   long long per = (rows + S - 1) / S;
-  hipLaunchKernelGGL((colsum_dma_kernel<false, CD_SLOTS>), dim3(cols / 256, S), dim3(256), 0, stream, X, rows, ld, per, 1.f, 0,
-                     (void*)part, (long long)cols);
+  hipLaunchKernelGGL((colsum_dma_kernel<false, CD_SLOTS>), dim3((cols + 255) / 256, S), dim3(256), 0, stream, X, rows,
+                     ld, (long long)cols, per, 1.f, 0, (void*)part, (long long)cols);
   TRIAD_CHECK_LAUNCH();
-  hipLaunchKernelGGL((colsum_dma_kernel<true, CD_SLOTS>), dim3(cols / 128, 1), dim3(256), 0, stream, (const void*)part,
-                     (long long)S, (long long)cols, (long long)S, alpha, out_bf16 ? 2 : 1, out, 0LL);
+  hipLaunchKernelGGL((colsum_dma_kernel<true, CD_SLOTS>), dim3((cols + 127) / 128, 1), dim3(256), 0, stream,
+                     (const void*)part, (long long)S, (long long)cols, (long long)cols, (long long)S, alpha,
+                     out_bf16 ? 2 : 1, out, 0LL);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

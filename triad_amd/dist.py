@@ -174,6 +174,13 @@ class GradBucketReducer:
         self.comm = torch.cuda.Stream(space.device) if self.cuda else None
         self.launched_in_backward = 0                           # overlap evidence (tests, logs)
         self._hooks = {}   # registered lazily: a frozen parameter (requires_grad False) takes no hook
+        # correctness gate (bench.py --gpus N > 1): with `check` set for a step, each
+        # bucket's local gradient is snapshotted right before its overlapped all-reduce, and after the
+        # step the same buckets are all-reduced again from the snapshots in the same order with the
+        # device otherwise idle; `check_result` compares the two bit for bit (max over ranks)
+        self.check = False
+        self.check_result = None
+        self._snap = None
 
     def _arm_hooks(self):
         for i, p in enumerate(self.space.params):
@@ -266,6 +273,8 @@ class GradBucketReducer:
         g = self._range(b)
         scale = 1.0 / self.world if self.average else 1.0
         if not self.cuda:
+            if self.check:
+                self._snap_range(b).copy_(g)
             if scale != 1.0:
                 g.mul_(scale)
             buf = g.to(torch.bfloat16) if self.wire == "bf16" else g
@@ -274,11 +283,53 @@ class GradBucketReducer:
         for s in self.streams[b] or {torch.cuda.current_stream(self.space.device)}:
             self.comm.wait_stream(s)
         with torch.cuda.stream(self.comm):
+            if self.check:
+                self._snap_range(b).copy_(g)
             if scale != 1.0:
                 g.mul_(scale)
             buf = g.to(torch.bfloat16) if self.wire == "bf16" else g
             work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.works[b] = (work, buf)
+
+    def _snap_range(self, b):
+        if self._snap is None or self._snap.numel() != self.space.flat_g.numel():
+            self._snap = torch.empty_like(self.space.flat_g)
+        s, e = self.buckets[b]
+        sp = self.space
+        hi = sp.offsets[e] if e < len(sp.params) else sp.numel
+        return self._snap[sp.offsets[s]:hi]
+
+    def _check_reference(self):
+        """The same buckets all-reduced again from their pre-reduction snapshots, in the same order,
+        one at a time with the device otherwise idle (no backward kernel co-resident with the
+        collective); compared bit for bit with what the overlapped reductions produced."""
+        dev = self.space.device
+        if self.cuda:
+            torch.cuda.synchronize(dev)
+        scale = 1.0 / self.world if self.average else 1.0
+        launched = [b for b in self.order if self.expected[b] > 0]
+        max_abs, differ = 0.0, 0
+        for b in launched:
+            ref = self._snap_range(b)
+            if scale != 1.0:
+                ref.mul_(scale)
+            buf = ref.to(torch.bfloat16) if self.wire == "bf16" else ref
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+            if self.wire == "bf16":
+                ref.copy_(buf)
+            got = self._range(b)
+            d = (got - ref).abs()
+            max_abs = max(max_abs, float(d.max())) if d.numel() else max_abs
+            differ += int((got != ref).sum())
+        if self.cuda:
+            torch.cuda.synchronize(dev)
+        t = torch.tensor([max_abs, float(differ)], dtype=torch.float64,
+                         device=dev if _is_nccl(self.group) else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        self.check_result = {"equal": bool(t[1] == 0), "max_abs": float(t[0]), "differing_elements_max_rank": int(t[1]),
+                             "world_size": self.world, "backend": dist.get_backend(self.group),
+                             "buckets": len(launched), "launched_in_backward": self.launched_in_backward,
+                             "wire": self.wire}
 
     def finish(self):
         """After backward: flush, then order the caller's stream after every reduction."""
@@ -310,3 +361,6 @@ class GradBucketReducer:
                 if cur is not None:
                     buf.record_stream(cur)
                 self._range(b).copy_(buf)
+        if self.check:
+            self._check_reference()
+            self.check = False

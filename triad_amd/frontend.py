@@ -554,8 +554,7 @@ class _SpecMask(torch.autograd.Function):
 
 
 def _spec_where(m, emb, h):
-    import os
-    if os.environ.get("TRIAD_DB_GEMM", "1") != "0" and h.dtype == torch.bfloat16 and emb.requires_grad:
+    if h.dtype == torch.bfloat16 and emb.requires_grad:
         return _SpecMask.apply(h, m, emb)
     return torch.where(m[..., None], emb.to(h.dtype), h)
 

@@ -22,7 +22,6 @@ from . import _lib
 from . import gemm as hipgemm
 from ._lib import call, ptr, stream_ptr
 
-MIN_TOKENS = 4096  # DistilBERT at B=256 (8,192 tokens) still gains 1.1-1.8x
 
 
 # Split-K factors measured per output-tile count on MI355X (round-1 A/B with
@@ -63,9 +62,15 @@ def _form_splits(M, out_f, in_f):
 
 
 def weight_grad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
-    """dW = dy2^T x2 (bf16 [O][K]) for dy2 [M][O], x2 [M][K] bf16 row-major, M % 64 == 0."""
+    """dW = dy2^T x2 (bf16 [O][K]) for dy2 [M][O], x2 [M][K] bf16 row-major (a token count that is
+    not a multiple of the GEMM's 64-deep k step is padded with zero rows, which add nothing)."""
     M, O = dy2.shape
     K = x2.shape[1]
+    if M % 64:
+        Mp = (M + 63) // 64 * 64
+        dy2 = torch.cat([dy2, dy2.new_zeros(Mp - M, O)])
+        x2 = torch.cat([x2, x2.new_zeros(Mp - M, K)])
+        M = Mp
     form, sp = _form_splits(M, O, K)
     slabs = torch.empty(sp * O * K, dtype=torch.float32, device=dy2.device)
     dw = torch.empty(O, K, dtype=torch.bfloat16, device=dy2.device)
@@ -159,7 +164,7 @@ def on_side_stream(fn, inputs):
 
 
 # On by default (with the modality streams; model.set_concurrent_streams / TRIAD_SIDE_STREAM_DW=0
-# turn it off): safe since every bias sum runs on the GEMM (ops.bias_grad).
+# turn it off): safe since every bias sum reads its rows by LDS-DMA (ops.bias_grad).
 SIDE_STREAM_DW = os.environ.get("TRIAD_SIDE_STREAM_DW", "1") != "0"
 
 
@@ -269,11 +274,11 @@ def _eligible(mod: nn.Linear, x: torch.Tensor) -> bool:
     # still run on the HIP GEMM, the weight gradient is simply not requested
     if not (x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
         return False
-    M = x.numel() // max(1, x.shape[-1])
-    # every size when the bias sums run on the GEMM (ops.bias_grad, the default): no bias gradient
-    # may fall back to PyTorch's reduction kernels beside another stream's GEMMs
-    low = 64 if os.environ.get("TRIAD_DB_GEMM", "1") != "0" else MIN_TOKENS
-    return M >= low and M % 64 == 0 and mod.in_features % 128 == 0 and mod.out_features % 128 == 0
+    # every token count: no bias gradient may fall back to PyTorch's reduction kernels beside another
+    # stream's GEMMs (ops.bias_grad takes every shape by LDS-DMA, weight_grad pads the tokens;
+    # DESIGN.md §2b). Widths must tile the split-K GEMM (every backbone Linear's do; LoRA's rank-8
+    # layers have no bias).
+    return x.numel() > 0 and mod.in_features % 128 == 0 and mod.out_features % 128 == 0
 
 
 class TriadLinear(nn.Linear):

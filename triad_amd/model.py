@@ -257,15 +257,13 @@ def _load_dinov2_base(vit, arch):
               OSError("torch.hub is not reachable offline and TRIAD_DINOV2_WEIGHTS is not set"))
 
 
-class ViTLoRAEmbedder(nn.Module):
-    """DINOv2(-reg) + LoRA + projection head + patch dropout (model.py:207-329)."""
+class _PatchTokenEmbedder(nn.Module):
+    """What ViTEmbedder (model.py:120-205) and ViTLoRAEmbedder (model.py:207-329) share: the DINOv2
+    patch tokens (get_intermediate_layers(x, n=1)[0]), the projection head and the patch dropout
+    (model.py:143-183 == 268-308: per-sample Bernoulli keep mask, kept tokens in order, zero-padded
+    to the longest), on the HIP head and gather kernels."""
 
-    def __init__(self, model_name="facebookresearch/dinov2", arch="dinov2_vitb14", embedding_dim=512,
-                 dropout_prob=0.1, lora_rank=8, lora_alpha=16):
-        super().__init__()
-        self.model = DinoVisionTransformer(arch)
-        _load_dinov2_base(self.model, arch)
-        self.model = install_fast_linear(apply_lora(self.model, lora_rank, lora_alpha))  # MLP fc1 / fc2
+    def _init_head(self, embedding_dim, dropout_prob):
         self.projection1 = nn.Linear(self.model.embed_dim, 512)
         self.layer_norm = nn.LayerNorm(512)
         self.projection2 = nn.Linear(512, embedding_dim)
@@ -295,7 +293,7 @@ class ViTLoRAEmbedder(nn.Module):
         self._mask_seeded = True
 
     def draw_keep_mask(self, B, N):
-        """Bernoulli(1 - drop) keep mask (model.py:282-284), drawn on the host.
+        """Bernoulli(1 - drop) keep mask (model.py:157-159 / 282-284), drawn on the host.
         Returns (this rank's (B, N) mask, padded output length)."""
         W, r = self.mask_world
         full = torch.bernoulli(torch.full((W * B, N), 1.0 - self.patch_dropout_rate),
@@ -303,7 +301,7 @@ class ViTLoRAEmbedder(nn.Module):
         return full[r * B:(r + 1) * B], int(full.sum(1).max())
 
     def patch_dropout(self, x, drop_rate, keep_mask=None):
-        """model.py:268-308: keep tokens of each sample in order, zero-pad to the longest."""
+        """model.py:143-183 / 268-308: keep tokens of each sample in order, zero-pad to the longest."""
         if not self.training or drop_rate == 0:
             return x
         B, N = x.shape[0], x.shape[1]
@@ -323,6 +321,34 @@ class ViTLoRAEmbedder(nn.Module):
     def forward(self, x, keep_mask=None):
         feats = self.encode_patches(x)
         return self.patch_dropout(feats, self.patch_dropout_rate, keep_mask)
+
+
+class ViTEmbedder(_PatchTokenEmbedder):
+    """DINOv2 (no LoRA, every parameter trainable) + projection head + patch dropout
+    (model.py:120-205). The reference's default arch has no register tokens ('dinov2_vitb14');
+    MultiModalModel uses ViTLoRAEmbedder, this class completes the import surface."""
+
+    def __init__(self, model_name="facebookresearch/dinov2", arch="dinov2_vitb14", embedding_dim=512,
+                 dropout_prob=0.1):
+        super().__init__()
+        self.model = DinoVisionTransformer(arch)
+        _load_dinov2_base(self.model, arch)
+        self.model = install_fast_linear(self.model)
+        self._init_head(embedding_dim, dropout_prob)
+        for p in self.parameters():   # model.py:136-141
+            p.requires_grad = True
+
+
+class ViTLoRAEmbedder(_PatchTokenEmbedder):
+    """DINOv2(-reg) + LoRA + projection head + patch dropout (model.py:207-329)."""
+
+    def __init__(self, model_name="facebookresearch/dinov2", arch="dinov2_vitb14", embedding_dim=512,
+                 dropout_prob=0.1, lora_rank=8, lora_alpha=16):
+        super().__init__()
+        self.model = DinoVisionTransformer(arch)
+        _load_dinov2_base(self.model, arch)
+        self.model = install_fast_linear(apply_lora(self.model, lora_rank, lora_alpha))  # MLP fc1 / fc2
+        self._init_head(embedding_dim, dropout_prob)
 
 
 class MultiModalModel(nn.Module):
@@ -530,8 +556,8 @@ def modality_streams_enabled() -> bool:
     (default, TRIAD_MODALITY_STREAMS unset or 1) or all three backbones on the caller's stream
     (TRIAD_MODALITY_STREAMS=0). Both modes give bit-identical results
     (test_ops_gpu.py::test_step_bit_identical_serial_and_concurrent): every column-sum reduction of
-    the step runs on the MFMA GEMM (ops.bias_grad) -- the reductions were what co-running streams
-    disturbed."""
+    the step reads its rows by LDS-DMA (ops.bias_grad) -- plain-load reductions were what
+    co-running streams disturbed."""
     return os.environ.get("TRIAD_MODALITY_STREAMS", "1") != "0"
 
 

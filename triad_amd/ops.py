@@ -88,77 +88,41 @@ def pack_keys(k: torch.Tensor, g: Geometry) -> torch.Tensor:
     return out
 
 
-def colsum(x, out_dtype=torch.float32, backbone=False):
-    """Column sums of a bf16 [rows][cols] matrix (bias gradients) at HBM rate (triad_colsum).
-    backbone: tag the launch as backbone work (bench.py keeps it out of the hot-path head figures)."""
+def bias_grad(x, out_dtype=torch.float32, meta=None):
+    """Column sums of a bf16 [rows][cols] matrix -- EVERY column sum of the step: the backbone and
+    head bias gradients and SpecAugment's masked_spec_embed -- fp32 accumulation, by
+    triad_colsum_dma (rows staged into an LDS ring by 16-byte LDS-DMA, VALU sums, a second pass
+    over the per-split partials; HBM-bound, 4.8 TB/s at 50,944 x 2,304,
+    profiles/r04_colsum_dma_ring.log). Why not a plain-load reduction (triad_colsum, PyTorch's
+    sum): with the backbones on concurrent streams, column-sum REDUCTIONS beside the library's MFMA
+    + LDS-DMA GEMMs returned disturbed partial sums in some launches (21-38 of 80 concurrent steps
+    differing from the serial one), while sums whose rows arrive by LDS-DMA stayed bit-identical
+    in every concurrent step (profiles/r04_stream_repeat_*.log). There is no other
+    form: a shape the kernel does not take directly (cols % 8, a misaligned or column-strided view)
+    is first copied into an aligned buffer padded to 8 columns (zeros), never summed another way.
+    meta: launch tag (default: backbone work)."""
+    if x.dim() != 2 or x.dtype != torch.bfloat16:
+        raise TriadError(f"bias_grad expects a 2-D bf16 matrix, got {tuple(x.shape)} {x.dtype}")
     rows, cols = x.shape
-    part = torch.empty(call("triad_colsum_splits", rows, cols) * cols, dtype=torch.float32, device=x.device)
+    if rows == 0:
+        return torch.zeros(cols, dtype=out_dtype, device=x.device)
+    if cols % 8 or x.stride(1) != 1 or x.stride(0) % 8 or x.data_ptr() % 16:
+        xp = torch.zeros(rows, _rup(cols, 8), dtype=torch.bfloat16, device=x.device)
+        xp[:, :cols].copy_(x)
+        return bias_grad(xp, out_dtype, meta)[:cols]
+    part = torch.empty(call("triad_colsum_dma_splits", rows, cols) * cols, dtype=torch.float32, device=x.device)
     out = torch.empty(cols, dtype=out_dtype, device=x.device)
-    call("triad_colsum", ptr(x), rows, cols, x.stride(0), ptr(part), 1.0, int(out_dtype == torch.bfloat16), ptr(out),
-         stream_ptr(x.device), meta=dict(backbone=True) if backbone else dict(tag="proj-bias", flops=0.0))
+    call("triad_colsum_dma", ptr(x), rows, cols, x.stride(0), ptr(part), 1.0, int(out_dtype == torch.bfloat16),
+         ptr(out), stream_ptr(x.device), meta=meta if meta is not None else dict(backbone=True))
     return out
 
 
-def _m16(dk):
-    """The tile GEMMs run on v_mfma_f32_16x16x32_bf16 (triad_tile_gemm_packed16): the 32x32x16
-    form's results bit for bit, 9-12 % faster for dQ and 3-5 % for dK at the c3 shapes -- the
-    clock the chip holds under load is higher for that MFMA shape (profiles/r04_bwd_micro_mfma16.log,
-    r04_bwd_micro_mfma16_dk.log; MI355X_MICROARCH.md, DVFS item 7). TRIAD_DQ_MFMA16 / TRIAD_DK_MFMA16
-    = 0 select the 32x32x16 direct-B form (A/B only)."""
-    return MFMA16_DQ if dk == 0 else MFMA16_DK
-
-
-_ONES = {}
-
-
-def bias_grad(x, out_dtype=torch.float32, meta=None):
-    """Column sums of a bf16 [rows][cols] matrix for the BACKBONE and head bias gradients (and
-    SpecAugment's masked_spec_embed), fp32 accumulation. Why not triad_colsum / PyTorch's sum: with
-    the backbones on concurrent streams, column-sum REDUCTIONS beside the library's MFMA + LDS-DMA
-    GEMMs returned disturbed partial sums in some launches (16-column groups off by ~1 %, 21-38 of
-    80 concurrent steps differing from the serial one), while sums whose rows arrive by LDS-DMA
-    stayed bit-identical in every concurrent step (tools/stream_repeat.py,
-    profiles/r04_stream_repeat_*.log). Forms (TRIAD_DB_FORM):
-      dma  (default, cols % 256 == 0): triad_colsum_dma -- rows staged by LDS-DMA, VALU sums, a
-           second pass over the per-split partials; HBM-bound, 4.8 TB/s at 50,944 x 2,304
-           (profiles/r04_colsum_dma_ring.log) and no MFMA time taken from the other stream;
-      gemm (and shapes dma does not take when cols % 128 == 0, rows % 64 == 0): the split-K MFMA
-           GEMM as x^T . ones, column 0 of a [cols][128] product (127 of 128 MFMA columns dead);
-    TRIAD_DB_GEMM=0 or any other shape: triad_colsum. meta: launch tag (default: backbone work)."""
-    rows, cols = x.shape
-    if (os.environ.get("TRIAD_DB_FORM", "dma") == "dma" and cols % 256 == 0 and x.stride(1) == 1
-            and x.stride(0) % 8 == 0):
-        # the rows staged by LDS-DMA, sums on the VALU (no MFMA work wasted on 127 dead columns)
-        part = torch.empty(call("triad_colsum_dma_splits", rows, cols) * cols, dtype=torch.float32, device=x.device)
-        out = torch.empty(cols, dtype=out_dtype, device=x.device)
-        call("triad_colsum_dma", ptr(x), rows, cols, x.stride(0), ptr(part), 1.0, int(out_dtype == torch.bfloat16),
-             ptr(out), stream_ptr(x.device), meta=meta if meta is not None else dict(backbone=True))
-        return out
-    if os.environ.get("TRIAD_DB_GEMM", "1") == "0" or cols % 128 or rows % 64 or x.stride(1) != 1:
-        return colsum(x, out_dtype, backbone=meta is None)
-    dev = x.device
-    ones = _ONES.get(dev.index)
-    if ones is None or ones.shape[0] < rows:
-        ones = _ONES[dev.index] = torch.ones(max(rows, 65536), 128, dtype=torch.bfloat16, device=dev)
-    # one round of >= 256 workgroups (cols / 128 output tiles x splits), splits a multiple of 8 with
-    # each split's workgroups on one XCD (gemm.hip tile_split), >= 512 rows per split
-    tiles = cols // 128
-    sp = min(-(-256 // tiles), rows // 512)
-    sp = (sp + 7) // 8 * 8 if sp >= 8 else max(1, sp)
-    form = 1 | (8 if sp % 8 == 0 else 0)
-    slabs = torch.empty(sp * cols * 128, dtype=torch.float32, device=dev)
-    c = torch.empty(cols, 128, dtype=torch.float32, device=dev)
-    call("triad_gemm_bf16_splitk_form", ptr(x), x.stride(0), 0, ptr(ones), 128, 0, cols, 128, rows, sp, None,
-         ptr(slabs), ptr(c), 0, form, stream_ptr(dev), meta=meta if meta is not None else dict(backbone=True))
-    return c[:, 0].to(out_dtype)
-
-
 def pack_b(B, nkt, dk, stream):
-    """B [nkt*32][512] bf16 -> its MFMA fragments in the direct-B GEMM's order (triad_bfrag_pack /
-    triad_bfrag_pack16, the form _m16 picks): one pass over B, after which each wave of the GEMM
-    streams its own columns into registers."""
+    """B [nkt*32][512] bf16 -> its v_mfma_f32_16x16x32_bf16 fragments in the direct-B GEMM's order
+    (triad_bfrag_pack16): one pass over B, after which each wave of the GEMM streams its own columns
+    into registers."""
     Bp = torch.empty(nkt * 32 * D, dtype=torch.bfloat16, device=B.device)
-    call("triad_bfrag_pack16" if _m16(dk) else "triad_bfrag_pack", ptr(B), nkt, dk, ptr(Bp), stream,
+    call("triad_bfrag_pack16", ptr(B), nkt, dk, ptr(Bp), stream,
          meta=dict(tag="bfrag-pack", flops=0.0))
     return Bp
 
@@ -167,27 +131,26 @@ def tile_gemm(dS, CT, dk, B, M, nkt, alpha, out, stream, meta=None, Bp=None):
     """dQ = alpha dS K (dk=0) / dK = alpha dS^T Q (dk=1) over the tiled dS, split-K over the CUs
     when the row panels alone leave them idle. (A stream-K form -- one run of (row panel, k tile)
     units per CU, no slab round trip -- measured slower: runs start at different k offsets, so CUs
-    of one XCD no longer share the streamed B panel in L2.) The direct-B forms over pack_b's
-    fragments (triad_tile_gemm_packed / _packed16, bit-identical to the LDS-ring triad_tile_gemm):
-    6-7 % faster than the ring at the c3 shapes (profiles/r03_tile_gemm_db_ab.log), the 16x16x32
-    one faster again (_m16); Bp: B already packed by pack_b."""
+    of one XCD no longer share the streamed B panel in L2.) The direct-B form over pack_b's
+    fragments on 16x16x32 MFMAs (triad_tile_gemm_packed16; the LDS-ring triad_tile_gemm is its
+    parity reference): 9-12 % faster for dQ and 3-5 % for dK than the 32x32x16 direct-B form it
+    replaced (profiles/r04_bwd_micro_mfma16.log), which was 6-7 % faster than the ring
+    (profiles/r03_tile_gemm_db_ab.log); Bp: B already packed by pack_b."""
     sp = _gemm_splits(M // 128, nkt, M)
     slabs = torch.empty(sp * M * D, dtype=torch.float32, device=out.device) if sp > 1 else None
     if Bp is None:
         Bp = pack_b(B, nkt, dk, stream)
-    call("triad_tile_gemm_packed16" if _m16(dk) else "triad_tile_gemm_packed", ptr(dS), CT, dk, ptr(Bp), M, nkt,
+    call("triad_tile_gemm_packed16", ptr(dS), CT, dk, ptr(Bp), M, nkt,
          ptr(alpha), sp, ptr(slabs), ptr(out), stream, meta=meta)
 
 
 def tile_gemm_slabs(dS, CT, dk, Bp, M, nkt, splits, slabs, stream, meta=None):
     """Unscaled fp32 split-K partial sums only (the recompute backward's per-chunk dQ), over pack_b's
     fragments."""
-    call("triad_tile_gemm_packed16_slabs" if _m16(dk) else "triad_tile_gemm_packed_slabs", ptr(dS), CT, dk,
+    call("triad_tile_gemm_packed16_slabs", ptr(dS), CT, dk,
          ptr(Bp), M, nkt, splits, ptr(slabs), stream, meta=meta)
 
 
-MFMA16_DQ = __import__("os").environ.get("TRIAD_DQ_MFMA16", "1") != "0"
-MFMA16_DK = __import__("os").environ.get("TRIAD_DK_MFMA16", "1") != "0"
 
 
 def _gemm_splits(wgs, nkt, M, cus=256, max_splits=8, t_tile=1.0e-6, hbm=5.0e12):
@@ -697,116 +660,101 @@ def _bf16_round(t):
     return t.detach().to(torch.bfloat16).to(torch.float32).contiguous()
 
 
-class _ProjectionHead(torch.autograd.Function):
+def _rows_view(h):
+    """(tensor, M, H, lda, n_per, bstride) addressing h's token rows in place when h is a bf16
+    [..., N, H] tensor whose rows are contiguous within each leading index (e.g. the ViT's patch
+    tokens sliced behind its CLS / register tokens); otherwise a contiguous bf16 copy."""
+    H = h.shape[-1]
+    if h.dtype == torch.bfloat16 and h.dim() >= 2 and h.stride(-1) == 1 and h.data_ptr() % 16 == 0:
+        N = h.shape[-2]
+        lead = h.shape[:-2]
+        lda = h.stride(-2)
+        if lda % 8 == 0 and lda >= H:
+            if len(lead) == 0:
+                return h, N, H, lda, max(N, 1), 0
+            if len(lead) == 1 and h.stride(0) % 8 == 0:
+                return h, lead[0] * N, H, lda, N, h.stride(0)
+    hb = h.to(torch.bfloat16).reshape(-1, H).contiguous()
+    return hb, hb.shape[0], H, H, hb.shape[0], 0
+
+
+class _ProjectionHeadRows(torch.autograd.Function):
+    """The projection head on row-panel GEMMs (rowgemm.hip): a workgroup owns 128 token rows x all
+    512 columns, so the LayerNorm runs in projection1's epilogue (triad_projhead_ln_fwd: y1, its
+    row mean / rstd and ln in one pass over the panel) and the LayerNorm backward in the epilogue of
+    projection2's input-gradient GEMM (triad_projhead_ln_bwd: dy1 and the dgamma / dbeta / db1
+    column partials); projection2 is triad_rowgemm_bias, dh the tiled GEMM, the weight gradients
+    the split-K GEMM. Numerics as autocast: bf16 GEMM outputs with the bias added before the one
+    rounding, the LayerNorm and its backward in fp32 over the bf16 y1 / dln."""
+
     @staticmethod
     def forward(ctx, h, w1, b1, gamma, beta, w2, b2, eps):
         _check_device(h, w1)
-        lead, H = h.shape[:-1], h.shape[-1]
-        M = h.numel() // H
+        H = h.shape[-1]
         if w1.shape != (D, H) or w2.shape != (D, D):
             raise TriadError("projection head expects Linear(H->512), Linear(512->512)")
         dev = h.device
         st = stream_ptr(dev)
-        Mp = _rup(max(M, 1), 128)
-        hb = _pad_rows(h.to(torch.bfloat16).reshape(M, H), Mp)  # cast first: one pass over a strided h
-        w1b = w1.detach().to(torch.bfloat16).contiguous()
-        w2b = w2.detach().to(torch.bfloat16).contiguous()
-        # autocast runs F.linear with the bias cast to bf16 (model.py:483/603)
+        bf = torch.bfloat16
+        lead = h.shape[:-1]
+        hv, M, _, lda, n_per, bstride = _rows_view(h)
+        P = call("triad_rowpanel_count", M)
+        Mp = P * 128
+        w1b = w1.detach().to(bf).contiguous()
+        w2b = w2.detach().to(bf).contiguous()
         b1r, b2r = _bf16_round(b1), _bf16_round(b2)
         g32 = gamma.detach().to(torch.float32).contiguous()
         be32 = beta.detach().to(torch.float32).contiguous()
-        y = torch.empty(M, D, dtype=torch.bfloat16, device=dev)
-        y1 = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
-        ln = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
-        if Mp > M:
-            y1[M:].zero_()
-            ln[M:].zero_()
-        mean = torch.empty(M, dtype=torch.float32, device=dev)
-        rstd = torch.empty(M, dtype=torch.float32, device=dev)
-        call("triad_projhead_fwd", ptr(hb), M, H, ptr(w1b), ptr(b1r), ptr(g32), ptr(be32), float(eps), ptr(w2b),
-             ptr(b2r), ptr(y), D, ptr(y1), ptr(ln), ptr(mean), ptr(rstd), st,
-             meta=dict(tag=f"proj{H}x{M}", flops=2.0 * M * (H * D + D * D)))
-        ctx.save_for_backward(hb, w1b, w2b, g32, y1, ln, mean, rstd)
-        ctx.shape = (lead, H, M, Mp)
+        w1p = torch.empty(H * D, dtype=bf, device=dev)
+        w2p = torch.empty(D * D, dtype=bf, device=dev)
+        call("triad_wpack", ptr(w1b), H, ptr(w1p), st, meta=dict(tag="proj-wpack", flops=0.0))
+        call("triad_wpack", ptr(w2b), D, ptr(w2p), st, meta=dict(tag="proj-wpack", flops=0.0))
+        y1 = torch.empty(Mp, D, dtype=bf, device=dev)
+        ln = torch.empty(Mp, D, dtype=bf, device=dev)
+        mean = torch.empty(Mp, dtype=torch.float32, device=dev)
+        rstd = torch.empty(Mp, dtype=torch.float32, device=dev)
+        call("triad_projhead_ln_fwd", ptr(hv), M, H, lda, n_per, bstride, ptr(w1p), ptr(b1r), ptr(g32), ptr(be32),
+             float(eps), ptr(y1), ptr(ln), ptr(mean), ptr(rstd), st,
+             meta=dict(tag=f"proj-fwd1x{M}", flops=2.0 * M * H * D))
+        y = torch.empty(Mp, D, dtype=bf, device=dev)
+        call("triad_rowgemm_bias", ptr(ln), M, D, D, ptr(w2p), ptr(b2r), ptr(y), st,
+             meta=dict(tag=f"proj-fwd2x{M}", flops=2.0 * M * D * D))
+        ctx.save_for_backward(h if hv is h else hv, w1b, w2b, g32, y1, ln, mean, rstd)
+        ctx.shape = (lead, H, M, Mp, hv is h)
         ctx.dtypes = (h.dtype, w1.dtype, b1.dtype, gamma.dtype, beta.dtype, w2.dtype, b2.dtype)
-        return y.view(*lead, D)
+        return y[:M].view(*lead, D)
 
     @staticmethod
     def backward(ctx, dy):
-        hb, w1b, w2b, g32, y1, ln, mean, rstd = ctx.saved_tensors
-        lead, H, M, Mp = ctx.shape
+        hs, w1b, w2b, g32, y1, ln, mean, rstd = ctx.saved_tensors
+        lead, H, M, Mp, in_place = ctx.shape
         dev = dy.device
         st = stream_ptr(dev)
-        f32 = torch.float32
-        dyp = _pad_rows(dy.reshape(M, D).to(torch.bfloat16), Mp)
-        if H % 256 == 0:
-            return _projhead_bwd_fused(ctx, dyp, hb, w1b, w2b, g32, y1, ln, mean, rstd)
-        # d ln = dy . W2          [Mp][512] fp32
-        dln = torch.empty(Mp, D, dtype=f32, device=dev)
-        call("triad_gemm_bf16", ptr(dyp), D, 1, ptr(w2b), D, 0, Mp, D, D, None, ptr(dln), D, 0, st)
-        # dW2 = dy^T . ln         [512][512], split-K over tokens
-        sp = _splitk(Mp, (D // 128) * (D // 128))
-        slabs = torch.empty(sp * max(D * D, D * H), dtype=f32, device=dev)
-        dw2 = torch.empty(D, D, dtype=f32, device=dev)
-        call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp, None, ptr(slabs), ptr(dw2), 0, st)
-        # db2 = column sums of dy
-        db2 = colsum(dyp, f32)
-        # LayerNorm backward -> dy1 (bf16), dgamma, dbeta
-        dy1 = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
-        if Mp > M:
-            dy1[M:].zero_()
-        nb = max(1, min(1024, (M + 3) // 4))
-        gpart = torch.empty(nb, 2, D, dtype=f32, device=dev)
-        call("triad_ln_bwd", ptr(dln), ptr(y1), ptr(mean), ptr(rstd), ptr(g32), M, ptr(dy1), ptr(gpart), nb, st)
-        dgb = torch.empty(2, D, dtype=f32, device=dev)
-        call("triad_sum_slabs", ptr(gpart), nb, 2 * D, None, 0, ptr(dgb), st)
-        # dW1 = dy1^T . h         [512][H], split-K
-        sp1 = _splitk(Mp, (D // 128) * (H // 128))
-        dw1 = torch.empty(D, H, dtype=f32, device=dev)
-        call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), 0,
-             st)
-        db1 = colsum(dy1, f32)
-        # dh = dy1 . W1           [Mp][H] bf16
-        dh = torch.empty(Mp, H, dtype=torch.bfloat16, device=dev)
-        call("triad_gemm_bf16", ptr(dy1), D, 1, ptr(w1b), H, 0, Mp, H, D, None, ptr(dh), H, 1, st)
+        f32, bf = torch.float32, torch.bfloat16
         hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
-        return (dh[:M].view(*lead, H).to(hd), dw1.to(w1d), db1.to(b1d), dgb[0].to(gd), dgb[1].to(bd), dw2.to(w2d),
+        dyp = _pad_rows(dy.reshape(M, D).to(bf), Mp)
+        w2p = pack_b(w2b, D // 32, 1, st)     # Bt = W2: dln = dy W2
+        P = Mp // 128
+        dy1 = torch.empty(Mp, D, dtype=bf, device=dev)
+        part = torch.empty(P, 3, D, dtype=f32, device=dev)
+        call("triad_projhead_ln_bwd", ptr(dyp), M, ptr(w2p), ptr(y1), ptr(mean), ptr(rstd), ptr(g32), ptr(dy1),
+             ptr(part), st, meta=dict(tag=f"proj-dX2x{M}", flops=2.0 * M * D * D))
+        cols = torch.empty(3, D, dtype=f32, device=dev)
+        call("triad_sum_slabs", ptr(part), P, 3 * D, None, 0, ptr(cols), st, meta=dict(tag="proj-cols", flops=0.0))
+        dh = hipgemm.mm(dy1, w1b, meta=dict(tag=f"proj-dX1x{M}", flops=2.0 * M * D * H))[:M]
+        db2 = bias_grad(dyp, bf if b2d == bf else f32, meta=dict(tag="proj-bias", flops=0.0))
+        hb = _pad_rows(hs.to(bf).reshape(M, H), Mp) if in_place or Mp > M else hs
+        (f2, sp2), (f1, sp1) = _dw_plan(Mp, D), _dw_plan(Mp, H)
+        slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
+        o2, o1 = int(w2d == bf), int(w1d == bf)
+        dw2 = torch.empty(D, D, dtype=bf if o2 else f32, device=dev)
+        call("triad_gemm_bf16_splitk_form", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2),
+             o2, f2, st, meta=dict(tag=f"proj-dW2x{M}", flops=2.0 * M * D * D))
+        dw1 = torch.empty(D, H, dtype=bf if o1 else f32, device=dev)
+        call("triad_gemm_bf16_splitk_form", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1),
+             o1, f1, st, meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
+        return (dh.view(*lead, H).to(hd), dw1.to(w1d), cols[2].to(b1d), cols[0].to(gd), cols[1].to(bd), dw2.to(w2d),
                 db2.to(b2d), None)
-
-
-def _projhead_bwd_fused(ctx, dyp, hb, w1b, w2b, g32, y1, ln, mean, rstd):
-    """Backward of the projection head on the fused row-panel kernel (triad_projhead_bwd: dln,
-    LayerNorm backward, dh and the dgamma / dbeta / db1 column sums in one pass over the rows) plus
-    the two weight-gradient GEMMs over the tokens (split-K) and db2."""
-    lead, H, M, Mp = ctx.shape
-    dev = dyp.device
-    st = stream_ptr(dev)
-    f32 = torch.float32
-    w2t = w2b.t().contiguous()
-    w1t = w1b.t().contiguous()
-    dy1 = torch.empty(Mp, D, dtype=torch.bfloat16, device=dev)
-    if Mp > M:
-        dy1[M:].zero_()
-    dh = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
-    ns = call("triad_projhead_bwd_slabs", M)
-    colpart = torch.empty(ns * 3 * D, dtype=f32, device=dev)
-    call("triad_projhead_bwd", ptr(dyp), M, H, ptr(w2t), ptr(w1t), ptr(y1), ptr(mean), ptr(rstd), ptr(g32), ptr(dy1),
-         ptr(dh), H, ptr(colpart), st, meta=dict(tag=f"proj{H}x{M}", flops=2.0 * M * (H * D + D * D)))
-    cols = torch.empty(3, D, dtype=f32, device=dev)
-    call("triad_sum_slabs", ptr(colpart), ns, 3 * D, None, 0, ptr(cols), st, meta=dict(tag="proj-cols", flops=0.0))
-    db2 = colsum(dyp, f32)
-    sp2 = _splitk(Mp, (D // 128) * (D // 128))
-    sp1 = _splitk(Mp, (D // 128) * (H // 128))
-    slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
-    dw2 = torch.empty(D, D, dtype=f32, device=dev)
-    call("triad_gemm_bf16_splitk", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2), 0, st,
-         meta=dict(tag=f"proj-dW2x{M}", flops=2.0 * M * D * D))
-    dw1 = torch.empty(D, H, dtype=f32, device=dev)
-    call("triad_gemm_bf16_splitk", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1), 0, st,
-         meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
-    hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
-    return (dh.view(*lead, H).to(hd), dw1.to(w1d), cols[2].to(b1d), cols[0].to(gd), cols[1].to(bd), dw2.to(w2d),
-            db2.to(b2d), None)
 
 
 class _ProjectionHeadPasses(torch.autograd.Function):
@@ -870,8 +818,8 @@ class _ProjectionHeadPasses(torch.autograd.Function):
         hd, w1d, b1d, gd, bd, w2d, b2d = ctx.dtypes
         # bf16 model weights (the trainer's shadowed Linear parameters): the gradients come out in
         # bf16 straight from the reductions, as autocast's bf16 GEMM / bias gradients do
-        # (on the GEMM like every bias sum of the step: the audio / text heads' backward runs on the
-        # concurrent backbone streams)
+        # (by LDS-DMA like every column sum of the step: the audio / text heads' backward runs on
+        # the concurrent backbone streams)
         db2 = bias_grad(dyp, torch.bfloat16 if b2d == torch.bfloat16 else f32, meta=dict(tag="proj-bias", flops=0.0))
         (f2, sp2), (f1, sp1) = _dw_plan(Mp, D), _dw_plan(Mp, H)
         slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
@@ -886,16 +834,14 @@ class _ProjectionHeadPasses(torch.autograd.Function):
                 db2.to(b2d), None)
 
 
-# Measured per call, kernel time only (tools/projhead_kernels.py, profiles/r02_projhead_kernels.log):
-# "passes" fwd 154 / bwd 443 us vs "fused" 177 / 596 us at 65,536 rows; lower at every c3 / c5 row count.
-PROJHEAD_FORM = "passes"
+# Forms: "rows" (row-panel GEMMs with the LayerNorm and its backward in the GEMM epilogues,
+# _ProjectionHeadRows) and "passes" (tiled GEMMs + LayerNorm row passes, _ProjectionHeadPasses).
+PROJHEAD_FORM = os.environ.get("TRIAD_PROJHEAD_FORM", "passes")
 
 
 def projection_head(h, proj1: torch.nn.Linear, layer_norm: torch.nn.LayerNorm, proj2: torch.nn.Linear, form=None):
-    """HIP projection head; returns bf16 (B, N, 512) like the autocast reference.
-    form "fused": the persistent row-panel kernels (projhead_rows.hip); "passes": tiled HIP GEMMs +
-    HIP LayerNorm row passes (_ProjectionHeadPasses)."""
-    fn = _ProjectionHeadPasses if (form or PROJHEAD_FORM) == "passes" else _ProjectionHead
+    """HIP projection head; returns bf16 (B, N, 512) like the autocast reference (model.py:68/116/326)."""
+    fn = {"passes": _ProjectionHeadPasses, "rows": _ProjectionHeadRows}[form or PROJHEAD_FORM]
     return fn.apply(h, proj1.weight, proj1.bias, layer_norm.weight, layer_norm.bias, proj2.weight,
                     proj2.bias, layer_norm.eps)
 
