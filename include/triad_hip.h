@@ -207,6 +207,14 @@ int triad_rowgemm_bias(const void* A, long long M, int K, long long lda, const v
 int triad_projhead_ln_bwd(const void* dy, long long M, const void* W2p, const void* y1, const float* mean,
                           const float* rstd, const float* gamma, void* dy1, float* part, hipStream_t stream);
 
+/* Inference similarity maps (model.py:355-368 compute_similarity_matrix; forward() 630-636,
+ * viz.py:182): sim[b][i][j] = temp * <f1[b][i] / max(||f1[b][i]||, eps), f2[b][j] / max(||f2[b][j]||,
+ * eps)>, f1 (B, N1, D), f2 (B, N2, D) contiguous bf16 16-byte aligned, D % 32 == 0, temp a device
+ * scalar, sim (B, N1, N2) fp32. One launch over all samples: normalisation in the prologue
+ * (operands rounded to bf16 after it, as F.normalize returns bf16), temperature in the epilogue. */
+int triad_similarity_maps(const void* f1, const void* f2, int B, int N1, int N2, int D, const float* temp, float eps,
+                          float* sim, hipStream_t stream);
+
 /* LayerNorm(512) forward of the library-GEMM projection head (model.py:68/116/326 under
  * autocast): ln = bf16((y1 - mean) rstd gamma + beta) over bf16 y1 [M][512], fp32 statistics
  * (biased variance, eps) kept in mean / rstd [M]. */

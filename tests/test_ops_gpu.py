@@ -118,6 +118,31 @@ def test_similarity_maps_match_reference(name):
     np.testing.assert_allclose(sim.cpu().numpy(), f["sim"], rtol=0, atol=1.5e-2)
 
 
+@pytest.mark.parametrize("B,N1,N2,Dd", [(1, 199, 256, 512), (3, 32, 205, 512), (2, 65, 1, 512), (4, 7, 130, 96)])
+def test_similarity_maps_one_launch(B, N1, N2, Dd):
+    """ops.similarity_maps (model.py:355-368) is ONE launch over all samples (triad_similarity_maps:
+    L2 normalisation in the prologue, temperature in the epilogue) -- against fp64
+    normalize -> bmm -> * temp on the same bf16 features; ragged tiles (N1, N2 not multiples of 64),
+    a single key, and a feature width padded to the kernel's 32."""
+    from triad_amd import _lib, ops
+    g = torch.Generator(device=dev).manual_seed(B * N1 + N2)
+    f1 = (torch.randn(B, N1, Dd, device=dev, generator=g) * 0.6).to(torch.bfloat16)
+    f2 = (torch.randn(B, N2, Dd, device=dev, generator=g) * 0.6).to(torch.bfloat16)
+    temp = torch.tensor(1.5, device=dev)
+    _lib.TIMERS = {"triad_similarity_maps": []}
+    try:
+        sim = ops.similarity_maps(f1, f2, temp)
+    finally:
+        launches, _lib.TIMERS = len(_lib.TIMERS["triad_similarity_maps"]), None
+    assert launches == 1
+    a = torch.nn.functional.normalize(f1.double(), dim=-1)
+    b = torch.nn.functional.normalize(f2.double(), dim=-1)
+    ref = torch.bmm(a, b.transpose(1, 2)) * 1.5
+    assert sim.shape == (B, N1, N2) and sim.dtype == torch.float32
+    err = float((sim.double() - ref).abs().max())
+    assert err < 1.5e-2 * 1.5, err   # operands rounded to bf16 after the normalisation (as F.normalize's bf16)
+
+
 def test_fused_adamw_matches_torch_with_onecycle_and_clip():
     from triad_amd import optim as fo
     torch.manual_seed(0)

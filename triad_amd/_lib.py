@@ -42,6 +42,7 @@ SIGNATURES = {
     "triad_gemm_bf16_splitk": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp],
     "triad_gemm_bf16_splitk_form": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp],
     "triad_wpack": [vp, i32, vp, vp],
+    "triad_similarity_maps": [vp, vp, i32, i32, i32, i32, vp, f32, vp, vp],
     "triad_rowpanel_count": [i64],
     "triad_projhead_ln_fwd": [vp, i64, i32, i64, i64, i64, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp],
     "triad_rowgemm_bias": [vp, i64, i32, i64, vp, vp, vp, vp],
@@ -136,6 +137,8 @@ def load():
                 _check_fresh()
             lib = C.CDLL(LIB_PATH)
             for name, args in SIGNATURES.items():
+                if LIB_PATH != DEFAULT_LIB and not hasattr(lib, name):
+                    continue   # an A/B variant built from older sources: only what it has
                 fn = getattr(lib, name)
                 fn.argtypes = args
                 fn.restype = RESTYPES.get(name, C.c_int)

@@ -31,7 +31,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I
          # no packed-FP32 VALU ops (v_pk_fma/add/mul_f32) in any kernel: round 3 removed them
          # when the compiler-vectorised conv0 in frontend.hip returned wrong values beside a
          # co-resident MFMA GEMM; round 4's isolated v_pk_* probes were clean beside the same
-         # GEMMs (tools/hazard_probe.py), so this is kept as a neutral setting, not a proven fix
+         # GEMMs (round 4's tools/hazard_probe.py, in git history), so this is kept as a neutral setting, not a proven fix
          # (DESIGN.md §2b). Device-side target feature; the host compile ignores it with a warning.
          "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"] + os.environ.get("TRIAD_EXTRA_FLAGS", "").split()
 # per-file extras: the pipelined forward wants scalar f32 VALU beside its MFMAs (SLP-packed

@@ -309,7 +309,7 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
   // stages, 5 ops each, stay in flight; hipcc waits for its B loads itself), barrier, 32 MFMAs with
   // the prefetch of stage st + DD (into slot (u + DD) % NB, read for the last time by stage st - 1,
   // before this barrier) issued after the first two row blocks
-  auto stage = [&](auto U, int st) {
+  auto stage = [&](auto U, int st) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
     TRIAD_VMCNT(5 * (DD - 1));
     __syncthreads();
@@ -340,15 +340,15 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
   };
 
   if (nst > 0) {   // (an empty split leaves its slab zero)
-    static_for<0, DD>([&](auto P) {
+    static_for<0, DD>([&](auto P) __attribute__((always_inline)) {
       constexpr int p = decltype(P)::value;
       db_stage<DK>(Dt, CT, Bp, mt0, kt0 + p, kt_last, lds + p * 4096, bq[p], wave, lane);
     });
     const int ngroups = nst / NB;
     for (int g = 0; g < ngroups; ++g)
-      static_for<0, NB>([&](auto U) { stage(U, g * NB + decltype(U)::value); });
+      static_for<0, NB>([&](auto U) __attribute__((always_inline)) { stage(U, g * NB + decltype(U)::value); });
     const int rem = nst - ngroups * NB, base = ngroups * NB;
-    static_for<0, NB - 1>([&](auto U) {
+    static_for<0, NB - 1>([&](auto U) __attribute__((always_inline)) {
       if (decltype(U)::value < rem) stage(U, base + decltype(U)::value);
     });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the past-the-end stages' LDS-DMA lands before exit

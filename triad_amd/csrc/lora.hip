@@ -163,7 +163,7 @@ __global__ __launch_bounds__(512, 2) void lora_tn_kernel(const bf16* __restrict_
     }
     // this thread's two 16-B pieces of a chunk: rows (tid >> 5) and +16, 16-B column (tid & 31)
     const int pr = tid >> 5, pc = tid & 31;
-    auto ld = [&](int c, int rr) -> bf16x8 {
+    auto ld = [&](int c, int rr) __attribute__((always_inline)) -> bf16x8 {
       const int m = m0 + rr;
       return m < M ? *(const bf16x8*)(Y + (long long)m * ldy + c * TN_O + pc * 8) : (bf16x8){};
     };

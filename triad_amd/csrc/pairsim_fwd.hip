@@ -271,7 +271,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   // walk cursors: prefetch (tile b+2), chain (tile b), epilogue (tile b-1); ring slots
   Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
   int fslot = 0, cslot = 0;
-  auto prefetch = [&](int b2) {
+  auto prefetch = [&](int b2) __attribute__((always_inline)) {
     if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j - j0, fc.kb, wave, lane);
     fc.next(nkb);
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
@@ -317,7 +317,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
 
   f32x16 cA, cB;
 
-  auto sync_tile = [&](int b) {
+  auto sync_tile = [&](int b) __attribute__((always_inline)) {
     // VMEM ops younger than tile b's DMA, at least: tile b+1's 4 pieces (if any) and, in
     // training, one epilogue's 2 dS stores (b >= 2); vmcnt counts both, in issue order
     // (3-slot ring; a 2-slot ring has no younger tile in flight)
@@ -331,7 +331,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  auto epi_end = [&](const f32x16& p) {
+  auto epi_end = [&](const f32x16& p) __attribute__((always_inline)) {
     if (e.m > e.m0) e.am = ec.kb * 32 + e.at;  // the tile raised the running max
     const float nn = e.nn2.x + e.nn2.y;
     accd += (double)nn;
@@ -361,7 +361,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
 
   // one tile iteration: chain of tile b into c (CH) with the epilogue of tile b-1 from p (EP,
   // FULL or masked), one element per two k-steps
-  auto iter = [&](auto CH, auto EP, auto FULLT, int b, f32x16& c, const f32x16& p) {
+  auto iter = [&](auto CH, auto EP, auto FULLT, int b, f32x16& c, const f32x16& p) __attribute__((always_inline)) {
     constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value, full = decltype(FULLT)::value;
     if constexpr (ch) {
       sync_tile(b);
@@ -393,7 +393,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   using T = std::true_type;
   using F = std::false_type;
   // epilogue variant of tile ec: FULL unless its sample's valid keys end inside it
-  auto tile_full = [&]() {
+  auto tile_full = [&]() __attribute__((always_inline)) {
     const int nk = a.klen ? min(a.klen[ec.j], a.Nk_eff) : a.Nk_eff;
     const int nv = __builtin_amdgcn_readfirstlane(nk - ec.kb * 32);
     e.nn2 = (f32x2){0.f, 0.f};
@@ -529,7 +529,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
                     __builtin_amdgcn_readfirstlane((int)((unsigned)(j1 - j0) * a.Nk_pad * (D * 2))), 0x00020000};
   Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
   int fslot = 0, cslot = 0;
-  auto prefetch = [&](int b2) {
+  auto prefetch = [&](int b2) __attribute__((always_inline)) {
     if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j - j0, fc.kb, wave, lane);
     fc.next(nkb);
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
@@ -575,7 +575,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
   e.at[0] = e.at[1] = 0;
   f32x4 cA[4], cB[4];
 
-  auto sync_tile = [&](int b) {
+  auto sync_tile = [&](int b) __attribute__((always_inline)) {
     const bool more = b + 1 < nblocks;
     const bool st = TRAIN && b >= 2;
     if (more && st) TRIAD_VMCNT(GLDS_PER_TILE + 2);
@@ -669,7 +669,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
   };
   using T = std::true_type;
   using F = std::false_type;
-  auto tile_full = [&]() {
+  auto tile_full = [&]() __attribute__((always_inline)) {
     const int nk = a.klen ? min(a.klen[ec.j], a.Nk_eff) : a.Nk_eff;
     const int nv = __builtin_amdgcn_readfirstlane(nk - ec.kb * 32);
     e.nn2 = (f32x2){0.f, 0.f};
@@ -680,7 +680,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
     e.lim[1] = (rok[1] ? min(32, nv) : 0) - 4 * g;
     return nv >= 32;
   };
-  auto copy = [&]() {
+  auto copy = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) cB[t] = cA[t];
   };

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void posconv_kernel(const bf16* __restrict__ x
   // fragments from L2 moved 4x the bytes and ran at ~1/5 of the MFMA rate).
   constexpr int NCH = KTOT / PC_KC, CH_PIECES = CG * PC_KC * 2 / 1024 / NWAVE;  // per wave
   const bf16* wg = wt + (size_t)g * CG * KTOT;
-  auto stage = [&](int ch, bf16* dst) {
+  auto stage = [&](int ch, bf16* dst) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < CH_PIECES; ++u) {
       const int piece = wave * CH_PIECES + u, row = piece * 2 + (lane >> 5), pc = lane & 31;

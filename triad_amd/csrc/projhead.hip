@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void colsum_dma_kernel(const void* __restrict_
   constexpr int PER16 = F32 ? 4 : 8;                    // columns per 16-byte piece
   const long long last16 = cols - c0 - PER16;           // the tile's last valid piece (cols % PER16 == 0)
   const long long off16 = (lane & 31) * PER16 <= last16 ? (lane & 31) * PER16 : last16;
-  auto issue = [&](int c, int slot) {
+  auto issue = [&](int c, int slot) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int p = 2 * wave + u;

@@ -126,13 +126,13 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
     for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = (f32x4){};
 
   bf16x8 bq[RP_NB][4];
-  auto load_stage = [&](int kt, int slot) {   // kt clamped: a stage past the end re-loads the last tile
+  auto load_stage = [&](int kt, int slot) __attribute__((always_inline)) {   // kt clamped: a stage past the end re-loads the last tile
     const int k = kt < nkt ? kt : nkt - 1;
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) bq[slot][cb] = *(const bf16x8*)(bsrc + (long long)k * 16384 + cb * 512);
     glds16(asrc + k * RP_K, lds + slot * RP_SLOT + wave * 512);
   };
-  auto stage = [&](auto U, int kt) {
+  auto stage = [&](auto U, int kt) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
     TRIAD_VMCNT(5 * (RP_DD - 1));   // this stage's A piece landed; the DD - 1 younger stages in flight
     __syncthreads();
@@ -151,11 +151,11 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
       }
     }
   };
-  static_for<0, RP_DD>([&](auto P) { load_stage(decltype(P)::value, decltype(P)::value); });
+  static_for<0, RP_DD>([&](auto P) __attribute__((always_inline)) { load_stage(decltype(P)::value, decltype(P)::value); });
   const int ngroups = nkt / RP_NB;
-  for (int g = 0; g < ngroups; ++g) static_for<0, RP_NB>([&](auto U) { stage(U, g * RP_NB + decltype(U)::value); });
+  for (int g = 0; g < ngroups; ++g) static_for<0, RP_NB>([&](auto U) __attribute__((always_inline)) { stage(U, g * RP_NB + decltype(U)::value); });
   const int rem = nkt - ngroups * RP_NB, base = ngroups * RP_NB;
-  static_for<0, RP_NB - 1>([&](auto U) {
+  static_for<0, RP_NB - 1>([&](auto U) __attribute__((always_inline)) {
     if (decltype(U)::value < rem) stage(U, base + decltype(U)::value);
   });
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
   // row sums over the 512 columns: in-lane over (cb, i), lanes q = 0..3 (xor 16, 32), then waves
   // v[r] (rows 16 (rb0 + r) + l16 of the panel) summed over the 512 columns and returned to every
   // lane holding the row
-  auto row_reduce = [&](auto& v, int rb0) {
+  auto row_reduce = [&](auto& v, int rb0) __attribute__((always_inline)) {
     constexpr int R = sizeof(v) / sizeof(float);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
   // per-column vectors (bias, gamma, beta) staged in LDS: each (cb) read is one broadcast ds_read_b128
   float* vec = red + 2304;
   const int cw = 64 * wave + 4 * q;   // + 16 cb: this lane's first column of a column block
-  auto col4 = [&](int which, int cb) { return *(const f32x4*)(vec + which * RP_N + cw + 16 * cb); };
+  auto col4 = [&](int which, int cb) __attribute__((always_inline)) { return *(const f32x4*)(vec + which * RP_N + cw + 16 * cb); };
   if (threadIdx.x < RP_N) {
     const int n = threadIdx.x;
     if (EPI != 2) vec[n] = a.bias[n];

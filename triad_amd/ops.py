@@ -905,31 +905,26 @@ def patch_dropout(x: torch.Tensor, keep_mask: torch.Tensor, n_out: Optional[int]
 # ----------------------------------------------------------------------------------------
 # Inference similarity maps (model.py:355-368) and the materialising debug path
 # ----------------------------------------------------------------------------------------
-def _bmm_nt(a: torch.Tensor, b: torch.Tensor, alpha: torch.Tensor) -> torch.Tensor:
-    """out[i] = alpha * a[i] . b[i]^T for (B,N1,D) x (B,N2,D) bf16 via the HIP GEMM (fp32 out)."""
-    B, N1, Dd = a.shape
-    N2 = b.shape[1]
-    M, N = _rup(N1, 128), _rup(N2, 128)
-    Kd = _rup(Dd, 64)
-    out = torch.empty(B, N1, N2, dtype=torch.float32, device=a.device)
-    ap = torch.zeros(M, Kd, dtype=torch.bfloat16, device=a.device)
-    bp = torch.zeros(N, Kd, dtype=torch.bfloat16, device=a.device)
-    cp = torch.empty(M, N, dtype=torch.float32, device=a.device)
-    st = stream_ptr(a.device)
-    for i in range(B):
-        ap[:N1, :Dd].copy_(a[i])
-        bp[:N2, :Dd].copy_(b[i])
-        call("triad_gemm_bf16", ptr(ap), Kd, 1, ptr(bp), Kd, 1, M, N, Kd, ptr(alpha), ptr(cp), N, 0, st)
-        out[i].copy_(cp[:N1, :N2])
-    return out
-
-
 def similarity_maps(f1: torch.Tensor, f2: torch.Tensor, temperature: torch.Tensor) -> torch.Tensor:
-    """normalize(f1) . normalize(f2)^T * temperature per sample, (B,N1,N2) fp32 (inference)."""
+    """normalize(f1) . normalize(f2)^T * temperature per sample, (B,N1,N2) fp32 (inference,
+    model.py:355-368): ONE launch over all B samples, the L2 normalisation in its prologue and the
+    temperature in its epilogue (triad_similarity_maps)."""
     _check_device(f1, f2)
     if f1.dim() == 2:
         f1 = f1.unsqueeze(0)
     if f2.dim() == 2:
         f2 = f2.unsqueeze(0)
+    if f1.shape[0] != f2.shape[0] or f1.shape[-1] != f2.shape[-1]:
+        raise TriadError(f"similarity_maps: {tuple(f1.shape)} vs {tuple(f2.shape)}")
+    B, N1, Dd = f1.shape
+    N2 = f2.shape[1]
+    a = f1.to(torch.bfloat16).contiguous()
+    b = f2.to(torch.bfloat16).contiguous()
+    if Dd % 32:   # zero-padded features (norms and dots unchanged)
+        a = torch.nn.functional.pad(a, (0, _rup(Dd, 32) - Dd))
+        b = torch.nn.functional.pad(b, (0, _rup(Dd, 32) - Dd))
     t = temperature.detach().reshape(1).to(torch.float32).contiguous()
-    return _bmm_nt(l2_normalize(f1), l2_normalize(f2), t)
+    out = torch.empty(B, N1, N2, dtype=torch.float32, device=f1.device)
+    call("triad_similarity_maps", ptr(a), ptr(b), B, N1, N2, a.shape[-1], ptr(t), 1e-12, ptr(out),
+         stream_ptr(f1.device), meta=dict(tag="simmap", flops=2.0 * B * N1 * N2 * Dd))
+    return out
