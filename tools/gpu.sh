@@ -61,11 +61,13 @@ for step in "$@"; do
         2> "gpurun_out/${tag}_benchenv${n}.err" ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${tag}_prof" -o bench \
-        -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --separate-steps 0 > "gpurun_out/${tag}_prof.log" 2>&1 ;;
+        -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --separate-steps 0 \
+        --single-stream-steps 0 --no-stream-check > "gpurun_out/${tag}_prof.log" 2>&1 ;;
     pmc:*)
       rest=${step#pmc:}; name=${rest%%:*}; ctr=${rest#*:}
       timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "gpurun_out/${tag}_pmc_${name}" -o run \
-        -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --separate-steps 0 > "gpurun_out/${tag}_pmc_${name}.log" 2>&1 ;;
+        -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --separate-steps 0 \
+        --single-stream-steps 0 --no-stream-check > "gpurun_out/${tag}_pmc_${name}.log" 2>&1 ;;
     profpy:*)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${tag}_profpy${n}" -o run \
         -- python3 ${step#profpy:} > "gpurun_out/${tag}_profpy${n}.log" 2>&1 ;;

@@ -89,25 +89,13 @@ __device__ __forceinline__ void stage_tile(i32x4 kr, const FwdArgs& a, bf16* dst
 // 16-byte store hidden from hipcc's waitcnt bookkeeping (it would otherwise drain vmcnt(0) --
 // the in-flight key DMA included -- before reusing the data registers); the trailing
 // s_nop 1 covers the store-data read (cdna_hip_programming.md §5.7). Counted in sync_tile.
-// TRIAD_DS_STORE_POL (0 plain, 1 sc1, 2 nt, 3 sc0 sc1, 4 sc1 nt): cache-policy bits of the unit-dS stores (A/B builds; the dS stream,
-// 5.9 GB at c3 AV, is read back only by the backward GEMMs, long after it left L2).
+// Cache policy of the unit-dS stores: plain. Round 5 built sc1 / nt / sc0 sc1 /
+// sc1 nt variants: training forward AV 3.04 ms plain vs 4.58-4.62 (sc1, sc0 sc1), 3.16 (nt),
+// 5.71 (sc1 nt); TV 0.54 vs 0.76 / 0.55 / 0.94 (profiles/r05_fwd_ds_store_policy_ab.log) --
+// letting L2 merge the 2 KB tiles before write-back is worth more than keeping them out of it.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-#ifndef TRIAD_DS_STORE_POL
-#define TRIAD_DS_STORE_POL 0
-#endif
-#if TRIAD_DS_STORE_POL == 1
-#define TRIAD_DS_STORE_POLICY "sc1"
-#elif TRIAD_DS_STORE_POL == 2
-#define TRIAD_DS_STORE_POLICY "nt"
-#elif TRIAD_DS_STORE_POL == 3
-#define TRIAD_DS_STORE_POLICY "sc0 sc1"
-#elif TRIAD_DS_STORE_POL == 4
-#define TRIAD_DS_STORE_POLICY "sc1 nt"
-#else
-#define TRIAD_DS_STORE_POLICY ""
-#endif
 __device__ __forceinline__ void store16(void* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off " TRIAD_DS_STORE_POLICY "\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {  // one v_cvt_pk_bf16_f32
