@@ -324,3 +324,35 @@ def test_vit_embedder_mirrors_the_reference_surface():
     assert emb.patch_dropout_rate == 0.1
     x = torch.zeros(2, 5, 512)
     assert emb.eval().patch_dropout(x, 0.1) is x and emb.train().patch_dropout(x, 0) is x
+
+
+def test_param_sumsq_is_a_segmented_sum_per_parameter(monkeypatch):
+    """optim.FlatParamSpace.param_sumsq: the per-chunk partials of triad_grad_sumsq (emulated here
+    from the chunk table) are summed per parameter by torch.segment_reduce over the table's
+    parameter order -- equal to the per-parameter sums of squares for any id order / repeats, with
+    zero for the parameters not asked for (no index_add_ atomics, so the clip coefficient does not
+    depend on the order the atomics land in)."""
+    from triad_amd import optim as fo
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(n)) for n in (5, fo.CHUNK * 2 + 7, 1, fo.CHUNK, 300)]
+    sp = fo.FlatParamSpace(ps, "cpu")
+    sp.flat_g.copy_(torch.randn(sp.numel))
+
+    def fake_call(name, *args, **kw):
+        assert name == "triad_grad_sumsq"
+        g = sp.flat_g.double()
+        table = np.frombuffer(args[1].numpy().tobytes(), dtype=fo._CHUNK_DT)
+        out = args[3]
+        for k, r in enumerate(table[:args[2]]):
+            out[k] = float((g[int(r["off"]):int(r["off"]) + int(r["n"])] ** 2).sum())
+    monkeypatch.setattr(fo, "call", fake_call)
+    monkeypatch.setattr(fo, "ptr", lambda t: t)
+    monkeypatch.setattr(fo, "stream_ptr", lambda d: None)
+    for ids in ([0, 1, 2, 3, 4], [3, 1, 1], [4], [2, 0]):
+        got = sp.param_sumsq(ids)
+        want = torch.zeros(len(ps), dtype=torch.float64)
+        for i in set(ids):
+            o = sp.offsets[i]
+            want[i] = (sp.flat_g[o:o + ps[i].numel()].double() ** 2).sum()
+        torch.testing.assert_close(got, want, rtol=1e-12, atol=0)
+

@@ -155,14 +155,30 @@ class FlatParamSpace:
         return [i for i in ids if self.touched[i]]
 
     def param_sumsq(self, ids: Sequence[int]) -> torch.Tensor:
-        """Per-parameter sum of squared gradients (float64, indexed by parameter id)."""
-        out = torch.zeros(len(self.params), dtype=torch.float64, device=self.device)
+        """Per-parameter sum of squared gradients (float64, indexed by parameter id). The per-chunk
+        partials are summed per parameter by a segmented reduction over the chunk table (ordered by
+        parameter), not index_add_'s atomics: the clip coefficient is then the same every run."""
+        ids = sorted(set(int(i) for i in ids))
         table, n, owner = self.chunks(ids)
-        if n:
-            part = torch.empty(n, dtype=torch.float64, device=self.device)
-            call("triad_grad_sumsq", ptr(self.flat_g), ptr(table), n, ptr(part), stream_ptr(self.device))
-            out.index_add_(0, owner, part)
-        return out
+        if not n:
+            return torch.zeros(len(self.params), dtype=torch.float64, device=self.device)
+        part = torch.empty(n, dtype=torch.float64, device=self.device)
+        call("triad_grad_sumsq", ptr(self.flat_g), ptr(table), n, ptr(part), stream_ptr(self.device))
+        return torch.segment_reduce(part, "sum", lengths=self._segment_lengths(ids), unsafe=True)
+
+    def _segment_lengths(self, ids: Sequence[int]) -> torch.Tensor:
+        """Chunks per parameter id (0 for the ids not in `ids`) as a device int64 tensor (cached)."""
+        key = ("seg",) + tuple(ids)
+        t = self._index_cache.get(key)
+        if t is None:
+            lens = [0] * len(self.params)
+            for i in ids:
+                lens[i] = (self.params[i].numel() + CHUNK - 1) // CHUNK
+            if len(self._index_cache) > 64:
+                self._index_cache.clear()
+            t = _lib.h2d(torch.tensor(lens, dtype=torch.long), self.device)
+            self._index_cache[key] = t
+        return t
 
     def master(self, i: int) -> torch.Tensor:
         """fp32 master of parameter i (a view of the flat buffer)."""
