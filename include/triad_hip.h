@@ -163,6 +163,13 @@ int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, 
 int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
                          int M, int N, int Kd, const float* bias, void* C, long long ldc, hipStream_t stream);
 
+/* triad_gemm_bf16_bias with the bias as the bf16 vector of the autocast model (what F.linear
+ * under autocast adds, widened to fp32 in the epilogue): bit-identical to passing its fp32
+ * widening, without that copy per call (model.py:68/116/326 heads, the backbone Linear layers). */
+int triad_gemm_bf16_bias_bf16(const void* A, long long lda, int a_kcontig, const void* B, long long ldb,
+                              int b_kcontig, int M, int N, int Kd, const void* bias, void* C, long long ldc,
+                              hipStream_t stream);
+
 /* Split-K GEMM (weight gradients of the projection heads, train.py:987 backward):
  * `splits` fp32 partial slabs [splits][M][N] in caller-owned `slabs`, then C = alpha * sum. */
 int triad_gemm_bf16_splitk(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,

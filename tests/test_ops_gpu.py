@@ -238,7 +238,9 @@ def test_trainer_fused_optimizer_matches_torch_adamw():
     clipping) becomes the .grad of an fp32 copy of the model under TriadTrainer(optimizer='torch')
     -- torch.optim.AdamW + clip_grad_norm_ -- which is stepped by the trainer's own optimizer code.
     Two steps; every parameter (the fused form's fp32 masters) within 1e-6 of torch's, per element
-    relative to |p| + the steps' summed learning rate, and every exp_avg_sq within 1e-6 relative.
+    relative to |p| + the steps' summed learning rate, and every exp_avg_sq within 1e-6 relative; the
+    clipped audio / text embedders' tolerance widens by the measured difference of the two clip
+    coefficients (torch's fp32 norm vs the fused fp64 one).
     (Round 4 compared two separately computed backward passes and needed a 2 % escape hatch.)"""
     import copy
     from triad_amd import checkpoint as ck
@@ -262,6 +264,16 @@ def test_trainer_fused_optimizer_matches_torch_adamw():
     fused_step = tr_f._optimizer_step
 
     lr_sum = [0.0]
+    p0 = {n: p.detach().clone() for n, p in params_t.items()}
+    snaps = []
+    # the clip coefficient of the audio / text embedders (clip_grad_norm_ at 10, train.py:1004-1006)
+    # is the one place the two forms compute differently on purpose: torch's norm accumulates in fp32
+    # (_foreach_norm), the fused form's in fp64. Their relative difference, per clipped module, widens
+    # that module's tolerance (an Adam update is scale-invariant except through eps).
+    clip_dev = {"audio_embedder.": 0.0, "text_embedder.": 0.0}
+
+    def coef(n):
+        return min(1.0, 10.0 / (n + 1e-6))
 
     def step_both():
         # the fused trainer's reduced gradient per parameter, fp32 (before clipping / AdamW)
@@ -269,6 +281,13 @@ def test_trainer_fused_optimizer_matches_torch_adamw():
         sp = tr_f.space
         snap = {names_f[id(p)]: sp.flat_g[sp.offsets[i]:sp.offsets[i] + p.numel()].view(p.shape).clone()
                 for i, p in enumerate(sp.params) if sp.touched[i]}
+        for pre in clip_dev:
+            gs = [g for n, g in snap.items() if n.startswith(pre)]
+            if gs:
+                n_t = float(torch.nn.utils.get_total_norm(gs, 2.0))
+                n_f = float(torch.tensor(math.sqrt(sum(float(g.double().pow(2).sum()) for g in gs))).float())
+                clip_dev[pre] = max(clip_dev[pre], abs(coef(n_t) / coef(n_f) - 1.0))
+        snaps.append(snap)
         out = fused_step()
         # the same gradients through the torch optimizer path of the trainer
         tr_t._update_frozen_params(tr_t.global_step)
@@ -294,7 +313,19 @@ def test_trainer_fused_optimizer_matches_torch_adamw():
         b = pt.detach().float()
         err = float(((a - b).abs() / (b.abs() + lr_sum[0])).max())
         worst = max(worst, err)
-        assert err <= 1e-6, (n, err)
+        tol = 1e-6 + sum(2 * d for pre, d in clip_dev.items() if n.startswith(pre))
+        if err > 0.5 * tol:
+            e = int(((a - b).abs() / (b.abs() + lr_sum[0])).flatten().argmax())
+            i = {id(q): k for k, q in enumerate(tr_f.space.params)}[id(dict(m.named_parameters())[n])]
+            o = tr_f.space.offsets[i] + e
+            st = next((opt.state[pt] for opt in (tr_t.opt_others, tr_t.opt_audio, tr_t.opt_text, tr_t.opt_vit)
+                       if pt in opt.state), {})
+            print("DIAG", n, "err", err, "fused", float(a.flatten()[e]), "torch", float(b.flatten()[e]),
+                  "p0", float(p0[n].flatten()[e]), "g", [float(sn[n].flatten()[e]) if n in sn else None for sn in snaps],
+                  "m f/t", float(tr_f.space.exp_avg[o]), float(st["exp_avg"].flatten()[e]) if st else None,
+                  "v f/t", float(tr_f.space.exp_avg_sq[o]), float(st["exp_avg_sq"].flatten()[e]) if st else None,
+                  "lr_sum", lr_sum[0], "clip", clip_dev)
+        assert err <= tol, (n, err, tol)
     # the second-moment state (a sum of squares: no cancellation) at 1e-6 relative as well
     sp = tr_f.space
     pos = {id(p): i for i, p in enumerate(sp.params)}
@@ -308,8 +339,9 @@ def test_trainer_fused_optimizer_matches_torch_adamw():
         vt = st["exp_avg_sq"].float()
         err = float((vf - vt).abs().max()) / (float(vt.abs().max()) + 1e-30)
         worst = max(worst, err)
-        assert err <= 1e-6, (n, "exp_avg_sq", err)
-    print("worst relative parameter difference", worst)
+        tol = 1e-6 + sum(3 * d for pre, d in clip_dev.items() if n.startswith(pre))
+        assert err <= tol, (n, "exp_avg_sq", err, tol)
+    print("worst relative difference", worst, "clip coefficient deviation", clip_dev)
 
 
 def test_trainer_bf16_model_weights_track_fp32_masters():
@@ -388,7 +420,7 @@ def test_triad_linear_matches_autocast_linear(M, K, O, bias):
                                             (66816, 3072, 768, True, False), (66816, 768, 3072, False, True),
                                             (256, 768, 768, True, False), (130, 768, 768, True, False)])
 def test_backbone_gemm_vs_fp32(M, N, K, bias, dx):
-    """gemm.linear / gemm.mm (triad_gemm_bf16_bias, tile form by shape; 130 rows -> vendor BLAS
+    """gemm.linear / gemm.mm (triad_gemm_bf16_bias[_bf16], tile form by shape; 130 rows -> vendor BLAS
     fallback) against an fp32 matmul of the same bf16 operands, bias added before the rounding."""
     from triad_amd import gemm
     g = torch.Generator(device=dev).manual_seed(M + N + K)
@@ -406,6 +438,23 @@ def test_backbone_gemm_vs_fp32(M, N, K, bias, dx):
     assert y.dtype == torch.bfloat16 and y.shape == (M, N)
     assert torch.allclose(y.float(), ref.to(torch.bfloat16).float(), rtol=1.6e-2, atol=1e-2 * float(ref.abs().max()))
     assert float((y.float() - ref).norm() / ref.norm()) < 3e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(50944, 512, 768), (16384, 768, 768), (8192, 512, 512), (256, 768, 768)])
+def test_gemm_bf16_bias_equals_its_fp32_widening(M, N, K):
+    """triad_gemm_bf16_bias_bf16 (the bias read as the bf16 vector, gemm.linear's path) is bit-identical
+    to triad_gemm_bf16_bias given that vector widened to fp32, at every tile form's shape."""
+    from triad_amd._lib import call, ptr, stream_ptr
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    a = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    w = torch.randn(N, K, device=dev, generator=g).to(torch.bfloat16)
+    b = torch.randn(N, device=dev, generator=g).to(torch.bfloat16)
+    b32 = b.float()
+    y16, y32 = (torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(2))
+    call("triad_gemm_bf16_bias_bf16", ptr(a), K, 1, ptr(w), K, 1, M, N, K, ptr(b), ptr(y16), N, stream_ptr())
+    call("triad_gemm_bf16_bias", ptr(a), K, 1, ptr(w), K, 1, M, N, K, ptr(b32), ptr(y32), N, stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(y16, y32)
 
 
 @pytest.mark.parametrize("rows,cols", [(50944, 768), (8192, 3072), (100, 8), (65536, 512), (7, 2304)])

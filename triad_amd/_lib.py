@@ -39,6 +39,7 @@ SIGNATURES = {
     "triad_tile_gemm_packed16_slabs": [vp, i64, i32, vp, i32, i32, i32, vp, vp],
     "triad_gemm_bf16": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, i32, vp],
     "triad_gemm_bf16_bias": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, vp],
+    "triad_gemm_bf16_bias_bf16": [vp, i64, i32, vp, i64, i32, i32, i32, i32, vp, vp, i64, vp],
     "triad_gemm_bf16_splitk": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp],
     "triad_gemm_bf16_splitk_form": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp],
     "triad_wpack": [vp, i32, vp, vp],

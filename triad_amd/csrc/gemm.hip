@@ -74,6 +74,13 @@ __device__ __forceinline__ bf16x8 frag_tr(const bf16* img, int n0, int s, int la
   return r;
 }
 
+// F.linear's bias for output column n, added before the one rounding: fp32, or bf16 as the
+// autocast model holds it (read as is, no fp32 copy of the vector per call)
+__device__ __forceinline__ float bias_at(const void* bias, int bias_bf16, int n) {
+  if (!bias) return 0.f;
+  return bias_bf16 ? (float)((const bf16*)bias)[n] : ((const float*)bias)[n];
+}
+
 // Workgroup -> (output tile, k split). Default: XCD-aware bijective remap of blockIdx.x -- blocks
 // sharing an XCD (bid % 8 under round-robin placement) get consecutive tiles, so the column tiles
 // of one row panel of A share that XCD's L2; blockIdx.y is the split. xsplit (split-K weight
@@ -99,7 +106,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
                                                       const bf16* __restrict__ B, long long ldb,
                                                       int M, int N, int Kd, const float* __restrict__ alpha_p,
                                                       OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                      long long slab_stride, const float* __restrict__ bias, int xsplit) {
+                                                      long long slab_stride, const void* __restrict__ bias, int bias_bf16, int xsplit) {
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * (A_ELEMS + B_ELEMS)];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -168,7 +175,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ A
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int n = n0 + wn * 64 + b * 32 + (lane & 31);
-      const float bn = bias ? bias[n] : 0.f;   // F.linear's bias, added before the one rounding
+      const float bn = bias_at(bias, bias_bf16, n);   // F.linear's bias, added before the one rounding
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int m = m0 + wm * 64 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
@@ -225,7 +232,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
                                                           const bf16* __restrict__ B, long long ldb, int M, int N,
                                                           int Kd, const float* __restrict__ alpha_p,
                                                           OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                          long long slab_stride, const float* __restrict__ bias, int xsplit) {
+                                                          long long slab_stride, const void* __restrict__ bias, int bias_bf16, int xsplit) {
   __shared__ __attribute__((aligned(16))) bf16 lds[GB_NB * GB_ST];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -292,7 +299,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16* __restrict
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int n = n0 + wn * 64 + b * 32 + (lane & 31);
-      const float bn = bias ? bias[n] : 0.f;   // F.linear's bias, added before the one rounding
+      const float bn = bias_at(bias, bias_bf16, n);   // F.linear's bias, added before the one rounding
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int m = m0 + wm * 64 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
@@ -361,7 +368,7 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
                                                          const bf16* __restrict__ B, long long ldb, int M, int N,
                                                          int Kd, const float* __restrict__ alpha_p,
                                                          OutT* __restrict__ C, long long ldc, int k_per_split,
-                                                         long long slab_stride, const float* __restrict__ bias, int xsplit) {
+                                                         long long slab_stride, const void* __restrict__ bias, int bias_bf16, int xsplit) {
   __shared__ __attribute__((aligned(16))) bf16 lds[2 * GW_ST];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -427,7 +434,7 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_kernel(const bf16* __restrict_
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int n = n0 + wn * 64 + b * 32 + (lane & 31);
-      const float bn = bias ? bias[n] : 0.f;
+      const float bn = bias_at(bias, bias_bf16, n);
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int m = m0 + wm * 128 + a * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
@@ -454,7 +461,7 @@ constexpr int kXcdSplit = 8;
 template <bool AK, bool BK_, typename OutT>
 int launch(const void* A, long long lda, const void* B, long long ldb, int M, int N, int Kd, const float* alpha,
            void* C, long long ldc, hipStream_t st, int splits = 1, long long slab_stride = 0,
-           const float* bias = nullptr, int form = 0) {
+           const void* bias = nullptr, int form = 0, int bias_bf16 = 0) {
   const int xsplit = (form & kXcdSplit) ? 1 : 0;
   form &= ~kXcdSplit;
   if (M % BM || N % BN || Kd % BK || lda % 8 || ldb % 8 || splits < 1) return TRIAD_EINVAL;
@@ -471,7 +478,7 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
   if (w4_ok && (form == 4 || form == 3)) {   // (form 3, the four-wave 256 x 256 tile, was retired in round 5)
     const int nwg = (M / GW_M) * (N / GW_N);
     hipLaunchKernelGGL((gemm_w8_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
-                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, xsplit);
+                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, bias_bf16, xsplit);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
@@ -479,13 +486,13 @@ int launch(const void* A, long long lda, const void* B, long long ldb, int M, in
       (form == 2 || M >= 8192 || Kd / splits >= 32768)) {
     const int nwg = (M / GB_M) * (N / BN);
     hipLaunchKernelGGL((gemm_big_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(512), 0, st, (const bf16*)A, lda,
-                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, xsplit);
+                       (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, bias_bf16, xsplit);
     TRIAD_CHECK_LAUNCH();
     return TRIAD_OK;
   }
   const int nwg = (M / BM) * (N / BN);
   hipLaunchKernelGGL((gemm_kernel<AK, BK_, OutT>), dim3(nwg, splits), dim3(256), 0, st, (const bf16*)A, lda,
-                     (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, xsplit);
+                     (const bf16*)B, ldb, M, N, Kd, alpha, (OutT*)C, ldc, kps, slab_stride, bias, bias_bf16, xsplit);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
@@ -527,8 +534,8 @@ int triad_gemm_bf16(const void* A, long long lda, int a_kcontig, const void* B, 
 // the output is tall (M >= 32768, M and N multiples of 256), the 256 x 128 ring for other tall
 // outputs, 128 x 128 below 8192 rows. 790-940 TFLOP/s; rocBLAS's own kernels run the same shapes
 // at 300-790.
-int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
-                         int M, int N, int Kd, const float* bias, void* C, long long ldc, hipStream_t stream) {
+static int gemm_bias_launch(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig, int M,
+                     int N, int Kd, const void* bias, int bias_bf16, void* C, long long ldc, hipStream_t stream) {
   // eight-wave 256 x 256 for every tall output it tiles; the 256 x 128 ring only when its tiles
   // fill the 256 CUs once (the 8,192-row text projection head at N = 512 has 128 such tiles, half
   // the chip, and runs on 256 128 x 128 tiles instead)
@@ -537,13 +544,26 @@ int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void
   else if (M >= 8192 && M % GB_M == 0 && (long long)(M / GB_M) * (N / BN) >= 256) form = 2;
 #define TRIAD_GEMM_B(AK, BKC)                                                                     \
   if (!!a_kcontig == AK && !!b_kcontig == BKC)                                                    \
-    return launch<AK, BKC, bf16>(A, lda, B, ldb, M, N, Kd, nullptr, C, ldc, stream, 1, 0, bias, form);
+    return launch<AK, BKC, bf16>(A, lda, B, ldb, M, N, Kd, nullptr, C, ldc, stream, 1, 0, bias, form, bias_bf16);
   TRIAD_GEMM_B(true, true)
   TRIAD_GEMM_B(true, false)
   TRIAD_GEMM_B(false, true)
   TRIAD_GEMM_B(false, false)
 #undef TRIAD_GEMM_B
   return TRIAD_EINVAL;
+}
+
+int triad_gemm_bf16_bias(const void* A, long long lda, int a_kcontig, const void* B, long long ldb, int b_kcontig,
+                         int M, int N, int Kd, const float* bias, void* C, long long ldc, hipStream_t stream) {
+  return gemm_bias_launch(A, lda, a_kcontig, B, ldb, b_kcontig, M, N, Kd, bias, 0, C, ldc, stream);
+}
+
+// The same with the bias as the bf16 vector the autocast model holds (F.linear under autocast
+// casts the bias to bf16 and adds it in fp32 before the one rounding): no fp32 copy per call.
+int triad_gemm_bf16_bias_bf16(const void* A, long long lda, int a_kcontig, const void* B, long long ldb,
+                              int b_kcontig, int M, int N, int Kd, const void* bias, void* C, long long ldc,
+                              hipStream_t stream) {
+  return gemm_bias_launch(A, lda, a_kcontig, B, ldb, b_kcontig, M, N, Kd, bias, 1, C, ldc, stream);
 }
 
 // Split-K form for short-and-wide outputs (weight gradients: M, N = 512 / H, Kd = tokens):

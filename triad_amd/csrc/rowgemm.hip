@@ -12,7 +12,7 @@
 //   * 8 waves, wave w owns output columns [64 w, 64 w + 64): 8 x 4 blocks of 16 x 16 on
 //     v_mfma_f32_16x16x32_bf16 (128 fp32 accumulators per lane);
 //   * A (the token rows, 128 x 32 bf16 = 8 KB per 32-deep k tile) through a 4-slot LDS ring by
-//     16-byte LDS-DMA, one 1 KB piece per wave per tile, chunks XOR-swizzled by row so the
+//     16-byte LDS-DMA, one 1 KB piece per wave per tile, chunks XOR-swizzled by row (rp_swz) so the
 //     fragment reads are conflict-free;
 //   * B (the weight, shared by every workgroup and L2-resident) pre-arranged once per call in
 //     MFMA-fragment order and streamed by each wave straight into registers with four ordinary
@@ -35,6 +35,9 @@ namespace {
 constexpr int RP_M = 128, RP_N = 512, RP_K = 32;   // panel rows, columns, k tile
 constexpr int RP_DD = 3, RP_NB = RP_DD + 1;        // stages in flight ahead, ring slots
 constexpr int RP_SLOT = RP_M * RP_K;              // elements per A ring slot (8 KB)
+// EPI 2 (LayerNorm backward) brings the panel's 128 y1 rows (128 KB) into LDS by LDS-DMA after the
+// k loop, behind the 16 KB the epilogue's row exchange / column vectors use
+constexpr int RP_Y1_OFF = 8192;                    // elements
 
 struct RPArgs {
   const bf16* A;            // token rows (two-level addressing below)
@@ -100,23 +103,33 @@ __global__ __launch_bounds__(256) void wpack_t_kernel(const bf16* __restrict__ W
   *(bf16x8*)(Bp + f * 8) = *(const bf16x8*)(W + (long long)n * K + k);
 }
 
+// A ring slot = [128 rows][32 k] bf16, 64 B per row: 16-byte chunk c of row r sits at chunk
+// c ^ rp_swz(r). ds_read_b128 serves a wave in four lane groups of 16 ({0-3, 12-15, 20-27}, ...,
+// MI355X_MICROARCH.md LDS table), bank = (byte / 4) mod 64; a fragment read has lane l at row
+// 16 rb + (l & 15), chunk l >> 4. Row r & 3 picks the 16-dword bank block, so each group needs its
+// four (chunk ^ swz) values distinct: swz = (-(r >> 2)) & 3 does that for all four groups (the plain
+// (r >> 2) & 3 left 2-way conflicts in every group: SQ_LDS_BANK_CONFLICT 41-44 % of the LDS cycles,
+// profiles/r05_projhead_pmc.txt).
+__device__ __forceinline__ int rp_swz(int r) { return (-(r >> 2)) & 3; }
+
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
-  // the A ring during the k loop; the epilogue reuses it (row exchange, per-column vectors)
-  __shared__ __attribute__((aligned(16))) bf16 lds[RP_NB * RP_SLOT];
+  // the A ring during the k loop; the epilogue reuses it (row exchange, per-column vectors; EPI 2:
+  // + the y1 panel)
+  __shared__ __attribute__((aligned(16))) bf16 lds[EPI == 2 ? RP_Y1_OFF + RP_M * RP_N : RP_NB * RP_SLOT];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, q = lane >> 4;
   const long long m0 = (long long)blockIdx.x * RP_M;
   const int nkt = a.K / RP_K;
 
   // this lane's LDS-DMA source row (fixed over the k loop): panel row 16 wave + (lane >> 2),
-  // 16-byte chunk (lane & 3) ^ ((row >> 2) & 3) of each 64-byte k-tile row
+  // 16-byte chunk (lane & 3) ^ rp_swz(row) of each 64-byte k-tile row
   const int pr = 16 * wave + (lane >> 2);
   const long long srow = m0 + pr < a.M ? m0 + pr : a.M - 1;
   const bf16* asrc = a.A + (srow / a.n_per) * a.bstride + (srow % a.n_per) * a.lda +
-                     8 * ((lane & 3) ^ ((pr >> 2) & 3));
+                     8 * ((lane & 3) ^ rp_swz(pr));
   // this lane's fragment reads: row 16 rb + l16, chunk q
-  const int aoff = l16 * RP_K + 8 * (q ^ ((l16 >> 2) & 3));   // + rb * 16 * RP_K (rb * 16 keeps (r >> 2) & 3)
+  const int aoff = l16 * RP_K + 8 * (q ^ rp_swz(l16));   // + rb * 16 * RP_K (rb * 16 keeps rp_swz)
   const bf16* bsrc = a.Bp + (long long)wave * 2048 + lane * 8;
 
   f32x4 acc[8][4];
@@ -160,6 +173,17 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
   });
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();   // every wave is done with the ring: the epilogue may reuse it
+  if constexpr (EPI == 2) {
+    // the panel's y1 rows, one 1 KB row per LDS-DMA piece (wave w: rows 16 w ..), 16-byte chunk c
+    // of row r at chunk c ^ (r & 15): the epilogue's 8-byte reads (16 rows x one chunk per half
+    // wave) are then conflict-free. One wait for all of it, instead of 16 dependent global loads
+    // per lane (SQ_WAIT_ANY 0.53 of this kernel's wave time with those, profiles/r05_projhead_pmc.txt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = 16 * wave + i;
+      glds16(a.y1 + (m0 + r) * RP_N + 8 * (lane ^ (r & 15)), lds + RP_Y1_OFF + r * RP_N);
+    }
+  }
 
   // lane holds, per (rb, cb): row m0 + 16 rb + l16, columns n0 + i, n0 = 64 wave + 16 cb + 4 q
   float* red = (float*)lds;   // row exchange (<= 2304 floats); per-column vectors at + 2304
@@ -278,9 +302,10 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
     // dy1 = bf16(rstd (g - mean(g) - xh mean(g xh))); column partials over the panel's rows:
     // dgamma = sum dln xh, dbeta = sum dln, db1 = sum dy1. y1 / mean / rstd have the panel-padded
     // row count and the forward wrote zeros in the pad rows (xh = 0, rstd = 0 there: dy1 and every
-    // partial get nothing from them) -- read unmasked. The scheduling fences keep hipcc from
-    // hoisting every row's loads at once (the live state -- packed dln, row statistics, the 48
-    // column partials -- then fits the register file without spills).
+    // partial get nothing from them) -- read unmasked (y1 from the LDS panel loaded after the k
+    // loop). The scheduling fences keep hipcc from hoisting every row's reads at once (the live
+    // state -- packed dln, row statistics, the 48 column partials -- then fits the register file
+    // without spills).
     unsigned dl[8][4][2];
 #pragma unroll
     for (int rb = 0; rb < 8; ++rb) {
@@ -292,18 +317,27 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
           dl[rb][cb][j] = pack_bf2(ok ? acc[rb][cb][2 * j] : 0.f, ok ? acc[rb][cb][2 * j + 1] : 0.f);
     }
     opaque(dl);   // packed here, once: the accumulators die (hipcc would sink each row's packing to its use)
-    const bf16* y1p = a.y1 + (m0 + l16) * RP_N + cw;          // + rb * 16 * RP_N + 16 cb
     bf16* op = a.out0 + (m0 + l16) * RP_N + cw;
+    // y1[row 16 rb + l16][cw + 16 cb .. + 3] from the LDS panel (swizzle above)
+    auto y1_at = [&](int rb, int cb) __attribute__((always_inline)) {
+      const int c = 8 * wave + 2 * cb + (q >> 1);
+      return *(const uint2*)(lds + RP_Y1_OFF + (16 * rb + l16) * RP_N + 8 * (c ^ l16) + 4 * (q & 1));
+    };
     float mu[8], rs[8], s1[8], s2[8];
 #pragma unroll
     for (int rb = 0; rb < 8; ++rb) {
       mu[rb] = a.mean[m0 + 16 * rb + l16];
       rs[rb] = a.rstd[m0 + 16 * rb + l16];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the y1 panel (and mean / rstd) landed
+    __syncthreads();
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
       s1[rb] = 0.f;
       s2[rb] = 0.f;
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
-        const uint2 t = *(const uint2*)(y1p + rb * 16 * RP_N + 16 * cb);
+        const uint2 t = y1_at(rb, cb);
         const unsigned yv[2] = {t.x, t.y};
         const f32x4 gm = col4(1, cb);
 #pragma unroll
@@ -353,7 +387,7 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
       const float m1 = s1[rb] * (1.f / RP_N), m2 = s2[rb] * (1.f / RP_N);
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
-        const uint2 t = *(const uint2*)(y1p + rb * 16 * RP_N + 16 * cb);
+        const uint2 t = y1_at(rb, cb);
         const unsigned yv[2] = {t.x, t.y};
         const f32x4 gm = col4(1, cb);
         float o[4];

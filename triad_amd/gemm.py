@@ -34,9 +34,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, meta
     if not (x2.is_cuda and _ok(M, N, K)):
         return F.linear(xb, wb, None if b is None else b.to(_BF))
     wc = wb if wb.is_contiguous() else wb.contiguous()
-    bias = None if b is None else b.detach().to(_BF).to(torch.float32).contiguous()
+    # the bias as autocast holds it (bf16), read by the epilogue as is: no cast launch when the
+    # model's bias already is bf16 (the trainer's shadowed Linear layers, the projection heads)
+    bias = None if b is None else b.detach().to(_BF).contiguous()
     out = torch.empty(M, N, dtype=_BF, device=x2.device)
-    call("triad_gemm_bf16_bias", ptr(x2), K, 1, ptr(wc), K, 1, M, N, K, ptr(bias), ptr(out), N,
+    call("triad_gemm_bf16_bias_bf16", ptr(x2), K, 1, ptr(wc), K, 1, M, N, K, ptr(bias), ptr(out), N,
          stream_ptr(x2.device), meta=meta or dict(backbone=True, flops=2.0 * M * N * K))
     return out.view(*xb.shape[:-1], N)
 

@@ -678,6 +678,33 @@ def _rows_view(h):
     return hb, hb.shape[0], H, H, hb.shape[0], 0
 
 
+def _head_weight_grads(w_refs, dyp, ln, dy1, hb, M, Mp, H, w1d, w2d):
+    """(dW2, dW1) of a projection head: dW2 = dy^T ln, dW1 = dy1^T h on the split-K GEMM
+    (_dw_plan), bf16 straight from the slab reduction for bf16 model weights. For bf16 weights at
+    their first use in the backward pass they go to the backbone weight-gradient side stream
+    (linear.on_side_stream), so the backbone's backward -- queued on this stream right after dh --
+    does not wait for them (VERDICT r4 #2: the heads' dW where the backbones leave CUs idle)."""
+    from . import linear as _lin
+
+    def run():
+        st = stream_ptr(dyp.device)
+        bf, f32 = torch.bfloat16, torch.float32
+        (f2, sp2), (f1, sp1) = _dw_plan(Mp, D), _dw_plan(Mp, H)
+        slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dyp.device)
+        o2, o1 = int(w2d == bf), int(w1d == bf)
+        dw2 = torch.empty(D, D, dtype=bf if o2 else f32, device=dyp.device)
+        call("triad_gemm_bf16_splitk_form", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2),
+             o2, f2, st, meta=dict(tag=f"proj-dW2x{M}", flops=2.0 * M * D * D))
+        dw1 = torch.empty(D, H, dtype=bf if o1 else f32, device=dyp.device)
+        call("triad_gemm_bf16_splitk_form", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1),
+             o1, f1, st, meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
+        return dw2, dw1
+
+    if dyp.is_cuda and _lin.side_stream_ok(*w_refs):
+        return _lin.on_side_stream(run, (dyp, ln, dy1, hb))
+    return run()
+
+
 class _ProjectionHeadRows(torch.autograd.Function):
     """The projection head on row-panel GEMMs (rowgemm.hip): a workgroup owns 128 token rows x all
     512 columns, so the LayerNorm runs in projection1's epilogue (triad_projhead_ln_fwd: y1, its
@@ -722,6 +749,7 @@ class _ProjectionHeadRows(torch.autograd.Function):
         ctx.save_for_backward(h if hv is h else hv, w1b, w2b, g32, y1, ln, mean, rstd)
         ctx.shape = (lead, H, M, Mp, hv is h)
         ctx.dtypes = (h.dtype, w1.dtype, b1.dtype, gamma.dtype, beta.dtype, w2.dtype, b2.dtype)
+        ctx.w_refs = (w1, w2)
         return y[:M].view(*lead, D)
 
     @staticmethod
@@ -744,15 +772,7 @@ class _ProjectionHeadRows(torch.autograd.Function):
         dh = hipgemm.mm(dy1, w1b, meta=dict(tag=f"proj-dX1x{M}", flops=2.0 * M * D * H))[:M]
         db2 = bias_grad(dyp, bf if b2d == bf else f32, meta=dict(tag="proj-bias", flops=0.0))
         hb = _pad_rows(hs.to(bf).reshape(M, H), Mp) if in_place or Mp > M else hs
-        (f2, sp2), (f1, sp1) = _dw_plan(Mp, D), _dw_plan(Mp, H)
-        slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
-        o2, o1 = int(w2d == bf), int(w1d == bf)
-        dw2 = torch.empty(D, D, dtype=bf if o2 else f32, device=dev)
-        call("triad_gemm_bf16_splitk_form", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2),
-             o2, f2, st, meta=dict(tag=f"proj-dW2x{M}", flops=2.0 * M * D * D))
-        dw1 = torch.empty(D, H, dtype=bf if o1 else f32, device=dev)
-        call("triad_gemm_bf16_splitk_form", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1),
-             o1, f1, st, meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
+        dw2, dw1 = _head_weight_grads(ctx.w_refs, dyp, ln, dy1, hb, M, Mp, H, w1d, w2d)
         return (dh.view(*lead, H).to(hd), dw1.to(w1d), cols[2].to(b1d), cols[0].to(gd), cols[1].to(bd), dw2.to(w2d),
                 db2.to(b2d), None)
 
@@ -794,6 +814,7 @@ class _ProjectionHeadPasses(torch.autograd.Function):
         ctx.save_for_backward(hb, w1b, w2b, g32, y1, ln, mean, rstd)
         ctx.shape = (lead, H, M, Mp)
         ctx.dtypes = (h.dtype, w1.dtype, b1.dtype, gamma.dtype, beta.dtype, w2.dtype, b2.dtype)
+        ctx.w_refs = (w1, w2)
         return y.view(*lead, D)
 
     @staticmethod
@@ -821,15 +842,7 @@ class _ProjectionHeadPasses(torch.autograd.Function):
         # (by LDS-DMA like every column sum of the step: the audio / text heads' backward runs on
         # the concurrent backbone streams)
         db2 = bias_grad(dyp, torch.bfloat16 if b2d == torch.bfloat16 else f32, meta=dict(tag="proj-bias", flops=0.0))
-        (f2, sp2), (f1, sp1) = _dw_plan(Mp, D), _dw_plan(Mp, H)
-        slabs = torch.empty(max(sp2 * D * D, sp1 * D * H), dtype=f32, device=dev)
-        o2, o1 = int(w2d == torch.bfloat16), int(w1d == torch.bfloat16)
-        dw2 = torch.empty(D, D, dtype=torch.bfloat16 if o2 else f32, device=dev)
-        call("triad_gemm_bf16_splitk_form", ptr(dyp), D, 0, ptr(ln), D, 0, D, D, Mp, sp2, None, ptr(slabs), ptr(dw2),
-             o2, f2, st, meta=dict(tag=f"proj-dW2x{M}", flops=2.0 * M * D * D))
-        dw1 = torch.empty(D, H, dtype=torch.bfloat16 if o1 else f32, device=dev)
-        call("triad_gemm_bf16_splitk_form", ptr(dy1), D, 0, ptr(hb), H, 0, D, H, Mp, sp1, None, ptr(slabs), ptr(dw1),
-             o1, f1, st, meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
+        dw2, dw1 = _head_weight_grads(ctx.w_refs, dyp, ln, dy1, hb, M, Mp, H, w1d, w2d)
         return (dh.view(*lead, H).to(hd), dw1.to(w1d), cols[2].to(b1d), cols[0].to(gd), cols[1].to(bd), dw2.to(w2d),
                 db2.to(b2d), None)
 
