@@ -265,7 +265,9 @@ int triad_global_znorm(const float* x, long long n, float eps, float* y, double*
  * triad_grad_sumsq: out[c] = sum g^2 over chunk c (grad norms train.py:992-1002,
  * clip_grad_norm_ train.py:1004-1006).
  * triad_adamw_step: torch.optim.AdamW (decoupled weight decay) with g scaled by scale[param]
- * (the clip factor, NULL = 1); pp[3*param] = {lr/bc1, 1/sqrt(bc2), 1 - lr*wd}. shadow (may be
+ * (the clip factor, NULL = 1); pp[3*param] = {lr/bc1, 1/sqrt(bc2), 1 - lr*wd}; omb1 / omb2 =
+ * 1 - beta1 / 1 - beta2 rounded from double, as torch passes them (1 - float(beta2) loses 1.3e-5
+ * of 1 - 0.999 to cancellation). shadow (may be
  * NULL): per parameter, (address of its bf16 model weight) - 2 * (flat offset), or 0; the step
  * then also writes bf16(p) there (mixed-precision model weights, the cast autocast would do).
  * triad_gather_grads: pieces = device array of {const void* src; int64 dst; int32 n; int32 f32};
@@ -273,8 +275,8 @@ int triad_global_znorm(const float* x, long long n, float eps, float* y, double*
  * gradients of every flat-space parameter into the flat fp32 gradient buffer. */
 int triad_grad_sumsq(const float* g, const void* chunks, int nchunks, double* out, hipStream_t stream);
 int triad_adamw_step(float* p, const float* g, float* m, float* v, const void* chunks, int nchunks,
-                     const float* pp, const float* scale, float beta1, float beta2, float eps,
-                     const unsigned long long* shadow, hipStream_t stream);
+                     const float* pp, const float* scale, float beta1, float beta2, float omb1, float omb2,
+                     float eps, const unsigned long long* shadow, hipStream_t stream);
 int triad_gather_grads(const void* pieces, int npieces, float* g, int accumulate, hipStream_t stream);
 
 /* dst[b][t] = idx[b][t] >= 0 ? src[b][idx[b][t]] : 0 (row_bytes per row). Patch-dropout

@@ -57,7 +57,7 @@ SIGNATURES = {
     "triad_colsum_dma": [vp, i64, i32, i64, vp, f32, i32, vp, vp],
     "triad_global_znorm": [vp, i64, f32, vp, vp, i32, vp],
     "triad_grad_sumsq": [vp, vp, i32, vp, vp],
-    "triad_adamw_step": [vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, vp, vp],
+    "triad_adamw_step": [vp, vp, vp, vp, vp, i32, vp, vp, f32, f32, f32, f32, f32, vp, vp],
     "triad_gather_grads": [vp, i32, vp, i32, vp],
     "triad_gather_rows": [vp, i64, vp, i32, i32, i32, vp, vp],
     "triad_l2norm_rows": [vp, i32, i32, f32, vp, vp],

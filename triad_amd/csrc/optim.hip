@@ -45,13 +45,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     const Chunk* __restrict__ chunks, const float* __restrict__ pp,
                                                     const float* __restrict__ scale, float beta1, float beta2,
-                                                    float eps, const unsigned long long* __restrict__ shadow) {
+                                                    float omb1, float omb2, float eps,
+                                                    const unsigned long long* __restrict__ shadow) {
   const Chunk c = chunks[blockIdx.x];
   // shadow[param]: address of the bf16 model weight minus 2 * (its flat offset), 0 = none
   bf16* const sh = shadow && shadow[c.param] ? (bf16*)(shadow[c.param]) : nullptr;
   const float step_size = pp[3 * c.param], inv_bc2 = pp[3 * c.param + 1], wdf = pp[3 * c.param + 2];
   const float sc = scale ? scale[c.param] : 1.f;
-  const float omb1 = 1.f - beta1, omb2 = 1.f - beta2;
   for (int i = threadIdx.x; i < c.n; i += blockDim.x) {
     const long long e = c.off + i;
     const float gr = g[e] * sc;
@@ -98,11 +98,11 @@ int triad_grad_sumsq(const float* g, const void* chunks, int nchunks, double* ou
 }
 
 int triad_adamw_step(float* p, const float* g, float* m, float* v, const void* chunks, int nchunks,
-                     const float* pp, const float* scale, float beta1, float beta2, float eps,
-                     const unsigned long long* shadow, hipStream_t stream) {
+                     const float* pp, const float* scale, float beta1, float beta2, float omb1, float omb2,
+                     float eps, const unsigned long long* shadow, hipStream_t stream) {
   if (nchunks <= 0) return TRIAD_OK;
   hipLaunchKernelGGL(adamw_kernel, dim3(nchunks), dim3(256), 0, stream, p, g, m, v, (const Chunk*)chunks, pp, scale,
-                     beta1, beta2, eps, shadow);
+                     beta1, beta2, omb1, omb2, eps, shadow);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }

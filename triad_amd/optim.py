@@ -276,7 +276,8 @@ class FusedAdamW(torch.optim.Optimizer):
         sp.check_shadows(ids)
         table, n, _ = sp.chunks(ids)
         call("triad_adamw_step", ptr(sp.flat_p), ptr(sp.flat_g), ptr(sp.exp_avg), ptr(sp.exp_avg_sq), ptr(table), n,
-             ptr(pp_dev), ptr(sp.scale), float(b1), float(b2), float(eps), ptr(sp.shadow_base),
+             ptr(pp_dev), ptr(sp.scale), float(b1), float(b2), float(1.0 - b1), float(1.0 - b2), float(eps),
+             ptr(sp.shadow_base),
              stream_ptr(sp.device))
         return loss
 
