@@ -194,22 +194,31 @@ int triad_gemm_bf16_form(const void* A, long long lda, int a_kcontig, const void
 /* Projection head on row-panel GEMMs (model.py:32-34,68 / 81-83,116 / 253-255,326 under bf16
  * autocast; csrc/rowgemm.hip): a workgroup owns 128 token rows x all 512 columns, so the LayerNorm
  * and its backward run in the GEMM epilogues. Weights are pre-arranged in MFMA-fragment order:
- * triad_wpack(W, K, Bp) for C = A W^T with W [512][K] bf16 (Bp: K * 512 bf16). Outputs have
- * triad_rowpanel_count(M) * 128 rows (rows >= M written as zeros).
- *   ln_fwd: y1 = bf16(h W1^T + b1), mean / rstd (fp32, biased variance + eps) of y1's rows,
- *           ln = bf16((y1 - mean) rstd gamma + beta); h row r at
- *           h + (r / n_per) * bstride + (r % n_per) * lda (a strided view read in place);
- *   rowgemm_bias: C = bf16(A W^T + bias) (projection2);
+ * triad_wpack(W, K, Bp) for C = A W^T with W [512][K] bf16 (Bp: K * 512 bf16); triad_wpack2 packs
+ * both weights of a head in one launch. Outputs have triad_rowpanel_count(M) * 128 rows (rows >= M
+ * written as zeros).
+ *   projhead_fwd: the whole forward in one kernel -- y1 = bf16(h W1^T + b1), mean / rstd (fp32,
+ *           biased variance + eps) of y1's rows, ln = bf16((y1 - mean) rstd gamma + beta), kept in
+ *           LDS as the A operand of y = bf16(ln W2^T + b2); y1 / ln / mean / rstd are stored for the
+ *           backward. h row r at h + (r / n_per) * bstride + (r % n_per) * lda (a strided view read
+ *           in place). Bit-identical to ln_fwd followed by rowgemm_bias;
+ *   ln_fwd: its first half (y1, mean / rstd, ln);
+ *   rowgemm_bias: C = bf16(A W^T + bias) (projection2 from ln in HBM);
  *   ln_bwd: dln = bf16(dy W2) (W2p = triad_bfrag_pack16(W2, 16, 1, .)), dy1 = bf16(rstd (g -
  *           mean(g) - xh mean(g xh))), g = dln gamma, and part [panels][3][512] column sums of
  *           dln xh (dgamma), dln (dbeta), dy1 (db1) per panel (reduce with triad_sum_slabs).
- * b1 / b2 fp32 holding bf16 values (autocast casts the bias), gamma / beta fp32. */
+ * Biases are the bf16 vectors autocast adds (b1, b2, bias: bf16 [512]); gamma / beta fp32. */
 int triad_wpack(const void* W, int K, void* Bp, hipStream_t stream);
+int triad_wpack2(const void* W1, int K1, void* Bp1, const void* W2, int K2, void* Bp2, hipStream_t stream);
 int triad_rowpanel_count(long long M);
+int triad_projhead_fwd(const void* h, long long M, int H, long long lda, long long n_per, long long bstride,
+                       const void* W1p, const void* b1, const float* gamma, const float* beta, float eps,
+                       const void* W2p, const void* b2, void* y1, void* ln, float* mean, float* rstd, void* y,
+                       hipStream_t stream);
 int triad_projhead_ln_fwd(const void* h, long long M, int H, long long lda, long long n_per, long long bstride,
-                          const void* W1p, const float* b1, const float* gamma, const float* beta, float eps, void* y1,
+                          const void* W1p, const void* b1, const float* gamma, const float* beta, float eps, void* y1,
                           void* ln, float* mean, float* rstd, hipStream_t stream);
-int triad_rowgemm_bias(const void* A, long long M, int K, long long lda, const void* Bp, const float* bias, void* C,
+int triad_rowgemm_bias(const void* A, long long M, int K, long long lda, const void* Bp, const void* bias, void* C,
                        hipStream_t stream);
 int triad_projhead_ln_bwd(const void* dy, long long M, const void* W2p, const void* y1, const float* mean,
                           const float* rstd, const float* gamma, void* dy1, float* part, hipStream_t stream);

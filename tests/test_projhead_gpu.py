@@ -136,3 +136,42 @@ def test_rows_form_reads_a_strided_view_in_place():
     ref = [y2.detach(), hc.grad] + [p.grad for m in (p1, ln, p2) for p in m.parameters()]
     for a, b in zip(got, ref):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,H", [(8192, 768), (300, 1024), (1, 768), (50944, 768)])
+def test_fused_forward_equals_its_two_halves(M, H):
+    """triad_projhead_fwd (projection1 + LayerNorm + projection2 in one kernel, the LN'd panel kept in
+    LDS) is bit-identical in y1 / ln / mean / rstd / y to triad_projhead_ln_fwd followed by
+    triad_rowgemm_bias over the stored ln (ragged last panel, one row, a step shape)."""
+    from triad_amd._lib import call, ptr, stream_ptr
+    g = torch.Generator(device=dev).manual_seed(M + H)
+    bf = torch.bfloat16
+    h = torch.randn(M, H, device=dev, generator=g).to(bf)
+    w1 = (torch.randn(512, H, device=dev, generator=g) / H ** 0.5).to(bf)
+    w2 = (torch.randn(512, 512, device=dev, generator=g) / 512 ** 0.5).to(bf)
+    b1, b2 = (torch.randn(512, device=dev, generator=g) * 0.1).to(bf), (torch.randn(512, device=dev, generator=g) * 0.1).to(bf)
+    gam = torch.rand(512, device=dev, generator=g) + 0.5
+    bet = torch.randn(512, device=dev, generator=g) * 0.1
+    P = call("triad_rowpanel_count", M)
+    Mp = P * 128
+    w1p, w2p = torch.empty(H * 512, dtype=bf, device=dev), torch.empty(512 * 512, dtype=bf, device=dev)
+    st = stream_ptr()
+    call("triad_wpack2", ptr(w1), H, ptr(w1p), ptr(w2), 512, ptr(w2p), st)
+    outs = []
+    for fused in (True, False):
+        y1, ln, y = (torch.full((Mp, 512), 7.0, dtype=bf, device=dev) for _ in range(3))
+        mean, rstd = torch.full((Mp,), 7.0, device=dev), torch.full((Mp,), 7.0, device=dev)
+        if fused:
+            call("triad_projhead_fwd", ptr(h), M, H, H, M, 0, ptr(w1p), ptr(b1), ptr(gam), ptr(bet), 1e-5, ptr(w2p),
+                 ptr(b2), ptr(y1), ptr(ln), ptr(mean), ptr(rstd), ptr(y), st)
+        else:
+            call("triad_projhead_ln_fwd", ptr(h), M, H, H, M, 0, ptr(w1p), ptr(b1), ptr(gam), ptr(bet), 1e-5, ptr(y1),
+                 ptr(ln), ptr(mean), ptr(rstd), st)
+            call("triad_rowgemm_bias", ptr(ln), M, 512, 512, ptr(w2p), ptr(b2), ptr(y), st)
+        outs.append((y1, ln, mean, rstd, y))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert float(outs[0][4][M:].float().abs().max() if Mp > M else 0.0) == 0.0   # pad rows written as zeros
+    ref = torch.nn.functional.linear(outs[0][1][:M].float(), w2.float(), b2.float())
+    assert float((outs[0][4][:M].float() - ref).abs().max()) <= 2e-2 * float(ref.abs().max())

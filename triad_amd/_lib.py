@@ -43,6 +43,8 @@ SIGNATURES = {
     "triad_gemm_bf16_splitk": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp],
     "triad_gemm_bf16_splitk_form": [vp, i64, i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, i32, i32, vp],
     "triad_wpack": [vp, i32, vp, vp],
+    "triad_wpack2": [vp, i32, vp, vp, i32, vp, vp],
+    "triad_projhead_fwd": [vp, i64, i32, i64, i64, i64, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, vp],
     "triad_similarity_maps": [vp, vp, i32, i32, i32, i32, vp, f32, vp, vp],
     "triad_rowpanel_count": [i64],
     "triad_projhead_ln_fwd": [vp, i64, i32, i64, i64, i64, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp],

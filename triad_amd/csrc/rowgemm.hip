@@ -2,8 +2,11 @@
 // LayerNorm(512) -> Linear(512->512) under bf16 autocast) on ROW-PANEL GEMMs: a workgroup owns 128
 // token rows x ALL 512 output columns, so the LayerNorm -- a reduction over those 512 columns --
 // and its backward run in the GEMM's epilogue instead of separate passes over HBM:
-//   triad_projhead_ln_fwd  y1 = bf16(h W1^T + b1); mean / rstd of y1's rows; ln = bf16(LN(y1))
-//   triad_rowgemm_bias     y2 = bf16(ln W2^T + b2)
+//   triad_projhead_fwd     the whole forward in one kernel: y1 = bf16(h W1^T + b1); mean / rstd of
+//                          y1's rows; ln = bf16(LN(y1)), kept in LDS as the A operand of
+//                          y = bf16(ln W2^T + b2) (y1 / ln / mean / rstd also stored for the backward)
+//   triad_projhead_ln_fwd  its first half alone (y1, mean / rstd, ln)
+//   triad_rowgemm_bias     C = bf16(A W^T + b) (its second half alone, from ln in HBM)
 //   triad_projhead_ln_bwd  dln = bf16(dy W2); dy1 = bf16(LN backward(dln)) + the dgamma / dbeta /
 //                          db1 column partials of the panel
 // (dh = dy1 W1 and the weight gradients stay on the tiled / split-K GEMMs: no row reduction there.)
@@ -38,6 +41,8 @@ constexpr int RP_SLOT = RP_M * RP_K;              // elements per A ring slot (8
 // EPI 2 (LayerNorm backward) brings the panel's 128 y1 rows (128 KB) into LDS by LDS-DMA after the
 // k loop, behind the 16 KB the epilogue's row exchange / column vectors use
 constexpr int RP_Y1_OFF = 8192;                    // elements
+// EPI 3 (the fused forward) keeps the LN'd panel (128 x 512 bf16 = 128 KB) in LDS after the ring
+constexpr int RP_PAN_OFF = RP_NB * RP_SLOT;        // elements
 
 struct RPArgs {
   const bf16* A;            // token rows (two-level addressing below)
@@ -45,7 +50,7 @@ struct RPArgs {
   long long M;              // valid rows
   int K;                    // contraction (multiple of 32)
   const bf16* Bp;           // packed weight fragments (triad_wpack / triad_bfrag_pack16 dk = 1)
-  const float* bias;        // [512] fp32 (bf16-rounded, as autocast's F.linear adds it)
+  const bf16* bias;         // [512] bf16 (autocast's F.linear bias; EPI 0: b, EPI 1 / 3: b1)
   const float* gamma;       // LayerNorm weight / bias [512] fp32
   const float* beta;
   float eps;
@@ -55,6 +60,9 @@ struct RPArgs {
   float* rstd;
   const bf16* y1;           // EPI 2: the forward's y1
   float* part;              // EPI 2: [panels][3][512] column partials (dgamma, dbeta, db1)
+  const bf16* Bp2;          // EPI 3: packed W2 fragments (triad_wpack(W2, 512))
+  const bf16* bias2;        // EPI 3: b2 [512] bf16
+  bf16* out2;               // EPI 3: y [M_pad][512] bf16
 };
 
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -112,11 +120,27 @@ __global__ __launch_bounds__(256) void wpack_t_kernel(const bf16* __restrict__ W
 // profiles/r05_projhead_pmc.txt).
 __device__ __forceinline__ int rp_swz(int r) { return (-(r >> 2)) & 3; }
 
+// both weights of a head in one launch (grid.y = 2)
+__global__ __launch_bounds__(256) void wpack2_kernel(const bf16* __restrict__ W1, int K1, bf16* __restrict__ Bp1,
+                                                     const bf16* __restrict__ W2, int K2, bf16* __restrict__ Bp2) {
+  const bf16* W = blockIdx.y ? W2 : W1;
+  const int K = blockIdx.y ? K2 : K1;
+  bf16* Bp = blockIdx.y ? Bp2 : Bp1;
+  const long long f = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= (long long)(K / RP_K) * 2048) return;
+  const int l = (int)(f & 63), cb = (int)((f >> 6) & 3), w = (int)((f >> 8) & 7);
+  const long long kt = f >> 11;
+  const int n = 64 * w + 16 * cb + (l & 15);
+  const long long k = kt * RP_K + 8 * (l >> 4);
+  *(bf16x8*)(Bp + f * 8) = *(const bf16x8*)(W + (long long)n * K + k);
+}
+
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
   // the A ring during the k loop; the epilogue reuses it (row exchange, per-column vectors; EPI 2:
   // + the y1 panel)
-  __shared__ __attribute__((aligned(16))) bf16 lds[EPI == 2 ? RP_Y1_OFF + RP_M * RP_N : RP_NB * RP_SLOT];
+  __shared__ __attribute__((aligned(16))) bf16 lds[EPI == 2 ? RP_Y1_OFF + RP_M * RP_N
+                                                  : EPI == 3 ? RP_PAN_OFF + RP_M * RP_N : RP_NB * RP_SLOT];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, q = lane >> 4;
   const long long m0 = (long long)blockIdx.x * RP_M;
@@ -219,9 +243,10 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
   auto col4 = [&](int which, int cb) __attribute__((always_inline)) { return *(const f32x4*)(vec + which * RP_N + cw + 16 * cb); };
   if (threadIdx.x < RP_N) {
     const int n = threadIdx.x;
-    if (EPI != 2) vec[n] = a.bias[n];
+    if (EPI != 2) vec[n] = (float)a.bias[n];
     if (EPI != 0) vec[RP_N + n] = a.gamma[n];
-    if (EPI == 1) vec[2 * RP_N + n] = a.beta[n];
+    if (EPI == 1 || EPI == 3) vec[2 * RP_N + n] = a.beta[n];
+    if (EPI == 3) vec[3 * RP_N + n] = (float)a.bias2[n];
   }
   __syncthreads();
 
@@ -239,7 +264,7 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
         *(uint2*)(a.out0 + m * RP_N + cw + 16 * cb) = o;
       }
     }
-  } else if constexpr (EPI == 1) {
+  } else if constexpr (EPI == 1 || EPI == 3) {
     // y1 = bf16(acc + b1) (autocast's F.linear output), stored at once and kept packed (exact bf16
     // values: 64 VGPRs instead of 128); LayerNorm in fp32 over the bf16 y1 row (F.layer_norm under
     // autocast): two-pass mean / biased variance, ln = bf16(xh gamma + beta)
@@ -293,7 +318,62 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
         float o[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = ok ? (bf_at(y[rb][cb], i) - mu) * rs * gm[i] + bt[i] : 0.f;
-        *(uint2*)(a.out1 + m * RP_N + cw + 16 * cb) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+        const uint2 lnv = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+        *(uint2*)(a.out1 + m * RP_N + cw + 16 * cb) = lnv;
+        if constexpr (EPI == 3) {
+          // the LN'd row into the LDS panel, 16-byte chunk c of row r at chunk c ^ (r & 15): the
+          // GEMM2 fragment reads (row 16 rb + l16, chunk 4 kt + q) are then conflict-free
+          const int c = 8 * wave + 2 * cb + (q >> 1);
+          *(uint2*)(lds + RP_PAN_OFF + (16 * rb + l16) * RP_N + 8 * (c ^ l16) + 4 * (q & 1)) = lnv;
+        }
+      }
+    }
+    if constexpr (EPI == 3) {
+      // projection2 over the panel: A = the LN'd rows from LDS (no HBM read, no ring, no barrier
+      // per k tile), B = W2's fragments streamed into registers three tiles ahead as in the k loop
+      __syncthreads();
+      const bf16* bsrc2 = a.Bp2 + (long long)wave * 2048 + lane * 8;
+      const bf16* pan = lds + RP_PAN_OFF + l16 * RP_N;
+#pragma unroll
+      for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = (f32x4){};
+      constexpr int NK2 = RP_N / RP_K;
+      auto load_b2 = [&](int kt, int slot) __attribute__((always_inline)) {
+        const int k = kt < NK2 ? kt : NK2 - 1;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) bq[slot][cb] = *(const bf16x8*)(bsrc2 + (long long)k * 16384 + cb * 512);
+      };
+      static_for<0, RP_DD>([&](auto P) __attribute__((always_inline)) { load_b2(decltype(P)::value, decltype(P)::value); });
+      static_for<0, NK2>([&](auto T) __attribute__((always_inline)) {
+        constexpr int kt = decltype(T)::value, u = kt % RP_NB;
+        bf16x8 af[8];
+#pragma unroll
+        for (int rb = 0; rb < 8; ++rb) af[rb] = *(const bf16x8*)(pan + rb * 16 * RP_N + 8 * ((4 * kt + q) ^ l16));
+#pragma unroll
+        for (int rb = 0; rb < 8; ++rb) {
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = mfma16(bq[u][cb], af[rb], acc[rb][cb]);
+          if (rb == 1) {
+            __builtin_amdgcn_sched_barrier(0);
+            load_b2(kt + RP_DD, (kt + RP_DD) % RP_NB);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      });
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads
+#pragma unroll
+      for (int rb = 0; rb < 8; ++rb) {
+        const long long m = m0 + 16 * rb + l16;
+        const bool ok = m < a.M;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const f32x4 b = col4(3, cb);
+          const uint2 o = ok ? make_uint2(pack_bf2(acc[rb][cb][0] + b[0], acc[rb][cb][1] + b[1]),
+                                          pack_bf2(acc[rb][cb][2] + b[2], acc[rb][cb][3] + b[3]))
+                             : make_uint2(0u, 0u);
+          *(uint2*)(a.out2 + m * RP_N + cw + 16 * cb) = o;
+        }
       }
     }
   } else {
@@ -451,6 +531,16 @@ int triad_wpack(const void* W, int K, void* Bp, hipStream_t stream) {
   return TRIAD_OK;
 }
 
+// triad_wpack of both weights of a head in one launch.
+int triad_wpack2(const void* W1, int K1, void* Bp1, const void* W2, int K2, void* Bp2, hipStream_t stream) {
+  if (!W1 || !Bp1 || !W2 || !Bp2 || K1 <= 0 || K1 % RP_K || K2 <= 0 || K2 % RP_K) return TRIAD_EINVAL;
+  const long long nfrag = (long long)((K1 > K2 ? K1 : K2) / RP_K) * 2048;
+  hipLaunchKernelGGL(wpack2_kernel, dim3((unsigned)((nfrag + 255) / 256), 2), dim3(256), 0, stream, (const bf16*)W1, K1,
+                     (bf16*)Bp1, (const bf16*)W2, K2, (bf16*)Bp2);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
 int triad_rowpanel_count(long long M) { return M > 0 ? (int)((M + RP_M - 1) / RP_M) : 0; }
 
 // y1 = bf16(h W1^T + b1), mean / rstd of y1's rows, ln = bf16(LN(y1)) (model.py:32-33 + LN,
@@ -458,24 +548,42 @@ int triad_rowpanel_count(long long M) { return M > 0 ? (int)((M + RP_M - 1) / RP
 // triad_wpack(W1, H); y1 / ln [panels * 128][512] bf16, mean / rstd [panels * 128] fp32 (rows >= M
 // written as zeros).
 int triad_projhead_ln_fwd(const void* h, long long M, int H, long long lda, long long n_per, long long bstride,
-                          const void* W1p, const float* b1, const float* gamma, const float* beta, float eps, void* y1,
+                          const void* W1p, const void* b1, const float* gamma, const float* beta, float eps, void* y1,
                           void* ln, float* mean, float* rstd, hipStream_t stream) {
   if (rp_check(h, M, H, lda, n_per, bstride, W1p, y1) || !b1 || !gamma || !beta || !ln || !mean || !rstd)
     return TRIAD_EINVAL;
-  RPArgs a{(const bf16*)h, lda, n_per, bstride, M, H, (const bf16*)W1p, b1, gamma, beta, eps,
-           (bf16*)y1, (bf16*)ln, mean, rstd, nullptr, nullptr};
+  RPArgs a{(const bf16*)h, lda, n_per, bstride, M, H, (const bf16*)W1p, (const bf16*)b1, gamma, beta, eps,
+           (bf16*)y1, (bf16*)ln, mean, rstd, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(rowpanel_kernel<1>, dim3(triad_rowpanel_count(M)), dim3(512), 0, stream, a);
+  TRIAD_CHECK_LAUNCH();
+  return TRIAD_OK;
+}
+
+// The projection head's forward in one kernel (model.py:32-34 / 68, autocast numerics): y1, mean /
+// rstd, ln as triad_projhead_ln_fwd, then y = bf16(ln W2^T + b2) from the LN'd panel kept in LDS
+// (bit-identical to triad_projhead_ln_fwd + triad_rowgemm_bias). W1p / W2p: triad_wpack(2); b1, b2
+// bf16 [512]; y [panels * 128][512] bf16 (rows >= M zero).
+int triad_projhead_fwd(const void* h, long long M, int H, long long lda, long long n_per, long long bstride,
+                       const void* W1p, const void* b1, const float* gamma, const float* beta, float eps,
+                       const void* W2p, const void* b2, void* y1, void* ln, float* mean, float* rstd, void* y,
+                       hipStream_t stream) {
+  if (rp_check(h, M, H, lda, n_per, bstride, W1p, y1) || !b1 || !gamma || !beta || !ln || !mean || !rstd || !W2p ||
+      !b2 || !y)
+    return TRIAD_EINVAL;
+  RPArgs a{(const bf16*)h, lda, n_per, bstride, M, H, (const bf16*)W1p, (const bf16*)b1, gamma, beta, eps,
+           (bf16*)y1, (bf16*)ln, mean, rstd, nullptr, nullptr, (const bf16*)W2p, (const bf16*)b2, (bf16*)y};
+  hipLaunchKernelGGL(rowpanel_kernel<3>, dim3(triad_rowpanel_count(M)), dim3(512), 0, stream, a);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
 }
 
 // C = bf16(A Bt + bias), A [M][K] rows at lda, C [panels * 128][512] (ld 512; rows >= M zero);
 // Bp: triad_wpack(W, K) for C = A W^T (model.py:34, projection2).
-int triad_rowgemm_bias(const void* A, long long M, int K, long long lda, const void* Bp, const float* bias, void* C,
+int triad_rowgemm_bias(const void* A, long long M, int K, long long lda, const void* Bp, const void* bias, void* C,
                        hipStream_t stream) {
   if (rp_check(A, M, K, lda, M, 0, Bp, C) || !bias) return TRIAD_EINVAL;
-  RPArgs a{(const bf16*)A, lda, M, 0, M, K, (const bf16*)Bp, bias, nullptr, nullptr, 0.f,
-           (bf16*)C, nullptr, nullptr, nullptr, nullptr, nullptr};
+  RPArgs a{(const bf16*)A, lda, M, 0, M, K, (const bf16*)Bp, (const bf16*)bias, nullptr, nullptr, 0.f,
+           (bf16*)C, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(rowpanel_kernel<0>, dim3(triad_rowpanel_count(M)), dim3(512), 0, stream, a);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
@@ -489,7 +597,8 @@ int triad_projhead_ln_bwd(const void* dy, long long M, const void* W2p, const vo
                           const float* rstd, const float* gamma, void* dy1, float* part, hipStream_t stream) {
   if (rp_check(dy, M, RP_N, RP_N, M, 0, W2p, dy1) || !y1 || !mean || !rstd || !gamma || !part) return TRIAD_EINVAL;
   RPArgs a{(const bf16*)dy, RP_N, M, 0, M, RP_N, (const bf16*)W2p, nullptr, gamma, nullptr, 0.f,
-           (bf16*)dy1, nullptr, const_cast<float*>(mean), const_cast<float*>(rstd), (const bf16*)y1, part};
+           (bf16*)dy1, nullptr, const_cast<float*>(mean), const_cast<float*>(rstd), (const bf16*)y1, part,
+           nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(rowpanel_kernel<2>, dim3(triad_rowpanel_count(M)), dim3(512), 0, stream, a);
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;

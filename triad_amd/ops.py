@@ -656,10 +656,6 @@ def _dw_plan(Mp, N):
     return 0, _splitk(Mp, (D // 128) * (N // 128))
 
 
-def _bf16_round(t):
-    return t.detach().to(torch.bfloat16).to(torch.float32).contiguous()
-
-
 def _rows_view(h):
     """(tensor, M, H, lda, n_per, bstride) addressing h's token rows in place when h is a bf16
     [..., N, H] tensor whose rows are contiguous within each leading index (e.g. the ViT's patch
@@ -707,11 +703,11 @@ def _head_weight_grads(w_refs, dyp, ln, dy1, hb, M, Mp, H, w1d, w2d):
 
 class _ProjectionHeadRows(torch.autograd.Function):
     """The projection head on row-panel GEMMs (rowgemm.hip): a workgroup owns 128 token rows x all
-    512 columns, so the LayerNorm runs in projection1's epilogue (triad_projhead_ln_fwd: y1, its
-    row mean / rstd and ln in one pass over the panel) and the LayerNorm backward in the epilogue of
-    projection2's input-gradient GEMM (triad_projhead_ln_bwd: dy1 and the dgamma / dbeta / db1
-    column partials); projection2 is triad_rowgemm_bias, dh the tiled GEMM, the weight gradients
-    the split-K GEMM. Numerics as autocast: bf16 GEMM outputs with the bias added before the one
+    512 columns, so the forward is ONE kernel (triad_projhead_fwd: projection1, the LayerNorm in its
+    epilogue -- y1, row mean / rstd, ln -- and projection2 from the LN'd panel kept in LDS) and the
+    LayerNorm backward runs in the epilogue of projection2's input-gradient GEMM
+    (triad_projhead_ln_bwd: dy1 and the dgamma / dbeta / db1 column partials); dh is the tiled GEMM,
+    the weight gradients the split-K GEMM. Numerics as autocast: bf16 GEMM outputs with the bias added before the one
     rounding, the LayerNorm and its backward in fp32 over the bf16 y1 / dln."""
 
     @staticmethod
@@ -729,23 +725,22 @@ class _ProjectionHeadRows(torch.autograd.Function):
         Mp = P * 128
         w1b = w1.detach().to(bf).contiguous()
         w2b = w2.detach().to(bf).contiguous()
-        b1r, b2r = _bf16_round(b1), _bf16_round(b2)
+        b1b, b2b = b1.detach().to(bf).contiguous(), b2.detach().to(bf).contiguous()   # as autocast adds them
         g32 = gamma.detach().to(torch.float32).contiguous()
         be32 = beta.detach().to(torch.float32).contiguous()
         w1p = torch.empty(H * D, dtype=bf, device=dev)
         w2p = torch.empty(D * D, dtype=bf, device=dev)
-        call("triad_wpack", ptr(w1b), H, ptr(w1p), st, meta=dict(tag="proj-wpack", flops=0.0))
-        call("triad_wpack", ptr(w2b), D, ptr(w2p), st, meta=dict(tag="proj-wpack", flops=0.0))
+        call("triad_wpack2", ptr(w1b), H, ptr(w1p), ptr(w2b), D, ptr(w2p), st, meta=dict(tag="proj-wpack", flops=0.0))
         y1 = torch.empty(Mp, D, dtype=bf, device=dev)
         ln = torch.empty(Mp, D, dtype=bf, device=dev)
         mean = torch.empty(Mp, dtype=torch.float32, device=dev)
         rstd = torch.empty(Mp, dtype=torch.float32, device=dev)
-        call("triad_projhead_ln_fwd", ptr(hv), M, H, lda, n_per, bstride, ptr(w1p), ptr(b1r), ptr(g32), ptr(be32),
-             float(eps), ptr(y1), ptr(ln), ptr(mean), ptr(rstd), st,
-             meta=dict(tag=f"proj-fwd1x{M}", flops=2.0 * M * H * D))
         y = torch.empty(Mp, D, dtype=bf, device=dev)
-        call("triad_rowgemm_bias", ptr(ln), M, D, D, ptr(w2p), ptr(b2r), ptr(y), st,
-             meta=dict(tag=f"proj-fwd2x{M}", flops=2.0 * M * D * D))
+        # the whole forward in one kernel: GEMM1 + LayerNorm epilogue, the LN'd panel kept in LDS as
+        # projection2's A operand (tagged as the two GEMMs' flops together)
+        call("triad_projhead_fwd", ptr(hv), M, H, lda, n_per, bstride, ptr(w1p), ptr(b1b), ptr(g32), ptr(be32),
+             float(eps), ptr(w2p), ptr(b2b), ptr(y1), ptr(ln), ptr(mean), ptr(rstd), ptr(y), st,
+             meta=dict(tag=f"proj-fwdx{M}", flops=2.0 * M * D * (H + D)))
         ctx.save_for_backward(h if hv is h else hv, w1b, w2b, g32, y1, ln, mean, rstd)
         ctx.shape = (lead, H, M, Mp, hv is h)
         ctx.dtypes = (h.dtype, w1.dtype, b1.dtype, gamma.dtype, beta.dtype, w2.dtype, b2.dtype)
