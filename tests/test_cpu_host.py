@@ -212,7 +212,8 @@ def test_weight_gradient_plans():
     for Mp in (65536, 50944, 43904):
         f2, s2 = ops._dw_plan(Mp, 512)
         f1, s1 = ops._dw_plan(Mp, 768)
-        assert (f2, s2) == (1 | 8, 32) and (f1, s1) == (4 | 8, 32)
+        assert (f2, s2) == (1 | 8, 32) and (f1, s1) == (4 | 8, 40)   # 40 x 6 tiles: 240 workgroups
+    assert ops._dw_plan(43808, 1024) == (4 | 8, 32)
     assert ops._dw_plan(8192, 512) == (0, 16) and ops._dw_plan(8192, 768)[0] == 0
     for O, K, xcd in ((768, 768, True), (2304, 768, True), (3072, 768, False), (768, 3072, False)):
         form, sp = linear._form_splits(50944, O, K)

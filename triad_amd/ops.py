@@ -650,9 +650,14 @@ def _dw_plan(Mp, N):
     visual 65,536 rows dW2 65.9 -> 54.6 us, dW1 86.4 -> 74.2; audio 50,944 rows dW2 56.1 -> 44.9,
     dW1 69.1 -> 63.6 (GEMM + slab reduction, profiles/r04_dw_xcd_ab.log; bit-identical to the
     default placement at equal form / splits). Short lists (the 8,192-row text head) keep _splitk's
-    one round of 128 x 128 workgroups (faster there)."""
+    one round of 128 x 128 workgroups (faster there). The 256 x 256 tile's split count fills the
+    256 CUs with whole XCD groups: (256 // tiles) rounded down to a multiple of 8 -- 40 splits x 6
+    tiles = 240 workgroups for the 768-wide dW1 (32 left 64 CUs idle), 32 x 8 for 1,024 wide."""
     if Mp >= 32768 and N % 256 == 0:
-        return (1 if N == D else 4) | 8, 32
+        if N == D:
+            return 1 | 8, 32
+        tiles = (D // 256) * (N // 256)
+        return 4 | 8, max(8, int(os.environ.get("TRIAD_DW1_SPLITS", (256 // tiles) // 8 * 8)))
     return 0, _splitk(Mp, (D // 128) * (N // 128))
 
 
