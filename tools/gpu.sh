@@ -15,6 +15,7 @@
 #   py:<script args>       python <script> (tools/ micro-benchmarks)    -> gpurun_out/<tag>_py<N>.log
 #   envpy:A=1,B=2:<script args>  the same with extra environment for this step
 #   profpy:<script args>   the same under rocprofv3 --kernel-trace --stats -> gpurun_out/<tag>_profpy<N>/
+#   envprofpy:A=1,B=2:<script args>  profpy with extra environment for this step
 #   pmcpy:<name>:<counters>:<script args>  one rocprofv3 --pmc pass over a python script
 # environment: extra env for every step may be given as STEP_ENV="A=1 B=2" (exported first).
 set -o pipefail
@@ -71,6 +72,11 @@ for step in "$@"; do
     profpy:*)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${tag}_profpy${n}" -o run \
         -- python3 ${step#profpy:} > "gpurun_out/${tag}_profpy${n}.log" 2>&1 ;;
+    envprofpy:*)
+      # envprofpy:A=1,B=2:<script args>  profpy with extra environment for this step only
+      rest=${step#envprofpy:}; ev=${rest%%:*}; script=${rest#*:}
+      ( export ${ev//,/ }; timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "gpurun_out/${tag}_profpy${n}" -o run -- python3 $script ) > "gpurun_out/${tag}_profpy${n}.log" 2>&1 ;;
     pmcpy:*)
       rest=${step#pmcpy:}; name=${rest%%:*}; rest=${rest#*:}; ctr=${rest%%:*}; script=${rest#*:}
       timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "gpurun_out/${tag}_pmcpy_${name}" -o run \
