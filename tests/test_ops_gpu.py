@@ -303,6 +303,8 @@ def test_trainer_fused_optimizer_matches_torch_adamw():
         tr_f.step(frames, audio, text, av_keep=keep[2 * s], tv_keep=keep[2 * s + 1])
     torch.cuda.synchronize()
     sd = ck.reference_state_dict(m, tr_f.space)
+    sd_t = ck.reference_state_dict(m_t)   # fp32 masters on both sides (the frozen ViT base is a bf16 model
+    #                                       weight with its fp32 master in vit's frozen_fp32, in both models)
     # Per element, relative to the most the two AdamW steps can have moved it (|p| + the sum of the
     # step learning rates: an Adam update is at most ~lr per element): a parameter whose two
     # updates nearly cancel (a zero-initialised bias) would make |p| alone an ill-conditioned scale.
@@ -312,8 +314,8 @@ def test_trainer_fused_optimizer_matches_torch_adamw():
     named = dict(m.named_parameters())
     bad = []
     for n, pt in params_t.items():
-        b = pt.detach().float()
-        a = sd[ck.to_reference_key(n)].float().to(b.device)
+        b = sd_t[ck.to_reference_key(n)].float().to(pt.device)
+        a = sd[ck.to_reference_key(n)].float().to(pt.device)
         rel = (a - b).abs() / (b.abs() + lr_sum[0])
         err = float(rel.max())
         worst = max(worst, err)
