@@ -20,7 +20,6 @@ gradients are never rewritten in HBM.
 """
 from __future__ import annotations
 
-import math
 import os
 from typing import Dict, Iterable, List, Sequence
 
@@ -101,6 +100,13 @@ class FlatParamSpace:
         self._shadow_ptrs = {int(i): self.params[i].data_ptr() for i in np.nonzero(self.shadowed)[0]}
         self._chunk_cache: Dict[tuple, tuple] = {}
         self._index_cache: Dict[tuple, torch.Tensor] = {}
+        # persistent pinned staging slots for the per-step host->device tables (gather pieces, AdamW
+        # scalars): a fresh pinned allocation per call, whenever the caching host allocator had no
+        # free block, could synchronise the device -- the bench trace showed the GPU idle for up to
+        # 7.6 ms in the optimizer phase (profiles/r05_bench_kernel_trace_summary.csv)
+        self._stage = [(None, None)] * 8
+        self._stage_next = 0
+        self._held = None   # (.grad tensors read by the last gather launch, its completion event)
 
     def check_shadows(self, ids: Sequence[int]):
         """Raise if a shadowed parameter's bf16 storage was reallocated (model.to(), p.data = ...)
@@ -185,6 +191,29 @@ class FlatParamSpace:
         p = self.params[i]
         return self.flat_p[self.offsets[i]:self.offsets[i] + p.numel()].view(p.shape)
 
+    def _h2d(self, raw: np.ndarray) -> torch.Tensor:
+        """Host bytes -> a fresh device uint8 tensor, copied on the current stream through the ring
+        of pinned staging slots (a slot is rewritten only after the copy that last used it has
+        completed -- several launches, i.e. about a step, earlier)."""
+        raw = np.ascontiguousarray(raw).view(np.uint8).reshape(-1)
+        if self.device.type != "cuda":
+            return torch.from_numpy(raw.copy())
+        n = raw.nbytes
+        slot = self._stage_next
+        self._stage_next = (slot + 1) % len(self._stage)
+        buf, ev = self._stage[slot]
+        if ev is not None:
+            ev.synchronize()
+        if buf is None or buf.numel() < n:
+            buf = torch.empty(max(2 * n, 1 << 16), dtype=torch.uint8, pin_memory=True)
+        buf[:n].numpy()[:] = raw
+        out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        out.copy_(buf[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._stage[slot] = (buf, ev)
+        return out
+
     @torch.no_grad()
     def gather_shadow_grads(self, accumulate: bool):
         """.grad of the gathered parameters (bf16 for the shadowed ones, fp32 for the rest) ->
@@ -192,7 +221,10 @@ class FlatParamSpace:
         reuse by the caching allocator)."""
         if not self.gathered.any():
             return
-        rows, ids = [], []
+        if self._held is not None:   # the previous gather has read its .grad tensors: release them
+            self._held[1].synchronize()
+            self._held = None
+        src, dst, cnt, f32s, ids, grads = [], [], [], [], [], []
         for i in np.nonzero(self.gathered)[0]:
             p = self.params[i]
             gr = p.grad
@@ -201,23 +233,31 @@ class FlatParamSpace:
             dt = torch.bfloat16 if self.shadowed[i] else torch.float32
             if gr.dtype != dt or not gr.is_contiguous():
                 gr = gr.to(dt).contiguous()
-                p.grad = gr
-            base, n, f32 = gr.data_ptr(), gr.numel(), int(dt == torch.float32)
-            for s0 in range(0, n, CHUNK):
-                rows.append((base + (2 + 2 * f32) * s0, self.offsets[i] + s0, min(CHUNK, n - s0), f32))
+            n, f32 = gr.numel(), int(dt == torch.float32)
+            s0 = np.arange(0, n, CHUNK, dtype=np.int64)
+            src.append(gr.data_ptr() + (2 + 2 * f32) * s0)
+            dst.append(self.offsets[i] + s0)
+            cnt.append(np.minimum(CHUNK, n - s0))
+            f32s.append(np.full(len(s0), f32, dtype=np.int32))
             ids.append(int(i))
-        if not rows:
+            grads.append(gr)
+        if not ids:
             return
-        arr = np.array(rows, dtype=_PIECE_DT)
-        host = torch.from_numpy(arr.view(np.uint8)).pin_memory() if self.device.type == "cuda" else \
-            torch.from_numpy(arr.view(np.uint8).copy())
-        table = host.to(self.device, non_blocking=True)
-        call("triad_gather_grads", ptr(table), len(rows), ptr(self.flat_g), int(accumulate and True),
+        arr = np.empty(sum(len(a) for a in src), dtype=_PIECE_DT)
+        arr["src"] = np.concatenate(src).astype(np.uint64)
+        arr["dst"] = np.concatenate(dst)
+        arr["n"] = np.concatenate(cnt)
+        arr["f32"] = np.concatenate(f32s)
+        table = self._h2d(arr)
+        call("triad_gather_grads", ptr(table), len(arr), ptr(self.flat_g), int(accumulate and True),
              stream_ptr(self.device))
-        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        if self.device.type == "cuda":
+            # gradients made on other streams (side-stream dW, modality streams) stay referenced
+            # until this launch has read them (instead of one record_stream per parameter)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._held = (grads, ev)
         for i in ids:
-            if cur is not None:  # grads made on other streams (side-stream dW, modality streams)
-                self.params[i].grad.record_stream(cur)
             self.params[i].grad = None
         self.touched[ids] = True
 
@@ -260,19 +300,16 @@ class FusedAdamW(torch.optim.Optimizer):
             return loss
         g = self.param_groups[0]
         lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
-        # fresh pinned block per step: the caching host allocator keeps it alive until the
-        # async H2D copy recorded on the stream has completed
-        host = torch.empty(3 * len(sp.params), dtype=torch.float32, pin_memory=sp.device.type == "cuda")
-        pp = host.numpy()
-        for i in ids:
-            sp.steps[i] += 1
-            t = int(sp.steps[i])
-            bc1 = 1.0 - b1 ** t
-            bc2 = 1.0 - b2 ** t
-            pp[3 * i] = lr / bc1
-            pp[3 * i + 1] = 1.0 / math.sqrt(bc2)
-            pp[3 * i + 2] = 1.0 - lr * wd
-        pp_dev = host.to(sp.device, non_blocking=True)
+        # per-parameter {lr / bc1, 1 / sqrt(bc2), 1 - lr wd} (float64 on the host, as torch computes
+        # them), staged through the space's pinned ring
+        idx = np.asarray(ids, dtype=np.int64)
+        sp.steps[idx] += 1
+        t = sp.steps[idx].astype(np.float64)
+        pp = np.zeros((len(sp.params), 3), dtype=np.float32)
+        pp[idx, 0] = lr / (1.0 - b1 ** t)
+        pp[idx, 1] = 1.0 / np.sqrt(1.0 - b2 ** t)
+        pp[idx, 2] = 1.0 - lr * wd
+        pp_dev = sp._h2d(pp).view(torch.float32)
         sp.check_shadows(ids)
         table, n, _ = sp.chunks(ids)
         call("triad_adamw_step", ptr(sp.flat_p), ptr(sp.flat_g), ptr(sp.exp_avg), ptr(sp.exp_avg_sq), ptr(table), n,
