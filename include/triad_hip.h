@@ -225,9 +225,10 @@ int triad_projhead_ln_bwd(const void* dy, long long M, const void* W2p, const vo
 
 /* Inference similarity maps (model.py:355-368 compute_similarity_matrix; forward() 630-636,
  * viz.py:182): sim[b][i][j] = temp * <f1[b][i] / max(||f1[b][i]||, eps), f2[b][j] / max(||f2[b][j]||,
- * eps)>, f1 (B, N1, D), f2 (B, N2, D) contiguous bf16 16-byte aligned, D % 32 == 0, temp a device
- * scalar, sim (B, N1, N2) fp32. One launch over all samples: normalisation in the prologue
- * (operands rounded to bf16 after it, as F.normalize returns bf16), temperature in the epilogue. */
+ * eps)>, f1 (B, N1, D), f2 (B, N2, D) contiguous bf16 16-byte aligned, D % 32 == 0, D <= 512, temp
+ * a device scalar, sim (B, N1, N2) fp32 16-byte aligned. One launch over all samples: a workgroup
+ * normalises 64 f1 rows and, block by block, 64 f2 rows into LDS (operands rounded to bf16 after
+ * it, as F.normalize returns bf16) and applies the temperature in the epilogue. */
 int triad_similarity_maps(const void* f1, const void* f2, int B, int N1, int N2, int D, const float* temp, float eps,
                           float* sim, hipStream_t stream);
 

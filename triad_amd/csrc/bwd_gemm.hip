@@ -237,6 +237,36 @@ __global__ __launch_bounds__(512) void bfrag_pack16_kernel(const bf16* __restric
 // LDS-DMA asm in between no longer ordered it). tests/test_isa_cpu.py checks the emitted waits.
 __device__ __forceinline__ bf16x8 bload16(const bf16* p) { return *(const bf16x8*)p; }
 
+// Cache policy of the dS loads (read once per GEMM): TRIAD_DS_LOAD_POL 0 plain, 1 nt, 2 sc1,
+// 3 sc0 sc1 (A/B builds, VERDICT r4 #3: keep the 5.8 GB dS stream from evicting the packed K / Q
+// fragments every workgroup re-reads from L2)
+#ifndef TRIAD_DS_LOAD_POL
+#define TRIAD_DS_LOAD_POL 0
+#endif
+#if TRIAD_DS_LOAD_POL == 1
+#define TRIAD_DS_LOAD_POLICY " nt"
+#elif TRIAD_DS_LOAD_POL == 2
+#define TRIAD_DS_LOAD_POLICY " sc1"
+#elif TRIAD_DS_LOAD_POL == 3
+#define TRIAD_DS_LOAD_POLICY " sc0 sc1"
+#else
+#define TRIAD_DS_LOAD_POLICY ""
+#endif
+__device__ __forceinline__ void glds16_ds(const void* gsrc, void* lds_base) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)LDS_PTR(void, lds_base));
+  TRIAD_LDS_DMA_CHECK(lds, 0);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off" TRIAD_DS_LOAD_POLICY "\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds)
+      : "memory");
+}
+
 // one stage = one 32-deep k tile kt (clamped to kt_last): 4 B loads + 1 A LDS-DMA piece per wave
 template <bool DK>
 __device__ __forceinline__ void db_stage(const bf16* __restrict__ Dt, long long CT, const bf16* Bp, int mt0, int kt,
@@ -249,7 +279,7 @@ __device__ __forceinline__ void db_stage(const bf16* __restrict__ Dt, long long 
   const int pos = half * 64 + lane;
   const int c = DK ? swz_k16(pos) : swz_q(pos);
   const long long tile = DK ? ((long long)ktk * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + ktk);
-  glds16(Dt + tile * 1024 + c * 8, adst + t * 1024 + half * 512);
+  glds16_ds(Dt + tile * 1024 + c * 8, adst + t * 1024 + half * 512);
 }
 
 template <int U, int N, class F>

@@ -933,6 +933,8 @@ def similarity_maps(f1: torch.Tensor, f2: torch.Tensor, temperature: torch.Tenso
     N2 = f2.shape[1]
     a = f1.to(torch.bfloat16).contiguous()
     b = f2.to(torch.bfloat16).contiguous()
+    if _rup(Dd, 32) > 512:
+        raise TriadError(f"similarity_maps: feature width {Dd} > 512 (the kernel's LDS tiles)")
     if Dd % 32:   # zero-padded features (norms and dots unchanged)
         a = torch.nn.functional.pad(a, (0, _rup(Dd, 32) - Dd))
         b = torch.nn.functional.pad(b, (0, _rup(Dd, 32) - Dd))
