@@ -237,11 +237,13 @@ __global__ __launch_bounds__(512) void bfrag_pack16_kernel(const bf16* __restric
 // LDS-DMA asm in between no longer ordered it). tests/test_isa_cpu.py checks the emitted waits.
 __device__ __forceinline__ bf16x8 bload16(const bf16* p) { return *(const bf16x8*)p; }
 
-// Cache policy of the dS loads (read once per GEMM): TRIAD_DS_LOAD_POL 0 plain, 1 nt, 2 sc1,
-// 3 sc0 sc1 (A/B builds, VERDICT r4 #3: keep the 5.8 GB dS stream from evicting the packed K / Q
-// fragments every workgroup re-reads from L2)
+// Cache policy of the dS loads (read once per GEMM): TRIAD_DS_LOAD_POL 0 plain, 1 nt (default),
+// 2 sc1, 3 sc0 sc1. VERDICT r4 #3 asked to keep the 5.8 GB dS stream from evicting the packed K / Q
+// fragments every workgroup re-reads from L2. Measured (tools/gpu_ab_dsload.sh, two alternated
+// rounds, profiles/r05_bwd_ds_load_policy_ab.log): nt AV dQ 2.586 -> 2.575 ms, AV dK 2.496 -> 2.480,
+// TV dQ 0.404 -> 0.390, TV dK equal; sc1 / sc0 sc1 within noise of plain.
 #ifndef TRIAD_DS_LOAD_POL
-#define TRIAD_DS_LOAD_POL 0
+#define TRIAD_DS_LOAD_POL 1
 #endif
 #if TRIAD_DS_LOAD_POL == 1
 #define TRIAD_DS_LOAD_POLICY " nt"

@@ -5,31 +5,24 @@
 // padded copies + one GEMM launch per sample).
 //
 // Workgroup = 4 waves = one sample b x 64 rows of f1 x ALL N2 columns (64-column blocks in a loop):
-//   * the f1 rows are L2-normalised once per workgroup into LDS (bf16, F.normalize's output type);
-//   * per 64-column block the f2 rows are normalised the same way into a second LDS tile, shared
-//     by the four waves (round 5's first form re-read every f2 row from global memory in every wave
-//     and every row tile, twice: ~8x the loads, 0.32 ms for a 256 x 199 x 256 map);
-//   * wave w owns rows 16 w .. 16 w + 15 against the block's 64 columns: 4 blocks of 16 x 16 on
-//     v_mfma_f32_16x16x32_bf16, the f2 fragment first, so each lane's four accumulators are four
-//     consecutive output columns of one row -> one 16-byte store.
-// Normalising a tile: thread t owns row t >> 2 and every fourth 16-byte chunk of it; the row's sum
-// of squares is combined over its 4 lanes, then the chunks are re-read, scaled by
-// 1 / max(||row||, eps), rounded to bf16 and stored at chunk c ^ (row & swz_mask) (the MFMA fragment
-// reads, 16 rows x one chunk per lane group, are then conflict-free at 1 KB rows). Rows past
-// N1 / N2 re-read the last row (in bounds) and are not stored.
+//   * wave w loads its 16 f1 rows once as MFMA A fragments (lane: one row, chunks 4 s + q, all 16
+//     k steps in flight), L2-normalises them in registers (the row's sum of squares over its four
+//     q lanes) and keeps them as bf16 -- F.normalize's output type;
+//   * per 64-column block the f2 rows are normalised the same way into ONE 64 KB LDS tile shared by
+//     the four waves (two workgroups per CU), every thread's 16 chunk loads in flight at once (round
+//     5's first form re-read every f2 row from global memory in every wave and row tile, twice,
+//     with one load in flight: 0.32 ms for a 256 x 199 x 256 map, 0.19 with a shared tile);
+//   * 4 blocks of 16 x 16 on v_mfma_f32_16x16x32_bf16 per wave, the f2 fragment first, so each
+//     lane's four accumulators are four consecutive output columns of one row -> one 16-byte store.
+// The LDS tile's rows are padded by 16 bytes (D + 8 elements): a fragment read (16 rows x one
+// 16-byte chunk per lane group) then covers 16 different bank quads at D = 512, and every address
+// stays linear in the k step (immediate offsets; an XOR swizzle cost one address VGPR per fragment).
+// Rows past N1 / N2 re-read the last row (in bounds) and are not stored. D <= 512.
 #include "common.h"
 
 namespace {
 
 constexpr int SM_ROWS = 64;
-
-// XOR mask of the chunk swizzle: (row & 15) when a row has a multiple of 16 chunks (D % 128 == 0,
-// conflict-free at D = 512), else the largest power-of-two group of chunks D / 8 is a multiple of
-// (>= 4 since D % 32 == 0), so a swizzled chunk never leaves its row
-__device__ __forceinline__ int swz_mask(int D) {
-  const int nc = D / 8, low = nc & -nc;
-  return (low < 16 ? low : 16) - 1;
-}
 
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -49,48 +42,85 @@ __device__ __forceinline__ bf16x8 scale8(bf16x8 v, float inv) {
   return o;
 }
 
+constexpr int SM_KMAX = 16;   // 32-deep k steps for D <= 512
+
+// f2 rows [r0, r0 + 64) of one sample, normalised, into the LDS tile: thread t owns row t >> 2 and
+// chunks t4, t4 + 4, ... (up to 16, all loads issued before the first use)
 __device__ __forceinline__ void norm_tile(const bf16* __restrict__ src, int nrows, int r0, int D, float eps,
                                           bf16* __restrict__ tile) {
   const int t = threadIdx.x, row = t >> 2, t4 = t & 3;
   const int r = r0 + row < nrows ? r0 + row : nrows - 1;
   const bf16* p = src + (long long)r * D;
-  const int nc = D / 8, g = swz_mask(D);
+  const int nc = D / 8, ld = D + 8;
+  bf16x8 v[SM_KMAX];
   float ss = 0.f;
-  for (int c = t4; c < nc; c += 4) ss += sumsq8(*(const bf16x8*)(p + 8 * c));
+#pragma unroll
+  for (int j = 0; j < SM_KMAX; ++j) {
+    const int c = t4 + 4 * j;
+    v[j] = c < nc ? *(const bf16x8*)(p + 8 * c) : bf16x8{};
+  }
+#pragma unroll
+  for (int j = 0; j < SM_KMAX; ++j) {
+    ss += sumsq8(v[j]);
+    asm volatile("" : "+v"(v[j]));   // keep the packed bf16 live, not 8 fp32 copies (re-unpacked below)
+  }
   ss += __shfl_xor(ss, 1);
   ss += __shfl_xor(ss, 2);
   const float inv = 1.f / fmaxf(sqrtf(ss), eps);
-  for (int c = t4; c < nc; c += 4)
-    *(bf16x8*)(tile + row * D + 8 * (c ^ (row & g))) = scale8(*(const bf16x8*)(p + 8 * c), inv);
+#pragma unroll
+  for (int j = 0; j < SM_KMAX; ++j) {
+    const int c = t4 + 4 * j;
+    if (c < nc) *(bf16x8*)(tile + row * ld + 8 * c) = scale8(v[j], inv);
+    if (j % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+  }
 }
 
-__global__ __launch_bounds__(256) void simmap_kernel(const bf16* __restrict__ f1, const bf16* __restrict__ f2, int N1,
-                                                     int N2, int D, const float* __restrict__ temp, float eps,
-                                                     float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) bf16 sm[];
-  bf16* ta = sm;                      // [64][D] normalised f1 rows
-  bf16* tb = sm + SM_ROWS * D;        // [64][D] normalised f2 rows of the current column block
+__global__ __launch_bounds__(256, 2) void simmap_kernel(const bf16* __restrict__ f1, const bf16* __restrict__ f2,
+                                                        int N1, int N2, int D, const float* __restrict__ temp,
+                                                        float eps, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) bf16 tb[];   // [64][D + 8] normalised f2 rows of a block
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l16 = lane & 15, q = lane >> 4;
   const long long b = blockIdx.y;
-  const int m0 = blockIdx.x * SM_ROWS;
-  const int m = m0 + 16 * wave + l16;
+  const int m = blockIdx.x * SM_ROWS + 16 * wave + l16;
+  const int ks = D / 32;
+  // this lane's A fragments: row m, chunk 4 s + q of every k step s, normalised in registers
+  bf16x8 af[SM_KMAX];
+  {
+    const bf16* ar = f1 + (b * N1 + (m < N1 ? m : N1 - 1)) * (long long)D + 8 * q;
+    float ss = 0.f;
+#pragma unroll
+    for (int s = 0; s < SM_KMAX; ++s) af[s] = s < ks ? *(const bf16x8*)(ar + 32 * s) : bf16x8{};
+#pragma unroll
+    for (int s = 0; s < SM_KMAX; ++s) {
+      ss += sumsq8(af[s]);
+      asm volatile("" : "+v"(af[s]));
+    }
+    ss += __shfl_xor(ss, 16);
+    ss += __shfl_xor(ss, 32);
+    const float inv = 1.f / fmaxf(sqrtf(ss), eps);
+#pragma unroll
+    for (int s = 0; s < SM_KMAX; ++s) {
+      af[s] = scale8(af[s], inv);
+      if (s % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  const bf16* bfr = tb + l16 * (D + 8) + 8 * q;   // + (16 cb) rows + 32 s: B fragment of (cb, s)
   const float t = *temp;
-  norm_tile(f1 + b * N1 * (long long)D, N1, m0, D, eps, ta);
-  const bf16* arow = ta + (16 * wave + l16) * D;
-  const int sw = l16 & swz_mask(D);   // fragment rows 16 j + l16: row & mask == l16 & mask
   float* orow = out + (b * N1 + (m < N1 ? m : 0)) * (long long)N2;
   for (int n0 = 0; n0 < N2; n0 += SM_ROWS) {
     __syncthreads();   // the previous block's fragment reads are done before tb is rewritten
     norm_tile(f2 + b * N2 * (long long)D, N2, n0, D, eps, tb);
     __syncthreads();
     f32x4 acc[4] = {};
-    for (int k = 0; k < D; k += 32) {
-      const int c = k / 8 + q;
-      const bf16x8 af = *(const bf16x8*)(arow + 8 * (c ^ sw));
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-        acc[cb] = mfma16(*(const bf16x8*)(tb + (16 * cb + l16) * D + 8 * (c ^ sw)), af, acc[cb]);
+    for (int s = 0; s < SM_KMAX; ++s) {
+      if (s < ks) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+          acc[cb] = mfma16(*(const bf16x8*)(bfr + 16 * cb * (D + 8) + 32 * s), af[s], acc[cb]);
+      }
+      if (s % 4 == 3) __builtin_amdgcn_sched_barrier(0);   // at most 16 B fragments in flight
     }
     if (m < N1) {
 #pragma unroll
@@ -117,15 +147,16 @@ extern "C" {
 // f1 (B, N1, D), f2 (B, N2, D) contiguous bf16 (D % 32 == 0, D <= 512), temp a device scalar, sim fp32.
 int triad_similarity_maps(const void* f1, const void* f2, int B, int N1, int N2, int D, const float* temp, float eps,
                           float* sim, hipStream_t stream) {
-  // two [64][D] bf16 tiles in LDS: D <= 512 (128 KB); the fp32 output pointer 16-byte aligned
+  // one [64][D + 8] bf16 tile in LDS (65 KB at D = 512), the A fragments in registers: D <= 512; the
+  // fp32 output pointer 16-byte aligned
   if (!f1 || !f2 || !temp || !sim || B <= 0 || N1 <= 0 || N2 <= 0 || D <= 0 || D % 32 || D > 512 || B > 65535 ||
       ((uintptr_t)f1 & 15) || ((uintptr_t)f2 & 15) || ((uintptr_t)sim & 15))
     return TRIAD_EINVAL;
-  const size_t lds = 2 * (size_t)SM_ROWS * D * sizeof(bf16);
+  const size_t lds = (size_t)SM_ROWS * (D + 8) * sizeof(bf16);
   // more than 64 KB of dynamic LDS: allow it once (an error here is cleared, the launch reports its own)
   static const bool attr = [] {
     if (hipFuncSetAttribute((const void*)simmap_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            2 * SM_ROWS * 512 * (int)sizeof(bf16)) != hipSuccess)
+                            SM_ROWS * (512 + 8) * (int)sizeof(bf16)) != hipSuccess)
       (void)hipGetLastError();
     return true;
   }();
