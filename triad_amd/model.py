@@ -126,16 +126,6 @@ _HUBERT_LARGE = dict(hidden_size=1024, num_hidden_layers=24, num_attention_heads
                      feat_extract_norm="layer", do_stable_layer_norm=True)
 
 
-# Host order of the three encoders in forward_triad. Autograd's device thread walks the backward
-# in reverse creation order, one branch at a time: with the ViT encoded first, its backward (the
-# big kernels of the main stream) is enqueued last, after the text branch's hundreds of small
-# launches, and the GPU ran the text stream alone for ~3 ms per step (profiles/
-# r05_bench_kernel_trace_summary_host_staging.csv). TRIAD_VIT_LAST=1 encodes the ViT after the audio
-# and text encoders, so its backward is enqueued first and the text branch's launches overlap it.
-# The host order of every RNG draw changes with it, identically in the serial and concurrent paths.
-VIT_LAST = os.environ.get("TRIAD_VIT_LAST", "0") != "0"
-
-
 class ProjectionHead(nn.Module):
     """Holder so `projection1`, `layer_norm`, `projection2` keep the reference names."""
 
@@ -471,18 +461,12 @@ class MultiModalModel(nn.Module):
         ve = self.visual_embedder
         streams = _modality_streams(frames)
         with torch.autocast("cuda", enabled=self.use_amp, dtype=self.amp_dtype):
-            vit_last = VIT_LAST
             if streams is None:
-                if not vit_last:
-                    patches = ve.encode_patches(frames)
-                    v_av = ve.patch_dropout(patches, ve.patch_dropout_rate, av_keep)
-                    v_tv = ve.patch_dropout(patches, ve.patch_dropout_rate, tv_keep)
+                patches = ve.encode_patches(frames)
+                v_av = ve.patch_dropout(patches, ve.patch_dropout_rate, av_keep)
+                v_tv = ve.patch_dropout(patches, ve.patch_dropout_rate, tv_keep)
                 audio_feats = self.audio_embedder(audio)
                 text_feats, attention_mask = self.text_embedder(text_list)
-                if vit_last:
-                    patches = ve.encode_patches(frames)
-                    v_av = ve.patch_dropout(patches, ve.patch_dropout_rate, av_keep)
-                    v_tv = ve.patch_dropout(patches, ve.patch_dropout_rate, tv_keep)
             else:
                 # the three backbones are independent until the heads: audio and text run on
                 # their own streams beside the ViT (and, since autograd runs each backward op on
@@ -491,18 +475,13 @@ class MultiModalModel(nn.Module):
                 main, s_audio, s_text = streams
                 s_audio.wait_stream(main)
                 s_text.wait_stream(main)
-                if not vit_last:
-                    patches = ve.encode_patches(frames)
-                    v_av = ve.patch_dropout(patches, ve.patch_dropout_rate, av_keep)
-                    v_tv = ve.patch_dropout(patches, ve.patch_dropout_rate, tv_keep)
+                patches = ve.encode_patches(frames)
+                v_av = ve.patch_dropout(patches, ve.patch_dropout_rate, av_keep)
+                v_tv = ve.patch_dropout(patches, ve.patch_dropout_rate, tv_keep)
                 with torch.cuda.stream(s_audio):
                     audio_feats = self.audio_embedder(audio)
                 with torch.cuda.stream(s_text):
                     text_feats, attention_mask = self.text_embedder(text_list)
-                if vit_last:
-                    patches = ve.encode_patches(frames)
-                    v_av = ve.patch_dropout(patches, ve.patch_dropout_rate, av_keep)
-                    v_tv = ve.patch_dropout(patches, ve.patch_dropout_rate, tv_keep)
                 main.wait_stream(s_audio)
                 main.wait_stream(s_text)
                 for t in (audio_feats, text_feats, attention_mask):
