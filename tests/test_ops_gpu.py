@@ -204,6 +204,69 @@ def test_flat_space_gathers_fp32_and_bf16_grads_with_accumulation():
     assert float(space.flat_g.abs().sum()) == 0.0
 
 
+def test_optimizer_stream_kernels_vector_tails_and_misaligned_sources():
+    """The optimizer phase's streaming kernels (optim.hip: float4 / bf16x8 per lane, scalar tails)
+    through the C-ABI on pieces the trainer's tables can hold: whole 16,384-element chunks, lengths
+    that are not multiples of 4 / 8, and gradient sources off 16-byte alignment (scalar path).
+    Gather: exact, with and without accumulation; sum of squares: to 1e-12 of a float64 sum; AdamW:
+    to 1e-5 relative / 1e-6 absolute of a float64 evaluation of torch's formula, bf16 shadow = the fp32 result rounded."""
+    from triad_amd import optim as fo
+    from triad_amd._lib import call, ptr, stream_ptr
+    g = torch.Generator(device=dev).manual_seed(11)
+    lens = [16384, 7, 8195, 4099, 16383, 1, 12]
+    f32 = [0, 0, 0, 1, 1, 1, 0]
+    mis = [0, 0, 1, 0, 1, 0, 1]          # source starts one element past a 16-byte boundary
+    offs = np.cumsum([0] + [(n + 63) // 64 * 64 for n in lens])
+    N = int(offs[-1])
+    flat = torch.zeros(N, device=dev)
+    srcs, want = [], torch.zeros(N, device=dev)
+    for rnd in range(2):
+        pieces = np.zeros(len(lens), dtype=fo._PIECE_DT)
+        keep = []
+        for k, (n, is32, m) in enumerate(zip(lens, f32, mis)):
+            base = torch.randn(n + 8, device=dev, generator=g).to(torch.float32 if is32 else torch.bfloat16)
+            s = base[m:m + n]
+            keep.append(base)
+            pieces[k] = (s.data_ptr(), offs[k], n, is32)
+            want[offs[k]:offs[k] + n] += s.float()
+        call("triad_gather_grads", ptr(fo._lib.h2d(torch.from_numpy(pieces.view(np.uint8).copy()), dev)), len(lens),
+             ptr(flat), rnd, stream_ptr())
+        torch.cuda.synchronize()
+        srcs.append(keep)
+        assert torch.equal(flat, want), rnd
+    chunks = np.zeros(len(lens), dtype=fo._CHUNK_DT)
+    for k, n in enumerate(lens):
+        chunks[k] = (offs[k], n, k)
+    table = fo._lib.h2d(torch.from_numpy(chunks.view(np.uint8).copy()), dev)
+    part = torch.empty(len(lens), dtype=torch.float64, device=dev)
+    call("triad_grad_sumsq", ptr(flat), ptr(table), len(lens), ptr(part), stream_ptr())
+    for k, n in enumerate(lens):
+        ref = float((flat[offs[k]:offs[k] + n].double() ** 2).sum())
+        assert abs(float(part[k]) - ref) <= 1e-12 * ref, (k, float(part[k]), ref)
+    p = torch.randn(N, device=dev, generator=g)
+    m = torch.randn(N, device=dev, generator=g) * 0.1
+    v = torch.rand(N, device=dev, generator=g) * 0.01
+    p0, m0, v0 = p.double(), m.double(), v.double()
+    nparam = len(lens)
+    pp = torch.tensor([[1e-3 / 0.1, 1 / math.sqrt(1e-3), 1 - 1e-5]] * nparam, device=dev).reshape(-1)
+    scale = torch.linspace(0.5, 1.0, nparam, device=dev)
+    shadow = [torch.zeros(n, dtype=torch.bfloat16, device=dev) for n in lens]
+    sb = torch.from_numpy(np.array([(s.data_ptr() - 2 * int(offs[k])) % (1 << 64) for k, s in enumerate(shadow)],
+                                   dtype=np.uint64).view(np.int64)).to(dev)
+    call("triad_adamw_step", ptr(p), ptr(flat), ptr(m), ptr(v), ptr(table), len(lens), ptr(pp), ptr(scale), 0.9, 0.999,
+         0.1, 1e-3, 1e-8, ptr(sb), stream_ptr())
+    torch.cuda.synchronize()
+    for k, n in enumerate(lens):
+        sl = slice(int(offs[k]), int(offs[k]) + n)
+        gr = flat[sl].double() * float(scale[k])
+        mv = m0[sl] + 0.1 * (gr - m0[sl])
+        vv = v0[sl] * 0.999 + 1e-3 * gr * gr
+        pv = p0[sl] * float(pp[3 * k + 2]) - float(pp[3 * k]) * (mv / (vv.sqrt() * float(pp[3 * k + 1]) + 1e-8))
+        for got, ref in ((p[sl], pv), (m[sl], mv), (v[sl], vv)):
+            torch.testing.assert_close(got.double(), ref, rtol=1e-5, atol=1e-6)
+        assert torch.equal(shadow[k], p[sl].to(torch.bfloat16)), k
+
+
 def test_trainer_step_runs_and_moves_params():
     from triad_amd.model import MultiModalModel
     from triad_amd.train import TriadTrainer

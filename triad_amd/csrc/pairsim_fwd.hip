@@ -8,7 +8,8 @@
 // each wave keeps its rows' bf16 fragments (32 x 512 = 128 VGPRs) for the whole launch.
 //  * key tiles (32 keys x 512 x bf16 = 32 KB) stream through a 3-slot LDS ring by 16-byte
 //    buffer LDS-DMA issued two tiles ahead; one counted `s_waitcnt vmcnt(N)` + s_barrier per
-//    tile (the next tile's DMA stays in flight across it);
+//    tile (the next tile's DMA stays in flight across it) -- per pair of tiles, 4 slots, in the
+//    eval form's 16 x 16 x 32 body;
 //  * the epilogue of tile b-1 (scale, max/argmax, clamp^2, unit dS, bf16 pack) is carried by
 //    tile b's 32-step MFMA chain, one element per two k-steps, so its VALU issues in the MFMA
 //    shadows.
@@ -26,7 +27,7 @@ constexpr int NS = D / 16;  // 32 k-steps
 constexpr int WAVES = 8;
 constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 query rows per workgroup
 constexpr int KT_ELEMS = 32 * D;
-constexpr int NBUF = 3;                  // key-tile LDS ring slots
+constexpr int NBUF = 3;                  // key-tile LDS ring slots (training body)
 constexpr int LDSPF = 2;                 // key fragments read from LDS ahead of their MFMA
 constexpr int REGION = 2;                // k-steps per scheduling region (sched_barrier spacing)
 constexpr int GLDS_PER_TILE = 32 / WAVES;  // 1-KB LDS-DMA pieces per wave per key tile (4)
@@ -221,7 +222,13 @@ struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in 
 // SHORTQ tags the launches over short query lists (text captions, Nq <= 32) with their own
 // symbol, so profiler summaries report the AV (long-query) launches' durations on their own; the
 // code is identical.
-constexpr int KBUF_ELEMS = NBUF * KT_ELEMS + 16 * WAVES;
+// The 16 x 16 x 32 body (eval form) meets at the ring barrier once per TWO key tiles: 4 slots,
+// pairs of tiles DMA'd together two tiles ahead (round 5, TRIAD_FWD_SYNC2 A/B, alternated x3 on
+// one box, profiles/r05_fwd_sync2_ab.log: eval AV 2.36 -> 2.30-2.32 ms, TV 0.408 -> 0.392-0.399;
+// the same pairing in the training body was 3 % slower, AV 3.00 -> 3.10, and is not used there).
+constexpr int NBUF16 = 4;
+template <bool TRAIN>
+constexpr int kbuf_elems = (TRAIN ? NBUF : NBUF16) * KT_ELEMS + 16 * WAVES;
 
 // One workgroup of the forward: 256-row block bx, key-sample split by (of gx row blocks) of
 // problem a. kbuf = the workgroup's LDS (key ring + reduction scratch).
@@ -491,7 +498,7 @@ __device__ __forceinline__ float epi_fixup16(Epi16& e, const f32x4 (&p)[4], floa
 
 template <bool TRAIN>
 __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const int bx, const int by, const int gx) {
-  double* red = (double*)(kbuf + NBUF * KT_ELEMS);
+  double* red = (double*)(kbuf + NBUF16 * KT_ELEMS);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i16 = lane & 15, g = lane >> 4;
@@ -520,7 +527,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
   auto prefetch = [&](int b2) __attribute__((always_inline)) {
     if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j - j0, fc.kb, wave, lane);
     fc.next(nkb);
-    fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
+    fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF16 - 1 ? 0 : fslot + 1);
   };
   prefetch(0);
   prefetch(1);
@@ -564,14 +571,17 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
   f32x4 cA[4], cB[4];
 
   auto sync_tile = [&](int b) __attribute__((always_inline)) {
-    const bool more = b + 1 < nblocks;
-    const bool st = TRAIN && b >= 2;
-    if (more && st) TRIAD_VMCNT(GLDS_PER_TILE + 2);
-    else if (more) TRIAD_VMCNT(GLDS_PER_TILE);
-    else if (st) TRIAD_VMCNT(2);
+    // one barrier per PAIR of key tiles (even b), both DMA'd together two tiles ahead; younger
+    // than them: the dS stores of iterations b-2 and b-1 (2 each, from iteration 1 on)
+    if (b & 1) return;
+    if (TRAIN && b >= 4) TRIAD_VMCNT(4);
+    else if (TRAIN && b >= 2) TRIAD_VMCNT(2);
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+  };
+  auto refill = [&](int b) __attribute__((always_inline)) {
+    if (!(b & 1)) { prefetch(b + 2); prefetch(b + 3); }
   };
 
   auto epi_end = [&](const f32x4 (&p)[4]) {
@@ -622,9 +632,9 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
     constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value, full = decltype(FULLT)::value;
     if constexpr (ch) {
       sync_tile(b);
-      prefetch(b + NBUF - 1);
+      refill(b);
       const char* kt = (const char*)kbuf + cslot * (KT_ELEMS * 2);
-      cslot = __builtin_amdgcn_readfirstlane(cslot == NBUF - 1 ? 0 : cslot + 1);
+      cslot = __builtin_amdgcn_readfirstlane(cslot == NBUF16 - 1 ? 0 : cslot + 1);
       constexpr int P = LDSPF16;
       bf16x8 af[P + 1][2];
 #pragma unroll
@@ -709,7 +719,7 @@ __device__ __forceinline__ void fwd_any(const FwdArgs& a, bf16* kbuf, const int 
 
 template <bool TRAIN, bool SHORTQ>
 __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd2_kernel(FwdArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 kbuf[KBUF_ELEMS];
+  __shared__ __attribute__((aligned(16))) bf16 kbuf[kbuf_elems<TRAIN>];
   fwd_any<TRAIN>(a, kbuf, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
@@ -728,7 +738,7 @@ struct MultiArgs {
 
 template <bool TRAIN>
 __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd_multi_kernel(MultiArgs m) {
-  __shared__ __attribute__((aligned(16))) bf16 kbuf[KBUF_ELEMS];
+  __shared__ __attribute__((aligned(16))) bf16 kbuf[kbuf_elems<TRAIN>];
   const int b = blockIdx.x;
   const int q = (m.n > 1 && b >= m.first[1]) ? 1 : 0;  // uniform
   const int local = b - m.first[q];
