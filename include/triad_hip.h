@@ -297,6 +297,21 @@ int triad_gather_rows(const void* src, long long src_rows, const int* idx, int B
 /* y = x / max(||x||_2, eps) per row, bf16 (F.normalize, model.py:363-364). */
 int triad_l2norm_rows(const void* x, int rows, int D, float eps, void* y, hipStream_t stream);
 
+/* Reference-precision retrieval (retrieval.py:106-114 aggregator_av_a2v / _v2a, the per-pair
+ * `matmul(q, k.t()) / temperature -> max over the item's tokens -> mean` of its N^2 double loop,
+ * retrieval.py:161-174 / 255-264), every pair in one launch, fp32 throughout:
+ * sim[i][j] = mean_{q < qlen[i]} max_{k < klen[j]} <Q[i][q], K[j][k]> / temp, Q (Bq, nq_pad, D) and
+ * K (Bk, nk_pad, D) contiguous fp32 16-byte aligned, zero-padded token lists (nq_pad, nk_pad
+ * multiples of 64, D % 32 == 0), qlen / klen device int32, sim (Bq, Bk) fp32. For fp32
+ * embeddings (model.use_amp == False, as the reference's retrieval embeds); the bf16 product
+ * path is triad_pairsim_fwd + triad_clip_reduce. */
+int triad_retrieval_maxmean_f32(const float* Q, const int* qlen, int Bq, int nq_pad, const float* K, const int* klen,
+                                int Bk, int nk_pad, int D, float temp, float* sim, hipStream_t stream);
+
+/* y = x / max(||x||_2, eps) per row, fp32 (F.normalize of the reference's fp32 retrieval embeddings,
+ * retrieval.py:93-94); x, y 16-byte aligned, D % 4 == 0. */
+int triad_l2norm_rows_f32(const float* x, int rows, int D, float eps, float* y, hipStream_t stream);
+
 /* Audio front-end (model.py:29-30,66: the HuBERT conv feature encoder's layer 0,
  * transformers HubertGroupNormConvLayer = conv -> GroupNorm(C groups) -> GELU), fused
  * GroupNorm + exact GELU over channels-last x[B][Tp][C] bf16 (C % 8 == 0, 256 % (C/8) == 0); the

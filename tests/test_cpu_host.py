@@ -195,6 +195,15 @@ def test_round4_entry_points_reject_bad_arguments():
     assert lib.triad_colsum_dma(fake, 1024, 768, 768, None, 1.0, 0, fake, None) == 1001
     assert lib.triad_colsum_dma_splits(50944, 768) == 171 and lib.triad_colsum_dma_splits(256, 768) == 4
     assert lib.triad_colsum_dma_splits(50944, 640) == 171 and lib.triad_colsum_dma_splits(50944, 12) == 0
+    # fp32 retrieval scorer: padded token counts multiples of 64, D % 32, 16-byte aligned lists
+    ok = (fake, fake, 24, 64, fake, fake, 24, 128, 512, 0.07, fake, None)
+    assert lib.triad_retrieval_maxmean_f32(*ok[:3], 100, *ok[4:]) == 1001                   # nq_pad % 64
+    assert lib.triad_retrieval_maxmean_f32(*ok[:7], 96, *ok[8:]) == 1001                    # nk_pad % 64
+    assert lib.triad_retrieval_maxmean_f32(*ok[:8], 500, *ok[9:]) == 1001                   # D % 32
+    assert lib.triad_retrieval_maxmean_f32(fake + 4, *ok[1:]) == 1001                       # misaligned
+    assert lib.triad_retrieval_maxmean_f32(*ok[:10], None, None) == 1001                    # no output
+    assert lib.triad_l2norm_rows_f32(fake, 10, 510, 1e-12, fake, None) == 1001              # D % 4
+    assert lib.triad_l2norm_rows_f32(fake + 8, 10, 512, 1e-12, fake, None) == 1001          # misaligned
 
 
 def test_side_stream_tables_key_by_device_ordinal():

@@ -63,6 +63,8 @@ SIGNATURES = {
     "triad_gather_grads": [vp, i32, vp, i32, vp],
     "triad_gather_rows": [vp, i64, vp, i32, i32, i32, vp, vp],
     "triad_l2norm_rows": [vp, i32, i32, f32, vp, vp],
+    "triad_l2norm_rows_f32": [vp, i32, i32, f32, vp, vp],
+    "triad_retrieval_maxmean_f32": [vp, vp, i32, i32, vp, vp, i32, i32, i32, f32, vp, vp],
     "triad_chgn_workspace_bytes": [i32, i32, i32],
     "triad_chgn_gelu_fwd": [vp, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, vp, vp],
     "triad_chgn_gelu_bwd": [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],

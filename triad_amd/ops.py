@@ -620,6 +620,16 @@ def l2_normalize(x: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
     return y
 
 
+def l2_normalize_f32(x: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
+    """F.normalize(x, dim=-1) in fp32 (the reference's fp32 retrieval embeddings, retrieval.py:93-94)."""
+    _check_device(x)
+    xc = x.to(torch.float32).contiguous()
+    y = torch.empty_like(xc)
+    rows = xc.numel() // xc.shape[-1]
+    call("triad_l2norm_rows_f32", ptr(xc), rows, xc.shape[-1], eps, ptr(y), stream_ptr(x.device))
+    return y
+
+
 # ----------------------------------------------------------------------------------------
 # Projection head: proj2(LN(proj1(h))) (model.py:32-34,68 / 81-83,116 / 253-255,326)
 # ----------------------------------------------------------------------------------------

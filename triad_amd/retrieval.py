@@ -15,9 +15,12 @@ Model-level entry points with the reference's names, arguments and return values
 `select_subset_indices`, `embed_av_subset`, `embed_tv_subset`, `compute_av_retrieval_metrics`,
 `compute_tv_retrieval_metrics` (retrieval.py:9-104, 146-188, 200-292). The dataset side (the
 reference's DataLoader over its video / CC3M datasets) is the caller's: any map-style dataset
-with the reference's item format works. Differences: the embedders run under the model's bf16
-autocast (the product path; the reference embeds in fp32), and the aggregation multiplies by
-1 / temperature in fp32 where the reference divides (rank-equivalent up to fp32 ties).
+with the reference's item format works. Precision: with `model.use_amp` (the default) the
+embedders run under the model's bf16 autocast and the pairs are scored on the bf16 MFMA kernel,
+multiplying by 1 / temperature in fp32 where the reference divides (the product path); with
+`model.use_amp = False` the drop-in matches the reference's arithmetic -- fp32 embeddings, fp32
+normalisation (triad_l2norm_rows_f32) and the fp32 scorer (triad_retrieval_maxmean_f32: the
+reference's division by the temperature, max, mean), so matrices agree to fp32 evaluation order.
 """
 from __future__ import annotations
 
@@ -45,10 +48,38 @@ def _pack(feats: Sequence[torch.Tensor], device, rows_multiple: int):
     return out, lens, n_max
 
 
+def _pack_f32(feats: Sequence[torch.Tensor], device):
+    """list of (n_i, D) -> zero-padded (N, n_pad, D) fp32 (n_pad a multiple of 64) + device lengths."""
+    n_pad = ops._rup(max(int(f.shape[0]) for f in feats), 64)
+    out = torch.zeros(len(feats), n_pad, D, dtype=torch.float32, device=device)
+    for i, f in enumerate(feats):
+        out[i, :f.shape[0]] = f.to(device, torch.float32)
+    lens = torch.tensor([int(f.shape[0]) for f in feats], dtype=torch.int32).to(device)
+    return out, lens, n_pad
+
+
+def aggregated_similarity_f32(queries: Sequence[torch.Tensor], items: Sequence[torch.Tensor], temperature: float,
+                              device="cuda") -> torch.Tensor:
+    """aggregated_similarity in the reference's fp32 arithmetic (retrieval.py:106-114: fp32 matmul,
+    division by the temperature, max, mean) -- all pairs in one triad_retrieval_maxmean_f32 launch."""
+    dev = torch.device(device)
+    Q, qlen, nq_pad = _pack_f32(queries, dev)
+    K, klen, nk_pad = _pack_f32(items, dev)
+    sim = torch.empty(len(queries), len(items), dtype=torch.float32, device=dev)
+    call("triad_retrieval_maxmean_f32", ptr(Q), ptr(qlen), len(queries), nq_pad, ptr(K), ptr(klen), len(items),
+         nk_pad, D, float(temperature), ptr(sim), stream_ptr(dev))
+    return sim
+
+
 def aggregated_similarity(queries: Sequence[torch.Tensor], items: Sequence[torch.Tensor], temperature: float,
-                          device="cuda") -> torch.Tensor:
+                          device="cuda", precision: str = "bf16") -> torch.Tensor:
     """(N_q x N_k) matrix of mean over each query's tokens of the max over each item's tokens of
-    <q, k> / temperature -- all pairs in one kernel launch."""
+    <q, k> / temperature -- all pairs in one kernel launch. precision "bf16": the product path
+    (bf16 operands on the MFMA pair kernel); "fp32": aggregated_similarity_f32."""
+    if precision == "fp32":
+        return aggregated_similarity_f32(queries, items, temperature, device)
+    if precision != "bf16":
+        raise ValueError(f"precision must be 'bf16' or 'fp32', not {precision!r}")
     dev = torch.device(device)
     Q, qlen, nq = _pack(queries, dev, 1)
     K, klen, nk = _pack(items, dev, 1)
@@ -99,21 +130,21 @@ def recall_at_k(sim: torch.Tensor, ks=(1, 5, 10, 20), ties: str = "reference") -
 
 
 def av_retrieval_metrics(audio_feats: List[torch.Tensor], video_feats: List[torch.Tensor], temperature: float,
-                         device="cuda") -> Dict[str, float]:
+                         device="cuda", precision: str = "bf16") -> Dict[str, float]:
     """compute_av_retrieval_metrics (retrieval.py:146-198) from embedded subsets
     (already L2-normalised as embed_av_subset does, retrieval.py:93-94)."""
-    a2v = aggregated_similarity(audio_feats, video_feats, temperature, device)
-    v2a = aggregated_similarity(video_feats, audio_feats, temperature, device)
+    a2v = aggregated_similarity(audio_feats, video_feats, temperature, device, precision)
+    v2a = aggregated_similarity(video_feats, audio_feats, temperature, device, precision)
     ra, rv = recall_at_k(a2v), recall_at_k(v2a)
     return {**{f"A->V_{k}": v for k, v in ra.items()}, **{f"V->A_{k}": v for k, v in rv.items()}}
 
 
 def tv_retrieval_metrics(text_feats: List[torch.Tensor], image_feats: List[torch.Tensor], temperature: float,
-                         device="cuda") -> Dict[str, float]:
+                         device="cuda", precision: str = "bf16") -> Dict[str, float]:
     """compute_tv_retrieval_metrics (retrieval.py:250-292) from embedded subsets (text trimmed
     to its attention mask, no normalisation)."""
-    t2v = aggregated_similarity(text_feats, image_feats, temperature, device)
-    v2t = aggregated_similarity(image_feats, text_feats, temperature, device)
+    t2v = aggregated_similarity(text_feats, image_feats, temperature, device, precision)
+    v2t = aggregated_similarity(image_feats, text_feats, temperature, device, precision)
     rt, rv = recall_at_k(t2v), recall_at_k(v2t)
     return {**{f"T->V_{k}": v for k, v in rt.items()}, **{f"V->T_{k}": v for k, v in rv.items()}}
 
@@ -167,8 +198,12 @@ def _collate_tv(batch):
 
 
 def _amp(model):
-    return torch.autocast("cuda", dtype=getattr(model, "amp_dtype", torch.bfloat16),
-                          enabled=bool(getattr(model, "use_amp", True)))
+    return torch.autocast("cuda", dtype=getattr(model, "amp_dtype", torch.bfloat16), enabled=_uses_amp(model))
+
+
+def _uses_amp(model) -> bool:
+    """bf16 product path unless the model was built with use_amp=False (then the reference's fp32)."""
+    return bool(getattr(model, "use_amp", True))
 
 
 def embed_av_subset(model, dataset, subset_indices, device="cuda", batch_size=8, num_workers=4,
@@ -192,7 +227,8 @@ def embed_av_subset(model, dataset, subset_indices, device="cuda", batch_size=8,
             with _amp(model):
                 vfeats = model.visual_embedder(frames)
                 afeats = model.audio_embedder(audio)
-            vfeats, afeats = ops.l2_normalize(vfeats), ops.l2_normalize(afeats)
+            norm = ops.l2_normalize if _uses_amp(model) else ops.l2_normalize_f32
+            vfeats, afeats = norm(vfeats), norm(afeats)
             for b in range(vfeats.shape[0]):
                 a_list[off + b] = afeats[b].to(out_device)
                 v_list[off + b] = vfeats[b].to(out_device)
@@ -231,7 +267,7 @@ def compute_av_retrieval_metrics(model, dataset, subset_file, device="cuda", sub
     indices = select_subset_indices(dataset, subset_file, subset_size=subset_size)
     a, v, _ = embed_av_subset(model, dataset, indices, device=device, batch_size=batch_size,
                               num_workers=num_workers, out_device=device)
-    return av_retrieval_metrics(a, v, model.temperature.item(), device)
+    return av_retrieval_metrics(a, v, model.temperature.item(), device, "bf16" if _uses_amp(model) else "fp32")
 
 
 def compute_tv_retrieval_metrics(model, dataset, subset_file, device="cuda", subset_size=1000, batch_size=8,
@@ -240,4 +276,4 @@ def compute_tv_retrieval_metrics(model, dataset, subset_file, device="cuda", sub
     indices = select_subset_indices(dataset, subset_file, subset_size=subset_size)
     t, im = embed_tv_subset(model, dataset, indices, device=device, batch_size=batch_size,
                             num_workers=num_workers, out_device=device)
-    return tv_retrieval_metrics(t, im, model.temperature.item(), device)
+    return tv_retrieval_metrics(t, im, model.temperature.item(), device, "bf16" if _uses_amp(model) else "fp32")
