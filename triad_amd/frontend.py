@@ -164,7 +164,7 @@ def _gemm_rows(a, a_row, lda, M, K, b, out, out_row, ldc):
     if M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and lda % 8 == 0 and ldc % 8 == 0:
         # the eight-wave 256 x 256 tile for every tall product, K = 512 included (the size policy's
         # 256 x 128 ring ran the 512-deep input gradients at 605-690 TFLOP/s, this form 745-815;
-        # bit-identical, tools/conv_gemm_ab.py, profiles/r04_conv_gemm_ab.log)
+        # bit-identical, profiles/r04_conv_gemm_ab.log; A/B tool in git history)
         form = 4 if M >= 32768 and M % 256 == 0 and N % 256 == 0 else 0
         call("triad_gemm_bf16_form", _addr(a, a_row, lda), lda, 1, ptr(b), K, 1, M, N, K, None,
              _addr(out, out_row, ldc), ldc, 1, form, stream_ptr(a.device), meta=dict(backbone=True))
@@ -178,7 +178,7 @@ def _conv_dw_plan(M, O, N):
     eight-wave 256 x 256 tile with one round of <= 256 workgroups (21 splits at N = 1536, 32 with
     each split on one XCD at N = 1024), >= 2,048 rows per split. 965 against 720 TFLOP/s for the
     former 8 splits of 256 x 128 tiles (192 workgroups) at 1.6 M rows x 1,536 -- 3.6 -> 2.65 ms per
-    call, ~1.9 ms per c3 step over the conv stack (tools/conv_dw_ab.py, profiles/r04_conv_dw_ab.log)."""
+    call, ~1.9 ms per c3 step over the conv stack (profiles/r04_conv_dw_ab.log; A/B tool in git history)."""
     if O % 256 or N % 256:
         return 0, 8
     sp = max(1, min(256 // ((O // 256) * (N // 256)), M // 2048))
