@@ -1,7 +1,8 @@
 """1000-way retrieval timed on the device: av_retrieval_metrics and
 tv_retrieval_metrics (both directions, N x N aggregated similarities in one pairsim launch each,
 ranks and R@1/5/10/20) at N = 1000 items with the c3 token counts (199 audio tokens, 256 visual
-tokens, ragged 8-32 caption tokens), features L2-normalised bf16. Beside it the CPU restatement
+tokens, ragged 8-32 caption tokens), features L2-normalised bf16; then the fp32 mode on the same
+values (one timed run per direction pair). Beside it the CPU restatement
 of retrieval.py's per-pair aggregation (its double loop over pairs, fp32 torch on the host's
 threads; written out here, not imported) timed on a small N and scaled by N^2 (labelled
 EXTRAPOLATED).
@@ -43,6 +44,14 @@ def main():
             ts.append(time.perf_counter() - t0)
         out[f"{name}_s"] = round(min(ts), 4)
         out[f"{name}_r1"] = round(list(m.values())[0], 4)
+        # the reference-precision mode (model.use_amp=False): the same lists in fp32, fp32 scorer
+        q32, k32 = [x.float() for x in q], [x.float() for x in k]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        m32 = fn(q32, k32, 0.07, precision="fp32")
+        torch.cuda.synchronize()
+        out[f"{name}_fp32_s"] = round(time.perf_counter() - t0, 4)
+        out[f"{name}_fp32_r1"] = round(list(m32.values())[0], 4)
     # the reference's per-pair loops on the host (both directions), small N, scaled by N^2
     n_cpu = int(os.environ.get("TRIAD_RETRIEVAL_CPU_N", "24"))
     qa, kv = [a.float() for a in audio[:n_cpu]], [v.float() for v in video[:n_cpu]]
