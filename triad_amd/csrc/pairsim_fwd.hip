@@ -225,7 +225,8 @@ struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in 
 // The 16 x 16 x 32 body (eval form) meets at the ring barrier once per TWO key tiles: 4 slots,
 // pairs of tiles DMA'd together two tiles ahead (round 5, TRIAD_FWD_SYNC2 A/B, alternated x3 on
 // one box, profiles/r05_fwd_sync2_ab.log: eval AV 2.36 -> 2.30-2.32 ms, TV 0.408 -> 0.392-0.399;
-// the same pairing in the training body was 3 % slower, AV 3.00 -> 3.10, and is not used there).
+// the same pairing in the training body was 3 % slower, AV 3.00 -> 3.10, and the training form on
+// this paired 16 x 16 x 32 body 4 % slower, AV 3.15 -> 3.27-3.30, profiles/r05_fwd_train16_ab.log).
 constexpr int NBUF16 = 4;
 template <bool TRAIN>
 constexpr int kbuf_elems = (TRAIN ? NBUF : NBUF16) * KT_ELEMS + 16 * WAVES;
