@@ -28,7 +28,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "tri-modal triples/sec (whole node) + loss parity, B=256 at 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
-TRACKED = ("triad_pairsim_fwd", "triad_pairsim_fwd_multi", "triad_pairsim_dS", "triad_gemm_bf16", "triad_gemm_bf16_bias_bf16", "triad_projhead_ln_fwd", "triad_rowgemm_bias", "triad_projhead_ln_bwd", "triad_wpack", "triad_wpack2",
+TRACKED = ("triad_pairsim_fwd", "triad_pairsim_fwd_multi", "triad_pairsim_diag", "triad_pairsim_dS", "triad_gemm_bf16", "triad_gemm_bf16_bias_bf16", "triad_projhead_ln_fwd", "triad_rowgemm_bias", "triad_projhead_ln_bwd", "triad_wpack", "triad_wpack2",
            "triad_projhead_fwd",
            "triad_gemm_bf16_splitk", "triad_gemm_bf16_splitk_form", "triad_tile_gemm", "triad_tile_gemm_packed16",
            "triad_tile_gemm_packed16_slabs",

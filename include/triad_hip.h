@@ -79,6 +79,12 @@ typedef struct triad_pairsim_problem {
  * no audio-text loss, model.py:635-636 is inference only). */
 int triad_pairsim_fwd_multi(const triad_pairsim_problem* problems, int n, hipStream_t stream);
 
+/* The diagonal-S part alone (diag_sim over every problem with diag != 0 and diagS != NULL; the
+ * regularisers' S blocks, model.py:417-418 / 524-525): triad_pairsim_fwd_multi over problems
+ * with diag = 0 followed by this equals triad_pairsim_fwd_multi over the problems as given, bit
+ * for bit -- the product path issues the two separately so the forward launch is timed alone. */
+int triad_pairsim_diag(const triad_pairsim_problem* problems, int n, hipStream_t stream);
+
 /* clip[i][j] = sum_q m_iq rowmax[j][i*Nq+q] / norm_i (AV: qmask NULL, norm = Nq;
  * TV: norm = max(sum_q m_iq, 1e-7)); qw[r] = d clip / d rowmax (may be NULL).
  * Replaces model.py:389-391 (mean over Na) / 509-512 (masked mean over Nt). */

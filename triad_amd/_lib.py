@@ -24,6 +24,7 @@ SIGNATURES = {
     "triad_pairsim_fwd": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, f32, i32, i32, vp, vp, vp, vp, vp,
                           i64, vp, vp, vp],
     "triad_pairsim_fwd_multi": [vp, i32, vp],
+    "triad_pairsim_diag": [vp, i32, vp],
     "triad_clip_reduce": [vp, i32, i32, i32, i32, vp, vp, vp, vp],
     "triad_diag_smooth": [vp, i32, i32, i32, i32, f64, vp, vp, vp, vp],
     "triad_diag_sparsity": [vp, i32, i32, i32, i32, f32, f64, vp, vp, vp, vp],

@@ -29,6 +29,7 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
                               const int* k_len, int xb, int ys, int jpw, hipStream_t stream);
 int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* xb, const int* ys, const int* jpw,
                                    int n, hipStream_t stream);
+int triad_pairsim_diag_launch(const triad_pairsim_problem* pr, int n, hipStream_t stream);
 
 namespace {
 
@@ -624,6 +625,17 @@ int triad_pairsim_fwd_multi(const triad_pairsim_problem* problems, int n, hipStr
     xb[i] = grid_for(p.R_pad, p.Bk, &jpw[i], &ys[i]);  // same decomposition as triad_pairsim_nparts
   }
   return triad_pairsim_fwd_multi_launch(problems, xb, ys, jpw, n, stream);
+}
+
+int triad_pairsim_diag(const triad_pairsim_problem* problems, int n, hipStream_t stream) {
+  if (!problems || n < 1 || n > 2) return TRIAD_EINVAL;
+  for (int i = 0; i < n; ++i) {
+    const triad_pairsim_problem& p = problems[i];
+    if (int e = check_shape(p.R, p.R_pad, p.Nq, p.Bk, p.Nk_pad, p.Nk_eff, D)) return e;
+    if (p.diag && p.diagS && (!p.Q || !p.K || !p.temp || p.diag_off < 0 || p.diag_off + p.Bq > p.Bk))
+      return TRIAD_EINVAL;
+  }
+  return triad_pairsim_diag_launch(problems, n, stream);
 }
 
 int triad_clip_reduce(const float* rowmax, int R_pad, int Nq, int Bq, int Bk, const float* qmask,

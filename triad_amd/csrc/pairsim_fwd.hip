@@ -783,6 +783,8 @@ __global__ __launch_bounds__(256) void diag_sim_kernel(const bf16* __restrict__ 
 
 }  // namespace
 
+int triad_pairsim_diag_launch(const triad_pairsim_problem* pr, int n, hipStream_t stream);
+
 // Grid: triad_pairsim_nparts' decomposition (pairsim.hip grid_for), so partial arrays match.
 // The diagonal S (diagS != null) comes from diag_sim_kernel, launched after on the same stream.
 int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad,
@@ -840,6 +842,11 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
   if (train) hipLaunchKernelGGL((pairsim_fwd_multi_kernel<true>), grid, block, 0, stream, m);
   else hipLaunchKernelGGL((pairsim_fwd_multi_kernel<false>), grid, block, 0, stream, m);
   TRIAD_CHECK_LAUNCH();
+  return triad_pairsim_diag_launch(pr, n, stream);
+}
+
+// diag_sim of every problem with a diagonal output (shapes validated by the caller)
+int triad_pairsim_diag_launch(const triad_pairsim_problem* pr, int n, hipStream_t stream) {
   for (int i = 0; i < n; ++i) {
     const triad_pairsim_problem& p = pr[i];
     if (p.diagS && p.diag) {
