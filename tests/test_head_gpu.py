@@ -288,9 +288,10 @@ def test_av_head_below_clamp_window():
 
 def _untile_dS(dS, R_pad, CT):
     """Tiled dS ([R_pad/32][CT][1024], lane L = query L&31 / half L>>5, value v = key
-    (v&3) + 8(v>>2) + 4(L>>5), the 32x32x16 accumulator order) -> dense [R_pad][CT*32] fp32."""
-    t = dS.float().view(R_pad // 32, CT, 2, 32, 4, 4)  # rt, ct, hh, q, v>>2, v&3
-    t = t.permute(0, 3, 1, 4, 2, 5)                     # rt, q, ct, v>>2, hh, v&3 -> key 8(v>>2)+4hh+(v&3)
+    (v&3) + 8(v>>2) + 4(L>>5), the 32x32x16 accumulator order; lane L's 16-byte chunks v>>3 = s
+    stored at chunk 64 s + L, common.h ds_chunk) -> dense [R_pad][CT*32] fp32."""
+    t = dS.float().view(R_pad // 32, CT, 2, 2, 32, 2, 4)  # rt, ct, s, hh, q, w2, w1 (v = 8s + 4w2 + w1)
+    t = t.permute(0, 4, 1, 2, 5, 3, 6)                     # rt, q, ct, s, w2, hh, w1 -> key 16s+8w2+4hh+w1
     return t.reshape(R_pad, CT * 32)
 
 

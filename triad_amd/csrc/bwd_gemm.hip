@@ -6,8 +6,9 @@
 // dS layout (written by pairsim_kernel straight from its MFMA accumulators): 32 x 32
 // tiles of 2 KB, tile (rt, ct) at ((rt * CT) + ct) * 1024 elements; inside a tile lane L
 // (query q = L & 31, hh = L >> 5) holds 16 bf16 at L*16 + v for keys
-// (v & 3) + 8 (v >> 2) + 4 hh -- the v_mfma_f32_32x32x16 accumulator order, stored as
-// one coalesced 2 KB write per wave.
+// (v & 3) + 8 (v >> 2) + 4 hh -- the v_mfma_f32_32x32x16 accumulator order, its 16-byte chunks
+// stored in ds_chunk order (common.h: two 1 KB runs, one per store instruction of the writing
+// wave). The loaders below place chunk c of that canonical order at LDS chunk c (swizzled).
 //
 // dQ reads a tile row-wise: lane L's 8 values v = 8s'..8s'+7 ARE the A fragment of
 // k-step s' (keys in the permuted order 16s' + 8(j>>2) + 4hh + (j&3)), so the B operand
@@ -68,7 +69,7 @@ __device__ __forceinline__ void ring_piece(const bf16* __restrict__ Dt, long lon
     const int pos = half * 64 + lane;
     const int c = DK ? swz_k(pos) : swz_q(pos);
     const long long tile = DK ? ((long long)kt * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + kt);
-    glds16(Dt + tile * 1024 + c * 8, dst + t * 1024 + half * 512);
+    glds16(Dt + tile * 1024 + ds_chunk(c) * 8, dst + t * 1024 + half * 512);
   } else {
     const int k = wave * 4 + piece - 1;
     const int c = lane ^ ((k & 3) << 2);
@@ -281,7 +282,7 @@ __device__ __forceinline__ void db_stage(const bf16* __restrict__ Dt, long long 
   const int pos = half * 64 + lane;
   const int c = DK ? swz_k16(pos) : swz_q(pos);
   const long long tile = DK ? ((long long)ktk * CT + (mt0 + t)) : ((long long)(mt0 + t) * CT + ktk);
-  glds16_ds(Dt + tile * 1024 + c * 8, adst + t * 1024 + half * 512);
+  glds16_ds(Dt + tile * 1024 + ds_chunk(c) * 8, adst + t * 1024 + half * 512);
 }
 
 template <int U, int N, class F>

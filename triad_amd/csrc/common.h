@@ -58,6 +58,14 @@ __device__ __forceinline__ void lds_dma_check(unsigned lds_byte_addr, int site) 
 #define TRIAD_VMCNT(n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory")
 #endif
 
+// Storage order of the 16-byte chunks of a 2 KB tile of the tiled dS (pairsim_fwd.hip, bwd_gemm.hip):
+// canonical chunk c -- lane L's values 8s..8s+7 (s = 0, 1) of the v_mfma_f32_32x32x16 accumulator
+// order are chunk 2L + s -- is stored at (c >> 1) + 64 (c & 1), so each of the forward's two 16-byte
+// stores per lane writes 1 KB contiguous (16 whole 64-byte lines) instead of 16 bytes of every 32.
+// Round 5: training forward AV 3.03 -> 2.92 ms, TV 0.535 -> 0.516 (profiles/r05_fwd_ds_contig_ab.log).
+// Readers map the canonical chunk through it (the LDS images they build are unchanged).
+__device__ __forceinline__ int ds_chunk(int c) { return (c >> 1) | ((c & 1) << 6); }
+
 // One 16-byte global->LDS DMA per lane (global_load_lds_dwordx4). The LDS
 // destination is the wave-uniform `lds_base` + lane*16; the global source is
 // per lane (CDNA4 LDS-DMA semantics).

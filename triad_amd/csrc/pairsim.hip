@@ -62,15 +62,15 @@ struct PairArgs {
   const int* klen;     // optional per-key-sample valid length (forward only; retrieval)
 };
 
-// Store this wave's 32x32 tile of dS (lane-contiguous accumulator order, 2 KB coalesced).
+// Store this wave's 32x32 tile of dS (accumulator order, chunks in ds_chunk order: two 1 KB runs).
 __device__ __forceinline__ void store_tile(bf16* dS, long long CT, int rt, long long ct, int lane,
                                            const bf16 (&v)[16]) {
-  bf16* dst = dS + ((long long)rt * CT + ct) * 1024 + lane * 16;
+  bf16* dst = dS + ((long long)rt * CT + ct) * 1024 + lane * 8;  // chunks 2 lane, 2 lane + 1 (ds_chunk)
   bf16x8 a, b;
 #pragma unroll
   for (int k = 0; k < 8; ++k) { a[k] = v[k]; b[k] = v[8 + k]; }
   *(bf16x8*)dst = a;
-  *(bf16x8*)(dst + 8) = b;
+  *(bf16x8*)(dst + 512) = b;
 }
 
 // Stage key tile (j, kb) into LDS buffer `dst`. Row t of the tile is one
@@ -337,7 +337,7 @@ __device__ __forceinline__ long long tile_elem(long long CT, int r, long long c)
   const int kl = (int)(c & 31);
   const int lane = (r & 31) + 32 * ((kl >> 2) & 1);
   const int v = (kl & 3) + 4 * (kl >> 3);
-  return ((long long)(r >> 5) * CT + (c >> 5)) * 1024 + lane * 16 + v;
+  return ((long long)(r >> 5) * CT + (c >> 5)) * 1024 + ds_chunk(2 * lane + (v >> 3)) * 8 + (v & 7);
 }
 
 // Four elements per thread per pass with all their loads issued together, 32-bit index math:

@@ -27,7 +27,10 @@ constexpr int NS = D / 16;  // 32 k-steps
 constexpr int WAVES = 8;
 constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 query rows per workgroup
 constexpr int KT_ELEMS = 32 * D;
-constexpr int NBUF = 3;                  // key-tile LDS ring slots (training body)
+#ifndef TRIAD_FWD_NBUF
+#define TRIAD_FWD_NBUF 3
+#endif
+constexpr int NBUF = TRIAD_FWD_NBUF;     // key-tile LDS ring slots (training body)
 constexpr int LDSPF = 2;                 // key fragments read from LDS ahead of their MFMA
 constexpr int REGION = 2;                // k-steps per scheduling region (sched_barrier spacing)
 constexpr int GLDS_PER_TILE = 32 / WAVES;  // 1-KB LDS-DMA pieces per wave per key tile (4)
@@ -181,9 +184,15 @@ __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 s
     e.nn2.y = fma_sq(cc.y, e.nn2.y);
     PIN(e.nn2);
     if constexpr (TRAIN) {
+#ifndef TRIAD_PROBE_NOMIN3
       e.mn = min3f(e.mn, p[v - 1], u);
+#endif
+#ifdef TRIAD_PROBE_NOMUL
+      e.pk[v >> 1] = pack_bf16x2(cc.x, cc.y);
+#else
       const f32x2 d = {mulf(cc.x, su2.x), mulf(cc.y, su2.y)};
       e.pk[v >> 1] = pack_bf16x2(d.x, d.y);
+#endif
       PIN(e.mn);
       PIN(e.pk[v >> 1]);
     }
@@ -273,8 +282,8 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
   };
   // prologue: NBUF - 1 tiles in flight
-  prefetch(0);
-  prefetch(1);
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i) prefetch(i);
 
   bf16x8 qf[NS];
   {
@@ -317,12 +326,21 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     // VMEM ops younger than tile b's DMA, at least: tile b+1's 4 pieces (if any) and, in
     // training, one epilogue's 2 dS stores (b >= 2); vmcnt counts both, in issue order
     // (3-slot ring; a 2-slot ring has no younger tile in flight)
-    const bool more = b + 1 < nblocks;
-    const bool st = TRAIN && b >= 2;
-    if (more && st) TRIAD_VMCNT(GLDS_PER_TILE + 2);
-    else if (more) TRIAD_VMCNT(GLDS_PER_TILE);
-    else if (st) TRIAD_VMCNT(2);
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (general ring: the DMAs of tiles b+1 .. b+NBUF-2 below nblocks and the stores of the
+    // epilogues of tiles b-NBUF+1 .. b-2; the oldest younger epilogue's stores are waited for)
+    const int nd = min(NBUF - 2, nblocks - 1 - b);
+    const int ns = TRAIN ? max(0, min(NBUF - 2, b - 1)) : 0;
+    switch (nd * 2 + ns * 16) {
+      case 2: TRIAD_VMCNT(GLDS_PER_TILE); break;
+      case 4: TRIAD_VMCNT(2 * GLDS_PER_TILE); break;
+      case 16: TRIAD_VMCNT(2); break;
+      case 18: TRIAD_VMCNT(GLDS_PER_TILE + 2); break;
+      case 20: TRIAD_VMCNT(2 * GLDS_PER_TILE + 2); break;
+      case 32: TRIAD_VMCNT(4); break;
+      case 34: TRIAD_VMCNT(GLDS_PER_TILE + 4); break;
+      case 36: TRIAD_VMCNT(2 * GLDS_PER_TILE + 4); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -335,9 +353,10 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       // some u below the window in this wave's tile: redo d (wave-uniform branch)
       const float st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup(e, p, su, lo) : nn;
       accd2 += (double)st;
-      bf16* d = dS_w + ((long long)ec.j * nkb + ec.kb) * 1024 + lane * 16;
+      // canonical chunks 2 lane, 2 lane + 1 at ds_chunk(): two 1 KB contiguous stores per wave
+      bf16* d = dS_w + ((long long)ec.j * nkb + ec.kb) * 1024 + lane * 8;
       store16(d, (u32x4){e.pk[0], e.pk[1], e.pk[2], e.pk[3]});
-      store16(d + 8, (u32x4){e.pk[4], e.pk[5], e.pk[6], e.pk[7]});
+      store16(d + 512, (u32x4){e.pk[4], e.pk[5], e.pk[6], e.pk[7]});
     }
     if (ec.kb == nkb - 1) {  // end of a key sample: combine the half-waves' max / argmax
       float m = e.m;
@@ -563,7 +582,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
   bf16* const dS_w = TRAIN ? a.dS + (long long)rt * a.CT * 1024 : nullptr;
   // this lane's 16-byte dS run inside a 32 x 32 tile, per query half: row 16 qb + i + 32 (g & 1), half h5
   const int h5 = g >> 1;
-  const int dso[2] = {(i16 + 32 * (g & 1)) * 16 + 8 * h5, (16 + i16 + 32 * (g & 1)) * 16 + 8 * h5};
+  const int dso[2] = {ds_chunk((i16 + 32 * (g & 1)) * 2 + h5) * 8, ds_chunk((16 + i16 + 32 * (g & 1)) * 2 + h5) * 8};
 
   Epi16 e;
   e.m[0] = e.m[1] = -INFINITY;
