@@ -184,15 +184,9 @@ __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 s
     e.nn2.y = fma_sq(cc.y, e.nn2.y);
     PIN(e.nn2);
     if constexpr (TRAIN) {
-#ifndef TRIAD_PROBE_NOMIN3
       e.mn = min3f(e.mn, p[v - 1], u);
-#endif
-#ifdef TRIAD_PROBE_NOMUL
-      e.pk[v >> 1] = pack_bf16x2(cc.x, cc.y);
-#else
       const f32x2 d = {mulf(cc.x, su2.x), mulf(cc.y, su2.y)};
       e.pk[v >> 1] = pack_bf16x2(d.x, d.y);
-#endif
       PIN(e.mn);
       PIN(e.pk[v >> 1]);
     }
