@@ -55,7 +55,10 @@ int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, in
                       double* st_part, const int* k_len, hipStream_t stream);
 
 /* One head's forward for triad_pairsim_fwd_multi: the arguments of triad_pairsim_fwd (D = 512,
- * no k_len) as a plain C struct. */
+ * no k_len) as a plain C struct, plus k_count (may be NULL): per key sample the number of kept
+ * keys, every key of the sample at or after it being a zero vector -- patch dropout's zero padding
+ * (model.py:301-302). The training forward then skips a sample's last 32-key tile when it holds no
+ * kept key (S == 0 there exactly), with results bit-identical to NULL. */
 typedef struct triad_pairsim_problem {
   const void* Q;
   const void* K;
@@ -70,6 +73,7 @@ typedef struct triad_pairsim_problem {
   void* dS;
   long long CT;
   double* st_part;
+  const int* k_count;
 } triad_pairsim_problem;
 
 /* The forwards of n (1 or 2) heads as ONE kernel launch over their union of workgroups, each

@@ -435,6 +435,52 @@ def test_pair_launch_matches_two_heads(B, Na, Nt, Nv, budget):
     assert _scalar_close(float(tg1.grad), float(tr.grad), 1e-3, 1e-5), (float(tg1.grad), float(tr.grad))
 
 
+def test_pair_launch_skips_zero_key_tiles_bit_identical():
+    """Keys straight from patch_dropout carry their kept count per sample (ops.KEPT_ROWS_ATTR):
+    the training pair forward then skips every sample's last 32-key tile that holds only zero
+    padding (kept <= 192 of Nk_pad = 224 here) and applies its epilogue in closed form. Against the
+    same inputs with the attribute removed (every tile multiplied): losses, statistics, clip
+    matrices and every gradient bit-identical -- including a (query sample, key sample) pair whose
+    real similarities are all negative, so the row max is the zero of the first skipped key."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(4242)
+    B, N, Na, Nt = 8, 256, 40, 16
+    counts = [210, 150, 192, 193, 100, 205, 160, 180]   # skip: 150, 192, 100, 160, 180
+    A = _rand_feats(g, (B, Na, 512))
+    T = _rand_feats(g, (B, Nt, 512))
+    X = _rand_feats(g, (B, N, 512))
+    e = torch.randn(512, generator=g)
+    e = e / e.norm()
+    A[0] = (e * 2.0 + 0.01 * torch.randn(Na, 512, generator=g)).to(torch.bfloat16).float()
+    X[2] = (-e * 1.5 + 0.01 * torch.randn(N, 512, generator=g)).to(torch.bfloat16).float()
+    keep_av = torch.zeros(B, N, dtype=torch.bool)
+    keep_tv = torch.zeros(B, N, dtype=torch.bool)
+    for j, c in enumerate(counts):
+        keep_av[j, torch.randperm(N, generator=g)[:c]] = True
+        keep_tv[j, torch.randperm(N, generator=g)[:max(1, c - 7)]] = True
+    mask = (torch.arange(Nt)[None, :] < torch.randint(1, Nt + 1, (B, 1), generator=g)).long()
+    outs = []
+    for strip in (False, True):
+        a = A.to(dev, torch.bfloat16).requires_grad_(True)
+        t = T.to(dev, torch.bfloat16).requires_grad_(True)
+        x = X.to(dev, torch.bfloat16).requires_grad_(True)
+        tg = torch.tensor(1.3, device=dev, requires_grad=True)
+        va = ops.patch_dropout(x, keep_av)
+        vt = ops.patch_dropout(x, keep_tv)
+        assert va.shape[1] == 210 and hasattr(va, ops.KEPT_ROWS_ATTR)
+        if strip:
+            delattr(va, ops.KEPT_ROWS_ATTR)
+            delattr(vt, ops.KEPT_ROWS_ATTR)
+        (la, sa, ca), (lt, st, ct) = ops.contrastive_heads_av_tv(a, va, t, vt, tg, mask.to(dev), threshold=0.005,
+                                                                 sparsity_weight=0.3)
+        (la[0] + lt[0]).backward()
+        outs.append([torch.stack(la), torch.stack(lt), sa, st, ca, ct, a.grad, t.grad, x.grad, tg.grad])
+    # the crafted pair: every real similarity of (audio 0, visual 2) is negative -> clip = mean of 0
+    assert float(outs[0][4][0, 2]) == 0.0
+    for got, want in zip(*outs):
+        assert torch.equal(got, want)
+
+
 @pytest.mark.parametrize("bk", [0, 1])
 def test_gemm_wide_bf16_nontemporal(bk):
     """Eight-wave form with a wide bf16 output (2304 columns, B k-contiguous or not)

@@ -120,7 +120,7 @@ class PairsimProblem(C.Structure):
     _fields_ = [("Q", vp), ("K", vp), ("R", i32), ("R_pad", i32), ("Nq", i32), ("Bq", i32), ("Bk", i32),
                 ("Nk_pad", i32), ("Nk_eff", i32), ("temp", vp), ("clamp_lo", f32), ("diag", i32), ("diag_off", i32),
                 ("rowmax", vp), ("argmax", vp), ("nn_part", vp), ("diagS", vp), ("dS", vp), ("CT", i64),
-                ("st_part", vp)]
+                ("st_part", vp), ("k_count", vp)]
 
 
 _lock = threading.Lock()

@@ -48,6 +48,7 @@ struct FwdArgs {
   long long CT;
   double* part2;
   const int* klen;
+  const int* kcount;  // training: kept keys per key sample (the rest zero vectors), or null
 };
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -220,6 +221,16 @@ struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in 
     j = __builtin_amdgcn_readfirstlane(k1 == 0 ? j + 1 : j);
     kb = __builtin_amdgcn_readfirstlane(k1);
   }
+  // the same walk over samples of tiles(j) = nkb - skip bit (j - j0) tiles each
+  __device__ __forceinline__ void next(int nkb, unsigned long long skip, int j0) {
+    const int k1 = kb + 1 == tiles(nkb, skip, j0) ? 0 : kb + 1;
+    j = __builtin_amdgcn_readfirstlane(k1 == 0 ? j + 1 : j);
+    kb = __builtin_amdgcn_readfirstlane(k1);
+  }
+  __device__ __forceinline__ int tiles(int nkb, unsigned long long skip, int j0) const {
+    const int d = j - j0;
+    return nkb - (d < 64 ? (int)((skip >> d) & 1ull) : 0);
+  }
 };
 
 // SHORTQ tags the launches over short query lists (text captions, Nq <= 32) with their own
@@ -250,7 +261,18 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   const int j0 = by * a.j_per_wg;
   const int j1 = min(a.Bk, j0 + a.j_per_wg);
   const int nkb = a.Nk_pad / 32;
-  const int nblocks = (j1 - j0) * nkb;
+  // Zero key tiles (training, kcount given): a key sample whose kept keys all lie before its last
+  // 32-key tile (kcount[j] <= 32 (nkb - 1); patch dropout zero-pads the rest) has only zero
+  // vectors there, so S == 0 exactly on that tile: it is not multiplied -- its epilogue is applied
+  // in closed form at the sample's end (the max against 0 at the tile's first key, zero unit dS,
+  // nothing added to the sums), bit-identical to computing it. Bit j - j0 of `skip`, for the
+  // workgroup's first 64 samples (later ones are computed).
+  unsigned long long skip = 0;
+  if (TRAIN && a.kcount && nkb > 1 && j1 > j0) {
+    const int jj = j0 + lane;
+    skip = __builtin_amdgcn_ballot_w64(jj < j1 && a.kcount[jj] <= 32 * (nkb - 1));
+  }
+  const int nblocks = (j1 - j0) * nkb - (int)__builtin_popcountll(skip);
   if (nblocks <= 0) {
     if (threadIdx.x == 0) {
       a.part[by * gx + bx] = 0.0;
@@ -272,7 +294,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   int fslot = 0, cslot = 0;
   auto prefetch = [&](int b2) __attribute__((always_inline)) {
     if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j - j0, fc.kb, wave, lane);
-    fc.next(nkb);
+    fc.next(nkb, skip, j0);
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
   };
   // prologue: NBUF - 1 tiles in flight
@@ -352,7 +374,19 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       store16(d, (u32x4){e.pk[0], e.pk[1], e.pk[2], e.pk[3]});
       store16(d + 512, (u32x4){e.pk[4], e.pk[5], e.pk[6], e.pk[7]});
     }
-    if (ec.kb == nkb - 1) {  // end of a key sample: combine the half-waves' max / argmax
+    const int etiles = ec.tiles(nkb, skip, j0);
+    if (ec.kb == etiles - 1) {  // end of a key sample: combine the half-waves' max / argmax
+      if (etiles < nkb) {  // its zero last tile (see `skip`): u = 0 from key 32 (nkb - 1) on
+        if (0.f > e.m) {
+          e.m = 0.f;
+          e.am = 32 * (nkb - 1) - 4 * h;
+        }
+        if (TRAIN) {
+          bf16* z = dS_w + ((long long)ec.j * nkb + nkb - 1) * 1024 + lane * 8;
+          store16(z, (u32x4){0u, 0u, 0u, 0u});
+          store16(z + 512, (u32x4){0u, 0u, 0u, 0u});
+        }
+      }
       float m = e.m;
       int am = e.am + 4 * h;
       const float m2 = __shfl_xor(m, 32);
@@ -365,7 +399,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       e.m = -INFINITY;
       e.am = 0;
     }
-    ec.next(nkb);
+    ec.next(nkb, skip, j0);
   };
 
   // one tile iteration: chain of tile b into c (CH) with the epilogue of tile b-1 from p (EP,
@@ -848,6 +882,7 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
     a.Nk_eff = p.Nk_eff; a.j_per_wg = jpw[order[i]]; a.temp = p.temp; a.clamp_lo = p.clamp_lo;
     a.rowmax = p.rowmax; a.argmax = p.argmax; a.part = p.nn_part;
     a.dS = (bf16*)p.dS; a.CT = p.CT; a.part2 = p.st_part; a.klen = nullptr;
+    a.kcount = p.dS ? p.k_count : nullptr;
     m.gx[i] = xb[order[i]] * (256 / ROWS_PER_WG);
     m.first[i + 1] = m.first[i] + m.gx[i] * ys[order[i]];
   }

@@ -324,6 +324,11 @@ def _head_begin(q, k, temperature, kind, q_mask, group, ds_budget, need_grad):
     h.dS = torch.empty((g.R_pad // 32) * h.CT * 1024, dtype=torch.bfloat16, device=dev) if write_ds else None
     h.st_part = torch.empty(h.nparts, dtype=torch.float64, device=dev) if write_ds else None
     h.q_dtype, h.k_dtype, h.t_dtype = q.dtype, k.dtype, temperature.dtype
+    # kept keys per sample when k comes straight from patch_dropout (zero rows after them): the
+    # training forward skips each sample's all-zero last key tile (triad_pairsim_problem.k_count)
+    kc = getattr(k, KEPT_ROWS_ATTR, None) if W == 1 and ZERO_TILE_SKIP else None
+    h.kcount = kc if (isinstance(kc, torch.Tensor) and kc.device == dev and kc.dtype == torch.int32
+                      and tuple(kc.shape) == (g.Bk,) and kc.is_contiguous()) else None
     return h
 
 
@@ -348,7 +353,7 @@ def _problem(h):
     g = h.g
     return _lib.PairsimProblem(ptr(h.Qb), ptr(h.Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, ptr(h.temp),
                                CLAMP_LO[h.kind], 1, h.rank * g.Bq, ptr(h.rowmax), ptr(h.argmax), ptr(h.nn_part),
-                               ptr(h.diagS), ptr(h.dS), h.CT, ptr(h.st_part))
+                               ptr(h.diagS), ptr(h.dS), h.CT, ptr(h.st_part), ptr(h.kcount))
 
 
 def _heads_launch(hs, st):
@@ -923,6 +928,14 @@ def dropout_indices(keep_mask: torch.Tensor, n_out: Optional[int] = None):
     return idx[:, :n_out], inv, n_out
 
 
+# attribute of patch_dropout's output: its kept-row count per sample (int32, on the device); rows
+# after it are zero, which the similarity forward exploits (_head_begin); a copy or view of the
+# tensor does not carry it
+KEPT_ROWS_ATTR = "_triad_kept_rows"
+# TRIAD_ZERO_TILE_SKIP=0: multiply the zero key tiles too (A/B; results are bit-identical)
+ZERO_TILE_SKIP = os.environ.get("TRIAD_ZERO_TILE_SKIP", "1") != "0"
+
+
 def patch_dropout(x: torch.Tensor, keep_mask: torch.Tensor, n_out: Optional[int] = None) -> torch.Tensor:
     """(B, N, D) -> (B, max_b kept_b, D): kept tokens in order, zero padded (model.py:282-307).
     n_out overrides the padded length (global negatives pad to the global maximum)."""
@@ -930,7 +943,10 @@ def patch_dropout(x: torch.Tensor, keep_mask: torch.Tensor, n_out: Optional[int]
     idx, inv, n_out = dropout_indices(keep_mask, n_out)
     idx_d = _lib.h2d(idx.contiguous(), x.device)
     inv_d = _lib.h2d(inv.contiguous(), x.device)
-    return _GatherRows.apply(x.contiguous(), idx_d, inv_d)
+    out = _GatherRows.apply(x.contiguous(), idx_d, inv_d)
+    kept = keep_mask.detach().to("cpu", torch.bool).sum(1).to(torch.int32).contiguous()
+    setattr(out, KEPT_ROWS_ATTR, _lib.h2d(kept, x.device))
+    return out
 
 
 # ----------------------------------------------------------------------------------------
