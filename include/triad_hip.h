@@ -55,10 +55,14 @@ int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, in
                       double* st_part, const int* k_len, hipStream_t stream);
 
 /* One head's forward for triad_pairsim_fwd_multi: the arguments of triad_pairsim_fwd (D = 512,
- * no k_len) as a plain C struct, plus k_count (may be NULL): per key sample the number of kept
- * keys, every key of the sample at or after it being a zero vector -- patch dropout's zero padding
- * (model.py:301-302). The training forward then skips a sample's last 32-key tile when it holds no
- * kept key (S == 0 there exactly), with results bit-identical to NULL. */
+ * no k_len) as a plain C struct, plus k_tiles (training only; NULL = every tile stored): compact
+ * key tiles. A key sample whose last 32-key tile holds only zero vectors (patch dropout's zero
+ * padding, model.py:301-302) may leave that tile out: K and the tiled dS then hold sample j's
+ * stored tiles at tile rows / columns k_tiles[j] .. k_tiles[j+1] - 1 (k_tiles: Bk + 1 entries, an
+ * exclusive prefix sum of nkb or nkb - 1 tiles per sample, nkb = Nk_pad / 32; a sample at index
+ * >= 64 within a forward workgroup's key split stores all nkb), CT >= k_tiles[Bk]. The left-out
+ * tile's S == 0 enters the row max in closed form. diagS (triad_pairsim_diag) needs the full
+ * padded K: give it the problems with the padded K and k_tiles NULL. */
 typedef struct triad_pairsim_problem {
   const void* Q;
   const void* K;
@@ -73,7 +77,7 @@ typedef struct triad_pairsim_problem {
   void* dS;
   long long CT;
   double* st_part;
-  const int* k_count;
+  const int* k_tiles;
 } triad_pairsim_problem;
 
 /* The forwards of n (1 or 2) heads as ONE kernel launch over their union of workgroups, each
@@ -131,6 +135,15 @@ int triad_dS_patch(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int
                    int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
                    float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
                    hipStream_t stream);
+
+/* triad_dS_patch over a dS holding only the stored key tiles (k_tiles = the stored-tile prefix sum
+ * the forward was given, triad_pairsim_problem.k_tiles; NULL = triad_dS_patch): a term landing in
+ * a sample's unstored all-zero last tile is dropped (it multiplies zero keys in dQ, and the keys'
+ * own gradient rows are padding); max_part still counts it. Same reference lines as above. */
+int triad_dS_patch_tiles(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad, int Nk_eff,
+                         int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
+                         float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
+                         const int* k_tiles, hipStream_t stream);
 
 /* dL/dtemp = sum_k w[k]*sum(p_k) + w[3]*d l_cal/d temp (has_cal: AV, model.py:420-424). */
 int triad_dtemp_finalize(const double* p0, int n0, const double* p1, int n1, const double* p2, int n2,

@@ -146,8 +146,8 @@ def test_pairsim_fwd_multi_rejects_bad_arguments():
     nul = prob()
     nul.rowmax = None
     assert f((_lib.PairsimProblem * 1)(nul), 1, None) == 1001
-    assert C.sizeof(_lib.PairsimProblem) == 136   # include/triad_hip.h layout, k_count last
-    assert _lib.PairsimProblem.k_count.offset == 128
+    assert C.sizeof(_lib.PairsimProblem) == 136   # include/triad_hip.h layout, k_tiles last
+    assert _lib.PairsimProblem.k_tiles.offset == 128
 
 
 def test_packed_tile_gemm_and_patch_reject_bad_arguments():

@@ -435,17 +435,20 @@ def test_pair_launch_matches_two_heads(B, Na, Nt, Nv, budget):
     assert _scalar_close(float(tg1.grad), float(tr.grad), 1e-3, 1e-5), (float(tg1.grad), float(tr.grad))
 
 
-def test_pair_launch_skips_zero_key_tiles_bit_identical():
+def test_pair_launch_compact_key_tiles():
     """Keys straight from patch_dropout carry their kept count per sample (ops.KEPT_ROWS_ATTR):
-    the training pair forward then skips every sample's last 32-key tile that holds only zero
-    padding (kept <= 192 of Nk_pad = 224 here) and applies its epilogue in closed form. Against the
-    same inputs with the attribute removed (every tile multiplied): losses, statistics, clip
-    matrices and every gradient bit-identical -- including a (query sample, key sample) pair whose
-    real similarities are all negative, so the row max is the zero of the first skipped key."""
+    the training pair forward then leaves every sample's all-zero last 32-key tile out of K and of
+    the tiled dS (kept <= 192 of Nk_pad = 224 here; ops._compact) and applies its S == 0 in closed
+    form; the dS patch, dQ and dK run over the stored tiles. Against the same inputs with the
+    attribute removed (every tile stored and multiplied): losses, statistics, clip matrices and the
+    temperature gradient bit-identical (the forward's sums and the patch partials see the same
+    values in the same order); the feature gradients within bf16 rounding (dQ / dK sum the same
+    nonzero products, split over the CUs differently). One (audio, visual) pair has only negative
+    real similarities, so its row maxima are the zero of the first left-out key."""
     ops = _ops()
     g = torch.Generator().manual_seed(4242)
     B, N, Na, Nt = 8, 256, 40, 16
-    counts = [210, 150, 192, 193, 100, 205, 160, 180]   # skip: 150, 192, 100, 160, 180
+    counts = [210, 150, 192, 193, 100, 205, 160, 180]   # left out: 150, 192, 100, 160, 180
     A = _rand_feats(g, (B, Na, 512))
     T = _rand_feats(g, (B, Nt, 512))
     X = _rand_feats(g, (B, N, 512))
@@ -459,26 +462,42 @@ def test_pair_launch_skips_zero_key_tiles_bit_identical():
         keep_av[j, torch.randperm(N, generator=g)[:c]] = True
         keep_tv[j, torch.randperm(N, generator=g)[:max(1, c - 7)]] = True
     mask = (torch.arange(Nt)[None, :] < torch.randint(1, Nt + 1, (B, 1), generator=g)).long()
+    compacted = []
+    orig = ops._compact
+
+    def spy(h):
+        orig(h)
+        compacted.append(h.Kc is not None)
+
     outs = []
-    for strip in (False, True):
-        a = A.to(dev, torch.bfloat16).requires_grad_(True)
-        t = T.to(dev, torch.bfloat16).requires_grad_(True)
-        x = X.to(dev, torch.bfloat16).requires_grad_(True)
-        tg = torch.tensor(1.3, device=dev, requires_grad=True)
-        va = ops.patch_dropout(x, keep_av)
-        vt = ops.patch_dropout(x, keep_tv)
-        assert va.shape[1] == 210 and hasattr(va, ops.KEPT_ROWS_ATTR)
-        if strip:
-            delattr(va, ops.KEPT_ROWS_ATTR)
-            delattr(vt, ops.KEPT_ROWS_ATTR)
-        (la, sa, ca), (lt, st, ct) = ops.contrastive_heads_av_tv(a, va, t, vt, tg, mask.to(dev), threshold=0.005,
-                                                                 sparsity_weight=0.3)
-        (la[0] + lt[0]).backward()
-        outs.append([torch.stack(la), torch.stack(lt), sa, st, ca, ct, a.grad, t.grad, x.grad, tg.grad])
+    try:
+        ops._compact = spy
+        for strip in (False, True):
+            a = A.to(dev, torch.bfloat16).requires_grad_(True)
+            t = T.to(dev, torch.bfloat16).requires_grad_(True)
+            x = X.to(dev, torch.bfloat16).requires_grad_(True)
+            tg = torch.tensor(1.3, device=dev, requires_grad=True)
+            va = ops.patch_dropout(x, keep_av)
+            vt = ops.patch_dropout(x, keep_tv)
+            assert va.shape[1] == 210 and hasattr(va, ops.KEPT_ROWS_ATTR)
+            if strip:
+                delattr(va, ops.KEPT_ROWS_ATTR)
+                delattr(vt, ops.KEPT_ROWS_ATTR)
+            (la, sa, ca), (lt, st, ct) = ops.contrastive_heads_av_tv(a, va, t, vt, tg, mask.to(dev),
+                                                                     threshold=0.005, sparsity_weight=0.3)
+            (la[0] + lt[0]).backward()
+            outs.append(([torch.stack(la), torch.stack(lt), sa, st, ca, ct, tg.grad], [a.grad, t.grad, x.grad]))
+    finally:
+        ops._compact = orig
+    assert compacted == [True, True, False, False]
     # the crafted pair: every real similarity of (audio 0, visual 2) is negative -> clip = mean of 0
-    assert float(outs[0][4][0, 2]) == 0.0
-    for got, want in zip(*outs):
+    assert float(outs[0][0][4][0, 2]) == 0.0
+    for got, want in zip(outs[0][0], outs[1][0]):
         assert torch.equal(got, want)
+    for got, want in zip(outs[0][1], outs[1][1]):
+        gf, wf = got.float(), want.float()
+        assert float((gf - wf).norm() / wf.norm()) < 2e-3
+        assert float((gf - wf).abs().max()) <= 2 ** -6 * float(wf.abs().max())
 
 
 @pytest.mark.parametrize("bk", [0, 1])

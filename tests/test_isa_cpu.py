@@ -155,3 +155,33 @@ def test_direct_b_loop_keeps_b_prefetch_in_flight(isa):
         assert waits and min(waits) >= 8, (sym, waits)
         priv, spills = _meta(asm, sym)
         assert (priv, spills) == (0, 0), (sym, priv, spills)
+
+
+def test_direct_b_tail_stages_drain_before_their_barrier(isa):
+    """Direct-B tile GEMMs (tile_gemm_db16_kernel): after the stage loop's back
+    branch, the trailing nst % NB stages issue no B loads (their prefetch feeds no later stage, so
+    hipcc removes it), so the loop's counted wait would under-count the VMEM ops in flight (round 5:
+    AV dK with a 2-stage tail was non-deterministic). Every barrier there must follow a vmcnt(0)."""
+    checked = 0
+    # (the row-panel kernels' epilogues have barriers of their own after the tail; only the
+    # direct-B tile GEMMs, whose epilogue has none, are checked mechanically here)
+    for f, pat in (("bwd_gemm.hip", "tile_gemm_db16_kernel"),):
+        for sym, lines in _kernels(isa[f]).items():
+            if pat not in sym or not any("Loop Header" in l for l in lines):
+                continue
+            hdr = next(i for i, l in enumerate(lines) if "Loop Header" in l)
+            label = lines[hdr].split(":")[0]
+            back = max(i for i, l in enumerate(lines)
+                       if re.match(r"s_(cbranch_\w+|branch)\s+" + re.escape(label) + r"$", l))
+            last_vm = None
+            tail_barriers = 0
+            for l in lines[back + 1:]:
+                m = re.match(r"s_waitcnt\s.*vmcnt\((\d+)\)", l)
+                if m:
+                    last_vm = int(m.group(1))
+                elif l.startswith("s_barrier"):
+                    tail_barriers += 1
+                    assert last_vm == 0, (f, sym, last_vm)
+            assert tail_barriers >= 1, (f, sym)
+            checked += 1
+    assert checked >= 4, checked

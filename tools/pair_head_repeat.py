@@ -31,7 +31,18 @@ def main():
     keep_tv = torch.rand(B, N, generator=g) < 0.75
     mask = torch.ones(B, Nt, dtype=torch.long, device=dev)
     first = None
+    heads = []
+    orig_compact = ops._compact
+
+    def spy(h):   # keep each head's compact dS to compare it across repeats
+        orig_compact(h)
+        heads.append(h)
+    ops._compact = spy
+
+    def valid_ds(h):   # the stored tiles' part of the tiled dS: [R_pad/32][nct] tiles of 1024
+        return h.dS.view(h.g.R_pad // 32, h.CT, 1024)[:, :h.nct].clone()
     for r in range(a.reps):
+        heads.clear()
         a_ = A.to(dev).requires_grad_(True)
         t_ = T.to(dev).requires_grad_(True)
         x = X.to(dev)
@@ -42,9 +53,14 @@ def main():
         tg = torch.tensor(1.5, device=dev, requires_grad=True)
         (la, _, _), (lt, _, _) = ops.contrastive_heads_av_tv(a_, va, t_, vt, tg, mask, threshold=0.8,
                                                              sparsity_weight=0.01)
+        torch.cuda.synchronize()
+        fwd_ds = [valid_ds(h) for h in heads]
         (la[0] + lt[0]).backward()
         torch.cuda.synchronize()
         cur = {"gA": a_.grad, "gT": t_.grad, "gVa": va.grad, "gVt": vt.grad}
+        if len(heads) == 2:
+            cur.update(dS_fwd_av=fwd_ds[0], dS_fwd_tv=fwd_ds[1], dS_bwd_av=valid_ds(heads[0]),
+                       dS_bwd_tv=valid_ds(heads[1]))
         if first is None:
             first = cur
             continue
@@ -53,6 +69,9 @@ def main():
             d = cur[k] != first[k]
             n = int(d.sum())
             rep[k] = n
+            if n and k.startswith("dS"):
+                rows = torch.nonzero((cur[k] != first[k]).any(-1))
+                rep[k + "_tiles(rt,ct)"] = rows[:8].tolist()
             if n and k.startswith("gV"):
                 rows = torch.nonzero(d.any(-1))
                 keys = rows[:, 1]

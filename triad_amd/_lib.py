@@ -32,6 +32,8 @@ SIGNATURES = {
     "triad_pairsim_dS": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, f32, i32, i32, vp, vp, vp, vp, vp,
                          vp, i64, vp, vp],
     "triad_dS_patch": [vp, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp, f32, vp, i32, vp],
+    "triad_dS_patch_tiles": [vp, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp, f32, vp, i32,
+                             vp, vp],
     "triad_dtemp_finalize": [vp, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp],
     "triad_tile_gemm": [vp, i64, i32, vp, i32, i32, vp, i32, vp, vp, vp],
     "triad_tile_gemm_slabs": [vp, i64, i32, vp, i32, i32, i32, vp, vp],
@@ -120,7 +122,7 @@ class PairsimProblem(C.Structure):
     _fields_ = [("Q", vp), ("K", vp), ("R", i32), ("R_pad", i32), ("Nq", i32), ("Bq", i32), ("Bk", i32),
                 ("Nk_pad", i32), ("Nk_eff", i32), ("temp", vp), ("clamp_lo", f32), ("diag", i32), ("diag_off", i32),
                 ("rowmax", vp), ("argmax", vp), ("nn_part", vp), ("diagS", vp), ("dS", vp), ("CT", i64),
-                ("st_part", vp), ("k_count", vp)]
+                ("st_part", vp), ("k_tiles", vp)]
 
 
 _lock = threading.Lock()

@@ -342,9 +342,15 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
   // stages, 5 ops each, stay in flight; hipcc waits for its B loads itself), barrier, 32 MFMAs with
   // the prefetch of stage st + DD (into slot (u + DD) % NB, read for the last time by stage st - 1,
   // before this barrier) issued after the first two row blocks
-  auto stage = [&](auto U, int st) __attribute__((always_inline)) {
+  // TAIL: one of the trailing nst % NB stages. Their own prefetches feed no later stage, so hipcc
+  // drops those B loads as dead: a tail stage has fewer than 5 (DD - 1) younger VMEM ops in flight
+  // and the counted wait would let it pass before its A piece landed (round 5: AV dK with 3 splits of
+  // 534 stages gave a different result in 3 of 7 repeats, tools/pair_head_repeat.py; 4 splits of 400
+  // -- no tail -- and 1 split were bit-stable). Tail stages drain vmcnt instead (<= 3 per launch).
+  auto stage = [&](auto U, int st, auto TAIL) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
-    TRIAD_VMCNT(5 * (DD - 1));
+    if constexpr (decltype(TAIL)::value) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else TRIAD_VMCNT(5 * (DD - 1));
     __syncthreads();
     const bf16* As = lds + u * 4096;
     bf16x8 af[8];
@@ -379,10 +385,12 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
     });
     const int ngroups = nst / NB;
     for (int g = 0; g < ngroups; ++g)
-      static_for<0, NB>([&](auto U) __attribute__((always_inline)) { stage(U, g * NB + decltype(U)::value); });
+      static_for<0, NB>([&](auto U) __attribute__((always_inline)) {
+        stage(U, g * NB + decltype(U)::value, std::false_type{});
+      });
     const int rem = nst - ngroups * NB, base = ngroups * NB;
     static_for<0, NB - 1>([&](auto U) __attribute__((always_inline)) {
-      if (decltype(U)::value < rem) stage(U, base + decltype(U)::value);
+      if (decltype(U)::value < rem) stage(U, base + decltype(U)::value, std::true_type{});
     });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the past-the-end stages' LDS-DMA lands before exit
   }

@@ -333,6 +333,15 @@ __global__ __launch_bounds__(256) void diag_sparsity_kernel(const float* __restr
 // forward: dS[r][j*Nk_pad + argmax[j][r]] += ratio * dclip[i][j] * qw[r]  (the backward of
 // max over keys, model.py:389/507, feeding mean/masked-mean and the CE).
 // part[block] = sum dclip * qw * rowmax (-> d/dtemp of this term).
+// Column of key `key` of key sample j in the tiled dS: j Nk_pad + key, or with compact key tiles
+// (kt = the stored-tile prefix sum, triad_pairsim_problem.k_tiles) 32 kt[j] + key, -1 when the key
+// lies in the sample's unstored all-zero last tile.
+__device__ __forceinline__ long long ds_col(const int* __restrict__ kt, int Nk_pad, int j, int key) {
+  if (!kt) return (long long)j * Nk_pad + key;
+  const int t0 = kt[j];
+  return key < 32 * (kt[j + 1] - t0) ? (long long)t0 * 32 + key : -1;
+}
+
 __device__ __forceinline__ long long tile_elem(long long CT, int r, long long c) {
   const int kl = (int)(c & 31);
   const int lane = (r & 31) + 32 * ((kl >> 2) & 1);
@@ -349,7 +358,7 @@ __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS
                                                            const float* __restrict__ rowmax,
                                                            const float* __restrict__ dclip,
                                                            const float* __restrict__ qw, float ratio,
-                                                           double* __restrict__ part) {
+                                                           double* __restrict__ part, const int* __restrict__ kt) {
   __shared__ double red[4];
   double acc = 0.0;
   const int total = Bk * R;   // < 2^31 (host check)
@@ -365,14 +374,15 @@ __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS
       w[u] = dclip[(size_t)i * Bk + j] * qw[r];
       rm[u] = rowmax[(size_t)j * R_pad + r];
       const int key = argmax[(size_t)j * R_pad + r];
-      p[u] = dS + tile_elem(CT, r, (long long)j * Nk_pad + key);
+      const long long c = ds_col(kt, Nk_pad, j, key);
+      p[u] = c < 0 ? nullptr : dS + tile_elem(CT, r, c);   // unstored zero tile: K there is zero
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) old[u] = (float)*p[u];
+    for (int u = 0; u < 4; ++u) old[u] = p[u] ? (float)*p[u] : 0.f;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (e0 + u * stride >= total) break;
-      *p[u] = (bf16)(old[u] + ratio * w[u]);
+      if (p[u]) *p[u] = (bf16)(old[u] + ratio * w[u]);
       acc += (double)w[u] * (double)rm[u];
     }
   }
@@ -384,7 +394,8 @@ __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS
 // per thread per pass, as above).
 __global__ __launch_bounds__(256) void dS_patch_diag_kernel(bf16* __restrict__ dS, long long CT, int Bq, int Nq,
                                                             int Nk_pad, int Nk_eff, int diag_off,
-                                                            const float* __restrict__ g, float ratio) {
+                                                            const float* __restrict__ g, float ratio,
+                                                            const int* __restrict__ kt) {
   const int total = Bq * Nq * Nk_eff;   // < 2^31 (host check)
   const int stride = gridDim.x * blockDim.x;
   for (int e0 = blockIdx.x * blockDim.x + threadIdx.x; e0 < total; e0 += 4 * stride) {
@@ -396,14 +407,15 @@ __global__ __launch_bounds__(256) void dS_patch_diag_kernel(bf16* __restrict__ d
       const int k = e % Nk_eff, iq = e / Nk_eff;
       const int i = iq / Nq;
       gv[u] = g[(size_t)iq * Nk_pad + k];
-      p[u] = dS + tile_elem(CT, iq, (long long)(i + diag_off) * Nk_pad + k);
+      const long long c = ds_col(kt, Nk_pad, i + diag_off, k);
+      p[u] = c < 0 ? nullptr : dS + tile_elem(CT, iq, c);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) old[u] = (float)*p[u];
+    for (int u = 0; u < 4; ++u) old[u] = p[u] ? (float)*p[u] : 0.f;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (e0 + u * stride >= total) break;
-      *p[u] = (bf16)(old[u] + ratio * gv[u]);
+      if (p[u]) *p[u] = (bf16)(old[u] + ratio * gv[u]);
     }
   }
 }
@@ -620,7 +632,8 @@ int triad_pairsim_fwd_multi(const triad_pairsim_problem* problems, int n, hipStr
   for (int i = 0; i < n; ++i) {
     const triad_pairsim_problem& p = problems[i];
     if (int e = check_shape(p.R, p.R_pad, p.Nq, p.Bk, p.Nk_pad, p.Nk_eff, D)) return e;
-    if (p.dS && (p.CT < (long long)p.Bk * (p.Nk_pad / 32) || !p.st_part)) return TRIAD_EINVAL;
+    // (compact key tiles: CT >= k_tiles[Bk] is the caller's, the prefix sum lives on the device)
+    if (p.dS && (p.CT < (p.k_tiles ? 1LL : (long long)p.Bk * (p.Nk_pad / 32)) || !p.st_part)) return TRIAD_EINVAL;
     if (!p.Q || !p.K || !p.temp || !p.rowmax || !p.argmax || !p.nn_part) return TRIAD_EINVAL;
     xb[i] = grid_for(p.R_pad, p.Bk, &jpw[i], &ys[i]);  // same decomposition as triad_pairsim_nparts
   }
@@ -696,23 +709,32 @@ int triad_pairsim_dS(const void* Q, const void* K, int R, int R_pad, int Nq, int
   return TRIAD_OK;
 }
 
-int triad_dS_patch(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad, int Nk_eff,
-                   int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
-                   float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
-                   hipStream_t stream) {
-  if (R <= 0 || Bk <= 0 || n_max_part <= 0 || CT < (long long)Bk * (Nk_pad / 32)) return TRIAD_EINVAL;
+int triad_dS_patch_tiles(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad, int Nk_eff,
+                         int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
+                         float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
+                         const int* k_tiles, hipStream_t stream) {
+  if (R <= 0 || Bk <= 0 || n_max_part <= 0 || Nk_pad % 32 || CT <= 0) return TRIAD_EINVAL;
+  if (!k_tiles && CT < (long long)Bk * (Nk_pad / 32)) return TRIAD_EINVAL;
   if ((long long)Bk * R >= (1LL << 31) || (long long)Bq * Nq * Nk_eff >= (1LL << 31)) return TRIAD_EINVAL;
   hipLaunchKernelGGL(dS_patch_max_kernel, dim3(n_max_part), dim3(256), 0, stream, (bf16*)dS, CT, R, R_pad, Nq, Bk,
-                     Nk_pad, argmax, rowmax, dclip, qw, ratio_max, max_part);
+                     Nk_pad, argmax, rowmax, dclip, qw, ratio_max, max_part, k_tiles);
   if (gdiag) {
     const long long total = (long long)Bq * Nq * Nk_eff;
     long long blocks = (total + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(dS_patch_diag_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (bf16*)dS, CT, Bq, Nq,
-                       Nk_pad, Nk_eff, diag_off, gdiag, ratio_diag);
+                       Nk_pad, Nk_eff, diag_off, gdiag, ratio_diag, k_tiles);
   }
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
+}
+
+int triad_dS_patch(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad, int Nk_eff,
+                   int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
+                   float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
+                   hipStream_t stream) {
+  return triad_dS_patch_tiles(dS, CT, R, R_pad, Nq, Bq, Bk, Nk_pad, Nk_eff, diag_off, argmax, rowmax, dclip, qw,
+                              ratio_max, gdiag, ratio_diag, max_part, n_max_part, nullptr, stream);
 }
 
 int triad_dtemp_finalize(const double* p0, int n0, const double* p1, int n1, const double* p2, int n2,

@@ -48,7 +48,7 @@ struct FwdArgs {
   long long CT;
   double* part2;
   const int* klen;
-  const int* kcount;  // training: kept keys per key sample (the rest zero vectors), or null
+  const int* ktiles;  // training: stored key tiles per sample as an exclusive prefix sum (compact K / dS), or null
 };
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -75,9 +75,8 @@ __device__ __forceinline__ void dma16(i32x4 rsrc, unsigned lds_addr, unsigned vo
 // One key tile (32 rows x 1 KB) into an LDS slot: 1-KB pieces, the row offset in soffset
 // (uniform), the source-side swizzle chunk ^ (row & 15) in voffset. Piece u of this wave's
 // GLDS_PER_TILE.
-__device__ __forceinline__ void stage_piece(i32x4 kr, const FwdArgs& a, bf16* dst, int j, int kb, int wave,
-                                            int lane, int u) {
-  const unsigned row0 = (unsigned)(j * a.Nk_pad + kb * 32 + wave * GLDS_PER_TILE);
+__device__ __forceinline__ void stage_piece(i32x4 kr, bf16* dst, int trow, int wave, int lane, int u) {
+  const unsigned row0 = (unsigned)(trow + wave * GLDS_PER_TILE);
   const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) bf16*)dst;
   asm volatile("" : "+v"(lane));  // recompute the lane offsets here, do not keep them live
   const int t = wave * GLDS_PER_TILE + u;
@@ -85,10 +84,10 @@ __device__ __forceinline__ void stage_piece(i32x4 kr, const FwdArgs& a, bf16* ds
         __builtin_amdgcn_readfirstlane((row0 + u) * (D * 2)));
 }
 
-__device__ __forceinline__ void stage_tile(i32x4 kr, const FwdArgs& a, bf16* dst, int j, int kb, int wave,
-                                           int lane) {
+// trow: the tile's first key row, relative to the buffer descriptor's base
+__device__ __forceinline__ void stage_tile(i32x4 kr, bf16* dst, int trow, int wave, int lane) {
 #pragma unroll
-  for (int u = 0; u < GLDS_PER_TILE; ++u) stage_piece(kr, a, dst, j, kb, wave, lane, u);
+  for (int u = 0; u < GLDS_PER_TILE; ++u) stage_piece(kr, dst, trow, wave, lane, u);
 }
 
 // 16-byte store hidden from hipcc's waitcnt bookkeeping (it would otherwise drain vmcnt(0) --
@@ -216,6 +215,7 @@ __device__ __forceinline__ float epi_fixup(Epi& e, const f32x16& p, float su, fl
 
 struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in the walk
   int j, kb;
+  int t = 0;  // tiles walked so far (fwd_body: the tile's index among the workgroup's stored tiles)
   __device__ __forceinline__ void next(int nkb) {  // readfirstlane: provably uniform (SGPRs)
     const int k1 = kb + 1 == nkb ? 0 : kb + 1;
     j = __builtin_amdgcn_readfirstlane(k1 == 0 ? j + 1 : j);
@@ -226,6 +226,7 @@ struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in 
     const int k1 = kb + 1 == tiles(nkb, skip, j0) ? 0 : kb + 1;
     j = __builtin_amdgcn_readfirstlane(k1 == 0 ? j + 1 : j);
     kb = __builtin_amdgcn_readfirstlane(k1);
+    t = __builtin_amdgcn_readfirstlane(t + 1);
   }
   __device__ __forceinline__ int tiles(int nkb, unsigned long long skip, int j0) const {
     const int d = j - j0;
@@ -261,18 +262,22 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   const int j0 = by * a.j_per_wg;
   const int j1 = min(a.Bk, j0 + a.j_per_wg);
   const int nkb = a.Nk_pad / 32;
-  // Zero key tiles (training, kcount given): a key sample whose kept keys all lie before its last
-  // 32-key tile (kcount[j] <= 32 (nkb - 1); patch dropout zero-pads the rest) has only zero
-  // vectors there, so S == 0 exactly on that tile: it is not multiplied -- its epilogue is applied
-  // in closed form at the sample's end (the max against 0 at the tile's first key, zero unit dS,
-  // nothing added to the sums), bit-identical to computing it. Bit j - j0 of `skip`, for the
-  // workgroup's first 64 samples (later ones are computed).
+  // Compact key tiles (training, ktiles given): a key sample whose kept keys all lie before its
+  // last 32-key tile holds only zero vectors there (patch dropout's padding), so S == 0 exactly on
+  // that tile; the caller's K and the tiled dS then store only the other tiles -- sample j's at
+  // tile rows ktiles[j] .. ktiles[j+1] - 1 -- and the tile is not multiplied: its epilogue is
+  // applied in closed form at the sample's end (the max against 0 at the tile's first key, nothing
+  // added to the sums). Bit j - j0 of `skip` (nkb - 1 stored tiles), for the workgroup's first
+  // 64 samples; the host stores every tile of any later one.
   unsigned long long skip = 0;
-  if (TRAIN && a.kcount && nkb > 1 && j1 > j0) {
+  int tile0 = j0 * nkb, ntile_wg = (j1 - j0) * nkb;   // the workgroup's first stored tile, count
+  if (TRAIN && a.ktiles && j1 > j0) {
     const int jj = j0 + lane;
-    skip = __builtin_amdgcn_ballot_w64(jj < j1 && a.kcount[jj] <= 32 * (nkb - 1));
+    skip = __builtin_amdgcn_ballot_w64(jj < j1 && a.ktiles[jj + 1] - a.ktiles[jj] < nkb);
+    tile0 = __builtin_amdgcn_readfirstlane(a.ktiles[j0]);
+    ntile_wg = __builtin_amdgcn_readfirstlane(a.ktiles[j1]) - tile0;
   }
-  const int nblocks = (j1 - j0) * nkb - (int)__builtin_popcountll(skip);
+  const int nblocks = ntile_wg;
   if (nblocks <= 0) {
     if (threadIdx.x == 0) {
       a.part[by * gx + bx] = 0.0;
@@ -285,15 +290,15 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   // offsets cover its j_per_wg samples (the host checks j_per_wg * Nk_pad * 1 KB < 2 GB), so the
   // whole key set may exceed 4 GB (global negatives). Descriptor words: base, stride 0,
   // num_records, gfx950 raw-buffer flags.
-  const unsigned long long kaddr = (unsigned long long)(a.K + (size_t)j0 * a.Nk_pad * D);
+  const unsigned long long kaddr = (unsigned long long)(a.K + (size_t)tile0 * 32 * D);
   const i32x4 kr = {__builtin_amdgcn_readfirstlane((int)(unsigned)kaddr),
                     __builtin_amdgcn_readfirstlane((int)((unsigned)(kaddr >> 32) & 0xffffu)),
-                    __builtin_amdgcn_readfirstlane((int)((unsigned)(j1 - j0) * a.Nk_pad * (D * 2))), 0x00020000};
+                    __builtin_amdgcn_readfirstlane((int)((unsigned)ntile_wg * 32 * (D * 2))), 0x00020000};
   // walk cursors: prefetch (tile b+2), chain (tile b), epilogue (tile b-1); ring slots
   Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
   int fslot = 0, cslot = 0;
   auto prefetch = [&](int b2) __attribute__((always_inline)) {
-    if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j - j0, fc.kb, wave, lane);
+    if (b2 < nblocks) stage_tile(kr, kbuf + fslot * KT_ELEMS, b2 * 32, wave, lane);   // stored tiles in walk order
     fc.next(nkb, skip, j0);
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
   };
@@ -370,22 +375,15 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       const float st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup(e, p, su, lo) : nn;
       accd2 += (double)st;
       // canonical chunks 2 lane, 2 lane + 1 at ds_chunk(): two 1 KB contiguous stores per wave
-      bf16* d = dS_w + ((long long)ec.j * nkb + ec.kb) * 1024 + lane * 8;
+      bf16* d = dS_w + ((long long)tile0 + ec.t) * 1024 + lane * 8;
       store16(d, (u32x4){e.pk[0], e.pk[1], e.pk[2], e.pk[3]});
       store16(d + 512, (u32x4){e.pk[4], e.pk[5], e.pk[6], e.pk[7]});
     }
     const int etiles = ec.tiles(nkb, skip, j0);
     if (ec.kb == etiles - 1) {  // end of a key sample: combine the half-waves' max / argmax
-      if (etiles < nkb) {  // its zero last tile (see `skip`): u = 0 from key 32 (nkb - 1) on
-        if (0.f > e.m) {
-          e.m = 0.f;
-          e.am = 32 * (nkb - 1) - 4 * h;
-        }
-        if (TRAIN) {
-          bf16* z = dS_w + ((long long)ec.j * nkb + nkb - 1) * 1024 + lane * 8;
-          store16(z, (u32x4){0u, 0u, 0u, 0u});
-          store16(z + 512, (u32x4){0u, 0u, 0u, 0u});
-        }
+      if (etiles < nkb && 0.f > e.m) {  // its zero last tile (see `skip`): u = 0 from key 32 (nkb - 1) on
+        e.m = 0.f;
+        e.am = 32 * (nkb - 1) - 4 * h;
       }
       float m = e.m;
       int am = e.am + 4 * h;
@@ -573,7 +571,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
   Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
   int fslot = 0, cslot = 0;
   auto prefetch = [&](int b2) __attribute__((always_inline)) {
-    if (b2 < nblocks) stage_tile(kr, a, kbuf + fslot * KT_ELEMS, fc.j - j0, fc.kb, wave, lane);
+    if (b2 < nblocks) stage_tile(kr, kbuf + fslot * KT_ELEMS, (fc.j - j0) * a.Nk_pad + fc.kb * 32, wave, lane);
     fc.next(nkb);
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF16 - 1 ? 0 : fslot + 1);
   };
@@ -882,7 +880,7 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
     a.Nk_eff = p.Nk_eff; a.j_per_wg = jpw[order[i]]; a.temp = p.temp; a.clamp_lo = p.clamp_lo;
     a.rowmax = p.rowmax; a.argmax = p.argmax; a.part = p.nn_part;
     a.dS = (bf16*)p.dS; a.CT = p.CT; a.part2 = p.st_part; a.klen = nullptr;
-    a.kcount = p.dS ? p.k_count : nullptr;
+    a.ktiles = p.dS ? p.k_tiles : nullptr;
     m.gx[i] = xb[order[i]] * (256 / ROWS_PER_WG);
     m.first[i + 1] = m.first[i] + m.gx[i] * ys[order[i]];
   }

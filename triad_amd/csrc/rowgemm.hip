@@ -169,9 +169,13 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
     for (int cb = 0; cb < 4; ++cb) bq[slot][cb] = *(const bf16x8*)(bsrc + (long long)k * 16384 + cb * 512);
     glds16(asrc + k * RP_K, lds + slot * RP_SLOT + wave * 512);
   };
-  auto stage = [&](auto U, int kt) __attribute__((always_inline)) {
+  // TAIL: a trailing stage (nkt % RP_NB): its prefetch's B loads are dead code hipcc removes, so
+  // fewer younger VMEM ops are in flight than the counted wait assumes -- drain instead (as the
+  // direct-B tile GEMM, bwd_gemm.hip)
+  auto stage = [&](auto U, int kt, auto TAIL) __attribute__((always_inline)) {
     constexpr int u = decltype(U)::value;
-    TRIAD_VMCNT(5 * (RP_DD - 1));   // this stage's A piece landed; the DD - 1 younger stages in flight
+    if constexpr (decltype(TAIL)::value) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else TRIAD_VMCNT(5 * (RP_DD - 1));   // this stage's A piece landed; the DD - 1 younger stages in flight
     __syncthreads();
     const bf16* As = lds + u * RP_SLOT;
     bf16x8 af[8];
@@ -190,10 +194,13 @@ __global__ __launch_bounds__(512, 1) void rowpanel_kernel(RPArgs a) {
   };
   static_for<0, RP_DD>([&](auto P) __attribute__((always_inline)) { load_stage(decltype(P)::value, decltype(P)::value); });
   const int ngroups = nkt / RP_NB;
-  for (int g = 0; g < ngroups; ++g) static_for<0, RP_NB>([&](auto U) __attribute__((always_inline)) { stage(U, g * RP_NB + decltype(U)::value); });
+  for (int g = 0; g < ngroups; ++g)
+    static_for<0, RP_NB>([&](auto U) __attribute__((always_inline)) {
+      stage(U, g * RP_NB + decltype(U)::value, std::false_type{});
+    });
   const int rem = nkt - ngroups * RP_NB, base = ngroups * RP_NB;
   static_for<0, RP_NB - 1>([&](auto U) __attribute__((always_inline)) {
-    if (decltype(U)::value < rem) stage(U, base + decltype(U)::value);
+    if (decltype(U)::value < rem) stage(U, base + decltype(U)::value, std::true_type{});
   });
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();   // every wave is done with the ring: the epilogue may reuse it

@@ -12,8 +12,10 @@ import math
 from dataclasses import dataclass
 from typing import Optional
 
+import functools
 import os
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -324,12 +326,92 @@ def _head_begin(q, k, temperature, kind, q_mask, group, ds_budget, need_grad):
     h.dS = torch.empty((g.R_pad // 32) * h.CT * 1024, dtype=torch.bfloat16, device=dev) if write_ds else None
     h.st_part = torch.empty(h.nparts, dtype=torch.float64, device=dev) if write_ds else None
     h.q_dtype, h.k_dtype, h.t_dtype = q.dtype, k.dtype, temperature.dtype
-    # kept keys per sample when k comes straight from patch_dropout (zero rows after them): the
-    # training forward skips each sample's all-zero last key tile (triad_pairsim_problem.k_count)
+    # kept keys per sample when k comes straight from patch_dropout (zero rows after them; host
+    # int32): the pair forward may then leave out each sample's all-zero last key tile (_compact)
     kc = getattr(k, KEPT_ROWS_ATTR, None) if W == 1 and ZERO_TILE_SKIP else None
-    h.kcount = kc if (isinstance(kc, torch.Tensor) and kc.device == dev and kc.dtype == torch.int32
-                      and tuple(kc.shape) == (g.Bk,) and kc.is_contiguous()) else None
+    h.kept = kc if (isinstance(kc, torch.Tensor) and kc.device.type == "cpu" and tuple(kc.shape) == (g.Bk,)) else None
+    h.Kc = h.ktiles = h.kmap = None
+    h.nct = g.C_pad // 32   # stored key tiles (all of them unless _compact)
     return h
+
+
+@functools.lru_cache(maxsize=64)
+def _fwd_keys_per_workgroup(R_pad, Bk):
+    """Key samples per forward workgroup: pairsim.hip grid_for's choice (the decomposition
+    triad_pairsim_nparts reports), restated so the host knows when compact key tiles apply."""
+    xb = R_pad // ROWS_PER_WG
+    best, ys = 1e30, 1
+    for y in range(1, Bk + 1):
+        j = -(-Bk // y)
+        ya = -(-Bk // j)
+        c = ((xb * ya + 255) // 256) * (j + 0.3)
+        if c < best - 1e-9:
+            best, ys = c, ya
+    jpw = -(-Bk // ys)
+    assert xb * (-(-Bk // jpw)) == call("triad_pairsim_nparts", R_pad, Bk)
+    return jpw
+
+
+_STAGE = [None] * 16   # (pinned host tensor, event after its copy), round robin
+_STAGE_NEXT = [0]
+
+
+def _stage_h2d(arr, dev):
+    """int32 numpy array -> device tensor (async) through a ring of pinned slots; a slot is reused
+    only after the event recorded behind its copy has completed, so a copy the stream has not run
+    yet never reads a refilled buffer."""
+    i = _STAGE_NEXT[0]
+    _STAGE_NEXT[0] = (i + 1) % len(_STAGE)
+    prev = _STAGE[i]
+    if prev is not None:
+        prev[1].synchronize()
+    host = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int32)).pin_memory()
+    out = host.to(dev, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    _STAGE[i] = (host, ev)
+    return out
+
+
+def _compact(h):
+    """Compact key tiles for a training head whose keys come from patch_dropout: every sample
+    whose kept keys all lie before its last 32-key tile leaves that all-zero tile out of K and of
+    the tiled dS (triad_pairsim_problem.k_tiles); the forward applies its S == 0 in closed form,
+    dQ / dK / the dS patch run over the stored tiles only and dK's rows go back to the padded layout
+    (zeros for the left-out keys: their gradient is padding, model.py:301-302). Skipped when the
+    forward's workgroups hold more than 64 key samples (its per-workgroup skip mask) or nothing is
+    left out."""
+    g = h.g
+    nkb = g.Nk_pad // 32
+    if h.kept is None or h.dS is None or nkb < 2 or _fwd_keys_per_workgroup(g.R_pad, g.Bk) > 64:
+        return
+    kept = h.kept.numpy()
+    tiles = np.where(kept <= 32 * (nkb - 1), nkb - 1, nkb).astype(np.int64)
+    if (tiles == nkb).all():
+        return
+    cb = np.zeros(g.Bk + 1, dtype=np.int32)
+    cb[1:] = np.cumsum(tiles)
+    nct = int(cb[-1])
+    tidx = (np.repeat(np.arange(g.Bk) * nkb - cb[:-1], tiles) + np.arange(nct)).astype(np.int64)
+    # dK row of each (sample, key < Nk) in the stored layout, -1 in a left-out tile (zero gradient)
+    key = np.arange(h.Nk)[None, :]
+    kmap = np.where(key < 32 * tiles[:, None], 32 * cb[:-1, None].astype(np.int64) + key, -1).astype(np.int32)
+    dev = h.Kb.device
+    # the three tables in ONE host-to-device copy from a staging slot held until the copy has run
+    nb = g.Bk + 1
+    tables = _stage_h2d(np.concatenate([cb, kmap.reshape(-1), tidx.astype(np.int32)]), dev)
+    h.ktiles = tables[:nb]
+    h.kmap = tables[nb:nb + kmap.size].view(1, -1)
+    h.nct = nct
+    kc = torch.empty(_rup(nct * 32, 128), D, dtype=torch.bfloat16, device=dev)
+    torch.index_select(h.Kb[:g.C_pad].view(g.Bk * nkb, 32 * D), 0, tables[nb + kmap.size:],
+                       out=kc[:nct * 32].view(nct, 32 * D))
+    kc[nct * 32:].zero_()
+    h.Kc = kc
+    h.CT = _rup(nct, 4)
+    h.dS = torch.empty((g.R_pad // 32) * h.CT * 1024, dtype=torch.bfloat16, device=dev)
+    if h.CT > nct:   # dK's last row panel reads the tail tiles: zeros, not stale memory
+        h.dS.view(g.R_pad // 32, h.CT, 1024)[:, nct:].zero_()
 
 
 def _fwd_meta(h):
@@ -349,11 +431,15 @@ def _head_launch(h, st):
          ptr(h.diagS), ptr(h.dS), h.CT, ptr(h.st_part), None, st, meta=_fwd_meta(h))
 
 
-def _problem(h):
+def _problem(h, padded_keys=False):
+    """The head's forward problem; padded_keys: with the full padded K and no k_tiles (the
+    diagonal-S launch, triad_pairsim_diag)."""
     g = h.g
-    return _lib.PairsimProblem(ptr(h.Qb), ptr(h.Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, ptr(h.temp),
-                               CLAMP_LO[h.kind], 1, h.rank * g.Bq, ptr(h.rowmax), ptr(h.argmax), ptr(h.nn_part),
-                               ptr(h.diagS), ptr(h.dS), h.CT, ptr(h.st_part), ptr(h.kcount))
+    compact = h.Kc is not None and not padded_keys
+    return _lib.PairsimProblem(ptr(h.Qb), ptr(h.Kc if compact else h.Kb), g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad,
+                               g.Nk_eff, ptr(h.temp), CLAMP_LO[h.kind], 1, h.rank * g.Bq, ptr(h.rowmax),
+                               ptr(h.argmax), ptr(h.nn_part), ptr(h.diagS), ptr(h.dS), h.CT, ptr(h.st_part),
+                               ptr(h.ktiles) if compact else None)
 
 
 def _heads_launch(hs, st):
@@ -361,9 +447,8 @@ def _heads_launch(hs, st):
     diagonal S blocks (triad_pairsim_diag) -- issued apart so the bench's live timing of the
     forward launch covers that kernel alone (bit-identical to the one-call form, which also
     launches the diagonal kernels)."""
-    probs = [_problem(h) for h in hs]
-    arr = (_lib.PairsimProblem * len(hs))(*probs)
-    fwd = (_lib.PairsimProblem * len(hs))(*probs)
+    arr = (_lib.PairsimProblem * len(hs))(*[_problem(h, padded_keys=True) for h in hs])
+    fwd = (_lib.PairsimProblem * len(hs))(*[_problem(h) for h in hs])
     for p in fwd:
         p.diag = 0
     ms = [_fwd_meta(h) for h in hs]
@@ -412,7 +497,8 @@ def _head_end(h, q_mask, thr, w_sparse, st):
     return out[:4].clone(), out[4:].clone(), clip_full
 
 
-_SAVED = ("Qb", "Kb", "argmax", "rowmax", "dclip", "qw", "gdiag", "temp", "dS", "st_part", "dgt_part")
+_SAVED = ("Qb", "Kb", "argmax", "rowmax", "dclip", "qw", "gdiag", "temp", "dS", "st_part", "dgt_part", "Kc", "ktiles",
+          "kmap")
 
 
 def _head_saved(h):
@@ -423,7 +509,7 @@ def _head_light(h):
     """h without its tensors (those travel through ctx.save_for_backward)."""
     c = _Head()
     for n in ("g", "kind", "W", "rank", "Nk", "n_el", "w_sparse", "nparts", "CT", "chunk", "group", "q_dtype",
-              "k_dtype", "t_dtype"):
+              "k_dtype", "t_dtype", "nct"):
         setattr(c, n, getattr(h, n))
     return c
 
@@ -432,7 +518,7 @@ def _head_backward(h, saved, needs, g_total, g_ce, g_reg, g_aux):
     """(gq, gk, gt) of one head; needs = (q, k, temperature) input-gradient flags."""
     if g_total is None and g_ce is None and g_reg is None and g_aux is None:
         return None, None, None
-    Qb, Kb, argmax, rowmax, dclip, qw, gdiag, temp, dS, st_part, dgt_part = saved
+    Qb, Kb, argmax, rowmax, dclip, qw, gdiag, temp, dS, st_part, dgt_part, Kc, ktiles, kmap = saved
     g, kind, W, rank, CT = h.g, h.kind, h.W, h.rank, h.CT
     dev = Qb.device
     st = stream_ptr(dev)
@@ -458,9 +544,9 @@ def _head_backward(h, saved, needs, g_total, g_ce, g_reg, g_aux):
         ratio_diag = (0.01 if kind == AV else h.w_sparse) * h.n_el / 0.3
         nmp = 1024
         max_part = torch.empty(nmp, dtype=torch.float64, device=dev)
-        call("triad_dS_patch", ptr(dS), CT, g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, rank * g.Bq,
+        call("triad_dS_patch_tiles", ptr(dS), CT, g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, rank * g.Bq,
              ptr(argmax), ptr(rowmax), ptr(dclip), ptr(qw), float(ratio_max), ptr(gdiag), float(ratio_diag),
-             ptr(max_part), nmp, st)
+             ptr(max_part), nmp, ptr(ktiles), st)
         alpha = (temp * c_nn).reshape(1).contiguous()
         w = torch.stack([c_nn, c_ce / temp[0], c_diag / temp[0], c_cal]).contiguous()
         parts = (st_part, h.nparts, max_part, nmp, dgt_part, g.Bq)
@@ -475,7 +561,7 @@ def _head_backward(h, saved, needs, g_total, g_ce, g_reg, g_aux):
             gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(h.q_dtype)
     if fast and needs[0]:
         dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device=dev)
-        tile_gemm(dS, CT, 0, Kb, g.R_pad, g.C_pad // 32, alpha, dQ, st,
+        tile_gemm(dS, CT, 0, Kb if Kc is None else Kc, g.R_pad, h.nct, alpha, dQ, st,
                   meta=dict(kind=kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, what="dQ"))
         gq = dQ[:g.R].view(g.Bq, g.Nq, D).to(h.q_dtype)
     if needs[1]:
@@ -488,7 +574,10 @@ def _head_backward(h, saved, needs, g_total, g_ce, g_reg, g_aux):
         if W > 1:
             from . import dist as tdist
             dK = tdist.reduce_scatter_rows(dK, g.Bq * Nk_pad, h.group)  # this rank's keys, all queries
-        gk = dK[:g.Bq * Nk_pad].view(g.Bq, Nk_pad, D)[:, :h.Nk].to(h.k_dtype)
+        if fast and kmap is not None:   # stored key tiles -> (B, Nk, 512) in one gather (left-out keys: zero)
+            gk = gather_rows(dK.view(1, Mk, D), kmap).view(g.Bq, h.Nk, D).to(h.k_dtype)
+        else:
+            gk = dK[:g.Bq * Nk_pad].view(g.Bq, Nk_pad, D)[:, :h.Nk].to(h.k_dtype)
     if needs[2]:
         dt = torch.empty(1, dtype=f32, device=dev)
         p0, n0, p1, n1, p2, n2 = parts
@@ -553,6 +642,9 @@ class _ContrastiveHeadPair(torch.autograd.Function):
         used = ds_working_bytes(ha.g, ha.chunk) if need_grad else 0
         ht = _head_begin(qt, kt, temperature, TV, qt_mask, group, max(0, budget - used), need_grad)
         st = stream_ptr(qa.device)
+        if ha.dS is not None and ht.dS is not None:   # one training launch: compact key tiles apply
+            _compact(ha)
+            _compact(ht)
         if (ha.dS is None) == (ht.dS is None):
             _heads_launch([ha, ht], st)
         else:  # one head over the dS budget: the multi launch needs one mode for both
@@ -928,11 +1020,11 @@ def dropout_indices(keep_mask: torch.Tensor, n_out: Optional[int] = None):
     return idx[:, :n_out], inv, n_out
 
 
-# attribute of patch_dropout's output: its kept-row count per sample (int32, on the device); rows
-# after it are zero, which the similarity forward exploits (_head_begin); a copy or view of the
-# tensor does not carry it
+# attribute of patch_dropout's output: its kept-row count per sample (host int32); rows after it
+# are zero, which the pair forward exploits (_compact); a copy or view of the tensor does not
+# carry it
 KEPT_ROWS_ATTR = "_triad_kept_rows"
-# TRIAD_ZERO_TILE_SKIP=0: multiply the zero key tiles too (A/B; results are bit-identical)
+# TRIAD_ZERO_TILE_SKIP=0: store and multiply the all-zero key tiles too (A/B)
 ZERO_TILE_SKIP = os.environ.get("TRIAD_ZERO_TILE_SKIP", "1") != "0"
 
 
@@ -944,8 +1036,7 @@ def patch_dropout(x: torch.Tensor, keep_mask: torch.Tensor, n_out: Optional[int]
     idx_d = _lib.h2d(idx.contiguous(), x.device)
     inv_d = _lib.h2d(inv.contiguous(), x.device)
     out = _GatherRows.apply(x.contiguous(), idx_d, inv_d)
-    kept = keep_mask.detach().to("cpu", torch.bool).sum(1).to(torch.int32).contiguous()
-    setattr(out, KEPT_ROWS_ATTR, _lib.h2d(kept, x.device))
+    setattr(out, KEPT_ROWS_ATTR, keep_mask.detach().to("cpu", torch.bool).sum(1).to(torch.int32))
     return out
 
 
