@@ -540,3 +540,33 @@ def test_pair_launch_eval_mode_matches_two_heads():
         assert torch.equal(x, y)
     total = ref_cpu.av_loss(A.double(), Va.double(), torch.tensor(1.3, dtype=torch.float64))[0]
     assert _scalar_close(float(la[0]), float(total))
+
+
+def test_pair_head_compact_c3_repeats_bit_stable():
+    """The c3-shaped training pair head (B = 256, Na = 199, Nt = 32, keys from patch_dropout so the
+    key tiles are compacted) run six times on identical inputs: every gradient bit-identical across
+    the repeats. Before the direct-B GEMMs' tail stages drained vmcnt, AV dK --
+    3 splits of 534 stages, a 2-stage tail -- differed in 3 of 7 such repeats."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(7)
+    B, N, Na, Nt = 256, 256, 199, 32
+    A = (torch.randn(B, Na, 512, generator=g) * 0.58).to(torch.bfloat16).to(dev)
+    T = (torch.randn(B, Nt, 512, generator=g) * 0.58).to(torch.bfloat16).to(dev)
+    X = (torch.randn(B, N, 512, generator=g) * 0.58).to(torch.bfloat16).to(dev)
+    keep_av = torch.rand(B, N, generator=g) < 0.75
+    keep_tv = torch.rand(B, N, generator=g) < 0.75
+    mask = torch.ones(B, Nt, dtype=torch.long, device=dev)
+    first = None
+    for _ in range(6):
+        a, t, x = (v.clone().requires_grad_(True) for v in (A, T, X))
+        tg = torch.tensor(1.5, device=dev, requires_grad=True)
+        (la, _, _), (lt, _, _) = ops.contrastive_heads_av_tv(a, ops.patch_dropout(x, keep_av), t,
+                                                             ops.patch_dropout(x, keep_tv), tg, mask,
+                                                             threshold=0.8, sparsity_weight=0.01)
+        (la[0] + lt[0]).backward()
+        cur = [a.grad, t.grad, x.grad, tg.grad]
+        if first is None:
+            first = cur
+        else:
+            for got, want in zip(cur, first):
+                assert torch.equal(got, want)
