@@ -14,19 +14,19 @@ from triad_amd import ops  # noqa: E402
 from triad_amd._lib import call, ptr, stream_ptr  # noqa: E402
 
 
-def run(B, Nq, Nk, dk, iters, force_sp=None, form=0):
+def run(B, Nq, Nk, dk, iters, force_sp=None, form=0, ct=0):
     g = ops.Geometry(B, Nq, B, Nk)
     gen = torch.Generator(device="cuda").manual_seed(0)
     q = (torch.randn(B, Nq, 512, device="cuda", generator=gen) * 0.58).to(torch.bfloat16)
     k = (torch.randn(B, Nk, 512, device="cuda", generator=gen) * 0.58).to(torch.bfloat16)
     Qb, Kb = ops.pack_queries(q, g), ops.pack_keys(k, g)
-    CT = ops._rup(g.C_pad // 32, 4)
+    CT = ops._rup(g.C_pad // 32, 4) if not ct else ct   # ct: compact key tiles (ops._compact's CT)
     dS = (torch.randn((g.R_pad // 32) * CT * 1024, device="cuda", generator=gen) * 1e-3).to(torch.bfloat16)
     alpha = torch.tensor([1.5], device="cuda")
     if dk:
         M, nkt, Bm = CT * 32, g.R_pad // 32, Qb
     else:
-        M, nkt, Bm = g.R_pad, g.C_pad // 32, Kb
+        M, nkt, Bm = g.R_pad, (ct or g.C_pad // 32), Kb
     sp = ops._gemm_splits(M // 128, nkt, M) if force_sp is None else force_sp
     out = torch.empty(M, 512, dtype=torch.bfloat16, device="cuda")
     slabs = torch.empty(sp * M * 512, dtype=torch.float32, device="cuda") if sp > 1 else None
@@ -76,16 +76,21 @@ if __name__ == "__main__":
     ap.add_argument("--sweep", action="store_true", help="every split count 1..8 (else the product rule)")
     ap.add_argument("--forms", default="0", help="comma-separated triad_tile_gemm_form forms, alternated")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--ct", default="0", help="AV,TV key-tile counts (compact layout; 0 = padded)")
+    ap.add_argument("--heads", default="AV,TV")
     a = ap.parse_args()
+    cts = dict(zip(("AV", "TV"), (int(v) for v in a.ct.split(","))))
     for r in range(a.rounds):
         for name, Nq, Nk in (("AV", 199, 212), ("TV", 32, 212)):
+            if name not in a.heads.split(","):
+                continue
             for dk in (0, 1):
                 for fsp in (range(1, 9) if a.sweep else (None,)):
                     for form in (int(f) for f in a.forms.split(",")):
-                        res = run(256, Nq, Nk, dk, a.iters, fsp, form)
+                        res = run(256, Nq, Nk, dk, a.iters, fsp, form, cts.get(name, 0))
                         if res is None:
                             continue
                         ms, tf, sp = res
                         print(json.dumps({"tag": os.path.basename(a.tag), "form": form, "round": r, "head": name,
-                                          "gemm": "dK" if dk else "dQ", "splits": sp, "ms": round(ms, 4),
+                                          "gemm": "dK" if dk else "dQ", "ct": cts.get(name, 0), "splits": sp, "ms": round(ms, 4),
                                           "algo_TFLOPs": round(tf, 1)}), flush=True)
