@@ -367,3 +367,35 @@ def test_param_sumsq_is_a_segmented_sum_per_parameter(monkeypatch):
             want[i] = (sp.flat_g[o:o + ps[i].numel()].double() ** 2).sum()
         torch.testing.assert_close(got, want, rtol=1e-12, atol=0)
 
+
+
+def test_compact_key_tile_tables_match_a_loop_restatement():
+    """ops.compact_tables (the compact key-tile layout the training pair forward / backward walk)
+    against a per-sample loop: every sample keeps its tiles up to its last non-zero one; a sample
+    whose kept count fits in nkb - 1 tiles leaves the last (all-zero) tile out."""
+    from triad_amd import ops
+    rng = np.random.default_rng(5)
+    for Bk, nkb in ((1, 2), (7, 3), (64, 7), (300, 7)):
+        Nk = 32 * nkb - int(rng.integers(0, 20))
+        kept = rng.integers(0, Nk + 1, size=Bk).astype(np.int32)
+        kept[0] = Nk                                # the batch's longest sample sets Nk
+        if Bk > 1:
+            kept[1] = 32 * (nkb - 1)                # boundary: exactly nkb - 1 full tiles
+        tabs = ops.compact_tables(kept, nkb, Nk)
+        cb_ref, tidx_ref, kmap_ref = [0], [], np.full((Bk, Nk), -1, dtype=np.int32)
+        for j in range(Bk):
+            nt = nkb - 1 if kept[j] <= 32 * (nkb - 1) else nkb
+            for kb in range(nt):
+                for k in range(32 * kb, min(32 * kb + 32, Nk)):
+                    kmap_ref[j, k] = 32 * (cb_ref[-1] + kb) + (k - 32 * kb)
+                tidx_ref.append(j * nkb + kb)
+            cb_ref.append(cb_ref[-1] + nt)
+        if cb_ref[-1] == Bk * nkb:
+            assert tabs is None
+            continue
+        cb, tidx, kmap = tabs
+        assert cb.dtype == np.int32 and kmap.dtype == np.int32
+        np.testing.assert_array_equal(cb, cb_ref)
+        np.testing.assert_array_equal(tidx, tidx_ref)
+        np.testing.assert_array_equal(kmap, kmap_ref)
+    assert ops.compact_tables(np.full(5, 70, np.int32), 3, 70) is None   # every sample needs all tiles

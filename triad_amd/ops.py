@@ -373,6 +373,27 @@ def _stage_h2d(arr, dev):
     return out
 
 
+def compact_tables(kept, nkb, Nk):
+    """Host tables of the compact key-tile layout (see _compact) for per-sample kept counts:
+    cb (Bk + 1 int32, triad_pairsim_problem.k_tiles: sample j's stored tiles are cb[j] ..
+    cb[j + 1] - 1), tidx (int64, the padded tile index j nkb + kb of each stored tile, in order) and
+    kmap ([Bk][Nk] int32: the compact key row of key (j, k), -1 in a left-out tile). None when no
+    sample leaves its last tile out."""
+    kept = np.asarray(kept)
+    tiles = np.where(kept <= 32 * (nkb - 1), nkb - 1, nkb).astype(np.int64)
+    if (tiles == nkb).all():
+        return None
+    Bk = kept.shape[0]
+    cb = np.zeros(Bk + 1, dtype=np.int32)
+    cb[1:] = np.cumsum(tiles)
+    nct = int(cb[-1])
+    tidx = (np.repeat(np.arange(Bk) * nkb - cb[:-1], tiles) + np.arange(nct)).astype(np.int64)
+    # dK row of each (sample, key < Nk) in the stored layout, -1 in a left-out tile (zero gradient)
+    key = np.arange(Nk)[None, :]
+    kmap = np.where(key < 32 * tiles[:, None], 32 * cb[:-1, None].astype(np.int64) + key, -1).astype(np.int32)
+    return cb, tidx, kmap
+
+
 def _compact(h):
     """Compact key tiles for a training head whose keys come from patch_dropout: every sample
     whose kept keys all lie before its last 32-key tile leaves that all-zero tile out of K and of
@@ -385,17 +406,11 @@ def _compact(h):
     nkb = g.Nk_pad // 32
     if h.kept is None or h.dS is None or nkb < 2 or _fwd_keys_per_workgroup(g.R_pad, g.Bk) > 64:
         return
-    kept = h.kept.numpy()
-    tiles = np.where(kept <= 32 * (nkb - 1), nkb - 1, nkb).astype(np.int64)
-    if (tiles == nkb).all():
+    tabs = compact_tables(h.kept.numpy(), nkb, h.Nk)
+    if tabs is None:
         return
-    cb = np.zeros(g.Bk + 1, dtype=np.int32)
-    cb[1:] = np.cumsum(tiles)
+    cb, tidx, kmap = tabs
     nct = int(cb[-1])
-    tidx = (np.repeat(np.arange(g.Bk) * nkb - cb[:-1], tiles) + np.arange(nct)).astype(np.int64)
-    # dK row of each (sample, key < Nk) in the stored layout, -1 in a left-out tile (zero gradient)
-    key = np.arange(h.Nk)[None, :]
-    kmap = np.where(key < 32 * tiles[:, None], 32 * cb[:-1, None].astype(np.int64) + key, -1).astype(np.int32)
     dev = h.Kb.device
     # the three tables in ONE host-to-device copy from a staging slot held until the copy has run
     nb = g.Bk + 1
