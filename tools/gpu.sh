@@ -17,6 +17,7 @@
 #   profpy:<script args>   the same under rocprofv3 --kernel-trace --stats -> gpurun_out/<tag>_profpy<N>/
 #   envprofpy:A=1,B=2:<script args>  profpy with extra environment for this step
 #   pmcpy:<name>:<counters>:<script args>  one rocprofv3 --pmc pass over a python script
+#   envpmcpy:A=1:<name>:<counters>:<script args>  the same with extra environment for this step
 # environment: extra env for every step may be given as STEP_ENV="A=1 B=2" (exported first).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -81,6 +82,12 @@ for step in "$@"; do
       rest=${step#pmcpy:}; name=${rest%%:*}; rest=${rest#*:}; ctr=${rest%%:*}; script=${rest#*:}
       timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "gpurun_out/${tag}_pmcpy_${name}" -o run \
         -- python3 $script > "gpurun_out/${tag}_pmcpy_${name}.log" 2>&1 ;;
+    envpmcpy:*)
+      # envpmcpy:A=1,B=2:<name>:<counters>:<script args>  pmcpy with extra environment for this step only
+      rest=${step#envpmcpy:}; ev=${rest%%:*}; rest=${rest#*:}; name=${rest%%:*}; rest=${rest#*:}
+      ctr=${rest%%:*}; script=${rest#*:}
+      ( export ${ev//,/ }; timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } --output-format csv \
+        -d "gpurun_out/${tag}_pmcpy_${name}" -o run -- python3 $script ) > "gpurun_out/${tag}_pmcpy_${name}.log" 2>&1 ;;
     py:*)
       timeout -k 10 600 python ${step#py:} > "gpurun_out/${tag}_py${n}.log" 2>&1 ;;
     envpy:*)
