@@ -8,9 +8,12 @@ clip, four AdamW + OneCycleLR steps; every module trainable (the post-unfreeze
 worst case), grad-accum 1. Random-init weights, synthetic data
 resident in HBM before the timed region.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5] [--global-negatives]
        (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0. The default (c3, Mode R) is the headline line; --config c2 / c5 time
+BASELINE.json's other single-GPU-sized configurations with their own per-kernel fractions, and
+--global-negatives times Mode G (BASELINE c4: every rank contrasts its queries against the keys of
+all ranks, RCCL all-gather / reduce-scatter inside the head).
 """
 from __future__ import annotations
 
@@ -28,14 +31,31 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "tri-modal triples/sec (whole node) + loss parity, B=256 at 1/2/4/8 MI355X"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
-TRACKED = ("triad_pairsim_fwd", "triad_pairsim_fwd_multi", "triad_pairsim_diag", "triad_pairsim_dS", "triad_gemm_bf16", "triad_gemm_bf16_bias_bf16", "triad_projhead_ln_fwd", "triad_rowgemm_bias", "triad_projhead_ln_bwd", "triad_wpack", "triad_wpack2",
-           "triad_projhead_fwd",
-           "triad_gemm_bf16_splitk", "triad_gemm_bf16_splitk_form", "triad_tile_gemm", "triad_tile_gemm_packed16",
-           "triad_tile_gemm_packed16_slabs",
-           "triad_bfrag_pack16", "triad_dS_patch", "triad_clip_reduce", "triad_losshead",
-           "triad_diag_smooth", "triad_diag_sparsity", "triad_dtemp_finalize",
-           "triad_colsum_dma", "triad_sum_slabs", "triad_gather_rows", "triad_global_znorm",
-           "triad_grad_sumsq", "triad_adamw_step", "triad_ln_fwd", "triad_ln_bwd3", "triad_gemm_bf16_bias")
+# every hot-path entry point of the library's C ABI (triad_amd/_lib.py: all launching entry points
+# but the backbone-only ones), so a kernel added or renamed on the path cannot drop out of the
+# per-kernel timing; backbone launches of the shared GEMM / column-sum entry points are tagged
+# and reported apart (kernel_report)
+from triad_amd._lib import hot_path_entry_points  # noqa: E402
+TRACKED = hot_path_entry_points()
+
+
+# BASELINE.json configurations a single GPU runs (configs[1], [2], [4] per rank; c1 is the CPU plumbing
+# case, c4 is c3 x 8 ranks with --global-negatives). phase: the trainer's loss mix (train.py:972-984)
+CONFIGS = {
+    "c3": dict(batch=256, px=224, audio_s=4, n_text=32, phase="full_joint", unit="triples/s",
+               audio_model="facebook/hubert-base-ls960", vit_arch="dinov2_vitb14_reg",
+               workload="c3: full tri-modal V+A+T train step, DINOv2-B/14-reg+LoRA / HuBERT-base / DistilBERT, "
+                        "full_joint, all modules trainable, patch dropout 0.25"),
+    "c2": dict(batch=128, px=224, audio_s=4, n_text=32, phase="av_focus", unit="pairs/s",
+               audio_model="facebook/hubert-base-ls960", vit_arch="dinov2_vitb14_reg",
+               workload="c2: image-audio train step (forward_audio_visual, train.py:954), DINOv2-B/14-reg+LoRA / "
+                        "HuBERT-base, B=128, 4 s audio, av_focus, all modules trainable, patch dropout 0.25"),
+    "c5": dict(batch=32, px=518, audio_s=10, n_text=32, phase="full_joint", unit="triples/s",
+               audio_model="facebook/hubert-large-ls960-ft", vit_arch="dinov2_vitl14_reg",
+               workload="c5 per rank: full tri-modal train step, DINOv2-L/14-reg+LoRA on 518 px frames (1369 "
+                        "patches) / HuBERT-large on 10 s audio (Na=499) / DistilBERT, full_joint, all modules "
+                        "trainable, patch dropout 0.25"),
+}
 
 
 def parse():
@@ -43,7 +63,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=256, help="triples per GPU")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c3",
+                    help="BASELINE configuration (c3 = the headline; c2 / c5 = their own lines)")
+    ap.add_argument("--global-negatives", action="store_true",
+                    help="Mode G: contrast against the keys of every rank (BASELINE c4 at N > 1)")
+    ap.add_argument("--batch", type=int, default=None, help="samples per GPU (default: the config's)")
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--cpu-head-batch", type=int, default=48, help="batch of the CPU hot-path timing (extrapolated)")
@@ -79,15 +103,16 @@ def setup_dist():
     return world, rank, local
 
 
-def synthetic(B, rank, device):
-    """SURVEY §8d inputs: frames N(0,1), audio N(0,0.1) 4 s @ 16 kHz, 32 random token ids."""
+def synthetic(B, rank, device, px=224, audio_s=4, n_text=32):
+    """SURVEY §8d inputs: frames N(0,1) (px x px), audio N(0,0.1) audio_s s @ 16 kHz, n_text random
+    token ids."""
     g = torch.Generator(device=device).manual_seed(1234 + rank)
-    frames = torch.randn(B, 3, 224, 224, generator=g, device=device)
-    audio = torch.randn(B, 64000, generator=g, device=device) * 0.1
+    frames = torch.randn(B, 3, px, px, generator=g, device=device)
+    audio = torch.randn(B, 16000 * audio_s, generator=g, device=device) * 0.1
     # token ids / mask stay on the host like the reference tokenizer's output (model.py:102-112);
     # the text embedder moves them with a pinned async copy each step
-    ids = torch.randint(1000, 30522, (B, 32), generator=torch.Generator().manual_seed(1234 + rank))
-    mask = torch.ones(B, 32, dtype=torch.long)
+    ids = torch.randint(1000, 30522, (B, n_text), generator=torch.Generator().manual_seed(1234 + rank))
+    mask = torch.ones(B, n_text, dtype=torch.long)
     return frames, audio, {"input_ids": ids.pin_memory(), "attention_mask": mask.pin_memory()}
 
 
@@ -183,6 +208,11 @@ def stream_bit_identity(dev, frames, audio, text):
 
 def main():
     a = parse()
+    cfg = CONFIGS[a.config]
+    if a.batch is None:
+        a.batch = cfg["batch"]
+    headline = a.config == "c3"
+    shared = cfg["phase"] == "full_joint"   # one frame batch for both heads (forward_triad)
     from triad_amd import _lib, blas
     blas.configure()   # torch's own GEMMs on rocBLAS, before the HIP runtime starts (triad_amd/blas.py)
     world, rank, local = setup_dist()
@@ -196,13 +226,15 @@ def main():
     # runtime kernel compilation on a fresh box.
     torch.backends.cudnn.benchmark = False
     torch.manual_seed(1234)
-    model = MultiModalModel(temperature=1.5, patch_sparsity_threshold=0.80, patch_sparsity_weight=0.01,
-                            visual_dropout_prob=0.25, use_amp=True).to(dev)
+    model = MultiModalModel(audio_model_name=cfg["audio_model"], temperature=1.5, patch_sparsity_threshold=0.80,
+                            patch_sparsity_weight=0.01, visual_dropout_prob=0.25, use_amp=True,
+                            vit_arch=cfg["vit_arch"]).to(dev)
     model.train()
     trainer = TriadTrainer(model, learning_rate=1e-4, total_updates=100000, unfreeze_audio_step=0,
-                           unfreeze_text_step=0, unfreeze_vit_step=0, device=dev)
-    frames, audio, text = synthetic(a.batch, rank, dev)
-    frames_tv = frames.roll(1, 0).contiguous() if a.separate_frames else None
+                           unfreeze_text_step=0, unfreeze_vit_step=0, device=dev,
+                           global_negatives=a.global_negatives)
+    frames, audio, text = synthetic(a.batch, rank, dev, cfg["px"], cfg["audio_s"], cfg["n_text"])
+    frames_tv = frames.roll(1, 0).contiguous() if (a.separate_frames and shared) else None
 
     # step watchdog (hang forensics): per-stream markers after every HIP entry point,
     # a monitor thread that writes which launch is in flight and exits non-zero when a step stalls
@@ -216,7 +248,7 @@ def main():
     def step():
         if wd is not None:
             wd.step_begin()
-        out = trainer.step(frames, audio, text, phase="full_joint", shared_frames=not a.separate_frames,
+        out = trainer.step(frames, audio, text, phase=cfg["phase"], shared_frames=not a.separate_frames,
                            frames_tv=frames_tv)
         if wd is not None:
             wd.step_end()
@@ -258,7 +290,7 @@ def main():
     loss = float(out["loss"])
     rep = kernel_report(timers)
     sep = None
-    if a.separate_steps > 0 and not a.separate_frames:
+    if a.separate_steps > 0 and not a.separate_frames and shared:
         # the --separate-frames figure beside the headline: AV and TV frames encoded separately
         frames_sep = frames.roll(1, 0).contiguous()
 
@@ -353,6 +385,7 @@ def main():
 
     if rank == 0:
         value = world * a.batch * a.steps / dt
+        mode_g = bool(trainer.global_negatives)
         # dominant hot-path kernel: the similarity forward of both heads in one launch (S = temp*Q K^T,
         # max/argmax, l_nonneg; S never leaves registers). Algorithmic FLOPs = 2*B^2*Nq*Nk_eff*512 per
         # head (AV: Nq = Na, TV: Nq = Nt). With TRIAD_PAIR_FWD=0 (two launches): the AV launch.
@@ -378,15 +411,25 @@ def main():
                 out.update(achieved_TFLOPs=tf, frac=tf / PEAK_BF16_TFLOPS)
             return out
         res = {
-            "metric": METRIC, "value": value, "unit": "triples/s", "n_gpus": world, "steps": a.steps,
+            "metric": METRIC if headline else f"{a.config} {cfg['unit'].replace('/s', '')}/sec (whole node)",
+            "value": value, "unit": cfg["unit"], "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic (frames N(0,1) 224px, audio N(0,0.1) 4s@16kHz, 32 random token ids); random-init weights",
-            "config": {"workload": "c3: full tri-modal V+A+T train step, DINOv2-B/14-reg+LoRA / HuBERT-base / "
-                                   "DistilBERT, full_joint, all modules trainable, patch dropout 0.25"
-                                   + (", AV/TV frames encoded separately" if a.separate_frames else
-                                      ", one frame batch per triple (dropout masks drawn per head)"),
-                       "global_batch": a.batch * world, "per_gpu_batch": a.batch, "parallelism": f"dp{world}"},
+            "data": f"synthetic (frames N(0,1) {cfg['px']}px, audio N(0,0.1) {cfg['audio_s']}s@16kHz, "
+                    f"{cfg['n_text']} random token ids); random-init weights",
+            "config": {"workload": cfg["workload"]
+                                   + ("" if not shared else ", AV/TV frames encoded separately" if a.separate_frames
+                                      else ", one frame batch per triple (dropout masks drawn per head)"),
+                       "name": a.config, "phase": cfg["phase"],
+                       "global_batch": a.batch * world, "per_gpu_batch": a.batch, "parallelism": f"dp{world}",
+                       "negatives": (f"global (Mode G): each rank's queries against all {a.batch * world} key "
+                                     f"samples (RCCL all-gather / reduce-scatter in the head)" if mode_g else
+                                     "local (Mode R): each rank's reference loss over its own batch"),
+                       "gradient_accumulation_steps": 1,
+                       "gradient_accumulation_note": "one triple = one sample through one optimizer step at "
+                                                     "grad-accum 1 (SURVEY 8d); the reference's __main__ "
+                                                     "accumulates 4 micro-batches (train.py:1167), which changes only "
+                                                     "how often the optimizer runs"},
             "loss": loss,
             "roofline": {"kernel": roof_key, "symbol": roof_sym, "bound": "mfma", "achieved": achieved,
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS,
@@ -423,13 +466,13 @@ def main():
             res["separate_frames"] = {"value": sep, "unit": "triples/s", "steps": a.separate_steps,
                                       "note": "AV and TV frame batches encoded separately, as the reference's "
                                               "two data loaders do (2x ViT work)"}
-        if world == 1 and a.stream_check:
+        if world == 1 and a.stream_check and headline:
             del trainer, model
             torch.cuda.empty_cache()
             bit = stream_bit_identity(dev, frames, audio, text)
             res["stream_bit_identity"] = bit
             print(f"[bench] serial vs concurrent step at B={a.batch}: {bit}", file=sys.stderr, flush=True)
-        if world == 1 and not a.no_cpu_baseline:
+        if world == 1 and not a.no_cpu_baseline and headline:
             from oracle import cpu_step
             # the threads this process may use: torch's intra-op pool honours OMP_NUM_THREADS (the GPU box
             # sets it to the job's CPU share; its affinity mask shows the whole machine, and oversubscribing

@@ -748,3 +748,17 @@ def test_bias_grad_matches_column_sum(rows, cols):
     shifted = wide[:, 1:cols + 1]          # data_ptr 2 bytes past an aligned row start
     shifted.copy_(x)
     assert torch.equal(ops.bias_grad(shifted), ops.bias_grad(x))
+
+def test_patch_dropout_refuses_a_device_mask():
+    """the compaction plan is host work, so a device keep mask would be a silent
+    device->host synchronisation every step; ops.patch_dropout refuses it (TriadError) and takes the
+    same mask from the host."""
+    from triad_amd import ops
+    from triad_amd._lib import TriadError
+    x = torch.randn(2, 16, 512, device="cuda").to(torch.bfloat16)
+    keep = torch.rand(2, 16, generator=torch.Generator().manual_seed(3)) < 0.75
+    with pytest.raises(TriadError):
+        ops.patch_dropout(x, keep.cuda())
+    out = ops.patch_dropout(x, keep)
+    assert out.shape[1] == int(keep.sum(1).max())
+    assert getattr(out, ops.KEPT_ROWS_ATTR).tolist() == keep.sum(1).tolist()

@@ -105,6 +105,33 @@ def test_retrieval_matches_reference_fixtures(name, precision):
     assert [metrics[f"{pre[1]}_r{x}"] for x in (1, 5, 10, 20)] == list(f["recall_kq"])
 
 
+@pytest.mark.parametrize("name", G.names("retrieval_av") + G.names("retrieval_tv"))
+def test_per_pair_aggregators_match_reference_fixtures(name):
+    """The reference's per-pair functions by name (aggregator_av_a2v / _v2a, aggregator_tv_t2v /
+    _v2t, retrieval.py:106-115, 190-198): Python floats equal to the fixture matrices' entries
+    within fp32 evaluation order, for a sample of pairs including the diagonal; and
+    compute_recall_at_k (retrieval.py:117-144) on the fixture's matrices returns its R@k."""
+    from triad_amd import retrieval
+    f = G.load(name)
+    q = [x.cuda() for x in torch.split(G.bf16(f["q"]), [int(n) for n in f["q_len"]])]
+    k = [x.cuda() for x in torch.split(G.bf16(f["k"]), [int(n) for n in f["k_len"]])]
+    temp = float(f["temp"])
+    av = str(f["kind"]) == "retrieval_av"
+    fwd = retrieval.aggregator_av_a2v if av else retrieval.aggregator_tv_t2v
+    bwd = retrieval.aggregator_av_v2a if av else retrieval.aggregator_tv_v2t
+    n = len(q)
+    scale = max(np.abs(f["sim_qk"]).max(), np.abs(f["sim_kq"]).max())
+    for i, j in [(0, 0), (1, 2), (n - 1, 0), (n // 2, n // 2), (3, n - 1)]:
+        a = fwd(q[i], k[j], temp)
+        b = bwd(q[j], k[i], temp)            # (a_feats, v_feats): V->A of video i against audio j
+        assert isinstance(a, float) and isinstance(b, float)
+        assert abs(a - f["sim_qk"][i, j]) <= 1e-5 * scale, (i, j, a, f["sim_qk"][i, j])
+        assert abs(b - f["sim_kq"][i, j]) <= 1e-5 * scale, (i, j, b, f["sim_kq"][i, j])
+    for key in ("qk", "kq"):
+        r = retrieval.compute_recall_at_k(f["sim_" + key])
+        assert [r[x] for x in ("r1", "r5", "r10", "r20")] == list(f["recall_" + key])
+
+
 def _near_tie_rows(ref, got):
     """Rows whose reference rank could move under the observed matrix error (the near-tie rule of
     DESIGN §2): some competitor j sits within twice the row's max |got - ref| of the diagonal."""

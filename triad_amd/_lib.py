@@ -115,6 +115,24 @@ RESTYPES = {"triad_pairsim_nparts": C.c_int, "triad_chgn_workspace_bytes": C.c_l
             "triad_colsum_splits": C.c_int, "triad_colsum_dma_splits": C.c_int, "triad_dense_nparts": C.c_int,
             "triad_rowpanel_count": C.c_int}
 
+# Entry points that serve ONLY the backbones' layers (frontend.py, postln.py, vit.py, attention.py):
+# not part of the hot path. Every other launching entry point is hot-path work and is
+# timed by bench.py (hot_path_entry_points), so a kernel added or renamed on the hot path is timed
+# by default; tests/test_cpu_host.py checks that no head module calls a name listed here.
+# Shared entry points (the GEMMs, column and slab sums) are hot-path ones whose backbone launches
+# carry meta=dict(backbone=True) and are reported apart.
+BACKBONE_ENTRY_POINTS = frozenset({
+    "triad_chgn_gelu_fwd", "triad_chgn_gelu_bwd", "triad_gemm_bf16_form", "triad_conv0_dw", "triad_c0gn_fwd",
+    "triad_posconv", "triad_posconv_dw", "triad_gemm_bf16_splitk", "triad_rows_nt", "triad_lora_update",
+    "triad_dropaddln_fwd", "triad_dropaddln_bwd", "triad_gelu_table", "triad_geludrop_fwd", "triad_geludrop_bwd",
+    "triad_dropout_keep", "triad_addln_fwd", "triad_addln_bwd", "triad_lora_tn", "triad_attn_dropmask",
+    "triad_attn_fwd_dropout", "triad_attn_bwd_dropout", "triad_attn_fwd", "triad_attn_bwd"})
+
+
+def hot_path_entry_points():
+    """Every entry point that launches work (not a size / count query) and is not backbone-only."""
+    return tuple(n for n in SIGNATURES if n not in RESTYPES and n not in BACKBONE_ENTRY_POINTS)
+
 
 
 class PairsimProblem(C.Structure):

@@ -93,23 +93,39 @@ def _fallback(name, what, err):
                   "download, or populate the HF cache).", RuntimeWarning, stacklevel=3)
 
 
+# architecture of a checkpoint NAME when only its name is known offline (AutoModel resolves it from
+# the checkpoint's config.json, which is not there): (name substring, model class, config class,
+# whether the HIP attention kernels serve it)
+_ARCH_BY_NAME = (("modernbert", "ModernBertModel", "ModernBertConfig", False),
+                 ("distilbert", "DistilBertModel", "DistilBertConfig", True),
+                 ("hubert", "HubertModel", "HubertConfig", True))
+
+
 def _hf_model(kind, name, config_overrides=None):
-    """Load `name` from the HF cache (or the hub with TRIAD_HF_ONLINE=1); when it is not there
-    (OSError -- the only failure that means "no such local checkpoint"), random-init its
-    architecture, warn and record it in RANDOM_INIT. Any other error propagates."""
+    """Load `name` from the HF cache (or the hub with TRIAD_HF_ONLINE=1) with `kind`
+    ("AutoModel" as model.py:80, or a concrete class as model.py:30); when it is not there
+    (OSError -- the only failure that means "no such local checkpoint"), random-init the
+    architecture its name denotes, warn and record it in RANDOM_INIT. Any other error propagates."""
     import transformers
     try:
         return install_fast_linear(getattr(transformers, kind).from_pretrained(
             name, local_files_only=not _hub_online()))
     except OSError as e:
-        _fallback(name, "random-init " + kind, e)
-    cfg_cls = {"HubertModel": transformers.HubertConfig, "DistilBertModel": transformers.DistilBertConfig}[kind]
-    cfg = cfg_cls(**(config_overrides or {}))
-    try:
-        cfg._attn_implementation = _register_attention()
-    except Exception:
-        pass
-    return install_fast_linear(getattr(transformers, kind)(cfg))
+        err = e
+    low = name.lower()
+    arch = next((a for a in _ARCH_BY_NAME if (a[1] == kind if kind != "AutoModel" else a[0] in low)), None)
+    if arch is None:
+        raise OSError(f"triad_amd: '{name}' is not available locally and its architecture is not one this "
+                      f"offline build can random-init ({', '.join(a[0] for a in _ARCH_BY_NAME)})") from err
+    _, model_cls, cfg_cls, triad_attn = arch
+    _fallback(name, "random-init " + model_cls, err)
+    cfg = getattr(transformers, cfg_cls)(**(config_overrides or {}))
+    if triad_attn:
+        try:
+            cfg._attn_implementation = _register_attention()
+        except Exception:
+            pass
+    return install_fast_linear(getattr(transformers, model_cls)(cfg))
 
 
 def _register_attention():
@@ -200,9 +216,11 @@ class HashTokenizer:
 
 
 class TextEmbedder(nn.Module):
-    """DistilBERT + projection head (model.py:72-118)."""
+    """BERT-like encoder + projection head (model.py:72-118). Like the reference, the default
+    encoder is ModernBERT-base (model.py:77) and MultiModalModel passes DistilBERT (model.py:335);
+    the encoder is whatever AutoModel resolves `model_name` to (model.py:80)."""
 
-    def __init__(self, embedding_dim=512, model_name="distilbert/distilbert-base-uncased"):
+    def __init__(self, embedding_dim=512, model_name="answerdotai/ModernBERT-base"):
         super().__init__()
         try:
             from transformers import AutoTokenizer
@@ -210,7 +228,7 @@ class TextEmbedder(nn.Module):
         except OSError as e:
             _fallback(model_name + " (tokenizer)", "HashTokenizer (hashed word ids)", e)
             self.tokenizer = HashTokenizer()
-        self.encoder = install_fused_distilbert(_hf_model("DistilBertModel", model_name))
+        self.encoder = install_fused_distilbert(_hf_model("AutoModel", model_name))  # no-op unless DistilBERT
         self.projection1 = nn.Linear(self.encoder.config.hidden_size, 512)
         self.layer_norm = nn.LayerNorm(512)
         self.projection2 = nn.Linear(512, embedding_dim)

@@ -352,24 +352,28 @@ def _fwd_keys_per_workgroup(R_pad, Bk):
     return jpw
 
 
-_STAGE = [None] * 16   # (pinned host tensor, event after its copy), round robin
+_STAGE = [None] * 16   # (persistent pinned int32 buffer, event after its last copy), round robin
 _STAGE_NEXT = [0]
 
 
 def _stage_h2d(arr, dev):
-    """int32 numpy array -> device tensor (async) through a ring of pinned slots; a slot is reused
-    only after the event recorded behind its copy has completed, so a copy the stream has not run
-    yet never reads a refilled buffer."""
+    """int32 numpy array -> device tensor (async) through a ring of persistent pinned slots (grow-only,
+    allocated once per slot: no per-call trip through the caching host allocator, which may
+    synchronise); a slot is refilled only after the event recorded behind its previous copy has
+    completed, so a copy the stream has not run yet never reads a refilled buffer."""
+    a = np.ascontiguousarray(arr, dtype=np.int32).reshape(-1)
     i = _STAGE_NEXT[0]
     _STAGE_NEXT[0] = (i + 1) % len(_STAGE)
     prev = _STAGE[i]
     if prev is not None:
         prev[1].synchronize()
-    host = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int32)).pin_memory()
-    out = host.to(dev, non_blocking=True)
+    buf = prev[0] if prev is not None and prev[0].numel() >= a.size else \
+        torch.empty(max(4096, 1 << (max(1, a.size) - 1).bit_length()), dtype=torch.int32, pin_memory=True)
+    buf.numpy()[:a.size] = a
+    out = buf[:a.size].to(dev, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
-    _STAGE[i] = (host, ev)
+    _STAGE[i] = (buf, ev)
     return out
 
 
@@ -434,9 +438,10 @@ def _fwd_meta(h):
     return dict(kind=h.kind, flops=2.0 * g.R * g.Bk * g.Nk_eff * D, grid=h.nparts * 512,
                 # algorithmic bytes: the feature operands + rowmax / argmax; the
                 # tiled unit-dS stream the training forward also writes is NOT algorithmic
-                # (bench.py reports it, from PMC, as traffic)
+                # (bench.py reports it, from PMC, as traffic): 2 KB per stored 32 x 32 tile, i.e.
+                # over the compacted key tiles when _compact left some out (h.nct of them)
                 bytes=2.0 * D * (g.R + g.Bk * g.Nk_eff) + 8.0 * g.Bk * g.R,
-                ds_bytes=(2.0 * g.R_pad * g.C_pad if h.dS is not None else 0.0))
+                ds_bytes=(2048.0 * (g.R_pad // 32) * h.nct if h.dS is not None else 0.0))
 
 
 def _head_launch(h, st):
@@ -1045,13 +1050,19 @@ ZERO_TILE_SKIP = os.environ.get("TRIAD_ZERO_TILE_SKIP", "1") != "0"
 
 def patch_dropout(x: torch.Tensor, keep_mask: torch.Tensor, n_out: Optional[int] = None) -> torch.Tensor:
     """(B, N, D) -> (B, max_b kept_b, D): kept tokens in order, zero padded (model.py:282-307).
-    n_out overrides the padded length (global negatives pad to the global maximum)."""
+    n_out overrides the padded length (global negatives pad to the global maximum).
+    keep_mask is a HOST (B, N) bool tensor: the padded length and the compaction plan are host
+    values, so a device mask would cost a device->host synchronisation every step; it is refused
+    rather than silently synchronised (the model draws its masks on the host, draw_keep_mask)."""
     _check_device(x)
+    if keep_mask.is_cuda:
+        raise TriadError("patch_dropout: keep_mask must be a host tensor (the compaction plan is built on the "
+                         "host; a device mask would synchronise the device every step) -- pass keep_mask.cpu()")
     idx, inv, n_out = dropout_indices(keep_mask, n_out)
     idx_d = _lib.h2d(idx.contiguous(), x.device)
     inv_d = _lib.h2d(inv.contiguous(), x.device)
     out = _GatherRows.apply(x.contiguous(), idx_d, inv_d)
-    setattr(out, KEPT_ROWS_ATTR, keep_mask.detach().to("cpu", torch.bool).sum(1).to(torch.int32))
+    setattr(out, KEPT_ROWS_ATTR, keep_mask.detach().to(torch.bool).sum(1).to(torch.int32))
     return out
 
 

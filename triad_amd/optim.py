@@ -224,6 +224,16 @@ class FlatParamSpace:
         if self._held is not None:   # the previous gather has read its .grad tensors: release them
             self._held[1].synchronize()
             self._held = None
+        self._gather_launch(accumulate)
+
+    def release_held_grads(self):
+        """Drop the .grad tensors the last gather read as soon as its launch has run (a non-blocking
+        event query; TriadTrainer.step polls it at the step's start and before backward), so the
+        caching allocator can reuse them during the step instead of only at the next gather."""
+        if self._held is not None and self._held[1].query():
+            self._held = None
+
+    def _gather_launch(self, accumulate: bool):
         src, dst, cnt, f32s, ids, grads = [], [], [], [], [], []
         for i in np.nonzero(self.gathered)[0]:
             p = self.params[i]

@@ -29,6 +29,7 @@ import os
 import random
 from typing import Dict, List, Sequence
 
+import numpy as np
 import torch
 
 from . import ops
@@ -48,10 +49,22 @@ def _pack(feats: Sequence[torch.Tensor], device, rows_multiple: int):
     return out, lens, n_max
 
 
-def _pack_f32(feats: Sequence[torch.Tensor], device):
-    """list of (n_i, D) -> zero-padded (N, n_pad, D) fp32 (n_pad a multiple of 64) + device lengths."""
+def _feature_width(*lists) -> int:
+    """The common feature width of every (n_i, D) tensor in `lists`; the fp32 scorer takes any
+    D that is a multiple of 32 (its 32-wide k step)."""
+    widths = {int(f.shape[-1]) for feats in lists for f in feats}
+    if len(widths) != 1:
+        raise ops.TriadError(f"retrieval features must share one width, got {sorted(widths)}")
+    (d,) = widths
+    if d <= 0 or d % 32:
+        raise ops.TriadError(f"the fp32 retrieval scorer needs a feature width that is a multiple of 32, got {d}")
+    return d
+
+
+def _pack_f32(feats: Sequence[torch.Tensor], device, d: int):
+    """list of (n_i, d) -> zero-padded (N, n_pad, d) fp32 (n_pad a multiple of 64) + device lengths."""
     n_pad = ops._rup(max(int(f.shape[0]) for f in feats), 64)
-    out = torch.zeros(len(feats), n_pad, D, dtype=torch.float32, device=device)
+    out = torch.zeros(len(feats), n_pad, d, dtype=torch.float32, device=device)
     for i, f in enumerate(feats):
         out[i, :f.shape[0]] = f.to(device, torch.float32)
     lens = torch.tensor([int(f.shape[0]) for f in feats], dtype=torch.int32).to(device)
@@ -63,12 +76,51 @@ def aggregated_similarity_f32(queries: Sequence[torch.Tensor], items: Sequence[t
     """aggregated_similarity in the reference's fp32 arithmetic (retrieval.py:106-114: fp32 matmul,
     division by the temperature, max, mean) -- all pairs in one triad_retrieval_maxmean_f32 launch."""
     dev = torch.device(device)
-    Q, qlen, nq_pad = _pack_f32(queries, dev)
-    K, klen, nk_pad = _pack_f32(items, dev)
+    d = _feature_width(queries, items)
+    Q, qlen, nq_pad = _pack_f32(queries, dev, d)
+    K, klen, nk_pad = _pack_f32(items, dev, d)
     sim = torch.empty(len(queries), len(items), dtype=torch.float32, device=dev)
     call("triad_retrieval_maxmean_f32", ptr(Q), ptr(qlen), len(queries), nq_pad, ptr(K), ptr(klen), len(items),
-         nk_pad, D, float(temperature), ptr(sim), stream_ptr(dev))
+         nk_pad, d, float(temperature), ptr(sim), stream_ptr(dev))
     return sim
+
+
+# ---- the reference's per-pair aggregators and recall (retrieval.py:106-144, 190-198) -----------
+# Same names, arguments and return types (a Python float / a dict of r1..r20). Each pair is one
+# launch of the fp32 scorer -- the reference's arithmetic (fp32 products, division by the
+# temperature, max, mean) -- so a caller looping over pairs as retrieval.py does gets its numbers;
+# the all-pairs matrices of compute_*_retrieval_metrics take one launch per direction instead.
+def _pair_maxmean(q_feats, k_feats, temperature) -> float:
+    dev = q_feats.device if q_feats.is_cuda else k_feats.device
+    return float(aggregated_similarity_f32([q_feats], [k_feats], float(temperature), dev)[0, 0])
+
+
+def aggregator_av_a2v(a_feats, v_feats, temperature):
+    """retrieval.py:106-110: mean over audio tokens of the max over visual tokens of a.v / temp."""
+    return _pair_maxmean(a_feats, v_feats, temperature)
+
+
+def aggregator_av_v2a(a_feats, v_feats, temperature):
+    """retrieval.py:112-115: mean over visual tokens of the max over audio tokens of a.v / temp."""
+    return _pair_maxmean(v_feats, a_feats, temperature)
+
+
+def aggregator_tv_t2v(t_feats, v_feats, temperature):
+    """retrieval.py:190-193: mean over text tokens of the max over visual tokens of t.v / temp."""
+    return _pair_maxmean(t_feats, v_feats, temperature)
+
+
+def aggregator_tv_v2t(t_feats, v_feats, temperature):
+    """retrieval.py:195-198: mean over visual tokens of the max over text tokens of t.v / temp."""
+    return _pair_maxmean(v_feats, t_feats, temperature)
+
+
+def compute_recall_at_k(sim_matrix):
+    """retrieval.py:117-144: R@1/5/10/20 of an N x N matrix (numpy or torch), the match at j = i,
+    ranks with the reference's own tie order (per-row numpy argsort of -row)."""
+    sim = sim_matrix if isinstance(sim_matrix, torch.Tensor) else torch.from_numpy(
+        np.asarray(sim_matrix, dtype=np.float32))
+    return recall_at_k(sim, ks=(1, 5, 10, 20), ties="reference")
 
 
 def aggregated_similarity(queries: Sequence[torch.Tensor], items: Sequence[torch.Tensor], temperature: float,
@@ -117,7 +169,6 @@ def ranks(sim: torch.Tensor, ties: str = "reference") -> torch.Tensor:
         return ahead.sum(1)
     if ties != "reference":
         raise ValueError(f"ties must be 'reference' or 'stable', not {ties!r}")
-    import numpy as np
     s = sim.detach().to(torch.float32).cpu().numpy()
     order = np.argsort(-s, axis=1)   # row-wise identical to the reference's per-row np.argsort(-row)
     return torch.from_numpy((order == np.arange(s.shape[0])[:, None]).argmax(1))

@@ -196,6 +196,8 @@ class TriadTrainer:
         """One training step (forward + backward [+ optimizer at the accumulation boundary]).
         Returns a dict of device tensors (nothing is synchronised)."""
         self._update_frozen_params(self.global_step)
+        if self.space is not None:
+            self.space.release_held_grads()
         m = self.model
         out: Dict[str, torch.Tensor] = {}
         av = tv = None
@@ -209,6 +211,8 @@ class TriadTrainer:
         av_loss = av[0] if av is not None else None
         tv_loss = tv[0] if tv is not None else None
         loss_total = self._loss_mix(phase, av_loss, tv_loss, progress)
+        if self.space is not None:
+            self.space.release_held_grads()
         if self.reducer is not None and (self.accumulation_counter + 1) % self.grad_accum == 0:
             self.reducer.begin(accumulate=self.accumulation_counter % self.grad_accum != 0)
         (loss_total / self.grad_accum).backward()
