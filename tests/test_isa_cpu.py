@@ -17,7 +17,11 @@
 3. The direct-B tile GEMM keeps its B prefetch in flight: in the steady-state loop every wait hipcc
    emits before an MFMA leaves >= 8 loads outstanding (two stages of four B loads), i.e. the
    restructured loop (whole groups of stages, no exit inside, unconditional prefetch) lets hipcc
-   count exactly instead of draining the ring at a merge point."""
+   count exactly instead of draining the ring at a merge point.
+4. Every hand-counted wait matches what hipcc emitted: the forward's sync_tile constants are
+   re-derived from the LDS-DMA pieces and dS stores per tile found in its stage loop, and every
+   tail stage of the direct-B and row-panel GEMMs drains (vmcnt(0)) before its barrier. Each check
+   fails when a counted constant is edited by one (verified by hand)."""
 import concurrent.futures as cf
 import os
 import re
@@ -163,8 +167,7 @@ def test_direct_b_tail_stages_drain_before_their_barrier(isa):
     hipcc removes it), so the loop's counted wait would under-count the VMEM ops in flight (round 5:
     AV dK with a 2-stage tail was non-deterministic). Every barrier there must follow a vmcnt(0)."""
     checked = 0
-    # (the row-panel kernels' epilogues have barriers of their own after the tail; only the
-    # direct-B tile GEMMs, whose epilogue has none, are checked mechanically here)
+    # (the row-panel kernels' tails: test_rowgemm_tail_stages_drain_before_their_barrier)
     for f, pat in (("bwd_gemm.hip", "tile_gemm_db16_kernel"),):
         for sym, lines in _kernels(isa[f]).items():
             if pat not in sym or not any("Loop Header" in l for l in lines):
@@ -184,4 +187,121 @@ def test_direct_b_tail_stages_drain_before_their_barrier(isa):
                     assert last_vm == 0, (f, sym, last_vm)
             assert tail_barriers >= 1, (f, sym)
             checked += 1
+    assert checked >= 4, checked
+
+
+def _loop_span(lines):
+    """(header index, back-branch index) of the kernel's first loop."""
+    hdr = next(i for i, l in enumerate(lines) if "Loop Header" in l)
+    label = lines[hdr].split(":")[0]
+    back = max(i for i, l in enumerate(lines) if re.match(r"s_(cbranch_\w+|branch)\s+" + re.escape(label) + r"$", l))
+    return hdr, back
+
+
+def _loop_lines(lines):
+    """Indices of the lines of the kernel's first loop: the header block and every block hipcc
+    annotates as in that loop (some are placed after the back branch)."""
+    hdr = next(i for i, l in enumerate(lines) if "Loop Header" in l)
+    tag = "Header=" + lines[hdr].split(":")[0].lstrip(".L")
+    out, inside = [], False
+    for i, l in enumerate(lines):
+        if re.match(r"^(\.LBB\d+_\d+:|; %bb\.\d+:)", l):
+            inside = i == hdr or (tag in l and "in Loop" in l)
+        if inside:
+            out.append(i)
+    return out
+
+
+def _asm_runs(lines, lo, hi, idx=None):
+    """Inside lines[lo:hi] (or at the indices idx): the runs of inline-asm VMEM ops ('D' = LDS-DMA piece, 'S' = store),
+    each run a maximal sequence of one kind with no other VMEM op or label between, as
+    (kind, count, first line); and the immediates of the inline-asm `s_waitcnt vmcnt(N)`."""
+    runs, waits, inside = [], [], False
+    for i in (range(lo, hi) if idx is None else idx):
+        t = lines[i]
+        if t.startswith(";;#ASMSTART"):
+            inside = True
+            continue
+        if t.startswith(";;#ASMEND"):
+            inside = False
+            continue
+        if re.match(r"^(\.LBB\d+_\d+:|; %bb\.\d+:|s_branch |s_cbranch_)", t):   # a block boundary ends a run
+            runs.append(("|", 0, i))
+            continue
+        if not t or t[0] in ";.":
+            continue
+        op = t.split()[0]
+        m = re.match(r"s_waitcnt\s.*vmcnt\((\d+)\)", t)
+        if m and inside:
+            waits.append(int(m.group(1)))
+        if not re.match(r"(global_|buffer_|flat_|scratch_)(load|store|atomic)", op):
+            continue
+        if inside and (op.startswith("global_load_lds") or (op.startswith("buffer_load") and re.search(r"\blds\b", t))):
+            k = "D"
+        elif inside and "_store" in op:
+            k = "S"
+        else:
+            k = "x"   # an ordinary (compiler-counted) VMEM op
+        if runs and runs[-1][0] == k:
+            runs[-1] = (k, runs[-1][1] + 1, runs[-1][2])
+        else:
+            runs.append((k, 1, i))
+    return [r for r in runs if r[0] != "|"], waits
+
+
+def test_forward_counted_waits_match_emitted_vmem(isa):
+    """The training forward's sync_tile (pairsim_fwd.hip) hand-counts its vmcnt: younger than the
+    key tile about to be read are the DMA pieces of nd = min(1, tiles left) later tiles and the dS
+    stores of ns = min(1, b - 1) earlier epilogues, so it waits vmcnt(nd G + ns S) for G pieces per
+    tile and S stores per epilogue. Here G and S are read off what hipcc emitted: every prefetch in
+    the stage loop is one run of G asm LDS-DMA pieces, every epilogue one run of S asm stores, the
+    runs alternate (a tile's pieces before the next epilogue's stores, nothing counted between), and
+    the counted waits in the loop are exactly {nd G + ns S} -- a constant off by one, a piece or a
+    store hipcc dropped or duplicated, or a reordering fails. The prologue's sync_tile(0) waits
+    vmcnt(nd G) after exactly NBUF - 1 = 2 prefetches."""
+    asm = isa["pairsim_fwd.hip"]
+    ks = {s: l for s, l in _kernels(asm).items()
+          if ("pairsim_fwd2_kernelILb1E" in s or "pairsim_fwd_multi_kernelILb1E" in s)}
+    assert len(ks) == 3, list(ks)   # training: fwd2 <SHORTQ 0/1>, multi
+    for sym, lines in ks.items():
+        hdr, _ = _loop_span(lines)
+        runs, waits = _asm_runs(lines, 0, 0, _loop_lines(lines))
+        d_runs = [n for k, n, _ in runs if k == "D"]
+        s_runs = [n for k, n, _ in runs if k == "S"]
+        assert d_runs and s_runs and len(set(d_runs)) == 1 and len(set(s_runs)) == 1, (sym, runs)
+        G, S = d_runs[0], s_runs[0]
+        assert (G, S) == (4, 2), (sym, G, S)   # GLDS_PER_TILE = 32 / WAVES; two 1 KB stores per tile
+        kinds = [k for k, _, _ in runs if k in "DS"]
+        assert kinds == ["D", "S"] * (len(kinds) // 2), (sym, kinds)
+        assert set(waits) == {0, G, S, G + S}, (sym, sorted(set(waits)), (G, S))
+        pro_runs, pro_waits = _asm_runs(lines, 0, hdr)
+        pro_d = [n for k, n, _ in pro_runs if k == "D"]
+        assert pro_d[:2] == [G, G] and set(pro_waits) <= {0, G}, (sym, pro_runs, pro_waits)
+
+
+def test_rowgemm_tail_stages_drain_before_their_barrier(isa):
+    """The row-panel projection GEMMs (rowgemm.hip) run whole groups of stages in the loop and the
+    trailing ones in straight-line code, like the direct-B tile GEMM; their B prefetches feed no
+    later stage there, so hipcc removes them and a counted wait would under-count (round 5's race).
+    Every barrier after the loop that is followed by MFMA work (a tail stage, or the fused form's
+    second GEMM from the LDS panel) must follow a vmcnt(0); the epilogue's own barriers (LDS
+    reductions, no MFMA) are not stages."""
+    checked = 0
+    for sym, lines in _kernels(isa["rowgemm.hip"]).items():
+        if not any("Loop Header" in l for l in lines):
+            continue
+        _, back = _loop_span(lines)
+        tail = lines[back + 1:]
+        last_vm, stages = None, 0
+        for i, l in enumerate(tail):
+            m = re.match(r"s_waitcnt\s.*vmcnt\((\d+)\)", l)
+            if m:
+                last_vm = int(m.group(1))
+            elif l.startswith("s_barrier"):
+                nxt = next((j for j in range(i + 1, len(tail)) if tail[j].startswith("s_barrier")), len(tail))
+                if any(t.startswith("v_mfma") for t in tail[i + 1:nxt]):
+                    stages += 1
+                    assert last_vm == 0, (sym, i, last_vm)
+        assert stages >= 1, sym
+        checked += 1
     assert checked >= 4, checked

@@ -213,6 +213,13 @@ __device__ __forceinline__ float epi_fixup(Epi& e, const f32x16& p, float su, fl
   return st;
 }
 
+// A wave-uniform int read through the scalar cache (s_load: lgkmcnt): a per-tile read of the key
+// lengths (retrieval) as a vector load made hipcc drain vmcnt(0) right after it in the tile loop --
+// the prefetched key tiles and the dS stores included. The lengths are written before the launch.
+__device__ __forceinline__ int load_uniform(const int* p, int i) {
+  return *((const __attribute__((address_space(4))) int*)p + i);
+}
+
 struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in the walk
   int j, kb;
   int t = 0;  // tiles walked so far (fwd_body: the tile's index among the workgroup's stored tiles)
@@ -349,18 +356,30 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     // (3-slot ring; a 2-slot ring has no younger tile in flight)
     // (general ring: the DMAs of tiles b+1 .. b+NBUF-2 below nblocks and the stores of the
     // epilogues of tiles b-NBUF+1 .. b-2; the oldest younger epilogue's stores are waited for)
+    // (only the cases the ring can reach are compiled, so each counted wait in the ISA decodes to
+    // one (nd, ns): tests/test_isa_cpu.py checks every one against the VMEM ops hipcc emitted)
     const int nd = min(NBUF - 2, nblocks - 1 - b);
     const int ns = TRAIN ? max(0, min(NBUF - 2, b - 1)) : 0;
-    switch (nd * 2 + ns * 16) {
-      case 2: TRIAD_VMCNT(GLDS_PER_TILE); break;
-      case 4: TRIAD_VMCNT(2 * GLDS_PER_TILE); break;
-      case 16: TRIAD_VMCNT(2); break;
-      case 18: TRIAD_VMCNT(GLDS_PER_TILE + 2); break;
-      case 20: TRIAD_VMCNT(2 * GLDS_PER_TILE + 2); break;
-      case 32: TRIAD_VMCNT(4); break;
-      case 34: TRIAD_VMCNT(GLDS_PER_TILE + 4); break;
-      case 36: TRIAD_VMCNT(2 * GLDS_PER_TILE + 4); break;
-      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    if constexpr (NBUF == 3) {
+      switch (nd * 2 + ns * 16) {
+        case 2: TRIAD_VMCNT(GLDS_PER_TILE); break;
+        case 16: TRIAD_VMCNT(2); break;
+        case 18: TRIAD_VMCNT(GLDS_PER_TILE + 2); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      }
+    } else {
+      static_assert(NBUF == 4, "sync_tile's counted waits cover 3- and 4-slot rings");
+      switch (nd * 2 + ns * 16) {
+        case 2: TRIAD_VMCNT(GLDS_PER_TILE); break;
+        case 4: TRIAD_VMCNT(2 * GLDS_PER_TILE); break;
+        case 16: TRIAD_VMCNT(2); break;
+        case 18: TRIAD_VMCNT(GLDS_PER_TILE + 2); break;
+        case 20: TRIAD_VMCNT(2 * GLDS_PER_TILE + 2); break;
+        case 32: TRIAD_VMCNT(4); break;
+        case 34: TRIAD_VMCNT(GLDS_PER_TILE + 4); break;
+        case 36: TRIAD_VMCNT(2 * GLDS_PER_TILE + 4); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      }
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -435,7 +454,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   using F = std::false_type;
   // epilogue variant of tile ec: FULL unless its sample's valid keys end inside it
   auto tile_full = [&]() __attribute__((always_inline)) {
-    const int nk = a.klen ? min(a.klen[ec.j], a.Nk_eff) : a.Nk_eff;
+    const int nk = a.klen ? min(load_uniform(a.klen, ec.j), a.Nk_eff) : a.Nk_eff;
     const int nv = __builtin_amdgcn_readfirstlane(nk - ec.kb * 32);
     e.nn2 = (f32x2){0.f, 0.f};
     e.mn = INFINITY;
@@ -714,7 +733,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
   using T = std::true_type;
   using F = std::false_type;
   auto tile_full = [&]() __attribute__((always_inline)) {
-    const int nk = a.klen ? min(a.klen[ec.j], a.Nk_eff) : a.Nk_eff;
+    const int nk = a.klen ? min(load_uniform(a.klen, ec.j), a.Nk_eff) : a.Nk_eff;
     const int nv = __builtin_amdgcn_readfirstlane(nk - ec.kb * 32);
     e.nn2 = (f32x2){0.f, 0.f};
     e.mn = INFINITY;
