@@ -423,7 +423,8 @@ def main():
                        "name": a.config, "phase": cfg["phase"],
                        "global_batch": a.batch * world, "per_gpu_batch": a.batch, "parallelism": f"dp{world}",
                        "negatives": (f"global (Mode G): each rank's queries against all {a.batch * world} key "
-                                     f"samples (RCCL all-gather / reduce-scatter in the head)" if mode_g else
+                                     f"samples (key all-gather, clip-row gather and key-gradient reduce-scatter inside the head, "
+                                     f"on the {dist.get_backend() if world > 1 else 'nccl'} backend)" if mode_g else
                                      "local (Mode R): each rank's reference loss over its own batch"),
                        "gradient_accumulation_steps": 1,
                        "gradient_accumulation_note": "one triple = one sample through one optimizer step at "
