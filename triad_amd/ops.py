@@ -816,10 +816,10 @@ def _rows_view(h):
 
 def _head_weight_grads(w_refs, dyp, ln, dy1, hb, M, Mp, H, w1d, w2d):
     """(dW2, dW1) of a projection head: dW2 = dy^T ln, dW1 = dy1^T h on the split-K GEMM
-    (_dw_plan), bf16 straight from the slab reduction for bf16 model weights. For bf16 weights at
-    their first use in the backward pass they go to the backbone weight-gradient side stream
-    (linear.on_side_stream), so the backbone's backward -- queued on this stream right after dh --
-    does not wait for them (VERDICT r4 #2: the heads' dW where the backbones leave CUs idle)."""
+    (_dw_plan), bf16 straight from the slab reduction for bf16 model weights. On the head's own
+    stream by default; with TRIAD_HEAD_DW_SIDE=1 bf16 weights at their first use in the backward pass
+    go to the backbone weight-gradient side stream (linear.on_side_stream) -- measured no faster, and
+    there they share the CUs of the audio backbone's backward GEMMs (HEAD_DW_SIDE_STREAM below)."""
     from . import linear as _lin
 
     def run():
@@ -836,9 +836,19 @@ def _head_weight_grads(w_refs, dyp, ln, dy1, hb, M, Mp, H, w1d, w2d):
              o1, f1, st, meta=dict(tag=f"proj-dW1x{M}", flops=2.0 * M * D * H))
         return dw2, dw1
 
-    if dyp.is_cuda and _lin.side_stream_ok(*w_refs):
+    if dyp.is_cuda and HEAD_DW_SIDE_STREAM and _lin.side_stream_ok(*w_refs):
         return _lin.on_side_stream(run, (dyp, ln, dy1, hb))
     return run()
+
+
+# The projection heads' weight gradients run in order on the head's own stream (default) or on the
+# backbone dW side stream (TRIAD_HEAD_DW_SIDE=1, round 5's form). Same box, alternated, bench step
+# (profiles/r06_head_dw_side_ab.log): throughput equal (1938.7 / 1936.8 side vs 1940.7 / 1936.7 own
+# stream), the heads' summed launch time 2.72-2.76 -> 2.33-2.35 ms per step: on the side stream the
+# visual / audio dW launches ran 40-52 us alone but 132-153 us (median) overlapped 75-81 % of their
+# time by HuBERT's backward GEMMs on the audio stream (profiles/r06_head_dw_trace_side_stream.txt,
+# tools/head_dw_trace.py) -- they shared CUs rather than filling idle ones.
+HEAD_DW_SIDE_STREAM = os.environ.get("TRIAD_HEAD_DW_SIDE", "0") == "1"
 
 
 class _ProjectionHeadRows(torch.autograd.Function):
