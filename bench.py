@@ -373,6 +373,11 @@ def main():
                                   / 1e12 / PEAK_BF16_TFLOPS
                                   for k, v in sorted(rep_o.items()) if v["flops"] and not k.endswith("[backbone]")
                                   and ("pairsim" in k or "tile_gemm" in k)}
+        # every hot-path launch of this mode too (the projection heads' GEMMs / passes included), so
+        # a launch's time alone on the CUs can be read beside its time on concurrent streams
+        single["kernels_ms"] = {k: {"avg_ms": v["ms"] / max(1, v["launches"]),
+                                    "launches_per_step": v["launches"] / a.single_stream_steps}
+                                for k, v in sorted(rep_o.items()) if not k.endswith("[backbone]")}
         pko = [k for k in rep_o if "[proj" in k]
         po_ms = sum(rep_o[k]["ms"] for k in pko) / a.single_stream_steps
         po_fl = sum(rep_o[k]["flops"] for k in pko) / a.single_stream_steps

@@ -75,7 +75,7 @@ def _kernels(asm):
             cur = m.group(1)
             out[cur] = []
         elif cur is not None:
-            if line.strip().startswith("s_endpgm"):
+            if line.strip().startswith(".Lfunc_end"):   # a kernel may have several s_endpgm exits
                 cur = None
             else:
                 out[cur].append(line.strip())
@@ -198,10 +198,11 @@ def _loop_span(lines):
     return hdr, back
 
 
-def _loop_lines(lines):
-    """Indices of the lines of the kernel's first loop: the header block and every block hipcc
-    annotates as in that loop (some are placed after the back branch)."""
-    hdr = next(i for i, l in enumerate(lines) if "Loop Header" in l)
+def _loop_lines(lines, hdr=None):
+    """Indices of the lines of one loop (default: the kernel's first): the header block and every
+    block hipcc annotates as in that loop (some are placed after the back branch)."""
+    if hdr is None:
+        hdr = next(i for i, l in enumerate(lines) if "Loop Header" in l)
     tag = "Header=" + lines[hdr].split(":")[0].lstrip(".L")
     out, inside = [], False
     for i, l in enumerate(lines):
@@ -264,19 +265,28 @@ def test_forward_counted_waits_match_emitted_vmem(isa):
           if ("pairsim_fwd2_kernelILb1E" in s or "pairsim_fwd_multi_kernelILb1E" in s)}
     assert len(ks) == 3, list(ks)   # training: fwd2 <SHORTQ 0/1>, multi
     for sym, lines in ks.items():
-        hdr, _ = _loop_span(lines)
-        runs, waits = _asm_runs(lines, 0, 0, _loop_lines(lines))
-        d_runs = [n for k, n, _ in runs if k == "D"]
-        s_runs = [n for k, n, _ in runs if k == "S"]
-        assert d_runs and s_runs and len(set(d_runs)) == 1 and len(set(s_runs)) == 1, (sym, runs)
-        G, S = d_runs[0], s_runs[0]
-        assert (G, S) == (4, 2), (sym, G, S)   # GLDS_PER_TILE = 32 / WAVES; two 1 KB stores per tile
-        kinds = [k for k, _, _ in runs if k in "DS"]
-        assert kinds == ["D", "S"] * (len(kinds) // 2), (sym, kinds)
-        assert set(waits) == {0, G, S, G + S}, (sym, sorted(set(waits)), (G, S))
-        pro_runs, pro_waits = _asm_runs(lines, 0, hdr)
-        pro_d = [n for k, n, _ in pro_runs if k == "D"]
-        assert pro_d[:2] == [G, G] and set(pro_waits) <= {0, G}, (sym, pro_runs, pro_waits)
+        # one stage loop per training body (the fast and the exact epilogue, FwdArgs::exact)
+        hdrs = [i for i, l in enumerate(lines) if "Loop Header" in l and "Depth=1" in l]
+        assert len(hdrs) == 2, (sym, len(hdrs))
+        prev = 0
+        for hdr in hdrs:
+            loop = _loop_lines(lines, hdr)
+            runs, waits = _asm_runs(lines, 0, 0, loop)
+            d_runs = [n for k, n, _ in runs if k == "D"]
+            s_runs = [n for k, n, _ in runs if k == "S"]
+            assert d_runs and s_runs and len(set(d_runs)) == 1 and len(set(s_runs)) == 1, (sym, runs)
+            G, S = d_runs[0], s_runs[0]
+            assert (G, S) == (4, 2), (sym, G, S)   # GLDS_PER_TILE = 32 / WAVES; two 1 KB stores per tile
+            kinds = [k for k, _, _ in runs if k in "DS"]
+            assert kinds == ["D", "S"] * (len(kinds) // 2), (sym, kinds)
+            assert set(waits) == {0, G, S, G + S}, (sym, sorted(set(waits)), (G, S))
+            # this body's prologue: the code since the previous loop outside any loop
+            inloop = set(loop)
+            pro = [i for i in range(prev, hdr) if i not in inloop]
+            pro_runs, pro_waits = _asm_runs(lines, 0, 0, pro)
+            pro_d = [n for k, n, _ in pro_runs if k == "D"]
+            assert pro_d[:2] == [G, G] and set(pro_waits) <= {0, G}, (sym, pro_runs, pro_waits)
+            prev = max(loop) + 1
 
 
 def test_rowgemm_tail_stages_drain_before_their_barrier(isa):

@@ -49,7 +49,16 @@ struct FwdArgs {
   double* part2;
   const int* klen;
   const int* ktiles;  // training: stored key tiles per sample as an exclusive prefix sum (compact K / dS), or null
+  int exact;          // training: exact epilogue (fwd_body<true, true>), see exact_epilogue()
 };
+
+// Which training epilogue a head runs. The fast form computes d = su * clamp(u, lo, 0) and redoes
+// the whole tile (89 VALU per wave, after the MFMA chain) when any u < lo; the exact form selects
+// per element inside the chain (+3 VALU per element). Measured on the c3 shapes
+// (profiles/r06_fwd_exact_ab.log, alternated three times, features N(0, 0.58^2)): TV (clamp -20,
+// most tiles hold some S < -20) 0.543-0.570 -> 0.493-0.497 ms with the exact form; AV (clamp -60,
+// few tiles reach it) 3.04 -> 3.14 ms. So: exact for windows whose lower clamp is at most 30 below 0.
+inline int exact_epilogue(float clamp_lo) { return clamp_lo >= -30.f ? 1 : 0; }
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
@@ -127,6 +136,8 @@ struct Epi {  // per-lane epilogue state (one 32-row block)
   float mn;   // min u over the tile: any u < lo/su sends the tile through epi_fixup
   float prev;  // previous element's c (pairs into one packed op)
   unsigned pk[8];
+  float prevd;  // EXACT: previous element's d
+  f32x2 st2;    // EXACT: sum of d^2 over the tile (pairs of elements)
 };
 
 // key offset of accumulator element v inside a 32-key tile, without the 4h lane part
@@ -154,6 +165,9 @@ __device__ __forceinline__ float fma_sq(float c, float acc) {  // acc + c * c
   asm("v_fmac_f32 %0, %1, %1" : "+v"(acc) : "v"(c));
   return acc;
 }
+// u >= lo ? c : 0 -- plain C so hipcc's hazard recognizer sees the VALU-written lane mask the
+// select reads (v_cmp + v_cndmask)
+__device__ __forceinline__ float selge(float u, float lo, float c) { return u >= lo ? c : 0.f; }
 __device__ __forceinline__ float mulf(float a, float b) {
   float r;
   asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -164,7 +178,7 @@ __device__ __forceinline__ float mulf(float a, float b) {
 // place (keeps the epilogue interleaved with the MFMA chain instead of sunk past it).
 #define PIN(v) asm volatile("" : "+v"(v))
 
-template <bool TRAIN, bool FULL>
+template <bool TRAIN, bool FULL, bool EXACT>
 __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 su2, float lo) {
   const float u = p[v];
   if constexpr (FULL) {
@@ -178,21 +192,41 @@ __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 s
   }
   // padded keys are zero vectors (u = 0): they add nothing below without a mask
   const float c = __builtin_amdgcn_fmed3f(u, lo, 0.f);
+  // EXACT: the unit gradient per element, d = c inside the window [lo, 0] and 0 below it (the
+  // clamp's gradient), and the window's sum of d^2 beside the sum of c^2 -- no per-tile slow form
+  float dd = 0.f;
+  if constexpr (TRAIN && EXACT) {
+    dd = selge(u, lo, c);
+    if (v & 1) {
+      e.st2.x = fma_sq(e.prevd, e.st2.x);
+      e.st2.y = fma_sq(dd, e.st2.y);
+      PIN(e.st2);
+    }
+  }
   if (v & 1) {
     const f32x2 cc = {e.prev, c};
     e.nn2.x = fma_sq(cc.x, e.nn2.x);
     e.nn2.y = fma_sq(cc.y, e.nn2.y);
     PIN(e.nn2);
     if constexpr (TRAIN) {
-      e.mn = min3f(e.mn, p[v - 1], u);
-      const f32x2 d = {mulf(cc.x, su2.x), mulf(cc.y, su2.y)};
+      f32x2 d;
+      if constexpr (EXACT) {
+        d = (f32x2){mulf(e.prevd, su2.x), mulf(dd, su2.y)};
+      } else {
+        e.mn = min3f(e.mn, p[v - 1], u);
+        d = (f32x2){mulf(cc.x, su2.x), mulf(cc.y, su2.y)};
+        PIN(e.mn);
+      }
       e.pk[v >> 1] = pack_bf16x2(d.x, d.y);
-      PIN(e.mn);
       PIN(e.pk[v >> 1]);
     }
   } else {
     e.prev = c;
     PIN(e.prev);
+    if constexpr (TRAIN && EXACT) {
+      e.prevd = dd;
+      PIN(e.prevd);
+    }
   }
   PIN(e.m);
   PIN(e.at);
@@ -254,8 +288,10 @@ template <bool TRAIN>
 constexpr int kbuf_elems = (TRAIN ? NBUF : NBUF16) * KT_ELEMS + 16 * WAVES;
 
 // One workgroup of the forward: 256-row block bx, key-sample split by (of gx row blocks) of
-// problem a. kbuf = the workgroup's LDS (key ring + reduction scratch).
-template <bool TRAIN>
+// problem a. kbuf = the workgroup's LDS (key ring + reduction scratch). EXACT (training): the
+// unit gradient exact per element inside the MFMA chain instead of the fast form plus a slow
+// per-tile redo when some u < lo (FwdArgs::exact, chosen per head by the host).
+template <bool TRAIN, bool EXACT = false>
 __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int bx, const int by, const int gx) {
   double* red = (double*)(kbuf + NBUF * KT_ELEMS);
 
@@ -390,8 +426,10 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     const float nn = e.nn2.x + e.nn2.y;
     accd += (double)nn;
     if (TRAIN) {
+      float st;
+      if constexpr (EXACT) st = e.st2.x + e.st2.y;
       // some u below the window in this wave's tile: redo d (wave-uniform branch)
-      const float st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup(e, p, su, lo) : nn;
+      else st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup(e, p, su, lo) : nn;
       accd2 += (double)st;
       // canonical chunks 2 lane, 2 lane + 1 at ds_chunk(): two 1 KB contiguous stores per wave
       bf16* d = dS_w + ((long long)tile0 + ec.t) * 1024 + lane * 8;
@@ -438,7 +476,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
         if (s + P < NS) af[(s + P) % (P + 1)] = *(const bf16x8*)(kt + xo[(s + P) & 7] + ((s + P) >> 3) * 256);
         c = mfma32(af[s % (P + 1)], qf[s], c);
         if constexpr (ep) {
-          if (s & 1) epi_elem<TRAIN, full>(e, p, s >> 1, su2, lo);
+          if (s & 1) epi_elem<TRAIN, full, EXACT>(e, p, s >> 1, su2, lo);
         }
         // scheduling regions of 4 k-steps: two epilogue elements interleave and fill each
         // other's VALU->SGPR-mask wait states
@@ -446,7 +484,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       }
     } else if constexpr (ep) {
 #pragma unroll
-      for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full>(e, p, v, su2, lo);
+      for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full, EXACT>(e, p, v, su2, lo);
     }
     if constexpr (ep) epi_end(p);
   };
@@ -458,6 +496,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     const int nv = __builtin_amdgcn_readfirstlane(nk - ec.kb * 32);
     e.nn2 = (f32x2){0.f, 0.f};
     e.mn = INFINITY;
+    if constexpr (EXACT) e.st2 = (f32x2){0.f, 0.f};
     e.m0 = e.m;
     e.lim = (rok ? min(32, nv) : 0) - 4 * h;
     return nv >= 32;
@@ -778,7 +817,10 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
 // Both bodies pass the same head tests (tests/test_head_gpu.py, 67 / 67 with either).
 template <bool TRAIN>
 __device__ __forceinline__ void fwd_any(const FwdArgs& a, bf16* kbuf, const int bx, const int by, const int gx) {
-  if constexpr (TRAIN) fwd_body<true>(a, kbuf, bx, by, gx);
+  if constexpr (TRAIN) {
+    if (a.exact) fwd_body<true, true>(a, kbuf, bx, by, gx);   // uniform per problem
+    else fwd_body<true, false>(a, kbuf, bx, by, gx);
+  }
   else fwd_body16<false>(a, kbuf, bx, by, gx);
 }
 
@@ -817,6 +859,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd_multi_kernel(MultiA
 // samples), 4 waves striding over 32-key tiles; query fragments in registers, key fragments
 // straight from global (L2-resident), query-on-row orientation so each accumulator
 // register stores 32 consecutive keys (128 B) per row.
+constexpr int DIAG_PF = 8;   // key fragments in flight per wave (diag_sim_kernel)
 __global__ __launch_bounds__(256) void diag_sim_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K, int Nq,
                                                        int Nk_pad, int Nk_eff, int diag_off,
                                                        const float* __restrict__ temp_p, float* __restrict__ diagS) {
@@ -833,9 +876,22 @@ __global__ __launch_bounds__(256) void diag_sim_kernel(const bf16* __restrict__ 
   const size_t kbase = (size_t)(i + diag_off) * Nk_pad;
   for (int kt = wave; kt < ntiles; kt += 4) {  // 4 waves (256 threads)
     const bf16* krow = K + (kbase + kt * 32 + l32) * D + 8 * h;  // rows < Nk_pad: in the allocation
+    // key fragments DIAG_PF steps ahead (hipcc counts the waits): one L2 round trip per PF
+    // k-steps instead of one per k-step (the fragment-at-use form waited vmcnt(0) before each
+    // MFMA: 0.17 ms per step for the two heads; same MFMA order, bit-identical)
+    constexpr int PF = DIAG_PF;
+    bf16x8 kf[PF];
+#pragma unroll
+    for (int s = 0; s < PF; ++s) kf[s] = *(const bf16x8*)(krow + 16 * s);
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads here (the scheduler sinks them to their use)
     f32x16 acc = {};
 #pragma unroll
-    for (int s = 0; s < NS; ++s) acc = mfma32(qf[s], *(const bf16x8*)(krow + 16 * s), acc);
+    for (int s = 0; s < NS; ++s) {
+      const bf16x8 cur = kf[s % PF];
+      if (s + PF < NS) kf[s % PF] = *(const bf16x8*)(krow + 16 * (s + PF));
+      acc = mfma32(qf[s], cur, acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const int key = kt * 32 + l32;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -862,6 +918,7 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
   a.j_per_wg = jpw; a.temp = temp; a.clamp_lo = clamp_lo;
   a.rowmax = rowmax; a.argmax = argmax; a.part = nn_part;
   a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part; a.klen = k_len;
+  a.exact = exact_epilogue(clamp_lo);
   const int xw = xb * (256 / ROWS_PER_WG);  // xb counts 256-row blocks
   const bool sq = Nq <= 32;
   const dim3 grid(xw, ys), block(64 * WAVES);
@@ -900,6 +957,7 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
     a.rowmax = p.rowmax; a.argmax = p.argmax; a.part = p.nn_part;
     a.dS = (bf16*)p.dS; a.CT = p.CT; a.part2 = p.st_part; a.klen = nullptr;
     a.ktiles = p.dS ? p.k_tiles : nullptr;
+    a.exact = exact_epilogue(p.clamp_lo);
     m.gx[i] = xb[order[i]] * (256 / ROWS_PER_WG);
     m.first[i + 1] = m.first[i] + m.gx[i] * ys[order[i]];
   }
