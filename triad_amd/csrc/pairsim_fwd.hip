@@ -27,6 +27,9 @@ constexpr int NS = D / 16;  // 32 k-steps
 constexpr int WAVES = 8;
 constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 query rows per workgroup
 constexpr int KT_ELEMS = 32 * D;
+#ifndef TRIAD_FWD_PAIRMAX
+#define TRIAD_FWD_PAIRMAX 1   // training epilogue: max / argmax per pair of elements (A/B knob)
+#endif
 #ifndef TRIAD_FWD_NBUF
 #define TRIAD_FWD_NBUF 3
 #endif
@@ -154,6 +157,11 @@ __device__ __forceinline__ float min3f(float a, float b, float c) {
   asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 __device__ __forceinline__ float maxf(float a, float b) {
   float r;
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -182,8 +190,22 @@ template <bool TRAIN, bool FULL, bool EXACT>
 __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 su2, float lo) {
   const float u = p[v];
   if constexpr (FULL) {
-    e.at = u > e.m ? vkey(v) : e.at;  // keys ascend with v: strict > keeps the first index
+    // per PAIR of elements (keys ascend with v): the pair's max against the running max in one
+    // v_max3, the pair's argmax (u1 > u0 strict, so a tie keeps the first key) taken only if the
+    // running max rose (strict, so an earlier key keeps ties) -- 5 VALU per pair instead of 6,
+    // the same max / argmax as element by element
+#if TRIAD_FWD_PAIRMAX
+    if (v & 1) {
+      const float u0 = p[v - 1];
+      const float mn = max3f(e.m, u0, u);
+      const int kp = u > u0 ? vkey(v) : vkey(v - 1);
+      e.at = mn > e.m ? kp : e.at;
+      e.m = mn;
+    }
+#else
+    e.at = u > e.m ? vkey(v) : e.at;
     e.m = maxf(u, e.m);
+#endif
   } else {
     PIN(e.lim);  // keep the 16 masks from being hoisted
     const bool better = vkey(v) < e.lim && u > e.m;
