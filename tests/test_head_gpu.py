@@ -571,3 +571,41 @@ def test_pair_head_compact_c3_repeats_bit_stable():
         else:
             for got, want in zip(cur, first):
                 assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_forward_epilogue_forms_agree(kind, monkeypatch):
+    """The training forward's two epilogues (pairsim_fwd.hip: the fast form with the per-tile slow
+    redo, and the exact per-element form; chosen per head by its clamp window, forced here by
+    TRIAD_FWD_EXACT) on both heads, with features large enough that many tiles hold S below the
+    window: losses and feature gradients bit-identical between the forms (same unit dS, same
+    sum of clamp^2), d/dtemp within fp32 summation order, both against the fp64 oracle."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(410 + kind)
+    B, Nq, Nv = 6, (49 if kind == 0 else 16), 70
+    Q = (torch.randn(B, Nq, 512, generator=g) * (1.4 if kind == 0 else 0.58)).to(torch.bfloat16).float()
+    V = (torch.randn(B, Nv, 512, generator=g) * (1.4 if kind == 0 else 0.58)).to(torch.bfloat16).float()
+    mask = (torch.arange(Nq)[None, :] < torch.randint(1, Nq + 1, (B, 1), generator=g)).long()
+    temp, thr, w = 1.5, 0.005, 0.3
+    Qr, Vr = Q.double().requires_grad_(True), V.double().requires_grad_(True)
+    tr = torch.tensor(temp, dtype=torch.float64, requires_grad=True)
+    total = (ref_cpu.av_loss(Qr, Vr, tr) if kind == 0 else ref_cpu.tv_loss(Qr, Vr, mask, tr, thr, w))[0]
+    total.backward()
+    tq, tk = _ties(Q, V, temp)
+    got = []
+    for form in ("0", "1"):
+        monkeypatch.setenv("TRIAD_FWD_EXACT", form)
+        Qg = Q.to(dev, torch.bfloat16).requires_grad_(True)
+        Vg = V.to(dev, torch.bfloat16).requires_grad_(True)
+        tg = torch.tensor(temp, device=dev, requires_grad=True)
+        kw = dict(q_mask=mask.to(dev), threshold=thr, sparsity_weight=w) if kind == 1 else {}
+        losses, st, clip = ops.contrastive_head(kind, Qg, Vg, tg, **kw)
+        losses[0].backward()
+        assert _scalar_close(float(losses[0]), float(total))
+        _check_grad(Qg.grad, Qr.grad.numpy(), tq)
+        _check_grad(Vg.grad, Vr.grad.numpy(), tk)
+        assert _scalar_close(float(tg.grad), float(tr.grad), 1e-3, 1e-5), (float(tg.grad), float(tr.grad))
+        got.append((torch.stack([x.detach() for x in losses]).cpu(), Qg.grad.cpu(), Vg.grad.cpu(), float(tg.grad)))
+    (l0, q0, v0, t0), (l1, q1, v1, t1) = got
+    assert torch.equal(l0, l1) and torch.equal(q0, q1) and torch.equal(v0, v1)
+    assert abs(t0 - t1) <= 1e-5 * max(abs(t0), 1e-6), (t0, t1)

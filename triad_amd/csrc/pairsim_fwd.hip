@@ -15,6 +15,7 @@
 //    shadows.
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -34,8 +35,14 @@ constexpr int KT_ELEMS = 32 * D;
 #define TRIAD_FWD_NBUF 3
 #endif
 constexpr int NBUF = TRIAD_FWD_NBUF;     // key-tile LDS ring slots (training body)
-constexpr int LDSPF = 2;                 // key fragments read from LDS ahead of their MFMA
-constexpr int REGION = 2;                // k-steps per scheduling region (sched_barrier spacing)
+#ifndef TRIAD_FWD_LDSPF
+#define TRIAD_FWD_LDSPF 2
+#endif
+#ifndef TRIAD_FWD_REGION
+#define TRIAD_FWD_REGION 2
+#endif
+constexpr int LDSPF = TRIAD_FWD_LDSPF;   // key fragments read from LDS ahead of their MFMA
+constexpr int REGION = TRIAD_FWD_REGION; // k-steps per scheduling region (sched_barrier spacing)
 constexpr int GLDS_PER_TILE = 32 / WAVES;  // 1-KB LDS-DMA pieces per wave per key tile (4)
 
 struct FwdArgs {
@@ -61,7 +68,12 @@ struct FwdArgs {
 // (profiles/r06_fwd_exact_ab.log, alternated three times, features N(0, 0.58^2)): TV (clamp -20,
 // most tiles hold some S < -20) 0.543-0.570 -> 0.493-0.497 ms with the exact form; AV (clamp -60,
 // few tiles reach it) 3.04 -> 3.14 ms. So: exact for windows whose lower clamp is at most 30 below 0.
-inline int exact_epilogue(float clamp_lo) { return clamp_lo >= -30.f ? 1 : 0; }
+// TRIAD_FWD_EXACT=0 / 1 forces one form for every head (parity tests of both bodies on both windows).
+inline int exact_epilogue(float clamp_lo) {
+  const char* v = getenv("TRIAD_FWD_EXACT");   // read per launch (host side, negligible)
+  if (v && (v[0] == '0' || v[0] == '1') && v[1] == 0) return v[0] - '0';
+  return clamp_lo >= -30.f ? 1 : 0;
+}
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
