@@ -29,7 +29,10 @@ constexpr int WAVES = 8;
 constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 query rows per workgroup
 constexpr int KT_ELEMS = 32 * D;
 #ifndef TRIAD_FWD_PAIRMAX
-#define TRIAD_FWD_PAIRMAX 1   // training epilogue: max / argmax per pair of elements (A/B knob)
+// training epilogue: max / argmax per pair of elements (5 VALU per pair instead of 6). Measured
+// slower: AV training 2.925 / 2.928 ms element by element against 2.952 / 2.953 per pair
+// (profiles/r06_fwd_variants_ab.log, alternated on one box); kept as an A/B knob, off
+#define TRIAD_FWD_PAIRMAX 0
 #endif
 #ifndef TRIAD_FWD_NBUF
 #define TRIAD_FWD_NBUF 3
