@@ -893,10 +893,17 @@ __global__ __launch_bounds__(64 * WAVES, 1) void pairsim_fwd_multi_kernel(MultiA
 // Diagonal blocks of S for the regularisers (model.py:417-418 / 524-525):
 // diagS[i][q][k] = temp * <Q[i*Nq + q], K[(i + diag_off)*Nk_pad + k]>, k < Nk_eff.
 // 1/B of the forward's FLOPs, kept out of the streaming kernel: grid (query blocks of 32,
-// samples), 4 waves striding over 32-key tiles; query fragments in registers, key fragments
+// samples), DIAG_WAVES waves striding over 32-key tiles; query fragments in registers, key fragments
 // straight from global (L2-resident), query-on-row orientation so each accumulator
 // register stores 32 consecutive keys (128 B) per row.
 constexpr int DIAG_PF = 8;   // key fragments in flight per wave (diag_sim_kernel)
+#ifndef TRIAD_DIAG_WAVES
+#define TRIAD_DIAG_WAVES 1
+#endif
+// waves per diag_sim workgroup, striding over the sample's key tiles. One: each wave loads its 32
+// query rows' fragments (32 KB) once for all of the sample's key tiles (four waves each loaded
+// them for two tiles); 1,792 one-wave workgroups fit the chip in one round at two waves per SIMD.
+constexpr int DIAG_WAVES = TRIAD_DIAG_WAVES;
 __global__ __launch_bounds__(256) void diag_sim_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K, int Nq,
                                                        int Nk_pad, int Nk_eff, int diag_off,
                                                        const float* __restrict__ temp_p, float* __restrict__ diagS) {
@@ -911,7 +918,7 @@ __global__ __launch_bounds__(256) void diag_sim_kernel(const bf16* __restrict__ 
   const float temp = *temp_p;
   const int ntiles = (Nk_eff + 31) / 32;
   const size_t kbase = (size_t)(i + diag_off) * Nk_pad;
-  for (int kt = wave; kt < ntiles; kt += 4) {  // 4 waves (256 threads)
+  for (int kt = wave; kt < ntiles; kt += DIAG_WAVES) {
     const bf16* krow = K + (kbase + kt * 32 + l32) * D + 8 * h;  // rows < Nk_pad: in the allocation
     // key fragments DIAG_PF steps ahead (hipcc counts the waits): one L2 round trip per PF
     // k-steps instead of one per k-step (the fragment-at-use form waited vmcnt(0) before each
@@ -965,7 +972,7 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
   else hipLaunchKernelGGL((pairsim_fwd2_kernel<false, false>), grid, block, 0, stream, a);
   TRIAD_CHECK_LAUNCH();
   if (diagS && diag) {
-    hipLaunchKernelGGL(diag_sim_kernel, dim3((Nq + 31) / 32, Bq), dim3(256), 0, stream, (const bf16*)Q,
+    hipLaunchKernelGGL(diag_sim_kernel, dim3((Nq + 31) / 32, Bq), dim3(64 * DIAG_WAVES), 0, stream, (const bf16*)Q,
                        (const bf16*)K, Nq, Nk_pad, Nk_eff, diag_off, temp, diagS);
     TRIAD_CHECK_LAUNCH();
   }
@@ -1010,7 +1017,7 @@ int triad_pairsim_diag_launch(const triad_pairsim_problem* pr, int n, hipStream_
   for (int i = 0; i < n; ++i) {
     const triad_pairsim_problem& p = pr[i];
     if (p.diagS && p.diag) {
-      hipLaunchKernelGGL(diag_sim_kernel, dim3((p.Nq + 31) / 32, p.Bq), dim3(256), 0, stream, (const bf16*)p.Q,
+      hipLaunchKernelGGL(diag_sim_kernel, dim3((p.Nq + 31) / 32, p.Bq), dim3(64 * DIAG_WAVES), 0, stream, (const bf16*)p.Q,
                          (const bf16*)p.K, p.Nq, p.Nk_pad, p.Nk_eff, p.diag_off, p.temp, p.diagS);
       TRIAD_CHECK_LAUNCH();
     }
