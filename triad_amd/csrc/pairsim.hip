@@ -613,6 +613,7 @@ int triad_pairsim_fwd(const void* Q, const void* K, int R, int R_pad, int Nq, in
   if (int e = check_shape(R, R_pad, Nq, Bk, Nk_pad, Nk_eff, D_)) return e;
   if (dS && (CT < (long long)Bk * (Nk_pad / 32) || !st_part)) return TRIAD_EINVAL;
   if (k_len && (dS || diagS)) return TRIAD_EINVAL;  // per-sample key lengths: forward-only use
+  if (diag && diagS && (diag_off < 0 || diag_off + Bq > Bk)) return TRIAD_EINVAL;
   PairArgs a = {};
   a.Q = (const bf16*)Q; a.K = (const bf16*)K;
   a.R = R; a.R_pad = R_pad; a.Nq = Nq; a.Bq = Bq; a.Bk = Bk; a.Nk_pad = Nk_pad; a.Nk_eff = Nk_eff;
@@ -635,6 +636,7 @@ int triad_pairsim_fwd_multi(const triad_pairsim_problem* problems, int n, hipStr
     // (compact key tiles: CT >= k_tiles[Bk] is the caller's, the prefix sum lives on the device)
     if (p.dS && (p.CT < (p.k_tiles ? 1LL : (long long)p.Bk * (p.Nk_pad / 32)) || !p.st_part)) return TRIAD_EINVAL;
     if (!p.Q || !p.K || !p.temp || !p.rowmax || !p.argmax || !p.nn_part) return TRIAD_EINVAL;
+    if (p.diag && p.diagS && (p.diag_off < 0 || p.diag_off + p.Bq > p.Bk)) return TRIAD_EINVAL;
     xb[i] = grid_for(p.R_pad, p.Bk, &jpw[i], &ys[i]);  // same decomposition as triad_pairsim_nparts
   }
   return triad_pairsim_fwd_multi_launch(problems, xb, ys, jpw, n, stream);

@@ -63,6 +63,8 @@ struct FwdArgs {
   const int* klen;
   const int* ktiles;  // training: stored key tiles per sample as an exclusive prefix sum (compact K / dS), or null
   int exact;          // training: exact epilogue (fwd_body<true, true>), see exact_epilogue()
+  float* diagS;       // training: S of the diagonal pairs written by the forward itself (or null)
+  int diag_off;       // query sample i pairs with key sample i + diag_off
 };
 
 // Which training epilogue a head runs. The fast form computes d = su * clamp(u, lo, 0) and redoes
@@ -338,6 +340,10 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   const int row = bx * ROWS_PER_WG + wave * 32 + ql;
   const bool rok = row < a.R;
   const int rt = (bx * ROWS_PER_WG + wave * 32) / 32;
+  // diagonal S (training): this lane's query sample / token, and the wave's sample range
+  const int lane_i = row / a.Nq, lane_q = row - lane_i * a.Nq;
+  const int wi_lo = (bx * ROWS_PER_WG + wave * 32) / a.Nq;
+  const int wi_hi = min(bx * ROWS_PER_WG + wave * 32 + 31, a.R - 1) / a.Nq;
 
   const int j0 = by * a.j_per_wg;
   const int j1 = min(a.Bk, j0 + a.j_per_wg);
@@ -490,6 +496,19 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       }
       e.m = -INFINITY;
       e.am = 0;
+    }
+    if (TRAIN && a.diagS) {
+      // the diagonal pairs' S (model.py:417-418 / 524-525) from the tile just reduced: 1/Bk of
+      // the tiles, so the 16 scattered stores per lane cost nothing measurable; left-out zero
+      // tiles keep the zeros the launcher wrote (S = 0 there)
+      const int jd = ec.j - a.diag_off;
+      if (jd >= wi_lo && jd <= wi_hi && rok && lane_i == jd) {
+        float* drow = a.diagS + ((size_t)lane_i * a.Nq + lane_q) * a.Nk_pad + ec.kb * 32 + 4 * h;
+        const int kmax = a.Nk_eff - ec.kb * 32 - 4 * h;
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          if (vkey(v) < kmax) drow[vkey(v)] = su * p[v];
+      }
     }
     ec.next(nkb, skip, j0);
   };
@@ -963,6 +982,13 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
   a.rowmax = rowmax; a.argmax = argmax; a.part = nn_part;
   a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part; a.klen = k_len;
   a.exact = exact_epilogue(clamp_lo);
+  // training: the forward writes the diagonal S itself (diag_sim_kernel recomputed 1/B of the
+  // forward's products); zeros first for the keys of left-out all-zero tiles
+  const bool diag_in_fwd = dS && diagS && diag;
+  if (diag_in_fwd) {
+    a.diagS = diagS; a.diag_off = diag_off;
+    if (hipMemsetAsync(diagS, 0, (size_t)Bq * Nq * Nk_pad * sizeof(float), stream) != hipSuccess) return TRIAD_EINVAL;
+  }
   const int xw = xb * (256 / ROWS_PER_WG);  // xb counts 256-row blocks
   const bool sq = Nq <= 32;
   const dim3 grid(xw, ys), block(64 * WAVES);
@@ -971,7 +997,7 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
   else if (sq) hipLaunchKernelGGL((pairsim_fwd2_kernel<false, true>), grid, block, 0, stream, a);
   else hipLaunchKernelGGL((pairsim_fwd2_kernel<false, false>), grid, block, 0, stream, a);
   TRIAD_CHECK_LAUNCH();
-  if (diagS && diag) {
+  if (diagS && diag && !diag_in_fwd) {
     hipLaunchKernelGGL(diag_sim_kernel, dim3((Nq + 31) / 32, Bq), dim3(64 * DIAG_WAVES), 0, stream, (const bf16*)Q,
                        (const bf16*)K, Nq, Nk_pad, Nk_eff, diag_off, temp, diagS);
     TRIAD_CHECK_LAUNCH();
@@ -1002,6 +1028,11 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
     a.dS = (bf16*)p.dS; a.CT = p.CT; a.part2 = p.st_part; a.klen = nullptr;
     a.ktiles = p.dS ? p.k_tiles : nullptr;
     a.exact = exact_epilogue(p.clamp_lo);
+    if (p.dS && p.diagS && p.diag) {   // training: diagonal S written by the forward (as fwd2_launch)
+      a.diagS = p.diagS; a.diag_off = p.diag_off;
+      if (hipMemsetAsync(p.diagS, 0, (size_t)p.Bq * p.Nq * p.Nk_pad * sizeof(float), stream) != hipSuccess)
+        return TRIAD_EINVAL;
+    }
     m.gx[i] = xb[order[i]] * (256 / ROWS_PER_WG);
     m.first[i + 1] = m.first[i] + m.gx[i] * ys[order[i]];
   }
@@ -1009,7 +1040,7 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
   if (train) hipLaunchKernelGGL((pairsim_fwd_multi_kernel<true>), grid, block, 0, stream, m);
   else hipLaunchKernelGGL((pairsim_fwd_multi_kernel<false>), grid, block, 0, stream, m);
   TRIAD_CHECK_LAUNCH();
-  return triad_pairsim_diag_launch(pr, n, stream);
+  return train ? TRIAD_OK : triad_pairsim_diag_launch(pr, n, stream);   // training: in the forward
 }
 
 // diag_sim of every problem with a diagonal output (shapes validated by the caller)

@@ -463,20 +463,24 @@ def _problem(h, padded_keys=False):
 
 
 def _heads_launch(hs, st):
-    """Every head's similarity forward in ONE launch (triad_pairsim_fwd_multi), then the heads'
-    diagonal S blocks (triad_pairsim_diag) -- issued apart so the bench's live timing of the
-    forward launch covers that kernel alone (bit-identical to the one-call form, which also
-    launches the diagonal kernels)."""
+    """Every head's similarity forward in ONE launch (triad_pairsim_fwd_multi). Training: the
+    forward also writes each head's diagonal S blocks from the tiles it reduces (round 6; the
+    separate diag_sim kernel recomputed 1/B of the products, 0.12 ms per step). Eval: the
+    diagonal blocks by triad_pairsim_diag, issued apart so the bench's live timing of the forward
+    launch covers that kernel alone."""
+    train = hs[0].dS is not None
     arr = (_lib.PairsimProblem * len(hs))(*[_problem(h, padded_keys=True) for h in hs])
     fwd = (_lib.PairsimProblem * len(hs))(*[_problem(h) for h in hs])
-    for p in fwd:
-        p.diag = 0
+    if not train:      # training: the forward writes the diagonal S itself (pairsim_fwd.hip)
+        for p in fwd:
+            p.diag = 0
     ms = [_fwd_meta(h) for h in hs]
     meta = dict(kind=-1, what="+".join("AV" if h.kind == AV else "TV" for h in hs),
                 flops=sum(m["flops"] for m in ms), bytes=sum(m["bytes"] for m in ms),
                 ds_bytes=sum(m["ds_bytes"] for m in ms), grid=sum(h.nparts for h in hs) * 512)
     call("triad_pairsim_fwd_multi", fwd, len(hs), st, meta=meta)
-    call("triad_pairsim_diag", arr, len(hs), st)
+    if not train:
+        call("triad_pairsim_diag", arr, len(hs), st)
 
 
 def _head_end(h, q_mask, thr, w_sparse, st):
