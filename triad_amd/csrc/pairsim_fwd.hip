@@ -73,6 +73,13 @@ struct FwdArgs {
 // (profiles/r06_fwd_exact_ab.log, alternated three times, features N(0, 0.58^2)): TV (clamp -20,
 // most tiles hold some S < -20) 0.543-0.570 -> 0.493-0.497 ms with the exact form; AV (clamp -60,
 // few tiles reach it) 3.04 -> 3.14 ms. So: exact for windows whose lower clamp is at most 30 below 0.
+// Training: the forward writes the diagonal S (default) or diag_sim_kernel recomputes it after the
+// forward (TRIAD_DIAG_IN_FWD=0, the round-5 form; A/B knob).
+inline bool diag_in_forward() {
+  const char* v = getenv("TRIAD_DIAG_IN_FWD");
+  return !(v && v[0] == '0' && v[1] == 0);
+}
+
 // TRIAD_FWD_EXACT=0 / 1 forces one form for every head (parity tests of both bodies on both windows).
 inline int exact_epilogue(float clamp_lo) {
   const char* v = getenv("TRIAD_FWD_EXACT");   // read per launch (host side, negligible)
@@ -984,7 +991,7 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
   a.exact = exact_epilogue(clamp_lo);
   // training: the forward writes the diagonal S itself (diag_sim_kernel recomputed 1/B of the
   // forward's products); zeros first for the keys of left-out all-zero tiles
-  const bool diag_in_fwd = dS && diagS && diag;
+  const bool diag_in_fwd = dS && diagS && diag && diag_in_forward();
   if (diag_in_fwd) {
     a.diagS = diagS; a.diag_off = diag_off;
     if (hipMemsetAsync(diagS, 0, (size_t)Bq * Nq * Nk_pad * sizeof(float), stream) != hipSuccess) return TRIAD_EINVAL;
@@ -1028,7 +1035,7 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
     a.dS = (bf16*)p.dS; a.CT = p.CT; a.part2 = p.st_part; a.klen = nullptr;
     a.ktiles = p.dS ? p.k_tiles : nullptr;
     a.exact = exact_epilogue(p.clamp_lo);
-    if (p.dS && p.diagS && p.diag) {   // training: diagonal S written by the forward (as fwd2_launch)
+    if (p.dS && p.diagS && p.diag && diag_in_forward()) {   // training: diagonal S by the forward
       a.diagS = p.diagS; a.diag_off = p.diag_off;
       if (hipMemsetAsync(p.diagS, 0, (size_t)p.Bq * p.Nq * p.Nk_pad * sizeof(float), stream) != hipSuccess)
         return TRIAD_EINVAL;
@@ -1040,7 +1047,7 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
   if (train) hipLaunchKernelGGL((pairsim_fwd_multi_kernel<true>), grid, block, 0, stream, m);
   else hipLaunchKernelGGL((pairsim_fwd_multi_kernel<false>), grid, block, 0, stream, m);
   TRIAD_CHECK_LAUNCH();
-  return train ? TRIAD_OK : triad_pairsim_diag_launch(pr, n, stream);   // training: in the forward
+  return (train && diag_in_forward()) ? TRIAD_OK : triad_pairsim_diag_launch(pr, n, stream);
 }
 
 // diag_sim of every problem with a diagonal output (shapes validated by the caller)
