@@ -658,6 +658,9 @@ int triad_pairsim_diag(const triad_pairsim_problem* problems, int n, hipStream_t
     if (int e = check_shape(p.R, p.R_pad, p.Nq, p.Bk, p.Nk_pad, p.Nk_eff, D)) return e;
     if (p.diag && p.diagS && (!p.Q || !p.K || !p.temp || p.diag_off < 0 || p.diag_off + p.Bq > p.Bk))
       return TRIAD_EINVAL;
+    // diag_sim addresses K in the padded layout (sample j at rows j * Nk_pad); a compact key set
+    // (k_tiles) has fewer rows and would be read past its end
+    if (p.diag && p.diagS && p.k_tiles) return TRIAD_EINVAL;
   }
   return triad_pairsim_diag_launch(problems, n, stream);
 }

@@ -74,7 +74,8 @@ struct FwdArgs {
 // most tiles hold some S < -20) 0.543-0.570 -> 0.493-0.497 ms with the exact form; AV (clamp -60,
 // few tiles reach it) 3.04 -> 3.14 ms. So: exact for windows whose lower clamp is at most 30 below 0.
 // Training: the forward writes the diagonal S (default) or diag_sim_kernel recomputes it after the
-// forward (TRIAD_DIAG_IN_FWD=0, the round-5 form; A/B knob).
+// forward (TRIAD_DIAG_IN_FWD=0, the round-5 form; A/B knob). triad_pairsim_fwd's own launch (padded
+// keys) reads it here; the pair launch's caller (ops._heads_launch) decides for triad_pairsim_fwd_multi.
 inline bool diag_in_forward() {
   const char* v = getenv("TRIAD_DIAG_IN_FWD");
   return !(v && v[0] == '0' && v[1] == 0);
@@ -1035,7 +1036,7 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
     a.dS = (bf16*)p.dS; a.CT = p.CT; a.part2 = p.st_part; a.klen = nullptr;
     a.ktiles = p.dS ? p.k_tiles : nullptr;
     a.exact = exact_epilogue(p.clamp_lo);
-    if (p.dS && p.diagS && p.diag && diag_in_forward()) {   // training: diagonal S by the forward
+    if (p.dS && p.diagS && p.diag) {   // training: diagonal S written by the forward (as fwd2_launch)
       a.diagS = p.diagS; a.diag_off = p.diag_off;
       if (hipMemsetAsync(p.diagS, 0, (size_t)p.Bq * p.Nq * p.Nk_pad * sizeof(float), stream) != hipSuccess)
         return TRIAD_EINVAL;
@@ -1047,7 +1048,10 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
   if (train) hipLaunchKernelGGL((pairsim_fwd_multi_kernel<true>), grid, block, 0, stream, m);
   else hipLaunchKernelGGL((pairsim_fwd_multi_kernel<false>), grid, block, 0, stream, m);
   TRIAD_CHECK_LAUNCH();
-  return (train && diag_in_forward()) ? TRIAD_OK : triad_pairsim_diag_launch(pr, n, stream);
+  // training: the diagonal S came from the forward (a problem that wants diag_sim instead passes
+  // diag = 0 here and calls triad_pairsim_diag with the PADDED key layout: the forward's K may be
+  // the compact one, which diag_sim cannot address)
+  return train ? TRIAD_OK : triad_pairsim_diag_launch(pr, n, stream);
 }
 
 // diag_sim of every problem with a diagonal output (shapes validated by the caller)

@@ -468,7 +468,9 @@ def _heads_launch(hs, st):
     separate diag_sim kernel recomputed 1/B of the products, 0.12 ms per step). Eval: the
     diagonal blocks by triad_pairsim_diag, issued apart so the bench's live timing of the forward
     launch covers that kernel alone."""
-    train = hs[0].dS is not None
+    # training: the forward writes the diagonal S itself unless TRIAD_DIAG_IN_FWD=0 (A/B knob: then
+    # triad_pairsim_diag recomputes it over the padded keys, as in round 5)
+    train = hs[0].dS is not None and os.environ.get("TRIAD_DIAG_IN_FWD", "1") != "0"
     arr = (_lib.PairsimProblem * len(hs))(*[_problem(h, padded_keys=True) for h in hs])
     fwd = (_lib.PairsimProblem * len(hs))(*[_problem(h) for h in hs])
     if not train:      # training: the forward writes the diagonal S itself (pairsim_fwd.hip)
