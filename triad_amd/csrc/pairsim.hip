@@ -349,9 +349,6 @@ __device__ __forceinline__ long long tile_elem(long long CT, int r, long long c)
   return ((long long)(r >> 5) * CT + (c >> 5)) * 1024 + ds_chunk(2 * lane + (v >> 3)) * 8 + (v & 7);
 }
 
-#ifndef TRIAD_PATCH_PROBE_WRITE_ONLY
-#define TRIAD_PATCH_PROBE_WRITE_ONLY 0   // timing probe of a read-free patch (values approximate)
-#endif
 // Four elements per thread per pass with all their loads issued together, 32-bit index math:
 // one element per pass (a dependent argmax -> dS round trip each, 64-bit divisions) made the AV
 // patch a latency-bound 0.3 ms launch at c3.
@@ -380,14 +377,8 @@ __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS
       const long long c = ds_col(kt, Nk_pad, j, key);
       p[u] = c < 0 ? nullptr : dS + tile_elem(CT, r, c);   // unstored zero tile: K there is zero
     }
-#if TRIAD_PATCH_PROBE_WRITE_ONLY
-    // TIMING PROBE ONLY (values approximate): no read of the patched element
-#pragma unroll
-    for (int u = 0; u < 4; ++u) old[u] = fminf(rm[u], 0.f);
-#else
 #pragma unroll
     for (int u = 0; u < 4; ++u) old[u] = p[u] ? (float)*p[u] : 0.f;
-#endif
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (e0 + u * stride >= total) break;

@@ -63,8 +63,6 @@ struct FwdArgs {
   const int* klen;
   const int* ktiles;  // training: stored key tiles per sample as an exclusive prefix sum (compact K / dS), or null
   int exact;          // training: exact epilogue (fwd_body<true, true>), see exact_epilogue()
-  float* diagS;       // training: S of the diagonal pairs written by the forward itself (or null)
-  int diag_off;       // query sample i pairs with key sample i + diag_off
 };
 
 // Which training epilogue a head runs. The fast form computes d = su * clamp(u, lo, 0) and redoes
@@ -73,14 +71,6 @@ struct FwdArgs {
 // (profiles/r06_fwd_exact_ab.log, alternated three times, features N(0, 0.58^2)): TV (clamp -20,
 // most tiles hold some S < -20) 0.543-0.570 -> 0.493-0.497 ms with the exact form; AV (clamp -60,
 // few tiles reach it) 3.04 -> 3.14 ms. So: exact for windows whose lower clamp is at most 30 below 0.
-// Training: the forward writes the diagonal S (default) or diag_sim_kernel recomputes it after the
-// forward (TRIAD_DIAG_IN_FWD=0, the round-5 form; A/B knob). triad_pairsim_fwd's own launch (padded
-// keys) reads it here; the pair launch's caller (ops._heads_launch) decides for triad_pairsim_fwd_multi.
-inline bool diag_in_forward() {
-  const char* v = getenv("TRIAD_DIAG_IN_FWD");
-  return !(v && v[0] == '0' && v[1] == 0);
-}
-
 // TRIAD_FWD_EXACT=0 / 1 forces one form for every head (parity tests of both bodies on both windows).
 inline int exact_epilogue(float clamp_lo) {
   const char* v = getenv("TRIAD_FWD_EXACT");   // read per launch (host side, negligible)
@@ -348,10 +338,6 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   const int row = bx * ROWS_PER_WG + wave * 32 + ql;
   const bool rok = row < a.R;
   const int rt = (bx * ROWS_PER_WG + wave * 32) / 32;
-  // diagonal S (training): this lane's query sample / token, and the wave's sample range
-  const int lane_i = row / a.Nq, lane_q = row - lane_i * a.Nq;
-  const int wi_lo = (bx * ROWS_PER_WG + wave * 32) / a.Nq;
-  const int wi_hi = min(bx * ROWS_PER_WG + wave * 32 + 31, a.R - 1) / a.Nq;
 
   const int j0 = by * a.j_per_wg;
   const int j1 = min(a.Bk, j0 + a.j_per_wg);
@@ -504,19 +490,6 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       }
       e.m = -INFINITY;
       e.am = 0;
-    }
-    if (TRAIN && a.diagS) {
-      // the diagonal pairs' S (model.py:417-418 / 524-525) from the tile just reduced: 1/Bk of
-      // the tiles, so the 16 scattered stores per lane cost nothing measurable; left-out zero
-      // tiles keep the zeros the launcher wrote (S = 0 there)
-      const int jd = ec.j - a.diag_off;
-      if (jd >= wi_lo && jd <= wi_hi && rok && lane_i == jd) {
-        float* drow = a.diagS + ((size_t)lane_i * a.Nq + lane_q) * a.Nk_pad + ec.kb * 32 + 4 * h;
-        const int kmax = a.Nk_eff - ec.kb * 32 - 4 * h;
-#pragma unroll
-        for (int v = 0; v < 16; ++v)
-          if (vkey(v) < kmax) drow[vkey(v)] = su * p[v];
-      }
     }
     ec.next(nkb, skip, j0);
   };
@@ -990,13 +963,6 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
   a.rowmax = rowmax; a.argmax = argmax; a.part = nn_part;
   a.dS = (bf16*)dS; a.CT = CT; a.part2 = st_part; a.klen = k_len;
   a.exact = exact_epilogue(clamp_lo);
-  // training: the forward writes the diagonal S itself (diag_sim_kernel recomputed 1/B of the
-  // forward's products); zeros first for the keys of left-out all-zero tiles
-  const bool diag_in_fwd = dS && diagS && diag && diag_in_forward();
-  if (diag_in_fwd) {
-    a.diagS = diagS; a.diag_off = diag_off;
-    if (hipMemsetAsync(diagS, 0, (size_t)Bq * Nq * Nk_pad * sizeof(float), stream) != hipSuccess) return TRIAD_EINVAL;
-  }
   const int xw = xb * (256 / ROWS_PER_WG);  // xb counts 256-row blocks
   const bool sq = Nq <= 32;
   const dim3 grid(xw, ys), block(64 * WAVES);
@@ -1005,7 +971,7 @@ int triad_pairsim_fwd2_launch(const void* Q, const void* K, int R, int R_pad, in
   else if (sq) hipLaunchKernelGGL((pairsim_fwd2_kernel<false, true>), grid, block, 0, stream, a);
   else hipLaunchKernelGGL((pairsim_fwd2_kernel<false, false>), grid, block, 0, stream, a);
   TRIAD_CHECK_LAUNCH();
-  if (diagS && diag && !diag_in_fwd) {
+  if (diagS && diag) {
     hipLaunchKernelGGL(diag_sim_kernel, dim3((Nq + 31) / 32, Bq), dim3(64 * DIAG_WAVES), 0, stream, (const bf16*)Q,
                        (const bf16*)K, Nq, Nk_pad, Nk_eff, diag_off, temp, diagS);
     TRIAD_CHECK_LAUNCH();
@@ -1036,11 +1002,6 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
     a.dS = (bf16*)p.dS; a.CT = p.CT; a.part2 = p.st_part; a.klen = nullptr;
     a.ktiles = p.dS ? p.k_tiles : nullptr;
     a.exact = exact_epilogue(p.clamp_lo);
-    if (p.dS && p.diagS && p.diag) {   // training: diagonal S written by the forward (as fwd2_launch)
-      a.diagS = p.diagS; a.diag_off = p.diag_off;
-      if (hipMemsetAsync(p.diagS, 0, (size_t)p.Bq * p.Nq * p.Nk_pad * sizeof(float), stream) != hipSuccess)
-        return TRIAD_EINVAL;
-    }
     m.gx[i] = xb[order[i]] * (256 / ROWS_PER_WG);
     m.first[i + 1] = m.first[i] + m.gx[i] * ys[order[i]];
   }
@@ -1048,10 +1009,9 @@ int triad_pairsim_fwd_multi_launch(const triad_pairsim_problem* pr, const int* x
   if (train) hipLaunchKernelGGL((pairsim_fwd_multi_kernel<true>), grid, block, 0, stream, m);
   else hipLaunchKernelGGL((pairsim_fwd_multi_kernel<false>), grid, block, 0, stream, m);
   TRIAD_CHECK_LAUNCH();
-  // training: the diagonal S came from the forward (a problem that wants diag_sim instead passes
-  // diag = 0 here and calls triad_pairsim_diag with the PADDED key layout: the forward's K may be
-  // the compact one, which diag_sim cannot address)
-  return train ? TRIAD_OK : triad_pairsim_diag_launch(pr, n, stream);
+  // the caller passes diag = 0 and launches triad_pairsim_diag over the PADDED keys (the forward's K
+  // may be the compact one, which diag_sim cannot address; triad_pairsim_diag refuses it)
+  return triad_pairsim_diag_launch(pr, n, stream);
 }
 
 // diag_sim of every problem with a diagonal output (shapes validated by the caller)

@@ -463,26 +463,21 @@ def _problem(h, padded_keys=False):
 
 
 def _heads_launch(hs, st):
-    """Every head's similarity forward in ONE launch (triad_pairsim_fwd_multi). Training: the
-    forward also writes each head's diagonal S blocks from the tiles it reduces (round 6; the
-    separate diag_sim kernel recomputed 1/B of the products, 0.12 ms per step). Eval: the
-    diagonal blocks by triad_pairsim_diag, issued apart so the bench's live timing of the forward
-    launch covers that kernel alone."""
-    # training: the forward writes the diagonal S itself unless TRIAD_DIAG_IN_FWD=0 (A/B knob: then
-    # triad_pairsim_diag recomputes it over the padded keys, as in round 5)
-    train = hs[0].dS is not None and os.environ.get("TRIAD_DIAG_IN_FWD", "1") != "0"
+    """Every head's similarity forward in ONE launch (triad_pairsim_fwd_multi), then the heads'
+    diagonal S blocks (triad_pairsim_diag over the padded keys) -- issued apart so the bench's live
+    timing of the forward launch covers that kernel alone. (Round 6 built the diagonal S into the
+    training forward's epilogue: the forward took 0.10 ms longer than the 0.125 ms kernel it saved,
+    same box alternated, profiles/r06_diag_in_fwd_ab.log; not kept.)"""
     arr = (_lib.PairsimProblem * len(hs))(*[_problem(h, padded_keys=True) for h in hs])
     fwd = (_lib.PairsimProblem * len(hs))(*[_problem(h) for h in hs])
-    if not train:      # training: the forward writes the diagonal S itself (pairsim_fwd.hip)
-        for p in fwd:
-            p.diag = 0
+    for p in fwd:
+        p.diag = 0
     ms = [_fwd_meta(h) for h in hs]
     meta = dict(kind=-1, what="+".join("AV" if h.kind == AV else "TV" for h in hs),
                 flops=sum(m["flops"] for m in ms), bytes=sum(m["bytes"] for m in ms),
                 ds_bytes=sum(m["ds_bytes"] for m in ms), grid=sum(h.nparts for h in hs) * 512)
     call("triad_pairsim_fwd_multi", fwd, len(hs), st, meta=meta)
-    if not train:
-        call("triad_pairsim_diag", arr, len(hs), st)
+    call("triad_pairsim_diag", arr, len(hs), st)
 
 
 def _head_end(h, q_mask, thr, w_sparse, st):
