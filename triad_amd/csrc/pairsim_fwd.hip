@@ -28,6 +28,9 @@ constexpr int NS = D / 16;  // 32 k-steps
 constexpr int WAVES = 8;
 constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 query rows per workgroup
 constexpr int KT_ELEMS = 32 * D;
+#ifndef TRIAD_FWD_SYNC_FAST
+#define TRIAD_FWD_SYNC_FAST 1   // sync_tile: steady-state wait tested first (A/B knob)
+#endif
 #ifndef TRIAD_FWD_PAIRMAX
 // training epilogue: max / argmax per pair of elements (5 VALU per pair instead of 6). Measured
 // slower: AV training 2.925 / 2.928 ms element by element against 2.952 / 2.953 per pair
@@ -433,6 +436,13 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     // one (nd, ns): tests/test_isa_cpu.py checks every one against the VMEM ops hipcc emitted)
     const int nd = min(NBUF - 2, nblocks - 1 - b);
     const int ns = TRAIN ? max(0, min(NBUF - 2, b - 1)) : 0;
+#if TRIAD_FWD_SYNC_FAST
+    // the steady state (nd = ns = 1: every tile but the first two and the last) tested first, so
+    // the per-tile path to the barrier is one compare and branch instead of the switch's tree
+    if (NBUF == 3 && TRAIN && __builtin_expect(b >= 2 && b <= nblocks - 2, 1)) {
+      TRIAD_VMCNT(GLDS_PER_TILE + 2);
+    } else
+#endif
     if constexpr (NBUF == 3) {
       switch (nd * 2 + ns * 16) {
         case 2: TRIAD_VMCNT(GLDS_PER_TILE); break;
