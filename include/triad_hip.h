@@ -42,9 +42,10 @@ int triad_pairsim_nparts(int R_pad, int Bk);
  * rowmax[j][r] = max_k S, argmax[j][r] = first argmax, nn_part[wg] = partial
  * sum of clamp(S, clamp_lo, 0)^2 (double), diagS[i][q][k] = S on the diagonal
  * pairs (j == i + diag_off) when diag != 0 and diagS != NULL.
- * If dS != NULL it also writes the unit l_nonneg gradient S*[clamp_lo <= S <= 0] in the
- * tiled dS layout ([R_pad/32][CT][1024] bf16, see triad_tile_gemm) and st_part[wg] =
- * sum S*S/temp over those entries, so the backward needs no recompute.
+ * If dS != NULL it also writes the unit l_nonneg gradient S*[clamp_lo <= S <= 0] divided by
+ * su = |temp| (su = 1 when temp == 0) in the tiled dS layout ([R_pad/32][CT][1024] bf16, see
+ * triad_tile_gemm) and st_part[wg] = sum S*S/temp over those entries, so the backward needs no
+ * recompute (the backward's GEMM alpha carries the factor su).
  * k_len (optional, forward-only: dS and diagS must be NULL): per-key-sample valid length,
  * keys >= k_len[j] are excluded (retrieval over trimmed token lists, retrieval.py:243-244).
  * Replaces model.py:370-392 (AV) / 490-514 (TV) token_sims + max, the
@@ -128,13 +129,15 @@ int triad_pairsim_dS(const void* Q, const void* K, int R, int R_pad, int Nq, int
                      const float* coef, void* dS, long long CT, double* dt_part, hipStream_t stream);
 
 /* Fast backward (only `total` differentiated): complete the forward's tiled unit l_nonneg
- * gradient in place: += ratio_max * dclip[i][j] * qw[r] at each row's argmax key (max backward,
- * model.py:389/507) and += ratio_diag * gdiag on the diagonal pairs. max_part[block] =
+ * gradient (stored divided by su = |temp|, see triad_pairsim_fwd) in place, in the same units:
+ * += ratio_max / su * dclip[i][j] * qw[r] at each row's argmax key (max backward,
+ * model.py:389/507) and += ratio_diag / su * gdiag on the diagonal pairs; temp = the forward's
+ * temperature (device, required). The GEMMs then take alpha = temp * c_nn * su. max_part[block] =
  * sum dclip*qw*rowmax (n_max_part blocks). */
 int triad_dS_patch(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad, int Nk_eff,
                    int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
                    float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
-                   hipStream_t stream);
+                   const float* temp, hipStream_t stream);
 
 /* triad_dS_patch over a dS holding only the stored key tiles (k_tiles = the stored-tile prefix sum
  * the forward was given, triad_pairsim_problem.k_tiles; NULL = triad_dS_patch): a term landing in
@@ -143,7 +146,7 @@ int triad_dS_patch(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int
 int triad_dS_patch_tiles(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad, int Nk_eff,
                          int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
                          float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
-                         const int* k_tiles, hipStream_t stream);
+                         const float* temp, const int* k_tiles, hipStream_t stream);
 
 /* dL/dtemp = sum_k w[k]*sum(p_k) + w[3]*d l_cal/d temp (has_cal: AV, model.py:420-424). */
 int triad_dtemp_finalize(const double* p0, int n0, const double* p1, int n1, const double* p2, int n2,

@@ -165,9 +165,12 @@ def test_packed_tile_gemm_and_patch_reject_bad_arguments():
     assert lib.triad_tile_gemm_packed16_slabs(fake, 8, 1, fake, 256, 0, 1, fake, None) == 1001      # nkt = 0
     # dS patch: CT too small for Bk samples of Nk_pad keys; Bk * R past 2^31 (32-bit index math)
     assert lib.triad_dS_patch(fake, 4, 256, 256, 32, 8, 8, 64, 60, 0, fake, fake, fake, fake, 1.0, None, 0.0,
-                              fake, 1024, None) == 1001
+                              fake, 1024, fake, None) == 1001
     assert lib.triad_dS_patch(fake, 1 << 40, 1 << 20, 1 << 20, 32, 8, 4096, 64, 60, 0, fake, fake, fake, fake, 1.0,
-                              None, 0.0, fake, 1024, None) == 1001
+                              None, 0.0, fake, 1024, fake, None) == 1001
+    # ... and the temperature the tiles are scaled by is required
+    assert lib.triad_dS_patch(fake, 1 << 20, 256, 256, 32, 8, 8, 64, 60, 0, fake, fake, fake, fake, 1.0, None, 0.0,
+                              fake, 1024, None, None) == 1001
     # loss head: B * B must fit an int
     assert lib.triad_losshead(fake, 50000, 0, fake, fake, 1, 1.0, fake, 1, 1.0, 0.0, fake, fake, fake, None) == 1001
 

@@ -50,7 +50,7 @@ def materialised(kind, t, dS, CT):
     forward(kind, t, dS, CT)
     mp = torch.empty(1024, dtype=torch.float64, device="cuda")
     call("triad_dS_patch", ptr(dS), CT, g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, 0, ptr(t["argmax"]),
-         ptr(t["rowmax"]), ptr(t["dclip"]), ptr(t["qw"]), 1.0, ptr(t["gdiag"]), 1.0, ptr(mp), 1024, st)
+         ptr(t["rowmax"]), ptr(t["dclip"]), ptr(t["qw"]), 1.0, ptr(t["gdiag"]), 1.0, ptr(mp), 1024, ptr(t["temp"]), st)
     dQ = torch.empty(g.R_pad, D, dtype=torch.bfloat16, device="cuda")
     dK = torch.empty(CT * 32, D, dtype=torch.bfloat16, device="cuda")
     ops.tile_gemm(dS, CT, 0, t["Kb"], g.R_pad, g.C_pad // 32, t["temp"], dQ, st)

@@ -31,9 +31,10 @@ SIGNATURES = {
     "triad_losshead": [vp, i32, i32, vp, vp, i32, f64, vp, i32, f64, f32, vp, vp, vp, vp],
     "triad_pairsim_dS": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, f32, i32, i32, vp, vp, vp, vp, vp,
                          vp, i64, vp, vp],
-    "triad_dS_patch": [vp, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp, f32, vp, i32, vp],
+    "triad_dS_patch": [vp, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp, f32, vp, i32, vp,
+                       vp],
     "triad_dS_patch_tiles": [vp, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp, f32, vp, i32,
-                             vp, vp],
+                             vp, vp, vp],
     "triad_dtemp_finalize": [vp, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp],
     "triad_tile_gemm": [vp, i64, i32, vp, i32, i32, vp, i32, vp, vp, vp],
     "triad_tile_gemm_slabs": [vp, i64, i32, vp, i32, i32, i32, vp, vp],

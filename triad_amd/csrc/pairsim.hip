@@ -329,8 +329,16 @@ __global__ __launch_bounds__(256) void diag_sparsity_kernel(const float* __restr
   if (threadIdx.x == 0) { part[i] = tot; dt_part[i] = dt; }
 }
 
+// The forward stores the unit l_nonneg gradient divided by su = |temp| (1 when temp == 0; the
+// per-element multiply moved here and into the tile GEMMs' alpha): the terms below are added
+// divided by su too, so the tiled dS holds dS_unit / su and alpha carries su.
+__device__ __forceinline__ float unit_scale(const float* temp) {
+  const float t = *temp;
+  return 1.f / (t != 0.f ? fabsf(t) : 1.f);
+}
+
 // Sparse (max) term of dS, added in place to the tiled unit l_nonneg gradient written by the
-// forward: dS[r][j*Nk_pad + argmax[j][r]] += ratio * dclip[i][j] * qw[r]  (the backward of
+// forward: dS[r][j*Nk_pad + argmax[j][r]] += ratio / su * dclip[i][j] * qw[r]  (the backward of
 // max over keys, model.py:389/507, feeding mean/masked-mean and the CE).
 // part[block] = sum dclip * qw * rowmax (-> d/dtemp of this term).
 // Column of key `key` of key sample j in the tiled dS: j Nk_pad + key, or with compact key tiles
@@ -358,9 +366,11 @@ __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS
                                                            const float* __restrict__ rowmax,
                                                            const float* __restrict__ dclip,
                                                            const float* __restrict__ qw, float ratio,
-                                                           double* __restrict__ part, const int* __restrict__ kt) {
+                                                           double* __restrict__ part, const int* __restrict__ kt,
+                                                           const float* __restrict__ temp) {
   __shared__ double red[4];
   double acc = 0.0;
+  const float rs = ratio * unit_scale(temp);
   const int total = Bk * R;   // < 2^31 (host check)
   const int stride = gridDim.x * blockDim.x;
   for (int e0 = blockIdx.x * blockDim.x + threadIdx.x; e0 < total; e0 += 4 * stride) {
@@ -382,7 +392,7 @@ __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (e0 + u * stride >= total) break;
-      if (p[u]) *p[u] = (bf16)(old[u] + ratio * w[u]);
+      if (p[u]) *p[u] = (bf16)(old[u] + rs * w[u]);
       acc += (double)w[u] * (double)rm[u];
     }
   }
@@ -390,13 +400,15 @@ __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS
   if (threadIdx.x == 0) part[blockIdx.x] = t;
 }
 
-// Diagonal regulariser term: dS[i*Nq+q][(i+off)*Nk_pad + k] += ratio * g[i][q][k] (four elements
-// per thread per pass, as above).
+// Diagonal regulariser term: dS[i*Nq+q][(i+off)*Nk_pad + k] += ratio / su * g[i][q][k] (four
+// elements per thread per pass, as above).
 __global__ __launch_bounds__(256) void dS_patch_diag_kernel(bf16* __restrict__ dS, long long CT, int Bq, int Nq,
                                                             int Nk_pad, int Nk_eff, int diag_off,
                                                             const float* __restrict__ g, float ratio,
-                                                            const int* __restrict__ kt) {
+                                                            const int* __restrict__ kt,
+                                                            const float* __restrict__ temp) {
   const int total = Bq * Nq * Nk_eff;   // < 2^31 (host check)
+  const float rs = ratio * unit_scale(temp);
   const int stride = gridDim.x * blockDim.x;
   for (int e0 = blockIdx.x * blockDim.x + threadIdx.x; e0 < total; e0 += 4 * stride) {
     float gv[4], old[4];
@@ -415,7 +427,7 @@ __global__ __launch_bounds__(256) void dS_patch_diag_kernel(bf16* __restrict__ d
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (e0 + u * stride >= total) break;
-      if (p[u]) *p[u] = (bf16)(old[u] + ratio * gv[u]);
+      if (p[u]) *p[u] = (bf16)(old[u] + rs * gv[u]);
     }
   }
 }
@@ -717,18 +729,18 @@ int triad_pairsim_dS(const void* Q, const void* K, int R, int R_pad, int Nq, int
 int triad_dS_patch_tiles(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad, int Nk_eff,
                          int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
                          float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
-                         const int* k_tiles, hipStream_t stream) {
-  if (R <= 0 || Bk <= 0 || n_max_part <= 0 || Nk_pad % 32 || CT <= 0) return TRIAD_EINVAL;
+                         const float* temp, const int* k_tiles, hipStream_t stream) {
+  if (R <= 0 || Bk <= 0 || n_max_part <= 0 || Nk_pad % 32 || CT <= 0 || !temp) return TRIAD_EINVAL;
   if (!k_tiles && CT < (long long)Bk * (Nk_pad / 32)) return TRIAD_EINVAL;
   if ((long long)Bk * R >= (1LL << 31) || (long long)Bq * Nq * Nk_eff >= (1LL << 31)) return TRIAD_EINVAL;
   hipLaunchKernelGGL(dS_patch_max_kernel, dim3(n_max_part), dim3(256), 0, stream, (bf16*)dS, CT, R, R_pad, Nq, Bk,
-                     Nk_pad, argmax, rowmax, dclip, qw, ratio_max, max_part, k_tiles);
+                     Nk_pad, argmax, rowmax, dclip, qw, ratio_max, max_part, k_tiles, temp);
   if (gdiag) {
     const long long total = (long long)Bq * Nq * Nk_eff;
     long long blocks = (total + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(dS_patch_diag_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (bf16*)dS, CT, Bq, Nq,
-                       Nk_pad, Nk_eff, diag_off, gdiag, ratio_diag, k_tiles);
+                       Nk_pad, Nk_eff, diag_off, gdiag, ratio_diag, k_tiles, temp);
   }
   TRIAD_CHECK_LAUNCH();
   return TRIAD_OK;
@@ -737,9 +749,9 @@ int triad_dS_patch_tiles(void* dS, long long CT, int R, int R_pad, int Nq, int B
 int triad_dS_patch(void* dS, long long CT, int R, int R_pad, int Nq, int Bq, int Bk, int Nk_pad, int Nk_eff,
                    int diag_off, const int* argmax, const float* rowmax, const float* dclip, const float* qw,
                    float ratio_max, const float* gdiag, float ratio_diag, double* max_part, int n_max_part,
-                   hipStream_t stream) {
+                   const float* temp, hipStream_t stream) {
   return triad_dS_patch_tiles(dS, CT, R, R_pad, Nq, Bq, Bk, Nk_pad, Nk_eff, diag_off, argmax, rowmax, dclip, qw,
-                              ratio_max, gdiag, ratio_diag, max_part, n_max_part, nullptr, stream);
+                              ratio_max, gdiag, ratio_diag, max_part, n_max_part, temp, nullptr, stream);
 }
 
 int triad_dtemp_finalize(const double* p0, int n0, const double* p1, int n1, const double* p2, int n2,

@@ -68,7 +68,7 @@ struct FwdArgs {
   int exact;          // training: exact epilogue (fwd_body<true, true>), see exact_epilogue()
 };
 
-// Which training epilogue a head runs. The fast form computes d = su * clamp(u, lo, 0) and redoes
+// Which training epilogue a head runs. The fast form stores d = clamp(u, lo, 0) and redoes
 // the whole tile (89 VALU per wave, after the MFMA chain) when any u < lo; the exact form selects
 // per element inside the chain (+3 VALU per element). Measured on the c3 shapes
 // (profiles/r06_fwd_exact_ab.log, alternated three times, features N(0, 0.58^2)): TV (clamp -20,
@@ -142,7 +142,7 @@ __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {  // one v_
 // once per launch) so that S = su * u with su = |temp| > 0 (su = 1, u = 0 when temp == 0):
 // max / argmax of S are those of u (rounding is monotone: rowmax = su * max u exactly), and
 // clamp(S, lo, 0) = su * clamp(u, lo / su, 0). Per element that leaves compare + 2 selects
-// (max / argmax), one med3 and half a packed FMA / multiply / convert -- no temperature
+// (max / argmax), one med3, one FMA and (training) half a convert -- no temperature
 // multiply, no per-element SGPR-to-VGPR key moves (argmax within a tile is an inline
 // constant, merged once per tile).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -165,9 +165,12 @@ struct Epi {  // per-lane epilogue state (one 32-row block)
 __device__ __forceinline__ constexpr int vkey(int v) { return (v & 3) + 8 * (v >> 2); }
 
 // One element of a tile's epilogue. FULL: every key of the tile is valid (no mask; padded
-// query rows are zero vectors, u = 0, and add nothing). Fast form of the unit l_nonneg
-// gradient: d = su * c, exact unless some u < lo/su (then c = lo/su but d = 0) -- the tile
-// minimum tracked here detects that and epi_fixup redoes d for such (rare) tiles.
+// query rows are zero vectors, u = 0, and add nothing). The stored unit l_nonneg gradient is
+// d = clamp(S, lo, 0) [S >= lo] / su -- in the window that is c itself, so no per-element
+// multiply (su enters the backward once: the tile GEMMs' alpha and the dS patch terms; round 6,
+// -1.5 % AV / -1.2 % TV training forward, profiles/r06_fwd_nosu_ab.log). Fast form: d = c,
+// exact unless some u < lo/su (then c = lo/su but d = 0) -- the tile minimum tracked here
+// detects that and epi_fixup redoes d for such (rare) tiles.
 // Plain VALU ops as asm: the compiler canonicalises NaNs around fminf/fmaxf/med3-with-inf
 // (extra v_max x, x per operand) and splits the packed f32 ops into scalar ones.
 __device__ __forceinline__ float min3f(float a, float b, float c) {
@@ -194,18 +197,13 @@ __device__ __forceinline__ float fma_sq(float c, float acc) {  // acc + c * c
 // u >= lo ? c : 0 -- plain C so hipcc's hazard recognizer sees the VALU-written lane mask the
 // select reads (v_cmp + v_cndmask)
 __device__ __forceinline__ float selge(float u, float lo, float c) { return u >= lo ? c : 0.f; }
-__device__ __forceinline__ float mulf(float a, float b) {
-  float r;
-  asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
 
 // Empty volatile asm that "modifies" v: the value is computed before this point and stays in
 // place (keeps the epilogue interleaved with the MFMA chain instead of sunk past it).
 #define PIN(v) asm volatile("" : "+v"(v))
 
 template <bool TRAIN, bool FULL, bool EXACT>
-__device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 su2, float lo) {
+__device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, float lo) {
   const float u = p[v];
   if constexpr (FULL) {
     // per PAIR of elements (keys ascend with v): the pair's max against the running max in one
@@ -249,12 +247,11 @@ __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 s
     e.nn2.y = fma_sq(cc.y, e.nn2.y);
     PIN(e.nn2);
     if constexpr (TRAIN) {
-      f32x2 d;
+      f32x2 d = cc;
       if constexpr (EXACT) {
-        d = (f32x2){mulf(e.prevd, su2.x), mulf(dd, su2.y)};
+        d = (f32x2){e.prevd, dd};
       } else {
         e.mn = min3f(e.mn, p[v - 1], u);
-        d = (f32x2){mulf(cc.x, su2.x), mulf(cc.y, su2.y)};
         PIN(e.mn);
       }
       e.pk[v >> 1] = pack_bf16x2(d.x, d.y);
@@ -272,16 +269,16 @@ __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, f32x2 s
   PIN(e.at);
 }
 
-// Slow form for a tile with some u < lo/su: d = su * u on [lo/su, 0], else 0; returns the
-// tile's sum of d^2 / su^2 (the fast form's sum of c^2 over-counts the clamped elements).
-__device__ __forceinline__ float epi_fixup(Epi& e, const f32x16& p, float su, float lo) {
+// Slow form for a tile with some u < lo/su: d = u on [lo/su, 0], else 0; returns the tile's
+// sum of d^2 (the fast form's sum of c^2 over-counts the clamped elements).
+__device__ __forceinline__ float epi_fixup(Epi& e, const f32x16& p, float lo) {
   float st = 0.f, dp = 0.f;
 #pragma unroll
   for (int v = 0; v < 16; ++v) {
     const float u = p[v];
     const float d = (u >= lo && u <= 0.f) ? u : 0.f;
     st = fmaf(d, d, st);
-    if (v & 1) e.pk[v >> 1] = pack_bf16x2(dp * su, d * su);
+    if (v & 1) e.pk[v >> 1] = pack_bf16x2(dp, d);
     else dp = d;
   }
   return st;
@@ -409,7 +406,6 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       qf[s] = __builtin_bit_cast(bf16x8, w);
     }
   }
-  const f32x2 su2 = {su, su};
   const float lo = a.clamp_lo / su;  // clamp window of u
   double accd = 0.0, accd2 = 0.0;
   // lane part of the swizzled LDS fragment offsets (bytes), k-step s reads chunk 2(s&7)+h
@@ -476,7 +472,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       float st;
       if constexpr (EXACT) st = e.st2.x + e.st2.y;
       // some u below the window in this wave's tile: redo d (wave-uniform branch)
-      else st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup(e, p, su, lo) : nn;
+      else st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup(e, p, lo) : nn;
       accd2 += (double)st;
       // canonical chunks 2 lane, 2 lane + 1 at ds_chunk(): two 1 KB contiguous stores per wave
       bf16* d = dS_w + ((long long)tile0 + ec.t) * 1024 + lane * 8;
@@ -523,7 +519,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
         if (s + P < NS) af[(s + P) % (P + 1)] = *(const bf16x8*)(kt + xo[(s + P) & 7] + ((s + P) >> 3) * 256);
         c = mfma32(af[s % (P + 1)], qf[s], c);
         if constexpr (ep) {
-          if (s & 1) epi_elem<TRAIN, full, EXACT>(e, p, s >> 1, su2, lo);
+          if (s & 1) epi_elem<TRAIN, full, EXACT>(e, p, s >> 1, lo);
         }
         // scheduling regions of 4 k-steps: two epilogue elements interleave and fill each
         // other's VALU->SGPR-mask wait states
@@ -531,7 +527,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
       }
     } else if constexpr (ep) {
 #pragma unroll
-      for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full, EXACT>(e, p, v, su2, lo);
+      for (int v = 0; v < 16; ++v) epi_elem<TRAIN, full, EXACT>(e, p, v, lo);
     }
     if constexpr (ep) epi_end(p);
   };
@@ -603,7 +599,7 @@ struct Epi16 {
 __device__ __forceinline__ constexpr int vkey16(int v) { return 16 * (v >> 3) + (v & 3); }
 
 template <bool TRAIN, bool FULL>
-__device__ __forceinline__ void epi_elem16(Epi16& e, const f32x4 (&p)[4], int v, f32x2 su2, float lo) {
+__device__ __forceinline__ void epi_elem16(Epi16& e, const f32x4 (&p)[4], int v, float lo) {
   const int qb = (v >> 2) & 1;
   const float u = p[v >> 2][v & 3];
   if constexpr (FULL) {
@@ -622,7 +618,7 @@ __device__ __forceinline__ void epi_elem16(Epi16& e, const f32x4 (&p)[4], int v,
     PIN(e.nn2);
     if constexpr (TRAIN) {
       e.mn = min3f(e.mn, p[v >> 2][(v & 3) - 1], u);
-      e.pk[v >> 1] = pack_bf16x2(mulf(e.prev, su2.x), mulf(c, su2.y));
+      e.pk[v >> 1] = pack_bf16x2(e.prev, c);
       PIN(e.mn);
       PIN(e.pk[v >> 1]);
     }
@@ -634,14 +630,14 @@ __device__ __forceinline__ void epi_elem16(Epi16& e, const f32x4 (&p)[4], int v,
   PIN(e.at[qb]);
 }
 
-__device__ __forceinline__ float epi_fixup16(Epi16& e, const f32x4 (&p)[4], float su, float lo) {
+__device__ __forceinline__ float epi_fixup16(Epi16& e, const f32x4 (&p)[4], float lo) {
   float st = 0.f, dp = 0.f;
 #pragma unroll
   for (int v = 0; v < 16; ++v) {
     const float u = p[v >> 2][v & 3];
     const float d = (u >= lo && u <= 0.f) ? u : 0.f;
     st = fmaf(d, d, st);
-    if (v & 1) e.pk[v >> 1] = pack_bf16x2(dp * su, d * su);
+    if (v & 1) e.pk[v >> 1] = pack_bf16x2(dp, d);
     else dp = d;
   }
   return st;
@@ -703,7 +699,6 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
         qf[qb][s] = __builtin_bit_cast(bf16x8, w);
       }
   }
-  const f32x2 su2 = {su, su};
   const float lo = a.clamp_lo / su;
   double accd = 0.0, accd2 = 0.0;
   // swizzled LDS key-fragment offsets (bytes): key row 16 kb2 + i, chunk 4 s + g
@@ -742,7 +737,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
     const float nn = e.nn2.x + e.nn2.y;
     accd += (double)nn;
     if (TRAIN) {
-      const float st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup16(e, p, su, lo) : nn;
+      const float st = __builtin_amdgcn_ballot_w64(e.mn < lo) ? epi_fixup16(e, p, lo) : nn;
       accd2 += (double)st;
       // lanes l and l ^ 32 hold the two halves of the same 16-element runs: swap one 8-byte
       // piece so each lane stores one 16-byte run (h5 = 0: elements 0..7, h5 = 1: 8..15)
@@ -807,12 +802,12 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
 #pragma unroll
           for (int qb = 0; qb < 2; ++qb)
             c[2 * kb2 + qb] = mfma16(af[s % (P + 1)][kb2], qf[qb][s], c[2 * kb2 + qb]);
-        if constexpr (ep) epi_elem16<TRAIN, full>(e, p, s, su2, lo);
+        if constexpr (ep) epi_elem16<TRAIN, full>(e, p, s, lo);
         __builtin_amdgcn_sched_barrier(0);
       }
     } else if constexpr (ep) {
 #pragma unroll
-      for (int v = 0; v < 16; ++v) epi_elem16<TRAIN, full>(e, p, v, su2, lo);
+      for (int v = 0; v < 16; ++v) epi_elem16<TRAIN, full>(e, p, v, lo);
     }
     if constexpr (ep) epi_end(p);
   };

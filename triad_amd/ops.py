@@ -560,15 +560,18 @@ def _head_backward(h, saved, needs, g_total, g_ce, g_reg, g_aux):
     gq = gk = gt = None
     if fast:
         # dS = c_nn * (unit l_nonneg grad [written by the forward] + ratio_max * max term
-        #               + ratio_diag * diagonal term); the ratios are host constants here
+        #               + ratio_diag * diagonal term); the ratios are host constants here. The
+        # forward stores the unit gradient divided by su = |temp| (1 at temp == 0), the patch adds
+        # its terms divided by su (reading temp on the device) and alpha carries su.
         ratio_max = h.n_el / 0.3
         ratio_diag = (0.01 if kind == AV else h.w_sparse) * h.n_el / 0.3
         nmp = 1024
         max_part = torch.empty(nmp, dtype=torch.float64, device=dev)
         call("triad_dS_patch_tiles", ptr(dS), CT, g.R, g.R_pad, g.Nq, g.Bq, g.Bk, g.Nk_pad, g.Nk_eff, rank * g.Bq,
              ptr(argmax), ptr(rowmax), ptr(dclip), ptr(qw), float(ratio_max), ptr(gdiag), float(ratio_diag),
-             ptr(max_part), nmp, ptr(ktiles), st)
-        alpha = (temp * c_nn).reshape(1).contiguous()
+             ptr(max_part), nmp, ptr(temp), ptr(ktiles), st)
+        su = torch.where(temp != 0, temp.abs(), torch.ones_like(temp))
+        alpha = (temp * c_nn * su).reshape(1).contiguous()
         w = torch.stack([c_nn, c_ce / temp[0], c_diag / temp[0], c_cal]).contiguous()
         parts = (st_part, h.nparts, max_part, nmp, dgt_part, g.Bq)
     else:
