@@ -259,7 +259,9 @@ def test_forward_counted_waits_match_emitted_vmem(isa):
     runs alternate (a tile's pieces before the next epilogue's stores, nothing counted between), and
     the counted waits in the loop are exactly {nd G + ns S} -- a constant off by one, a piece or a
     store hipcc dropped or duplicated, or a reordering fails. The prologue's sync_tile(0) waits
-    vmcnt(nd G) after exactly NBUF - 1 = 2 prefetches."""
+    vmcnt(nd G) after exactly NBUF - 1 = 2 prefetches. The loop runs two tiles per trip (the
+    accumulator sets alternate, TRIAD_FWD_PINGPONG); an odd last tile runs in straight-line code
+    after it, whose counted waits must decode to some (nd, ns) as well."""
     asm = isa["pairsim_fwd.hip"]
     ks = {s: l for s, l in _kernels(asm).items()
           if ("pairsim_fwd2_kernelILb1E" in s or "pairsim_fwd_multi_kernelILb1E" in s)}
@@ -269,6 +271,7 @@ def test_forward_counted_waits_match_emitted_vmem(isa):
         hdrs = [i for i, l in enumerate(lines) if "Loop Header" in l and "Depth=1" in l]
         assert len(hdrs) == 2, (sym, len(hdrs))
         prev = 0
+        allruns, allwaits = _asm_runs(lines, 0, len(lines))
         for hdr in hdrs:
             loop = _loop_lines(lines, hdr)
             runs, waits = _asm_runs(lines, 0, 0, loop)
@@ -280,13 +283,24 @@ def test_forward_counted_waits_match_emitted_vmem(isa):
             kinds = [k for k, _, _ in runs if k in "DS"]
             assert kinds == ["D", "S"] * (len(kinds) // 2), (sym, kinds)
             assert set(waits) == {0, G, S, G + S}, (sym, sorted(set(waits)), (G, S))
-            # this body's prologue: the code since the previous loop outside any loop
+            # this body's prologue: the code outside any loop since the previous body's last dS
+            # store (hipcc may hoist the prologue prefetches both bodies share above the branch
+            # between them: then only the first body's region holds them)
             inloop = set(loop)
             pro = [i for i in range(prev, hdr) if i not in inloop]
+            pro_runs, _ = _asm_runs(lines, 0, 0, pro)
+            last_s = max([ln for k, _, ln in pro_runs if k == "S"], default=-1)
+            pro = [i for i in pro if i > last_s]
             pro_runs, pro_waits = _asm_runs(lines, 0, 0, pro)
             pro_d = [n for k, n, _ in pro_runs if k == "D"]
-            assert pro_d[:2] == [G, G] and set(pro_waits) <= {0, G}, (sym, pro_runs, pro_waits)
+            assert pro_d and set(pro_d) == {G} and set(pro_waits) <= {0, G}, (sym, pro_runs, pro_waits)
+            if prev == 0:
+                assert pro_d[:2] == [G, G], (sym, pro_runs)
             prev = max(loop) + 1
+        # everywhere (the odd-tile step after each loop included): pieces come G per tile, stores S
+        # per epilogue, and every counted wait is one of nd G + ns S
+        assert {n for k, n, _ in allruns if k == "D"} == {G} and {n for k, n, _ in allruns if k == "S"} == {S}, sym
+        assert set(allwaits) <= {0, G, S, G + S}, (sym, sorted(set(allwaits)))
 
 
 def test_rowgemm_tail_stages_drain_before_their_barrier(isa):

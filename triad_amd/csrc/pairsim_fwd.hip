@@ -28,6 +28,9 @@ constexpr int NS = D / 16;  // 32 k-steps
 constexpr int WAVES = 8;
 constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 query rows per workgroup
 constexpr int KT_ELEMS = 32 * D;
+#ifndef TRIAD_FWD_PINGPONG
+#define TRIAD_FWD_PINGPONG 1   // two tiles per loop trip, accumulator sets alternating (A/B knob)
+#endif
 #ifndef TRIAD_FWD_SYNC_FAST
 #define TRIAD_FWD_SYNC_FAST 1   // sync_tile: steady-state wait tested first (A/B knob)
 #endif
@@ -545,7 +548,25 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     return nv >= 32;
   };
 
-  // chain(b) accumulates into cA while the epilogue of b-1 reads cB; cB = cA after each chain
+  // chain(b) accumulates into one register set while the epilogue of b-1 reads the other
+#if TRIAD_FWD_PINGPONG
+  // two tiles per trip with the sets' roles swapped (no 16-register copy per tile; a copy once
+  // per launch when the tile count is even)
+  auto step = [&](int b, f32x16& c, const f32x16& p) __attribute__((always_inline)) {
+    if (tile_full()) iter(T{}, T{}, T{}, b, c, p);
+    else iter(T{}, T{}, F{}, b, c, p);
+  };
+  iter(T{}, F{}, T{}, 0, cB, cA);
+  int b = 1;
+  for (; b + 1 < nblocks; b += 2) {
+    step(b, cA, cB);
+    step(b + 1, cB, cA);
+  }
+  if (b < nblocks) {
+    step(b, cA, cB);
+    cB = cA;
+  }
+#else
   iter(T{}, F{}, T{}, 0, cA, cB);
   cB = cA;
   for (int b = 1; b < nblocks; ++b) {
@@ -553,6 +574,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     else iter(T{}, T{}, F{}, b, cA, cB);
     cB = cA;
   }
+#endif
   if (tile_full()) iter(F{}, T{}, T{}, nblocks, cA, cB);
   else iter(F{}, T{}, F{}, nblocks, cA, cB);
 
