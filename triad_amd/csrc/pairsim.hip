@@ -357,6 +357,9 @@ __device__ __forceinline__ long long tile_elem(long long CT, int r, long long c)
   return ((long long)(r >> 5) * CT + (c >> 5)) * 1024 + ds_chunk(2 * lane + (v >> 3)) * 8 + (v & 7);
 }
 
+#ifndef PATCH_U
+#define PATCH_U 4   // elements per thread per pass (A/B knob; round 6, tools/gpu_ab_patch.sh,
+#endif              // profiles/r06_patch_ilp_ab.log: 8 / 16 and 2048 / 4096 workgroups 2-20 % slower)
 // Four elements per thread per pass with all their loads issued together, 32-bit index math:
 // one element per pass (a dependent argmax -> dS round trip each, 64-bit divisions) made the AV
 // patch a latency-bound 0.3 ms launch at c3.
@@ -373,11 +376,11 @@ __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS
   const float rs = ratio * unit_scale(temp);
   const int total = Bk * R;   // < 2^31 (host check)
   const int stride = gridDim.x * blockDim.x;
-  for (int e0 = blockIdx.x * blockDim.x + threadIdx.x; e0 < total; e0 += 4 * stride) {
-    float w[4], rm[4], old[4];
-    bf16* p[4];
+  for (int e0 = blockIdx.x * blockDim.x + threadIdx.x; e0 < total; e0 += PATCH_U * stride) {
+    float w[PATCH_U], rm[PATCH_U], old[PATCH_U];
+    bf16* p[PATCH_U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PATCH_U; ++u) {
       const int e = min(e0 + u * stride, total - 1);
       const int j = e / R, r = e - j * R;
       const int i = r / Nq;
@@ -388,9 +391,9 @@ __global__ __launch_bounds__(256) void dS_patch_max_kernel(bf16* __restrict__ dS
       p[u] = c < 0 ? nullptr : dS + tile_elem(CT, r, c);   // unstored zero tile: K there is zero
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) old[u] = p[u] ? (float)*p[u] : 0.f;
+    for (int u = 0; u < PATCH_U; ++u) old[u] = p[u] ? (float)*p[u] : 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PATCH_U; ++u) {
       if (e0 + u * stride >= total) break;
       if (p[u]) *p[u] = (bf16)(old[u] + rs * w[u]);
       acc += (double)w[u] * (double)rm[u];
