@@ -28,12 +28,18 @@ constexpr int NS = D / 16;  // 32 k-steps
 constexpr int WAVES = 8;
 constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 query rows per workgroup
 constexpr int KT_ELEMS = 32 * D;
+#ifndef TRIAD_FWD_KPAD
+#define TRIAD_FWD_KPAD 1   // training ring: padded unswizzled rows, immediate ds_read offsets (A/B knob;
+#endif                   // AV -0.3 %, TV -0.6 %: profiles/r06_fwd_kpad_ab.log)
 #ifndef TRIAD_FWD_PINGPONG
 #define TRIAD_FWD_PINGPONG 1   // two tiles per loop trip, accumulator sets alternating (A/B knob)
 #endif
 #ifndef TRIAD_FWD_SYNC_FAST
 #define TRIAD_FWD_SYNC_FAST 1   // sync_tile: steady-state wait tested first (A/B knob)
 #endif
+#ifndef TRIAD_FWD_TREEMAX
+#define TRIAD_FWD_TREEMAX 0   // FULL tiles: max3 tree + reverse first-index scan (A/B knob; -8 VALU
+#endif                      // per tile, timing equal: profiles/r06_fwd_treemax_ab.log)
 #ifndef TRIAD_FWD_PAIRMAX
 // training epilogue: max / argmax per pair of elements (5 VALU per pair instead of 6). Measured
 // slower: AV training 2.925 / 2.928 ms element by element against 2.952 / 2.953 per pair
@@ -121,6 +127,23 @@ __device__ __forceinline__ void stage_piece(i32x4 kr, bf16* dst, int trow, int w
 __device__ __forceinline__ void stage_tile(i32x4 kr, bf16* dst, int trow, int wave, int lane) {
 #pragma unroll
   for (int u = 0; u < GLDS_PER_TILE; ++u) stage_piece(kr, dst, trow, wave, lane, u);
+}
+
+// Training body's ring (TRIAD_FWD_KPAD): rows unswizzled at a 1040-byte stride (one 16-byte pad
+// per row), so the 32 rows' reads of one chunk start 4 banks apart (conflict-free per 8 lanes of
+// a 16-byte read) and a k-step's LDS offset is lane part + 32 s -- an immediate on every ds_read
+// instead of a per-read address OR (the XOR swizzle's chunk depends on the lane).
+constexpr int KROW_PAD_BYTES = D * 2 + 16;
+constexpr int KT_SLOT_BYTES = 32 * KROW_PAD_BYTES;
+__device__ __forceinline__ void stage_tile_pad(i32x4 kr, bf16* dst, int trow, int wave, int lane) {
+  const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) bf16*)dst;
+  asm volatile("" : "+v"(lane));
+#pragma unroll
+  for (int u = 0; u < GLDS_PER_TILE; ++u) {
+    const int t = wave * GLDS_PER_TILE + u;
+    dma16(kr, __builtin_amdgcn_readfirstlane(lds0 + t * KROW_PAD_BYTES), (unsigned)(lane * 16),
+          __builtin_amdgcn_readfirstlane((unsigned)(trow + t) * (D * 2)));
+  }
 }
 
 // 16-byte store hidden from hipcc's waitcnt bookkeeping (it would otherwise drain vmcnt(0) --
@@ -213,7 +236,19 @@ __device__ __forceinline__ void epi_elem(Epi& e, const f32x16& p, int v, float l
     // v_max3, the pair's argmax (u1 > u0 strict, so a tie keeps the first key) taken only if the
     // running max rose (strict, so an earlier key keeps ties) -- 5 VALU per pair instead of 6,
     // the same max / argmax as element by element
-#if TRIAD_FWD_PAIRMAX
+#if TRIAD_FWD_TREEMAX
+    // the tile's max (with the running max folded in) by a v_max3 tree at the first element, then
+    // the first key holding it by a reverse scan, one compare + select per element: 40 VALU per
+    // tile instead of 48. e.at is read only when the tile raised the running max (epi_end), and
+    // then the first key equal to the new max is the one the element-by-element strict walk keeps.
+    if (v == 0) {
+      const float t0 = max3f(p[0], p[1], p[2]), t1 = max3f(p[3], p[4], p[5]), t2 = max3f(p[6], p[7], p[8]);
+      const float t3 = max3f(p[9], p[10], p[11]), t4 = max3f(p[12], p[13], p[14]);
+      const float t5 = max3f(t0, t1, t2), t6 = max3f(t3, t4, p[15]);
+      e.m = max3f(t5, t6, e.m);
+    }
+    e.at = p[15 - v] == e.m ? vkey(15 - v) : e.at;
+#elif TRIAD_FWD_PAIRMAX
     if (v & 1) {
       const float u0 = p[v - 1];
       const float mn = max3f(e.m, u0, u);
@@ -325,7 +360,8 @@ struct Cursor {  // wave-uniform position (sample j, key block kb) of a tile in 
 // this paired 16 x 16 x 32 body 4 % slower, AV 3.15 -> 3.27-3.30, profiles/r05_fwd_train16_ab.log).
 constexpr int NBUF16 = 4;
 template <bool TRAIN>
-constexpr int kbuf_elems = (TRAIN ? NBUF : NBUF16) * KT_ELEMS + 16 * WAVES;
+constexpr int kbuf_elems = (TRAIN ? NBUF * (TRIAD_FWD_KPAD ? KT_SLOT_BYTES / 2 : KT_ELEMS) : NBUF16 * KT_ELEMS) + 16 * WAVES;
+constexpr int KSLOT_ELEMS = TRIAD_FWD_KPAD ? KT_SLOT_BYTES / 2 : KT_ELEMS;   // training ring slot
 
 // One workgroup of the forward: 256-row block bx, key-sample split by (of gx row blocks) of
 // problem a. kbuf = the workgroup's LDS (key ring + reduction scratch). EXACT (training): the
@@ -333,7 +369,7 @@ constexpr int kbuf_elems = (TRAIN ? NBUF : NBUF16) * KT_ELEMS + 16 * WAVES;
 // per-tile redo when some u < lo (FwdArgs::exact, chosen per head by the host).
 template <bool TRAIN, bool EXACT = false>
 __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int bx, const int by, const int gx) {
-  double* red = (double*)(kbuf + NBUF * KT_ELEMS);
+  double* red = (double*)(kbuf + NBUF * KSLOT_ELEMS);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -381,7 +417,11 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   Cursor fc{j0, 0}, cc{j0, 0}, ec{j0, 0};
   int fslot = 0, cslot = 0;
   auto prefetch = [&](int b2) __attribute__((always_inline)) {
+#if TRIAD_FWD_KPAD
+    if (b2 < nblocks) stage_tile_pad(kr, kbuf + fslot * KSLOT_ELEMS, b2 * 32, wave, lane);   // stored tiles in walk order
+#else
     if (b2 < nblocks) stage_tile(kr, kbuf + fslot * KT_ELEMS, b2 * 32, wave, lane);   // stored tiles in walk order
+#endif
     fc.next(nkb, skip, j0);
     fslot = __builtin_amdgcn_readfirstlane(fslot == NBUF - 1 ? 0 : fslot + 1);
   };
@@ -411,10 +451,16 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
   }
   const float lo = a.clamp_lo / su;  // clamp window of u
   double accd = 0.0, accd2 = 0.0;
-  // lane part of the swizzled LDS fragment offsets (bytes), k-step s reads chunk 2(s&7)+h
+  // lane part of the LDS fragment offsets (bytes), k-step s reads chunk 2s+h of row ql
+#if TRIAD_FWD_KPAD
+  const int xo0 = ql * KROW_PAD_BYTES + h * 16;
+  auto koff = [&](int s) __attribute__((always_inline)) { return xo0 + 32 * s; };
+#else
   int xo[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) xo[k] = ql * (D * 2) + (((2 * k + h) ^ (ql & 15)) * 16);
+  auto koff = [&](int s) __attribute__((always_inline)) { return xo[s & 7] + (s >> 3) * 256; };
+#endif
   // this wave's dS row block (TRAIN): tile (rt, ct) at (rt*CT + ct)*1024 elements
   bf16* const dS_w = TRAIN ? a.dS + (long long)rt * a.CT * 1024 : nullptr;
 
@@ -510,16 +556,16 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     if constexpr (ch) {
       sync_tile(b);
       prefetch(b + NBUF - 1);
-      const char* kt = (const char*)kbuf + cslot * (KT_ELEMS * 2);
+      const char* kt = (const char*)kbuf + cslot * (KSLOT_ELEMS * 2);
       cslot = __builtin_amdgcn_readfirstlane(cslot == NBUF - 1 ? 0 : cslot + 1);
       constexpr int P = LDSPF;
       bf16x8 af[P + 1];
 #pragma unroll
-      for (int s = 0; s < P; ++s) af[s] = *(const bf16x8*)(kt + xo[s & 7] + (s >> 3) * 256);
+      for (int s = 0; s < P; ++s) af[s] = *(const bf16x8*)(kt + koff(s));
       c = (f32x16){};
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        if (s + P < NS) af[(s + P) % (P + 1)] = *(const bf16x8*)(kt + xo[(s + P) & 7] + ((s + P) >> 3) * 256);
+        if (s + P < NS) af[(s + P) % (P + 1)] = *(const bf16x8*)(kt + koff(s + P));
         c = mfma32(af[s % (P + 1)], qf[s], c);
         if constexpr (ep) {
           if (s & 1) epi_elem<TRAIN, full, EXACT>(e, p, s >> 1, lo);
