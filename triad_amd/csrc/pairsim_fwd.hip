@@ -28,6 +28,9 @@ constexpr int NS = D / 16;  // 32 k-steps
 constexpr int WAVES = 8;
 constexpr int ROWS_PER_WG = 32 * WAVES;  // 256 query rows per workgroup
 constexpr int KT_ELEMS = 32 * D;
+#ifndef TRIAD_FWD_PF_AT
+#define TRIAD_FWD_PF_AT 9   // k-step after which the next tile's DMA is issued; -1: before the chain
+#endif                     // (round 6: 9 vs -1 AV -2.2 %, TV -2.5 %; 1-27 swept, profiles/r06_fwd_pf_at_ab.log)
 #ifndef TRIAD_FWD_KPAD
 #define TRIAD_FWD_KPAD 1   // training ring: padded unswizzled rows, immediate ds_read offsets (A/B knob;
 #endif                   // AV -0.3 %, TV -0.6 %: profiles/r06_fwd_kpad_ab.log)
@@ -555,7 +558,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
     constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value, full = decltype(FULLT)::value;
     if constexpr (ch) {
       sync_tile(b);
-      prefetch(b + NBUF - 1);
+      if (TRIAD_FWD_PF_AT < 0) prefetch(b + NBUF - 1);
       const char* kt = (const char*)kbuf + cslot * (KSLOT_ELEMS * 2);
       cslot = __builtin_amdgcn_readfirstlane(cslot == NBUF - 1 ? 0 : cslot + 1);
       constexpr int P = LDSPF;
@@ -573,6 +576,13 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
         // scheduling regions of 4 k-steps: two epilogue elements interleave and fill each
         // other's VALU->SGPR-mask wait states
         if (s % REGION == REGION - 1) __builtin_amdgcn_sched_barrier(0);
+        // TRIAD_FWD_PF_AT >= 0: the next DMA issued inside the chain (its slot was last read
+        // before this tile's barrier), off the barrier -> first MFMA path
+        if (s == TRIAD_FWD_PF_AT) {
+          __builtin_amdgcn_sched_barrier(0);
+          prefetch(b + NBUF - 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     } else if constexpr (ep) {
 #pragma unroll
