@@ -293,6 +293,9 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+#ifndef TRIAD_DB_PF_RB
+#define TRIAD_DB_PF_RB 3   // row block after which a stage's prefetch is issued (A/B knob; round 6:
+#endif                     // 3 vs 1: -0.6 to -0.8 % on all four c3 GEMMs, profiles/r06_bwd_pf_rb_ab.log)
 // DD stages in flight ahead of the one being multiplied (A ring slots = B register ring depth =
 // NB = DD + 1); one workgroup barrier per stage. DD = 3 for dQ and dK (dK with two k tiles per
 // stage, as its 32x32x16 form had, would spill).
@@ -341,7 +344,7 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
   // stage st in ring slot u = st % NB: wait for its A piece (the counted vmcnt: the DD - 1 younger
   // stages, 5 ops each, stay in flight; hipcc waits for its B loads itself), barrier, 32 MFMAs with
   // the prefetch of stage st + DD (into slot (u + DD) % NB, read for the last time by stage st - 1,
-  // before this barrier) issued after the first two row blocks
+  // before this barrier) issued after row block TRIAD_DB_PF_RB
   // TAIL: one of the trailing nst % NB stages. Their own prefetches feed no later stage, so hipcc
   // drops those B loads as dead: a tail stage has fewer than 5 (DD - 1) younger VMEM ops in flight
   // and the counted wait would let it pass before its A piece landed (round 5: AV dK with 3 splits of
@@ -369,7 +372,7 @@ __global__ __launch_bounds__(512, 1) void tile_gemm_db16_kernel(const bf16* __re
     for (int rb = 0; rb < 8; ++rb) {
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = mfma16(af[rb], bq[u][cb], acc[rb][cb]);
-      if (rb == 1) {
+      if (rb == TRIAD_DB_PF_RB) {
         __builtin_amdgcn_sched_barrier(0);
         db_stage<DK>(Dt, CT, Bp, mt0, kt0 + st + DD, kt_last, lds + ((u + DD) % NB) * 4096, bq[(u + DD) % NB],
                      wave, lane);
