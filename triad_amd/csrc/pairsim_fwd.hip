@@ -657,7 +657,16 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a, bf16* kbuf, const int
 // (q + 32 ((k >> 2) & 1)) * 16 + (k & 3) + 4 (k >> 3)): per query half and key half a lane's four
 // keys are one 8-byte piece of a 16-element run whose other pieces lane l ^ 32 holds.
 constexpr int NS16 = D / 32;  // 16 k-steps
-constexpr int LDSPF16 = 2;
+// Eval body: two tiles per loop trip with the accumulator sets alternating (no per-tile copy), which
+// fits the register file only with LDS fragments one k-step ahead instead of two (249 VGPRs, no
+// spill; with two ahead it spills 24): AV -2.9 %, TV -2.5 % (round 6, profiles/r06_fwd_eval_pingpong_ab.log)
+#ifndef TRIAD_FWD16_LDSPF
+#define TRIAD_FWD16_LDSPF 1
+#endif
+#ifndef TRIAD_FWD16_PINGPONG
+#define TRIAD_FWD16_PINGPONG 1   // (A/B knob)
+#endif
+constexpr int LDSPF16 = TRIAD_FWD16_LDSPF;
 
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -907,6 +916,22 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
     for (int t = 0; t < 4; ++t) cB[t] = cA[t];
   };
 
+#if TRIAD_FWD16_PINGPONG
+  auto step = [&](int b, f32x4 (&c)[4], const f32x4 (&p)[4]) __attribute__((always_inline)) {
+    if (tile_full()) iter(T{}, T{}, T{}, b, c, p);
+    else iter(T{}, T{}, F{}, b, c, p);
+  };
+  iter(T{}, F{}, T{}, 0, cB, cA);
+  int b = 1;
+  for (; b + 1 < nblocks; b += 2) {
+    step(b, cA, cB);
+    step(b + 1, cB, cA);
+  }
+  if (b < nblocks) {
+    step(b, cA, cB);
+    copy();
+  }
+#else
   iter(T{}, F{}, T{}, 0, cA, cB);
   copy();
   for (int b = 1; b < nblocks; ++b) {
@@ -914,6 +939,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
     else iter(T{}, T{}, F{}, b, cA, cB);
     copy();
   }
+#endif
   if (tile_full()) iter(F{}, T{}, T{}, nblocks, cA, cB);
   else iter(F{}, T{}, F{}, nblocks, cA, cB);
 
