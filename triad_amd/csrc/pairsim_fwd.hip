@@ -660,6 +660,9 @@ constexpr int NS16 = D / 32;  // 16 k-steps
 // Eval body: two tiles per loop trip with the accumulator sets alternating (no per-tile copy), which
 // fits the register file only with LDS fragments one k-step ahead instead of two (249 VGPRs, no
 // spill; with two ahead it spills 24): AV -2.9 %, TV -2.5 % (round 6, profiles/r06_fwd_eval_pingpong_ab.log)
+#ifndef TRIAD_FWD16_PF_AT
+#define TRIAD_FWD16_PF_AT 8   // eval body: k-step after which a tile pair's DMA is issued (A/B knob;
+#endif                      // 8 vs -1: AV -2.3 %, TV -1.3 %, 3 / 5 / 8 swept, profiles/r06_fwd_eval_pf_at_ab.log)
 #ifndef TRIAD_FWD16_LDSPF
 #define TRIAD_FWD16_LDSPF 1
 #endif
@@ -865,7 +868,7 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
     constexpr bool ch = decltype(CH)::value, ep = decltype(EP)::value, full = decltype(FULLT)::value;
     if constexpr (ch) {
       sync_tile(b);
-      refill(b);
+      if (TRIAD_FWD16_PF_AT < 0) refill(b);
       const char* kt = (const char*)kbuf + cslot * (KT_ELEMS * 2);
       cslot = __builtin_amdgcn_readfirstlane(cslot == NBUF16 - 1 ? 0 : cslot + 1);
       constexpr int P = LDSPF16;
@@ -891,6 +894,10 @@ __device__ __forceinline__ void fwd_body16(const FwdArgs& a, bf16* kbuf, const i
             c[2 * kb2 + qb] = mfma16(af[s % (P + 1)][kb2], qf[qb][s], c[2 * kb2 + qb]);
         if constexpr (ep) epi_elem16<TRAIN, full>(e, p, s, lo);
         __builtin_amdgcn_sched_barrier(0);
+        if (s == TRIAD_FWD16_PF_AT) {   // the pair's DMA inside the chain (as fwd_body's TRIAD_FWD_PF_AT)
+          refill(b);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     } else if constexpr (ep) {
 #pragma unroll
